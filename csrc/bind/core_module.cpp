@@ -1,0 +1,298 @@
+// pybind11 bindings for the zest host core (`zest_amd._core`).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "blake3.h"
+#include "cdc.h"
+#include "common.h"
+#include "lz4.h"
+#include "xet_hash.h"
+#include "xorb.h"
+#include "bind_extra.h"
+
+namespace py = pybind11;
+using namespace zest;
+
+namespace {
+
+ByteSpan span_of(const py::buffer& b) {
+  py::buffer_info info = b.request();
+  return ByteSpan(static_cast<const uint8_t*>(info.ptr), size_t(info.size) * size_t(info.itemsize));
+}
+
+py::bytes to_bytes(const uint8_t* p, size_t n) { return py::bytes(reinterpret_cast<const char*>(p), n); }
+py::bytes to_bytes(const Bytes& b) { return to_bytes(b.data(), b.size()); }
+py::bytes to_bytes(const xet::Hash& h) { return to_bytes(h.data(), 32); }
+
+xet::Hash hash_of(const py::bytes& b) {
+  std::string s = b;
+  if (s.size() != 32) throw Error("InvalidHash", "hash must be 32 bytes");
+  xet::Hash h;
+  std::memcpy(h.data(), s.data(), 32);
+  return h;
+}
+
+std::vector<xet::HashSize> leaves_of(const py::list& l) {
+  std::vector<xet::HashSize> out;
+  out.reserve(l.size());
+  for (auto item : l) {
+    auto t = item.cast<py::tuple>();
+    out.push_back({hash_of(t[0].cast<py::bytes>()), t[1].cast<uint64_t>()});
+  }
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_core, m) {
+  m.doc() = "zest MI355X-native framework: host core (C++17)";
+  static py::exception<Error> zerr(m, "ZestError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const Error& e) {
+      py::handle cls = zerr;
+      py::object exc = cls(py::str(e.what()));
+      exc.attr("code") = e.code();
+      PyErr_SetObject(zerr.ptr(), exc.ptr());
+    }
+  });
+
+  // ---------------- BLAKE3 ----------------
+  m.def("blake3", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    uint8_t out[32];
+    {
+      py::gil_scoped_release nogil;
+      blake3::hash(s.data, s.size, out);
+    }
+    return to_bytes(out, 32);
+  });
+  m.def("blake3_keyed", [](py::bytes key, py::buffer b) {
+    std::string k = key;
+    if (k.size() != 32) throw Error("InvalidKey", "key must be 32 bytes");
+    ByteSpan s = span_of(b);
+    uint8_t out[32];
+    {
+      py::gil_scoped_release nogil;
+      blake3::keyed_hash(reinterpret_cast<const uint8_t*>(k.data()), s.data, s.size, out);
+    }
+    return to_bytes(out, 32);
+  });
+  m.def("blake3_backend", &blake3::simd_backend);
+  m.def("blake3_force_backend", [](const std::string& n) { return blake3::force_backend(n.c_str()); });
+
+  // ---------------- Xet hashing ----------------
+  m.attr("DATA_KEY") = to_bytes(xet::kDataKey, 32);
+  m.attr("INTERNAL_NODE_KEY") = to_bytes(xet::kInternalNodeKey, 32);
+  m.def("chunk_hash", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    xet::Hash h;
+    {
+      py::gil_scoped_release nogil;
+      h = xet::chunk_hash(s.data, s.size);
+    }
+    return to_bytes(h);
+  });
+  m.def("internal_node_hash", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    return to_bytes(xet::internal_node_hash(s.data, s.size));
+  });
+  m.def("xet_hex", [](py::bytes b) { return xet::to_hex(hash_of(b)); });
+  m.def("from_xet_hex", [](const std::string& s) { return to_bytes(xet::from_hex(s)); });
+  m.def("bytewise_hex", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    return xet::to_bytewise_hex(s.data, s.size);
+  });
+  m.def("merkle_root", [](py::list l) { return to_bytes(xet::merkle_root(leaves_of(l))); });
+  m.def("file_hash", [](py::list l) { return to_bytes(xet::file_hash(leaves_of(l))); });
+  m.def("file_hash_from_root", [](py::bytes root) { return to_bytes(xet::file_hash_from_root(hash_of(root), false)); });
+  m.def("next_merge_cut", [](py::list l) {
+    auto v = leaves_of(l);
+    return xet::next_merge_cut(v.data(), v.size());
+  });
+  m.def("chunk_ends", [](py::buffer b, size_t target) {
+    ByteSpan s = span_of(b);
+    xet::CdcParams p;
+    p.target = target;
+    p.min_size = target / 8;
+    p.max_size = target * 2;
+    std::vector<uint64_t> e;
+    {
+      py::gil_scoped_release nogil;
+      e = xet::chunk_ends(s.data, s.size, p);
+    }
+    return e;
+  }, py::arg("data"), py::arg("target") = 65536);
+  m.def("gear_window_hash", [](py::buffer b, size_t i) { return xet::gear_window_hash(span_of(b).data, i); });
+  // Whole-buffer Xet file hash (CDC + chunk hashes + Merkle + salt) — `zest` equivalent of
+  // hf_xet.hash_files for in-memory data.
+  m.def("xet_file_hash", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    xet::Hash h;
+    {
+      py::gil_scoped_release nogil;
+      auto ends = xet::chunk_ends(s.data, s.size);
+      std::vector<xet::HashSize> leaves;
+      leaves.reserve(ends.size());
+      uint64_t prev = 0;
+      for (uint64_t e : ends) {
+        leaves.push_back({xet::chunk_hash(s.data + prev, e - prev), e - prev});
+        prev = e;
+      }
+      h = xet::file_hash(leaves);
+    }
+    return to_bytes(h);
+  });
+
+  // ---------------- LZ4 / BG4 ----------------
+  m.def("xxh32", [](py::buffer b, uint32_t seed) {
+    ByteSpan s = span_of(b);
+    return lz4::xxh32(s.data, s.size, seed);
+  }, py::arg("data"), py::arg("seed") = 0);
+  m.def("lz4_compress_frame", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    Bytes out;
+    {
+      py::gil_scoped_release nogil;
+      out = lz4::compress_frame(s.data, s.size);
+    }
+    return to_bytes(out);
+  });
+  m.def("lz4_decompress_frame", [](py::buffer b, size_t expected) {
+    ByteSpan s = span_of(b);
+    Bytes out;
+    {
+      py::gil_scoped_release nogil;
+      out = lz4::decompress_frame(s.data, s.size, expected);
+    }
+    return to_bytes(out);
+  }, py::arg("data"), py::arg("expected") = 0);
+  m.def("lz4_compress_block", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    Bytes out(lz4::block_bound(s.size));
+    size_t n = lz4::compress_block(s.data, s.size, out.data(), out.size());
+    return to_bytes(out.data(), n);
+  });
+  m.def("lz4_decompress_block", [](py::buffer b, size_t cap) {
+    ByteSpan s = span_of(b);
+    Bytes out(cap);
+    size_t n = lz4::decompress_block(s.data, s.size, out.data(), 0, cap);
+    return to_bytes(out.data(), n);
+  });
+  m.def("bg4_split", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    Bytes out(s.size);
+    bg4::split(s.data, s.size, out.data());
+    return to_bytes(out);
+  });
+  m.def("bg4_join", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    Bytes out(s.size);
+    bg4::join(s.data, s.size, out.data());
+    return to_bytes(out);
+  });
+  m.def("compress_chunk", [](py::buffer b, const std::string& policy) {
+    ByteSpan s = span_of(b);
+    xet::CompressionPolicy p = policy == "none" ? xet::CompressionPolicy::None
+                               : policy == "lz4" ? xet::CompressionPolicy::LZ4
+                               : policy == "bg4" ? xet::CompressionPolicy::BG4
+                                                 : xet::CompressionPolicy::Auto;
+    Bytes out;
+    xet::Scheme sc;
+    {
+      py::gil_scoped_release nogil;
+      sc = xet::compress_chunk(s.data, s.size, p, out);
+    }
+    return py::make_tuple(int(sc), to_bytes(out));
+  }, py::arg("data"), py::arg("policy") = "auto");
+  m.def("decompress_chunk", [](int scheme, py::buffer b, size_t ulen) {
+    ByteSpan s = span_of(b);
+    Bytes out(ulen);
+    xet::decompress_chunk(xet::Scheme(scheme), s.data, s.size, out.data(), ulen);
+    return to_bytes(out);
+  });
+
+  // ---------------- Xorb ----------------
+  m.def("index_chunks", [](py::buffer b) {
+    ByteSpan s = span_of(b);
+    auto idx = xet::index_chunks(s.data, s.size);
+    py::list out;
+    for (auto& e : idx)
+      out.append(py::make_tuple(e.header_off, e.clen, int(e.scheme), e.ulen, e.unpacked_off));
+    return out;
+  });
+  m.def("parse_footer", [](py::buffer b) -> py::object {
+    ByteSpan s = span_of(b);
+    size_t st = 0;
+    auto f = xet::parse_footer(s.data, s.size, &st);
+    if (!f) return py::none();
+    py::dict d;
+    d["xorb_hash"] = to_bytes(f->xorb_hash);
+    py::list hs;
+    for (auto& h : f->chunk_hashes) hs.append(to_bytes(h));
+    d["chunk_hashes"] = hs;
+    d["chunk_boundaries"] = f->chunk_boundaries;
+    d["unpacked_offsets"] = f->unpacked_offsets;
+    d["footer_start"] = st;
+    return d;
+  });
+  m.def("extract_chunk_range", [](py::buffer b, uint32_t start, uint32_t end, bool with_hashes) {
+    ByteSpan s = span_of(b);
+    Bytes out;
+    std::vector<xet::HashSize> hs;
+    {
+      py::gil_scoped_release nogil;
+      xet::extract_chunk_range(s.data, s.size, start, end, out, with_hashes ? &hs : nullptr);
+    }
+    if (!with_hashes) return py::object(to_bytes(out));
+    py::list l;
+    for (auto& h : hs) l.append(py::make_tuple(to_bytes(h.hash), h.size));
+    return py::object(py::make_tuple(to_bytes(out), l));
+  }, py::arg("data"), py::arg("start"), py::arg("end"), py::arg("with_hashes") = false);
+  m.def("verify_xorb", [](py::buffer b, py::object expected) {
+    ByteSpan s = span_of(b);
+    if (expected.is_none()) {
+      py::gil_scoped_release nogil;
+      xet::verify_xorb(s.data, s.size, nullptr);
+    } else {
+      xet::Hash h = hash_of(expected.cast<py::bytes>());
+      py::gil_scoped_release nogil;
+      xet::verify_xorb(s.data, s.size, &h);
+    }
+  }, py::arg("data"), py::arg("expected") = py::none());
+
+  py::class_<xet::XorbBuilder>(m, "XorbBuilder")
+      .def(py::init([](const std::string& policy) {
+             xet::CompressionPolicy p = policy == "none" ? xet::CompressionPolicy::None
+                                        : policy == "lz4" ? xet::CompressionPolicy::LZ4
+                                        : policy == "bg4" ? xet::CompressionPolicy::BG4
+                                                          : xet::CompressionPolicy::Auto;
+             return new xet::XorbBuilder(p);
+           }),
+           py::arg("policy") = "auto")
+      .def("fits", &xet::XorbBuilder::fits)
+      .def("add_chunk", [](xet::XorbBuilder& self, py::buffer b) {
+        ByteSpan s = span_of(b);
+        py::gil_scoped_release nogil;
+        return self.add_chunk(s.data, s.size);
+      })
+      .def("num_chunks", &xet::XorbBuilder::num_chunks)
+      .def("serialized_size", &xet::XorbBuilder::serialized_size)
+      .def("unpacked_size", &xet::XorbBuilder::unpacked_size)
+      .def("hash", [](const xet::XorbBuilder& self) { return to_bytes(self.hash()); })
+      .def("chunk_hashes", [](const xet::XorbBuilder& self) {
+        py::list l;
+        for (auto& h : self.chunk_hashes()) l.append(to_bytes(h));
+        return l;
+      })
+      .def("chunk_ulens", &xet::XorbBuilder::chunk_ulens)
+      .def("chunk_boundaries", &xet::XorbBuilder::chunk_boundaries)
+      .def("serialize", [](const xet::XorbBuilder& self, bool footer) { return to_bytes(self.serialize(footer)); },
+           py::arg("with_footer") = true)
+      .def("clear", &xet::XorbBuilder::clear);
+
+  bind_extra(m);
+}

@@ -1,0 +1,34 @@
+"""Shared pytest configuration.
+
+Markers:
+  gpu   — needs a real MI355X (HIP device); the CPU CI runs `-m "not gpu"`.
+  slow  — multi-second tests (still CPU).
+"""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an AMD MI355X GPU (HIP)")
+    config.addinivalue_line("markers", "slow: slow CPU test")
+
+
+def _ensure_built():
+    # Build native extensions in-tree once per session if missing (cheap no-op when up to date).
+    from tools.build import build
+
+    build(only=None)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def native_build():
+    if os.environ.get("ZEST_SKIP_BUILD") != "1":
+        _ensure_built()
+    yield
