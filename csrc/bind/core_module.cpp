@@ -1,5 +1,6 @@
 // pybind11 bindings for the zest host core (`zest_amd._core`).
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <cstring>
@@ -126,6 +127,35 @@ PYBIND11_MODULE(_core, m) {
     }
     return e;
   }, py::arg("data"), py::arg("target") = 65536);
+  m.def("select_boundaries", [](py::buffer cand, uint64_t n, size_t mn, size_t mx) {
+    py::buffer_info bi = cand.request();
+    if (bi.itemsize != 8) throw Error("InvalidArgument", "candidates must be uint64");
+    return xet::select_boundaries(static_cast<const uint64_t*>(bi.ptr), size_t(bi.size), n, mn, mx);
+  });
+  // Greedy xorb packing (xorb <= max_bytes serialized, <= max_chunks chunks), as an uploader
+  // does: returns the xorb index of every chunk given its serialized size (header + payload).
+  m.def("plan_xorbs", [](py::buffer ser_sizes, uint64_t max_bytes, uint32_t max_chunks) {
+    py::buffer_info bi = ser_sizes.request();
+    if (bi.itemsize != 8) throw Error("InvalidArgument", "sizes must be uint64");
+    const uint64_t* s = static_cast<const uint64_t*>(bi.ptr);
+    const size_t n = size_t(bi.size);
+    py::array_t<int64_t> out(n);
+    auto o = out.mutable_unchecked<1>();
+    int64_t x = 0;
+    uint64_t bytes = 0;
+    uint32_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (cnt > 0 && (bytes + s[i] > max_bytes || cnt + 1 > max_chunks)) {
+        ++x;
+        bytes = 0;
+        cnt = 0;
+      }
+      o(i) = x;
+      bytes += s[i];
+      ++cnt;
+    }
+    return out;
+  });
   m.def("gear_window_hash", [](py::buffer b, size_t i) { return xet::gear_window_hash(span_of(b).data, i); });
   // Whole-buffer Xet file hash (CDC + chunk hashes + Merkle + salt) — `zest` equivalent of
   // hf_xet.hash_files for in-memory data.

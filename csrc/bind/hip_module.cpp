@@ -1,0 +1,104 @@
+// pybind11 bindings for the HIP/CDNA4 kernel library (`zest_amd._hip`).  All entry points take
+// raw device pointers (ints) and a hipStream_t (int, e.g. torch.cuda.current_stream().cuda_stream);
+// shape/bounds validation happens in zest_amd/ops before launch.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstddef>
+#include <stdexcept>
+#include <string>
+
+#include "../gpu/zgpu.h"
+
+namespace py = pybind11;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "zest HIP kernels for AMD Instinct MI355X (gfx950)";
+  m.attr("TERM_BYTES") = sizeof(ZgTerm);
+  m.attr("CHUNK_BYTES") = sizeof(ZgChunk);
+  m.attr("MERKLE_JOB_BYTES") = sizeof(ZgMerkleJob);
+  m.attr("ARCH") = "gfx950";
+
+  m.def("device_count", &zg_device_count);
+  // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host
+  // allocator) and raw async copies on a caller-provided stream.
+  m.def("host_malloc", [](size_t n) {
+    void* p = nullptr;
+    {
+      py::gil_scoped_release nogil;
+      check(hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault), "hipHostMalloc");
+    }
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("host_free", [](uintptr_t p) {
+    py::gil_scoped_release nogil;
+    check(hipHostFree(reinterpret_cast<void*>(p)), "hipHostFree");
+  });
+  m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
+    check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault, S(st)),
+          "hipMemcpyAsync");
+  });
+  m.def("index_terms", [](uintptr_t src, uintptr_t terms, int n, uintptr_t chunks, uintptr_t err, uintptr_t st) {
+    check(zg_index_terms(P<const uint8_t>(src), P<const ZgTerm>(terms), n, P<ZgChunk>(chunks),
+                         P<unsigned long long>(err), S(st)),
+          "zg_index_terms");
+  });
+  m.def("place_chunks", [](uintptr_t src, uint64_t src_n, uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n,
+                           uint64_t lo, uint64_t hi, uintptr_t err, uintptr_t st) {
+    check(zg_place_chunks(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, lo, hi,
+                          P<unsigned long long>(err), S(st)),
+          "zg_place_chunks");
+  });
+  m.def("hash_chunks", [](uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n, uintptr_t hashes, uintptr_t sizes,
+                          uint32_t base, uintptr_t st) {
+    check(zg_hash_chunks(P<const uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, P<uint8_t>(hashes),
+                         P<uint64_t>(sizes), base, S(st)),
+          "zg_hash_chunks");
+  });
+  m.def("hash_ranges", [](uintptr_t buf, uintptr_t offs, uintptr_t lens, int n, uintptr_t out, int key_mode,
+                          uintptr_t st) {
+    check(zg_hash_ranges(P<const uint8_t>(buf), P<const uint64_t>(offs), P<const uint32_t>(lens), n,
+                         P<uint8_t>(out), key_mode, S(st)),
+          "zg_hash_ranges");
+  });
+  m.def("merkle_scratch_bytes", &zg_merkle_scratch_bytes);
+  m.def("merkle", [](uintptr_t hashes, uintptr_t sizes, uintptr_t jobs, int n_jobs, uintptr_t roots,
+                     uintptr_t scratch, uint64_t scratch_bytes, uintptr_t st) {
+    check(zg_merkle(P<const uint8_t>(hashes), P<const uint64_t>(sizes), P<const ZgMerkleJob>(jobs), n_jobs,
+                    P<uint8_t>(roots), P<uint8_t>(scratch), scratch_bytes, S(st)),
+          "zg_merkle");
+  });
+  m.def("compare_hashes", [](uintptr_t got, uintptr_t want, int n, uintptr_t err, uintptr_t st) {
+    check(zg_compare_hashes(P<const uint8_t>(got), P<const uint8_t>(want), n, P<unsigned long long>(err), S(st)),
+          "zg_compare_hashes");
+  });
+  m.def("cdc_candidates", [](uintptr_t data, uint64_t n, uint64_t mask, uintptr_t out, uintptr_t count, uint64_t cap,
+                             uintptr_t st) {
+    check(zg_cdc_candidates(P<const uint8_t>(data), n, mask, P<uint64_t>(out), P<unsigned long long>(count), cap,
+                            S(st)),
+          "zg_cdc_candidates");
+  });
+  m.def("fill_synthetic", [](uintptr_t dst, uint64_t n, uint64_t seed, uint64_t off, int mode, uintptr_t st) {
+    check(zg_fill_synthetic(P<uint8_t>(dst), n, seed, off, mode, S(st)), "zg_fill_synthetic");
+  });
+  m.def("pack_chunks", [](uintptr_t data, uintptr_t data_off, uintptr_t lens, uintptr_t out_off, int n, uintptr_t out,
+                          uintptr_t st) {
+    check(zg_pack_chunks(P<const uint8_t>(data), P<const uint64_t>(data_off), P<const uint32_t>(lens),
+                         P<const uint64_t>(out_off), n, P<uint8_t>(out), S(st)),
+          "zg_pack_chunks");
+  });
+}

@@ -91,3 +91,28 @@ uint64_t gear_window_hash(const uint8_t* data, size_t i) {
 }
 
 }  // namespace zest::xet
+
+namespace zest::xet {
+
+std::vector<uint64_t> select_boundaries(const uint64_t* cand, size_t n_cand, uint64_t n, size_t min_size,
+                                        size_t max_size) {
+  std::vector<uint64_t> ends;
+  ends.reserve(n / (min_size + max_size) * 2 + 4);
+  uint64_t s = 0;
+  size_t k = 0;
+  while (s < n) {
+    while (k < n_cand && cand[k] < s + min_size) ++k;
+    uint64_t e;
+    if (k < n_cand && cand[k] - s <= max_size) {
+      e = cand[k];
+    } else {
+      e = s + max_size;
+    }
+    if (e >= n) e = n;
+    ends.push_back(e);
+    s = e;
+  }
+  return ends;
+}
+
+}  // namespace zest::xet

@@ -43,3 +43,11 @@ std::vector<uint64_t> chunk_ends(const uint8_t* data, size_t n, CdcParams p = {}
 uint64_t gear_window_hash(const uint8_t* data, size_t i);
 
 }  // namespace zest::xet
+
+namespace zest::xet {
+// Apply the min/max chunk-size rule to sorted candidate END offsets (positions i+1 whose
+// full-window gear hash matched) over a stream of n bytes -> chunk END offsets.  Used with the
+// GPU candidate kernel (csrc/gpu/synth.hip); equivalent to Chunker over the same bytes.
+std::vector<uint64_t> select_boundaries(const uint64_t* cand, size_t n_cand, uint64_t n, size_t min_size,
+                                        size_t max_size);
+}  // namespace zest::xet

@@ -1,0 +1,190 @@
+// K5 GearHash CDC candidates, K7 xorb packing, and synthetic-content generators (gfx950).
+//
+// CDC: the Xet gear hash only depends on the last 64 bytes (h = (h << 1) + G[b]), so every
+// position's hash is recomputable from a 63-byte warm-up: each lane scans its own 256-byte
+// segment independently and appends the END offsets (i + 1) whose hash has (h & mask) == 0.
+// Chunk selection (min 8 KiB / max 128 KiB rule) runs on the host over the sparse candidates.
+#include <hip/hip_runtime.h>
+
+#include "../core/gear_table.h"
+#include "zgpu.h"
+
+namespace {
+
+__constant__ uint64_t kGearDev[256] = ZEST_GEAR_TABLE_INIT;
+
+constexpr uint32_t kSeg = 256;
+
+struct ByteReader {
+  const uint8_t* base;
+  uint64_t cached_addr = ~0ull;
+  uint32_t w = 0;
+  __device__ __forceinline__ uint32_t get(uint64_t i) {
+    const uint64_t a = reinterpret_cast<uintptr_t>(base) + i;
+    const uint64_t aw = a & ~3ull;
+    if (aw != cached_addr) {
+      w = *reinterpret_cast<const uint32_t*>(aw);
+      cached_addr = aw;
+    }
+    return (w >> (8 * (a & 3))) & 0xFF;
+  }
+};
+
+__global__ void __launch_bounds__(256) k_cdc_candidates(const uint8_t* __restrict__ data, uint64_t n, uint64_t mask,
+                                                        uint64_t* __restrict__ out, unsigned long long* count,
+                                                        uint64_t cap) {
+  __shared__ uint64_t gear[256];
+  gear[threadIdx.x] = kGearDev[threadIdx.x];
+  __syncthreads();
+  const uint64_t seg = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t start = seg * kSeg;
+  if (start >= n) return;
+  const uint64_t end = start + kSeg < n ? start + kSeg : n;
+  ByteReader rd{data};
+  uint64_t h = 0;
+  const uint64_t warm = start >= 63 ? start - 63 : 0;
+  for (uint64_t i = warm; i < start; ++i) h = (h << 1) + gear[rd.get(i)];
+  for (uint64_t i = start; i < end; ++i) {
+    h = (h << 1) + gear[rd.get(i)];
+    if ((h & mask) == 0) {
+      const unsigned long long k = atomicAdd(count, 1ull);
+      if (k < cap) out[k] = i + 1;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Byte `pos` of the synthetic stream.
+__device__ __forceinline__ uint32_t synth_byte(uint64_t seed, uint64_t pos, int mode) {
+  if (mode == 0) {
+    const uint64_t w = splitmix64(seed ^ ((pos >> 3) * 0xD1B54A32D192ED03ull));
+    return uint32_t(w >> (8 * (pos & 7))) & 0xFF;
+  }
+  // bf16 ~ N(0, 0.02) element e = pos >> 1 (Box-Muller on one hashed uniform pair)
+  const uint64_t e = pos >> 1;
+  const uint64_t h = splitmix64(seed ^ (e * 0xA24BAED4963EE407ull));
+  const float u1 = (float((h >> 40) & 0xFFFFFF) + 0.5f) * (1.0f / 16777216.0f);
+  const float u2 = float((h >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
+  const float z = sqrtf(-2.0f * __logf(u1)) * __cosf(6.28318530718f * u2) * 0.02f;
+  const uint32_t bits = __float_as_uint(z);
+  const uint32_t bf = (bits + 0x7FFFu + ((bits >> 16) & 1u)) >> 16;  // RNE (no NaNs possible here)
+  return (pos & 1) ? (bf >> 8) & 0xFF : bf & 0xFF;
+}
+
+__global__ void __launch_bounds__(256) k_fill(uint8_t* __restrict__ dst, uint64_t n, uint64_t seed, uint64_t stream_off,
+                                              int mode) {
+  // Each thread produces 16 destination-aligned bytes.
+  const uint64_t da = reinterpret_cast<uintptr_t>(dst);
+  const uint64_t lead = (16 - (da & 15)) & 15;  // bytes before the first aligned vector
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    for (uint64_t i = 0; i < lead && i < n; ++i) dst[i] = uint8_t(synth_byte(seed, stream_off + i, mode));
+  }
+  if (n <= lead) return;
+  const uint64_t body = n - lead;
+  const uint64_t nvec = body >> 4;
+  for (uint64_t v = t; v < nvec; v += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t pos = stream_off + lead + 16 * v;
+    uint32_t w[4];
+    if (mode == 0 && (pos & 7) == 0) {
+      const uint64_t a = splitmix64(seed ^ ((pos >> 3) * 0xD1B54A32D192ED03ull));
+      const uint64_t b = splitmix64(seed ^ (((pos >> 3) + 1) * 0xD1B54A32D192ED03ull));
+      w[0] = uint32_t(a);
+      w[1] = uint32_t(a >> 32);
+      w[2] = uint32_t(b);
+      w[3] = uint32_t(b >> 32);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        w[k] = synth_byte(seed, pos + 4 * k, mode) | (synth_byte(seed, pos + 4 * k + 1, mode) << 8) |
+               (synth_byte(seed, pos + 4 * k + 2, mode) << 16) | (synth_byte(seed, pos + 4 * k + 3, mode) << 24);
+      }
+    }
+    reinterpret_cast<uint4*>(dst + lead)[v] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  if (t == 0) {
+    for (uint64_t i = lead + 16 * nvec; i < n; ++i) dst[i] = uint8_t(synth_byte(seed, stream_off + i, mode));
+  }
+}
+
+// Pack: one wave per chunk writes [header | payload] (scheme 0) at out + out_off[i].
+__global__ void __launch_bounds__(256) k_pack(const uint8_t* __restrict__ data, const uint64_t* __restrict__ data_off,
+                                              const uint32_t* __restrict__ lens, const uint64_t* __restrict__ out_off,
+                                              int n, uint8_t* __restrict__ out) {
+  const int c = __builtin_amdgcn_readfirstlane(int(blockIdx.x * 4 + (threadIdx.x >> 6)));
+  if (c >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t len = lens[c];
+  uint8_t* o = out + out_off[c];
+  if (lane < 8) {
+    uint32_t b;
+    switch (lane) {
+      case 0: b = 0; break;                       // version
+      case 1: b = len & 0xFF; break;              // compressed len (LE u24)
+      case 2: b = (len >> 8) & 0xFF; break;
+      case 3: b = (len >> 16) & 0xFF; break;
+      case 4: b = 0; break;                       // scheme: none
+      case 5: b = len & 0xFF; break;              // uncompressed len
+      case 6: b = (len >> 8) & 0xFF; break;
+      default: b = (len >> 16) & 0xFF; break;
+    }
+    o[lane] = uint8_t(b);
+  }
+  // payload copy (dst arbitrary alignment): simple strided 4-byte funnel copy
+  const uint8_t* s = data + data_off[c];
+  uint8_t* d = o + 8;
+  const uintptr_t dAddr = reinterpret_cast<uintptr_t>(d);
+  uint32_t head = uint32_t((4 - (dAddr & 3)) & 3);
+  if (head > len) head = len;
+  if (lane < head) d[lane] = s[lane];
+  const uint32_t nw = (len - head) >> 2;
+  const uint8_t* s2 = s + head;
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(s2);
+  const uint32_t k = uint32_t(sa & 3);
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+  uint32_t* dw = reinterpret_cast<uint32_t*>(d + head);
+  for (uint32_t w = lane; w < nw; w += 64) {
+    const uint32_t a = sw[w];
+    dw[w] = k ? __builtin_amdgcn_alignbyte(sw[w + 1], a, k) : a;
+  }
+  const uint32_t done = head + 4 * nw;
+  if (lane < len - done) d[done + lane] = s[done + lane];
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t zg_cdc_candidates(const uint8_t* data, uint64_t n, uint64_t mask, uint64_t* out,
+                             unsigned long long* count, uint64_t capacity, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t segs = (n + kSeg - 1) / kSeg;
+  hipLaunchKernelGGL(k_cdc_candidates, dim3(uint32_t((segs + 255) / 256)), dim3(256), 0, stream, data, n, mask, out,
+                     count, capacity);
+  return hipGetLastError();
+}
+
+hipError_t zg_fill_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t stream_offset, int mode,
+                             hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t vecs = n / 16 + 1;
+  uint64_t blocks = (vecs + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(k_fill, dim3(uint32_t(blocks)), dim3(256), 0, stream, dst, n, seed, stream_offset, mode);
+  return hipGetLastError();
+}
+
+hipError_t zg_pack_chunks(const uint8_t* data, const uint64_t* data_off, const uint32_t* lens, const uint64_t* out_off,
+                          int n, uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack, dim3((n + 3) / 4), dim3(256), 0, stream, data, data_off, lens, out_off, n, out);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// Device-side descriptors and the C ABI of the zest HIP/CDNA4 kernel library (gfx950).
+//
+// Pipeline for one batch of fetched xorb ranges ("terms"):
+//   zg_index_terms   one thread per term walks the 8-byte chunk headers -> ChunkDesc[]   (K4)
+//   zg_place_chunks  one wave per chunk: scheme 0 -> aligned copy, LZ4/BG4 -> LDS decode (K3)
+//   zg_hash_chunks   one wave per chunk: keyed BLAKE3 of the placed bytes -> chunk hashes (K1)
+//   zg_merkle_files  one workgroup per file: Xet Merkle tree -> root -> file hash compare (K2)
+// plus zg_cdc_candidates (K5), zg_pack_xorbs (K7) and synthetic data generators.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// A fetched byte run holding whole chunks [chunk 0 .. n_chunks) of one xorb range.
+typedef struct ZgTerm {
+  uint64_t src;         // byte offset of the first chunk header in the src (staging) buffer
+  uint64_t src_len;     // bytes in the run
+  uint64_t dst;         // byte offset of the first chunk's output in the dst (arena) buffer
+  uint32_t chunk_base;  // index of the first chunk in the ChunkDesc / hash arrays
+  uint32_t n_chunks;    // chunks the run must contain
+  uint64_t ulen;        // expected total uncompressed bytes (0 = don't check)
+} ZgTerm;
+
+typedef struct ZgChunk {
+  uint64_t src;     // payload offset in src buffer (after the 8-byte header)
+  uint64_t dst;     // output offset in dst buffer
+  uint32_t clen;    // compressed payload length
+  uint32_t ulen;    // uncompressed length
+  uint32_t scheme;  // 0 none, 1 LZ4 frame, 2 BG4+LZ4 frame
+  uint32_t term;    // owning term (for error reports)
+} ZgChunk;
+
+// One Merkle job: n leaves (hash[32] + size) -> root; optional expected file hash compare.
+typedef struct ZgMerkleJob {
+  uint64_t leaf_base;  // index of the first leaf in the hash/size arrays
+  uint64_t n_leaves;
+  uint32_t want_file_hash;  // 1: result = file hash (keyed zero-salt of root); 0: raw root
+  uint32_t pad;
+} ZgMerkleJob;
+
+// Error word layout written by kernels (first error wins via atomicCAS):
+//   code << 32 | index.  Codes:
+enum {
+  ZG_OK = 0,
+  ZG_ERR_HEADER = 1,       // bad chunk header (version/scheme)
+  ZG_ERR_RANGE = 2,        // chunk extends past its run
+  ZG_ERR_COUNT = 3,        // run has a different chunk count / size than planned
+  ZG_ERR_LZ4 = 4,          // malformed LZ4 frame / block
+  ZG_ERR_SIZE = 5,         // decoded size != header ulen
+  ZG_ERR_HASH = 6,         // hash mismatch
+  ZG_ERR_CAPACITY = 7,     // chunk larger than kernel capacity
+};
+
+// All launchers return hipError_t of the launch and never synchronize.
+hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
+                          unsigned long long* err, hipStream_t stream);
+// Descriptors are bounds-checked in-kernel against src_n / dst_n (bytes).
+hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                           const ZgChunk* chunks, int n_chunks, uint64_t clip_lo, uint64_t clip_hi,
+                           unsigned long long* err, hipStream_t stream);
+hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
+                          uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, hipStream_t stream);
+// Hash raw (offset, len) messages with the Xet data key: out[i] = keyed(DATA_KEY, buf[off:off+len]).
+hipError_t zg_hash_ranges(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,
+                          uint8_t* hashes, int key_mode, hipStream_t stream);
+hipError_t zg_merkle(const uint8_t* leaf_hashes, const uint64_t* leaf_sizes, const ZgMerkleJob* jobs,
+                     int n_jobs, uint8_t* roots, uint8_t* scratch, uint64_t scratch_bytes,
+                     hipStream_t stream);
+size_t zg_merkle_scratch_bytes(uint64_t max_leaves_per_job, int n_jobs);
+hipError_t zg_compare_hashes(const uint8_t* got, const uint8_t* want, int n, unsigned long long* err,
+                             hipStream_t stream);
+// CDC: candidate END offsets (i+1) where the full-window gear hash has (h & mask) == 0.
+hipError_t zg_cdc_candidates(const uint8_t* data, uint64_t n, uint64_t mask, uint64_t* out,
+                             unsigned long long* count, uint64_t capacity, hipStream_t stream);
+// Synthetic content.  mode 0: uniform random bytes; mode 1: bf16 ~ N(0, 0.02).
+hipError_t zg_fill_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t stream_offset, int mode,
+                             hipStream_t stream);
+// Pack uncompressed chunks into serialized xorb bodies: header (version 0, scheme 0) + payload.
+hipError_t zg_pack_chunks(const uint8_t* data, const uint64_t* data_off, const uint32_t* lens,
+                          const uint64_t* out_off, int n, uint8_t* out, hipStream_t stream);
+
+int zg_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif

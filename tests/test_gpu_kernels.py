@@ -1,0 +1,236 @@
+"""Numerics of the HIP/CDNA4 kernels vs the C++ host oracle (bit-exact: hashes and bytes).
+
+Marked `gpu`: runs on a real MI355X.  The same ops also have CPU paths (tested in
+test_ops_cpu.py) that the gloo multi-process tests use.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from zest_amd import _core as C
+from zest_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ops.hip()  # must load: no silent fallback
+
+
+def _bf16(n, seed=0):
+    w = np.random.default_rng(seed).standard_normal(n).astype(np.float32) * 0.02
+    return (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+
+
+def test_hash_ranges_matches_cpu_all_sizes_and_alignments():
+    rng = random.Random(1)
+    data = rng.randbytes(1 << 21)
+    buf = ops.padded_empty(len(data), DEV)
+    buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    sizes = [0, 1, 3, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 4097, 8192, 65535, 65536, 65537, 100_000,
+             131_071, 131_072]
+    offs, lens = [], []
+    for s in sizes:
+        for a in range(4):
+            offs.append(1000 + a + 7 * len(offs))
+            lens.append(s)
+    for _ in range(200):
+        lens.append(rng.randint(0, 131_072))
+        offs.append(rng.randint(0, len(data) - 131_072))
+    got = ops.hash_ranges(buf, offs, lens).cpu().numpy()
+    for i, (o, l) in enumerate(zip(offs, lens)):
+        assert got[i].tobytes() == C.chunk_hash(data[o:o + l]), (o, l)
+    # other key modes
+    got_plain = ops.hash_ranges(buf, offs[:40], lens[:40], ops.KEY_PLAIN).cpu().numpy()
+    got_node = ops.hash_ranges(buf, offs[:40], lens[:40], ops.KEY_NODE).cpu().numpy()
+    for i in range(40):
+        o, l = offs[i], lens[i]
+        assert got_plain[i].tobytes() == C.blake3(data[o:o + l])
+        assert got_node[i].tobytes() == C.internal_node_hash(data[o:o + l])
+
+
+def _make_runs(policy, seed=0):
+    rng = random.Random(seed)
+    parts = [rng.randbytes(700_000), _bf16(400_000, seed), b"zest xorb ingest test line. " * 20_000,
+             bytes(300_000)]
+    data = b"".join(parts)
+    ends = C.chunk_ends(data)
+    b = C.XorbBuilder(policy)
+    prev = 0
+    for e in ends:
+        b.add_chunk(data[prev:e])
+        prev = e
+    return data, ends, b
+
+
+@pytest.mark.parametrize("policy", ["none", "lz4", "bg4", "auto"])
+def test_ingest_matches_cpu(policy):
+    data, ends, b = _make_runs(policy)
+    body = b.serialize(False)
+    nck = len(ends)
+    # Split the run into 3 terms at chunk boundaries; place them at odd src/dst offsets.
+    bounds = b.chunk_boundaries()
+    cuts = [0, nck // 3, 2 * nck // 3, nck]
+    src_gap, dst_gap = 13, 7
+    src = ops.padded_empty(len(body) + 64, DEV)
+    terms = np.zeros(3, dtype=ops.TERM_DTYPE)
+    src_host = bytearray(len(body) + 64)
+    soff = src_gap
+    uoffs = [0] + list(ends)
+    for t in range(3):
+        c0, c1 = cuts[t], cuts[t + 1]
+        r0 = 0 if c0 == 0 else bounds[c0 - 1]
+        r1 = bounds[c1 - 1]
+        run = body[r0:r1]
+        src_host[soff:soff + len(run)] = run
+        terms[t] = (soff, len(run), dst_gap + uoffs[c0], c0, c1 - c0, uoffs[c1] - uoffs[c0])
+        soff += len(run) + 3
+    src = ops.padded_empty(len(src_host), DEV)
+    src.copy_(torch.frombuffer(src_host, dtype=torch.uint8))
+    dst = ops.padded_empty(len(data) + 2 * dst_gap, DEV)
+    dst.fill_(0xAB)
+    hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=DEV)
+    ops.ingest_terms(src, dst, terms, hashes)
+    torch.cuda.synchronize()
+    out = dst.cpu().numpy().tobytes()
+    assert out[dst_gap:dst_gap + len(data)] == data
+    assert out[:dst_gap] == b"\xab" * dst_gap and out[dst_gap + len(data):] == b"\xab" * dst_gap
+    want = b"".join(b.chunk_hashes())
+    assert hashes.cpu().numpy().tobytes() == want
+
+
+def test_ingest_clip_window():
+    data, ends, b = _make_runs("auto", seed=3)
+    body = b.serialize(False)
+    nck = len(ends)
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(bytearray(body), dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, nck, len(data))
+    dst = ops.padded_empty(len(data), DEV)
+    dst.zero_()
+    hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=DEV)
+    lo, hi = 123_457, 987_653
+    ops.ingest_terms(src, dst, terms, hashes, clip=(lo, hi))
+    out = dst.cpu().numpy().tobytes()
+    assert out[lo:hi] == data[lo:hi]
+    assert out[:lo] == bytes(lo) and out[hi:] == bytes(len(data) - hi)
+    # hashes are only meaningful for chunks entirely inside the clip window
+    got = hashes.cpu().numpy()
+    want = b.chunk_hashes()
+    starts = [0] + ends[:-1]
+    inside = [i for i, (a, e) in enumerate(zip(starts, ends)) if a >= lo and e <= hi]
+    assert inside and all(got[i].tobytes() == want[i] for i in inside)
+
+
+def test_ingest_detects_corruption():
+    data, ends, b = _make_runs("auto", seed=5)
+    body = bytearray(b.serialize(False))
+    body[0] = 7  # bad header version
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(body, dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, len(ends), len(data))
+    dst = ops.padded_empty(len(data), DEV)
+    hashes = torch.zeros((len(ends), 32), dtype=torch.uint8, device=DEV)
+    with pytest.raises(ops.IngestError):
+        ops.ingest_terms(src, dst, terms, hashes)
+
+
+def test_ingest_real_hf_xet_xorbs(tmp_path):
+    hf_xet = pytest.importorskip("hf_xet")
+    import glob
+    import time
+    files = []
+    for name, d in (("bf", _bf16(500_000, 9)), ("txt", b"hello xet world " * 30_000)):
+        f = tmp_path / name
+        f.write_bytes(d)
+        files.append(f)
+    hf_xet.upload_files([str(f) for f in files], "local://" + str(tmp_path / "cas"),
+                        ("t", int(time.time()) + 3600), None, None, "model")
+    for x in glob.glob(str(tmp_path / "cas/xet/xorbs/xorbs/default.*")):
+        blob = open(x, "rb").read()
+        foot = C.parse_footer(blob)
+        idx = C.index_chunks(blob)
+        run = blob[:foot["footer_start"]]
+        ulen = sum(e[3] for e in idx)
+        src = ops.padded_empty(len(run), DEV)
+        src.copy_(torch.frombuffer(bytearray(run), dtype=torch.uint8))
+        dst = ops.padded_empty(ulen, DEV)
+        terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+        terms[0] = (0, len(run), 0, 0, len(idx), ulen)
+        hashes = torch.zeros((len(idx), 32), dtype=torch.uint8, device=DEV)
+        ops.ingest_terms(src, dst, terms, hashes)
+        assert [bytes(h) for h in hashes.cpu().numpy()] == foot["chunk_hashes"]
+        want = C.extract_chunk_range(run, 0, len(idx))
+        assert dst.cpu().numpy().tobytes() == want
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 9, 10, 37, 1000, 20_000])
+def test_merkle_matches_cpu(n):
+    rng = np.random.default_rng(n)
+    hs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sz = rng.integers(1, 131_072, size=n).astype(np.int64)
+    leaves = [(hs[i].tobytes(), int(sz[i])) for i in range(n)]
+    h_d = torch.from_numpy(hs).to(DEV)
+    s_d = torch.from_numpy(sz).to(DEV)
+    # two jobs: whole list + a sub-range
+    jobs = [(0, n), (n // 3, n - n // 3)]
+    roots = ops.merkle_roots(h_d, s_d, jobs, file_hash=True).cpu().numpy()
+    assert roots[0].tobytes() == C.file_hash(leaves)
+    assert roots[1].tobytes() == C.file_hash(leaves[n // 3:])
+    raw = ops.merkle_roots(h_d, s_d, jobs[:1], file_hash=False).cpu().numpy()
+    assert raw[0].tobytes() == C.merkle_root(leaves)
+
+
+def test_cdc_candidates_match_cpu_chunker():
+    rng = random.Random(11)
+    data = rng.randbytes(3_000_000) + _bf16(500_000, 1) + bytes(200_000)
+    t = ops.padded_empty(len(data), DEV)
+    t.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    cand = ops.cdc_candidates(t)
+    ends = ops.select_chunks(cand, len(data))
+    assert list(map(int, ends)) == C.chunk_ends(data)
+
+
+def test_pack_chunks_matches_builder():
+    rng = random.Random(4)
+    data = rng.randbytes(900_000)
+    ends = C.chunk_ends(data)
+    b = C.XorbBuilder("none")
+    prev = 0
+    for e in ends:
+        b.add_chunk(data[prev:e])
+        prev = e
+    body = b.serialize(False)
+    starts = np.array([0] + ends[:-1], dtype=np.uint64)
+    lens = np.diff(np.array([0] + ends, dtype=np.uint64)).astype(np.uint32)
+    out_off = np.array([0] + b.chunk_boundaries()[:-1], dtype=np.uint64) + 5
+    d = ops.padded_empty(len(data) + 3, DEV)
+    d[3:].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    out = ops.padded_empty(len(body) + 5, DEV)
+    out.zero_()
+    ops.pack_chunks(d, starts + 3, lens, out_off, out)
+    assert out.cpu().numpy().tobytes()[5:] == body
+
+
+def test_fill_synthetic_deterministic():
+    a = ops.padded_empty(1 << 20, DEV)
+    b = ops.padded_empty((1 << 20) + 5, DEV)
+    ops.fill_synthetic(a, 42, 0, 0)
+    ops.fill_synthetic(b[5:], 42, 0, 0)  # different dst alignment, same stream
+    assert torch.equal(a, b[5:5 + (1 << 20)])
+    c = ops.padded_empty(1000, DEV)
+    ops.fill_synthetic(c, 42, 12345, 0)  # stream offset selects the same bytes
+    assert torch.equal(c, a[12345:13345])
+    f = ops.padded_empty(1 << 20, DEV)
+    ops.fill_synthetic(f, 7, 0, 1)
+    v = f.view(torch.bfloat16).float()
+    assert abs(v.std().item() - 0.02) < 0.002 and abs(v.mean().item()) < 0.002

@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks on one MI355X: throughput of every HIP kernel in zest_amd.ops.
+
+Prints one JSON line per kernel: {"kernel", "gbps", "ms", "bytes", ...}.  Uses HIP events around
+`--iters` back-to-back launches after a warm-up; data is random (not zero-filled).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from zest_amd import _core as C
+from zest_amd import ops
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    n = int(a.gib * (1 << 30))
+    sel = set(a.only.split(",")) if a.only else None
+
+    def want(k):
+        return sel is None or k in sel
+
+    H = ops.hip()
+    st = torch.cuda.current_stream().cuda_stream
+    arena = ops.padded_empty(n, dev)
+    ops.fill_synthetic(arena, 1, 0, 0)
+    torch.cuda.synchronize()
+
+    if want("fill"):
+        ms = timed(lambda: ops.fill_synthetic(arena, 1, 0, 0), a.iters)
+        emit(kernel="fill_synthetic_random", bytes=n, ms=ms, gbps=n / ms / 1e6)
+
+    # fixed 64 KiB chunks over the arena
+    csize = 65536
+    nck = n // csize
+    offs = np.arange(nck, dtype=np.uint64) * csize
+    lens = np.full(nck, csize, dtype=np.uint32)
+    offs_d = torch.from_numpy(offs.view(np.int64)).to(dev)
+    lens_d = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty((nck, 32), dtype=torch.uint8, device=dev)
+    if want("hash"):
+        ms = timed(lambda: H.hash_ranges(arena.data_ptr(), offs_d.data_ptr(), lens_d.data_ptr(), nck,
+                                         out.data_ptr(), 0, st), a.iters)
+        emit(kernel="blake3_xet_chunks_64k", bytes=n, ms=ms, gbps=n / ms / 1e6, chunks=nck)
+        # correctness spot check
+        h = out[:4].cpu().numpy()
+        host = arena[:4 * csize].cpu().numpy().tobytes()
+        assert all(h[i].tobytes() == C.chunk_hash(host[i * csize:(i + 1) * csize]) for i in range(4))
+
+    if want("cdc"):
+        cap = n // 4096
+        cand = torch.empty(cap, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def run_cdc():
+            cnt.zero_()
+            H.cdc_candidates(arena.data_ptr(), n, ops.XET_MASK, cand.data_ptr(), cnt.data_ptr(), cap, st)
+        ms = timed(run_cdc, a.iters)
+        emit(kernel="cdc_candidates", bytes=n, ms=ms, gbps=n / ms / 1e6, candidates=int(cnt.item()))
+
+    # serialized xorb body of uncompressed chunks for place/index
+    if want("place") or want("ingest"):
+        body_n = nck * (csize + 8)
+        body = ops.padded_empty(body_n, dev)
+        data_off = offs
+        out_off = np.arange(nck, dtype=np.uint64) * (csize + 8)
+        ops.pack_chunks(arena, data_off, lens, out_off, body)
+        dst = ops.padded_empty(n, dev)
+        per_term = 1024  # 64 MiB terms
+        nterm = (nck + per_term - 1) // per_term
+        terms = np.zeros(nterm, dtype=ops.TERM_DTYPE)
+        for t in range(nterm):
+            c0, c1 = t * per_term, min(nck, (t + 1) * per_term)
+            terms[t] = (c0 * (csize + 8), (c1 - c0) * (csize + 8), c0 * csize, c0, c1 - c0, (c1 - c0) * csize)
+        ws = ops.IngestWorkspace(dev, nterm, nck)
+        hashes = torch.empty((nck, 32), dtype=torch.uint8, device=dev)
+        ms = timed(lambda: ops.ingest_terms(body, dst, terms, hashes, ws=ws, check=False), a.iters)
+        emit(kernel="ingest_none(index+place+hash)", bytes=n, ms=ms, gbps=n / ms / 1e6)
+        ops.raise_on_error(ws.err)
+        assert torch.equal(dst[:1 << 20], arena[:1 << 20])
+        tdev = ws.terms
+        ms = timed(lambda: H.index_terms(body.data_ptr(), tdev.data_ptr(), nterm, ws.chunks.data_ptr(),
+                                         ws.err.data_ptr(), st), a.iters)
+        emit(kernel="index_terms", bytes=body_n, ms=ms, gbps=body_n / ms / 1e6, terms=nterm)
+        ms = timed(lambda: H.place_chunks(body.data_ptr(), body_n, dst.data_ptr(), n, ws.chunks.data_ptr(), nck, 0,
+                                          n, ws.err.data_ptr(), st), a.iters)
+        emit(kernel="place_raw(+lz4 scan)", bytes=n, ms=ms, gbps=n / ms / 1e6)
+        ms = timed(lambda: H.hash_chunks(dst.data_ptr(), n, ws.chunks.data_ptr(), nck, hashes.data_ptr(), 0, 0, st),
+                   a.iters)
+        emit(kernel="hash_chunks", bytes=n, ms=ms, gbps=n / ms / 1e6)
+        del body, dst
+
+    if want("lz4"):
+        # bf16-like data, compressed on the host (LZ4 / BG4 frames), decoded on the GPU
+        m = min(n, 256 << 20)
+        w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
+        raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+        ends = C.chunk_ends(raw)
+        for policy in ("lz4", "bg4"):
+            b = C.XorbBuilder(policy)
+            prev = 0
+            terms_l = []
+            bodies = []
+            src_off = 0
+            cbase = 0
+            for e in ends:
+                if not b.fits(e - prev):
+                    body_b = b.serialize(False)
+                    bodies.append(body_b)
+                    terms_l.append((src_off, len(body_b), 0, cbase, b.num_chunks(), b.unpacked_size()))
+                    src_off += len(body_b)
+                    cbase += b.num_chunks()
+                    b.clear()
+                b.add_chunk(raw[prev:e])
+                prev = e
+            body_b = b.serialize(False)
+            bodies.append(body_b)
+            terms_l.append((src_off, len(body_b), 0, cbase, b.num_chunks(), b.unpacked_size()))
+            blob = b"".join(bodies)
+            terms = np.zeros(len(terms_l), dtype=ops.TERM_DTYPE)
+            uo = 0
+            for i, t in enumerate(terms_l):
+                terms[i] = (t[0], t[1], uo, t[3], t[4], t[5])
+                uo += t[5]
+            src = ops.padded_empty(len(blob), dev)
+            src.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+            dst = ops.padded_empty(m, dev)
+            nck2 = int(terms["n_chunks"].sum())
+            hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
+            ws = ops.IngestWorkspace(dev, len(terms), nck2)
+            ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), a.iters)
+            ops.raise_on_error(ws.err)
+            assert dst.cpu().numpy().tobytes() == raw[:m]
+            emit(kernel=f"ingest_{policy}(bf16)", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m)
+
+    if want("merkle"):
+        nl = 80_000
+        hs = torch.randint(0, 256, (nl * 8, 32), dtype=torch.uint8, device=dev)
+        sz = torch.randint(8192, 131072, (nl * 8,), dtype=torch.int64, device=dev)
+        jobs = [(i * nl, nl) for i in range(8)]
+        ms = timed(lambda: ops.merkle_roots(hs, sz, jobs), a.iters)
+        emit(kernel="merkle_8x80k_leaves", ms=ms, leaves=nl * 8)
+
+    if want("h2d"):
+        pin = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+        d = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        ms = timed(lambda: d.copy_(pin, non_blocking=True), a.iters)
+        emit(kernel="h2d_pinned_1GiB", bytes=1 << 30, ms=ms, gbps=(1 << 30) / ms / 1e6)
+
+
+if __name__ == "__main__":
+    t0 = time.time()
+    main()
+    print(json.dumps({"total_s": time.time() - t0}))

@@ -1,0 +1,327 @@
+"""Device pull engine: fetched xorb runs -> HBM arena (decode + verify) -> intra-node swarm exchange.
+
+One process per GPU.  Each rank owns a contiguous, byte-balanced share of the model's
+reconstruction terms (SURVEY §2.E P1 "term-parallel fetch", sharded by owner rank) and streams it
+in rounds through a pinned-host -> HBM staging ring:
+
+    copy stream : hipMemcpyAsync(origin span k -> staging[k % S])           (CDN/PCIe ingest)
+    compute     : index_terms -> place (copy | LZ4/BG4 decode) -> chunk hashes  (zest_amd.ops)
+    RCCL        : round-k regions exchanged peer-to-peer over xGMI (batch_isend_irecv), overlapped
+                  with round k+1 ingest (every GPU acts as a BitTorrent peer)
+    end         : chunk-hash all-reduce (have-map, C2) -> Merkle file hashes on every rank (K2) ->
+                  compare with the repository's file hashes -> error all-reduce (C3)
+
+The reference's equivalent is parallel_download.zig:91-204 (16 concurrent term fetches, batch
+barrier, ordered writes) plus swarm.zig's peer fallback; here the "peers" of one node are GPUs and
+the payload never bounces through the host after ingest.  The origin (what a CDN would have
+returned for each term's url_range) lives in pinned host memory, so the measured pipeline is
+everything zest does after bytes arrive from the network.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import ops
+from .synthetic import SyntheticWorld
+
+
+@dataclass
+class RoundWork:
+    term_a: int          # index range into world.terms (this rank's terms in this round)
+    term_b: int
+    c0: int              # first global chunk
+    n_chunks: int
+    span_off: int        # offset of the round's bytes in this rank's origin store
+    span_len: int
+    region: tuple        # arena [lo, hi) produced by this rank this round
+    terms_dev: torch.Tensor | None = None  # TERM_DTYPE records (src relative to the staging slot)
+
+
+class OriginStore:
+    """Pinned host memory holding the CDN response bytes for this rank's terms."""
+
+    def __init__(self, nbytes: int, device: torch.device):
+        self.n = int(nbytes)
+        self.device = device
+        if device.type == "cuda":
+            self._H = ops.hip()
+            self.ptr = self._H.host_malloc(max(1, self.n))
+            self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.n)).from_address(self.ptr))
+        else:
+            self._H = None
+            self.array = np.empty(max(1, self.n), dtype=np.uint8)
+            self.ptr = self.array.ctypes.data
+
+    def close(self):
+        if self._H is not None and self.ptr:
+            self._H.host_free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def plan_rank_terms(world: SyntheticWorld, n_ranks: int) -> list[tuple[int, int]]:
+    """Contiguous, byte-balanced split of the term list among ranks."""
+    T = world.terms
+    cu = np.cumsum(T["ulen"].astype(np.float64))
+    total = cu[-1] if len(cu) else 0.0
+    bounds = [0]
+    for r in range(1, n_ranks):
+        bounds.append(int(np.searchsorted(cu, total * r / n_ranks, side="left")) + 1)
+    bounds.append(len(T))
+    bounds = np.maximum.accumulate(np.minimum(np.array(bounds), len(T)))
+    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(n_ranks)]
+
+
+def split_rounds(world: SyntheticWorld, a: int, b: int, n_rounds: int) -> list[tuple[int, int]]:
+    T = world.terms
+    if b <= a:
+        return [(a, a)] * n_rounds
+    cu = np.cumsum(T["ulen"][a:b].astype(np.float64))
+    total = cu[-1]
+    cuts = [a]
+    for k in range(1, n_rounds):
+        cuts.append(a + int(np.searchsorted(cu, total * k / n_rounds, side="left")) + 1)
+    cuts.append(b)
+    cuts = np.maximum.accumulate(np.minimum(np.array(cuts), b))
+    return [(int(cuts[k]), int(cuts[k + 1])) for k in range(n_rounds)]
+
+
+class DevicePuller:
+    def __init__(self, world: SyntheticWorld, arena: torch.Tensor, rank: int = 0, n_ranks: int = 1,
+                 round_bytes: int = 1 << 30, slots: int = 3, group=None, verify_received: bool = False,
+                 exchange: str = "p2p"):
+        self.world = world
+        self.arena = arena
+        self.device = arena.device
+        self.rank, self.n_ranks = rank, n_ranks
+        self.group = group
+        self.verify_received = verify_received
+        self.exchange = exchange
+        self.is_cuda = self.device.type == "cuda"
+        T = world.terms
+        self.rank_terms = plan_rank_terms(world, n_ranks)
+        max_share = max((int(T["ulen"][a:b].sum()) for a, b in self.rank_terms), default=0)
+        self.n_rounds = max(1, -(-max_share // round_bytes))
+        # rounds[k][r] = (a, b) term range for rank r in round k
+        per_rank = [split_rounds(world, a, b, self.n_rounds) for a, b in self.rank_terms]
+        self.rounds_all = [[per_rank[r][k] for r in range(n_ranks)] for k in range(self.n_rounds)]
+        # this rank's origin layout: its terms' serialized bytes back to back, in order
+        a_r, b_r = self.rank_terms[rank]
+        ser_len = T["ser_len"][a_r:b_r].astype(np.int64)
+        self.term_origin_off = np.concatenate([[0], np.cumsum(ser_len)]).astype(np.int64)  # relative to a_r
+        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device)
+        self.rounds: list[RoundWork] = []
+        max_span, max_terms, max_chunks = 0, 1, 1
+        for k in range(self.n_rounds):
+            a, b = self.rounds_all[k][rank]
+            span_off = int(self.term_origin_off[a - a_r])
+            span_len = int(self.term_origin_off[b - a_r] - self.term_origin_off[a - a_r])
+            if b > a:
+                c0 = int(T["c0"][a])
+                nck = int(T["c1"][b - 1] - c0)
+                rec = np.zeros(b - a, dtype=ops.TERM_DTYPE)
+                rec["src"] = self.term_origin_off[a - a_r:b - a_r] - span_off
+                rec["src_len"] = T["ser_len"][a:b]
+                rec["dst"] = T["dst"][a:b]
+                rec["chunk_base"] = T["c0"][a:b] - c0
+                rec["n_chunks"] = T["c1"][a:b] - T["c0"][a:b]
+                rec["ulen"] = T["ulen"][a:b]
+                region = (int(T["dst"][a]), int(T["dst"][b - 1] + T["ulen"][b - 1]))
+                terms_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+            else:
+                c0, nck, rec, region, terms_dev = 0, 0, None, (0, 0), None
+            self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev))
+            max_span = max(max_span, span_len)
+            max_terms = max(max_terms, b - a)
+            max_chunks = max(max_chunks, nck)
+        self.regions = [[self._region(k, r) for r in range(n_ranks)] for k in range(self.n_rounds)]
+        self.slots = max(1, min(slots, self.n_rounds))
+        self.staging = [ops.padded_empty(max_span, self.device) for _ in range(self.slots)]
+        self.ws = ops.IngestWorkspace(self.device, max_terms, max_chunks)
+        self.hashes = torch.zeros((world.n_chunks, 32), dtype=torch.uint8, device=self.device)
+        self.sizes = torch.from_numpy(world.chunk_len.astype(np.int64)).to(self.device)
+        self.expected = torch.from_numpy(world.file_hashes.copy()).to(self.device)
+        self.err = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.jobs = world.merkle_jobs()
+        if self.is_cuda:
+            H = ops.hip()
+            rec = np.zeros(len(self.jobs), dtype=ops.MERKLE_JOB_DTYPE)
+            rec["leaf_base"] = [j[0] for j in self.jobs]
+            rec["n_leaves"] = [j[1] for j in self.jobs]
+            rec["want_file_hash"] = 1
+            self.jobs_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+            self.merkle_sb = H.merkle_scratch_bytes(max(j[1] for j in self.jobs), len(self.jobs))
+            self.merkle_scratch = torch.empty(self.merkle_sb, dtype=torch.uint8, device=self.device)
+            self.roots = torch.empty((len(self.jobs), 32), dtype=torch.uint8, device=self.device)
+            self.copy_stream = torch.cuda.Stream(self.device)
+            self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
+            self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
+        self.bytes_received = sum(hi - lo for k in range(self.n_rounds) for r, (lo, hi) in
+                                  enumerate(self.regions[k]) if r != rank)
+        self.bytes_ingested = int(self.term_origin_off[-1])
+
+    def _region(self, k, r):
+        a, b = self.rounds_all[k][r]
+        T = self.world.terms
+        if b <= a:
+            return (0, 0)
+        return (int(T["dst"][a]), int(T["dst"][b - 1] + T["ulen"][b - 1]))
+
+    # ------------------------------------------------------------------------------------------
+    def build_origin(self, pack_batch_bytes: int = 4 << 30) -> None:
+        """Serialize this rank's terms ([header | payload]*) from the content in the arena into
+        the pinned origin store (GPU pack kernel + D2H).  Untimed setup."""
+        w = self.world
+        T = w.terms
+        a_r, b_r = self.rank_terms[self.rank]
+        if b_r <= a_r:
+            return
+        if not self.is_cuda:
+            raise RuntimeError("CPU worlds build the origin from host contents (build_origin_host)")
+        H = ops.hip()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        tmp = ops.padded_empty(min(pack_batch_bytes, self.origin.n) + (64 << 20), self.device)
+        t = a_r
+        while t < b_r:
+            base = int(self.term_origin_off[t - a_r])
+            u = t
+            while u < b_r and self.term_origin_off[u + 1 - a_r] - base <= tmp.numel():
+                u += 1
+            if u == t:
+                raise RuntimeError("term larger than pack batch")
+            c0, c1 = int(T["c0"][t]), int(T["c1"][u - 1])
+            lens = w.chunk_len[c0:c1]
+            ser = lens.astype(np.uint64) + np.uint64(8)
+            out_off = (np.cumsum(ser) - ser).astype(np.uint64)
+            ops.pack_chunks(self.arena, w.chunk_off[c0:c1], lens, out_off, tmp)
+            n = int(self.term_origin_off[u - a_r] - base)
+            H.memcpy_async(self.origin.ptr + base, tmp.data_ptr(), n, st)
+            torch.cuda.synchronize(self.device)
+            t = u
+
+    def build_origin_host(self, contents: dict[str, bytes]) -> None:
+        w = self.world
+        T = w.terms
+        a_r, b_r = self.rank_terms[self.rank]
+        pos = 0
+        for t in range(a_r, b_r):
+            f = w.xet_files[int(T["file"][t])]
+            data = contents[f.path]
+            for c in range(int(T["c0"][t]), int(T["c1"][t])):
+                rel = int(w.chunk_off[c]) - f.arena_off
+                n = int(w.chunk_len[c])
+                hdr = bytes([0, n & 255, (n >> 8) & 255, (n >> 16) & 255, 0, n & 255, (n >> 8) & 255, (n >> 16) & 255])
+                self.origin.array[pos:pos + 8] = np.frombuffer(hdr, dtype=np.uint8)
+                self.origin.array[pos + 8:pos + 8 + n] = np.frombuffer(data[rel:rel + n], dtype=np.uint8)
+                pos += 8 + n
+
+    # ------------------------------------------------------------------------------------------
+    def _exchange(self, k: int):
+        import torch.distributed as dist
+        lo_me, hi_me = self.regions[k][self.rank]
+        p2p = []
+        for p in range(self.n_ranks):
+            if p == self.rank:
+                continue
+            if hi_me > lo_me:
+                p2p.append(dist.P2POp(dist.isend, self.arena[lo_me:hi_me], p, self.group))
+            lo, hi = self.regions[k][p]
+            if hi > lo:
+                p2p.append(dist.P2POp(dist.irecv, self.arena[lo:hi], p, self.group))
+        if not p2p:
+            return []
+        return dist.batch_isend_irecv(p2p)
+
+    def step(self) -> dict:
+        """One full pull of the model onto every rank.  Returns per-step stats."""
+        import torch.distributed as dist
+        dev = self.device
+        self.hashes.zero_()  # err is NOT reset: the first error of any step persists until check()
+        works = []
+        if self.is_cuda:
+            H = ops.hip()
+            comp = torch.cuda.current_stream(dev)
+            st = comp.cuda_stream
+            for k, rw in enumerate(self.rounds):
+                s = k % self.slots
+                with torch.cuda.stream(self.copy_stream):
+                    self.copy_stream.wait_event(self.slot_free[s])
+                    if rw.span_len:
+                        H.memcpy_async(self.staging[s].data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
+                                       self.copy_stream.cuda_stream)
+                    self.h2d_done[s].record(self.copy_stream)
+                comp.wait_event(self.h2d_done[s])
+                if rw.term_b > rw.term_a:
+                    nt = rw.term_b - rw.term_a
+                    src = self.staging[s]
+                    self.ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
+                    H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), nt, self.ws.chunks.data_ptr(),
+                                  self.err.data_ptr(), st)
+                    H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(),
+                                   self.ws.chunks.data_ptr(), rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
+                    H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), self.ws.chunks.data_ptr(), rw.n_chunks,
+                                  self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
+                self.slot_free[s].record(comp)
+                if self.n_ranks > 1:
+                    works += self._exchange(k)
+        else:
+            for k, rw in enumerate(self.rounds):
+                if rw.term_b > rw.term_a:
+                    span = torch.from_numpy(self.origin.array[rw.span_off:rw.span_off + rw.span_len])
+                    rec = np.frombuffer(rw.terms_dev.numpy().tobytes(), dtype=ops.TERM_DTYPE)
+                    ops.ingest_terms(span, self.arena, rec, self.hashes, hash_base=rw.c0)
+                if self.n_ranks > 1:
+                    works += self._exchange(k)
+        for w in works:
+            w.wait()
+        if self.n_ranks > 1:
+            dist.all_reduce(self.hashes.view(torch.int32), op=dist.ReduceOp.SUM, group=self.group)
+        if self.verify_received and self.n_ranks > 1:
+            self._verify_received()
+        if self.is_cuda:
+            H.merkle(self.hashes.data_ptr(), self.sizes.data_ptr(), self.jobs_dev.data_ptr(), len(self.jobs),
+                     self.roots.data_ptr(), self.merkle_scratch.data_ptr(), self.merkle_sb, st)
+            H.compare_hashes(self.roots.data_ptr(), self.expected.data_ptr(), len(self.jobs), self.err.data_ptr(), st)
+        else:
+            roots = ops.merkle_roots(self.hashes, self.sizes, self.jobs)
+            if not torch.equal(roots, self.expected):
+                self.err.fill_((6 << 32) | int((roots != self.expected).any(1).nonzero()[0].item()))
+        if self.n_ranks > 1:
+            dist.all_reduce(self.err, op=dist.ReduceOp.MAX, group=self.group)
+        return {"rounds": self.n_rounds}
+
+    def check(self) -> None:
+        ops.raise_on_error(self.err)
+
+    def _verify_received(self):
+        """Re-hash every chunk that arrived from a peer and compare with the owner's hash."""
+        w = self.world
+        T = w.terms
+        a_r, b_r = self.rank_terms[self.rank]
+        mask = np.ones(w.n_chunks, dtype=bool)
+        if b_r > a_r:
+            mask[int(T["c0"][a_r]):int(T["c1"][b_r - 1])] = False
+        idx = np.flatnonzero(mask)
+        if len(idx) == 0:
+            return
+        got = ops.hash_ranges(self.arena, w.chunk_off[idx], w.chunk_len[idx])
+        want = self.hashes[torch.from_numpy(idx).to(self.device)]
+        bad = (got != want).any(1)
+        if self.is_cuda:
+            first = torch.where(bad.any(), torch.argmax(bad.to(torch.int32)), torch.tensor(-1, device=self.device))
+            self.err.copy_(torch.where(first >= 0, (6 << 32) + first, self.err))
+        elif bool(bad.any()):
+            self.err.fill_((6 << 32) | int(bad.nonzero()[0].item()))
+
+    def close(self):
+        self.origin.close()

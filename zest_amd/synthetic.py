@@ -1,0 +1,275 @@
+"""Synthetic Xet world: a model repository materialized as files -> CDC chunks -> xorbs -> terms.
+
+This plays the role of HuggingFace's Xet storage for offline benchmarks and tests (there is no
+network): it produces exactly what a Xet uploader would (CDC boundaries with the real gear table,
+keyed-BLAKE3 chunk hashes, 64 MiB xorbs packed across files, per-file reconstruction terms,
+Merkle file hashes) and the byte runs a CAS/CDN returns for each term's url_range
+(`[8-byte chunk header | payload]*`).  Reference context: the reconstruction JSON consumed at
+xet_bridge.zig:133-142 and parallel_download.zig:102-126 (terms + fetch_info url_range).
+
+GPU path (`build_on_device`): content generation, CDC candidates, chunk hashes, Merkle file
+hashes and xorb packing all run as HIP kernels (zest_amd.ops); the host only selects boundaries
+over the sparse candidates and plans xorbs/terms (vectorized numpy + _core.plan_xorbs).
+CPU path (`build_on_host`): the same plan from the C++ host core, for small models in tests.
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _core, models, ops
+
+MAX_XORB_BYTES = 64 << 20
+MAX_XORB_CHUNKS = 8192
+FILE_ALIGN = 4096
+MODES = {"random": 0, "bf16": 1}
+
+
+def _file_seed(seed: int, idx: int) -> int:
+    return int.from_bytes(hashlib.blake2b(f"{seed}:{idx}".encode(), digest_size=8).digest(), "little")
+
+
+@dataclass
+class FileEntry:
+    path: str
+    size: int
+    arena_off: int
+    header: bytes          # safetensors header bytes (b"" for regular files)
+    data_seed: int
+    xet: bool              # Xet-backed (weights) vs regular small file
+    content: bytes = b""   # for regular (non-Xet) files
+
+
+class SyntheticWorld:
+    """Layout + Xet metadata of one synthetic repository."""
+
+    def __init__(self, spec: models.ModelSpec | str, seed: int = 0, mode: str = "random",
+                 revision_sha: str | None = None, max_xorb_bytes: int = MAX_XORB_BYTES):
+        self.spec = models.get(spec) if isinstance(spec, str) else spec
+        self.max_xorb_bytes = max_xorb_bytes
+        self.seed = seed
+        self.mode = mode
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {list(MODES)}")
+        self.shards = self.spec.shards()
+        self.files: list[FileEntry] = []
+        off = 0
+        for i, sh in enumerate(self.shards):
+            self.files.append(FileEntry(sh.path, sh.size, off, sh.header, _file_seed(seed, i), True))
+            off = (off + sh.size + FILE_ALIGN - 1) // FILE_ALIGN * FILE_ALIGN
+        self.arena_bytes = off
+        for path, content in self.spec.small_files(self.shards).items():
+            self.files.append(FileEntry(path, len(content), -1, b"", 0, False, content))
+        self.commit = revision_sha or hashlib.sha1(f"{self.spec.repo_id}:{seed}:{mode}".encode()).hexdigest()
+        self.xet_files = [f for f in self.files if f.xet]
+        # filled by build_*
+        self.chunk_off = None   # uint64 arena offset of each chunk (global arena order)
+        self.chunk_len = None   # uint32
+        self.chunk_file = None  # int32 file index (into xet_files)
+        self.file_chunk0 = None  # first global chunk per xet file
+        self.file_nchunks = None
+        self.file_hashes = None  # uint8 [n_files, 32]
+        self.chunk_hashes = None  # uint8 [n_chunks, 32] (host copy)
+        self.xorb_of = None       # int64 per chunk
+        self.ser_off = None       # uint64 offset of the chunk header inside its xorb
+        self.terms = None         # structured array, see _plan_terms
+
+    # ------------------------------------------------------------------------------------------
+    @property
+    def model_bytes(self) -> int:
+        return sum(f.size for f in self.xet_files)
+
+    @property
+    def n_chunks(self) -> int:
+        return 0 if self.chunk_len is None else len(self.chunk_len)
+
+    def file_bytes_host(self, f: FileEntry) -> bytes:
+        """Regenerate a file's bytes on the host (small models / tests)."""
+        if not f.xet:
+            return f.content
+        data = np.empty(f.size - len(f.header), dtype=np.uint8)
+        _host_fill(data, f.data_seed, MODES[self.mode])
+        return f.header + data.tobytes()
+
+    # ------------------------------------------------------------------------------------------
+    # Device build (bench path)
+    # ------------------------------------------------------------------------------------------
+    def generate_on_device(self, arena: torch.Tensor) -> None:
+        """Write every Xet file's bytes at its arena offset (header + synthetic weights)."""
+        for f in self.xet_files:
+            hdr = torch.frombuffer(bytearray(f.header), dtype=torch.uint8)
+            arena[f.arena_off:f.arena_off + len(f.header)].copy_(hdr)
+            data = arena[f.arena_off + len(f.header):f.arena_off + f.size]
+            ops.fill_synthetic(data, f.data_seed, 0, MODES[self.mode])
+
+    def build_on_device(self, arena: torch.Tensor, hash_batch: int = 1 << 20) -> None:
+        """CDC + chunk hashes + file hashes + xorb/term plan, from content already in `arena`."""
+        offs, lens, fidx = [], [], []
+        for i, f in enumerate(self.xet_files):
+            region = arena[f.arena_off:f.arena_off + f.size]
+            cand = ops.cdc_candidates(region)
+            ends = ops.select_chunks(cand, f.size)
+            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+            offs.append(starts + np.uint64(f.arena_off))
+            lens.append((ends - starts).astype(np.uint32))
+            fidx.append(np.full(len(ends), i, dtype=np.int32))
+        self._set_chunks(np.concatenate(offs), np.concatenate(lens), np.concatenate(fidx))
+        dev = arena.device
+        hashes = torch.empty((self.n_chunks, 32), dtype=torch.uint8, device=dev)
+        for a in range(0, self.n_chunks, hash_batch):
+            b = min(self.n_chunks, a + hash_batch)
+            hashes[a:b] = ops.hash_ranges(arena, self.chunk_off[a:b], self.chunk_len[a:b])
+        sizes = torch.from_numpy(self.chunk_len.astype(np.int64)).to(dev)
+        fh = ops.merkle_roots(hashes, sizes, self.merkle_jobs(), file_hash=True)
+        self.chunk_hashes = hashes.cpu().numpy()
+        self.file_hashes = fh.cpu().numpy()
+        self._plan_xorbs()
+
+    # ------------------------------------------------------------------------------------------
+    # Host build (tests / small models)
+    # ------------------------------------------------------------------------------------------
+    def build_on_host(self) -> dict[str, bytes]:
+        contents = {}
+        offs, lens, fidx, hs = [], [], [], []
+        for i, f in enumerate(self.xet_files):
+            data = self.file_bytes_host(f)
+            contents[f.path] = data
+            ends = np.asarray(_core.chunk_ends(data), dtype=np.uint64)
+            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+            offs.append(starts + np.uint64(f.arena_off))
+            lens.append((ends - starts).astype(np.uint32))
+            fidx.append(np.full(len(ends), i, dtype=np.int32))
+            for a, b in zip(starts.tolist(), ends.tolist()):
+                hs.append(np.frombuffer(_core.chunk_hash(data[a:b]), dtype=np.uint8))
+        self._set_chunks(np.concatenate(offs), np.concatenate(lens), np.concatenate(fidx))
+        self.chunk_hashes = np.stack(hs) if hs else np.zeros((0, 32), np.uint8)
+        fh = []
+        for i in range(len(self.xet_files)):
+            a, n = int(self.file_chunk0[i]), int(self.file_nchunks[i])
+            leaves = [(self.chunk_hashes[j].tobytes(), int(self.chunk_len[j])) for j in range(a, a + n)]
+            fh.append(np.frombuffer(_core.file_hash(leaves), dtype=np.uint8))
+        self.file_hashes = np.stack(fh)
+        self._plan_xorbs()
+        return contents
+
+    # ------------------------------------------------------------------------------------------
+    def _set_chunks(self, offs, lens, fidx):
+        self.chunk_off = offs
+        self.chunk_len = lens
+        self.chunk_file = fidx
+        nf = len(self.xet_files)
+        self.file_nchunks = np.bincount(fidx, minlength=nf).astype(np.int64)
+        self.file_chunk0 = np.concatenate([[0], np.cumsum(self.file_nchunks)[:-1]]).astype(np.int64)
+
+    def merkle_jobs(self):
+        return [(int(a), int(n)) for a, n in zip(self.file_chunk0, self.file_nchunks)]
+
+    def file_hash_hex(self, i: int) -> str:
+        return _core.xet_hex(self.file_hashes[i].tobytes())
+
+    def _plan_xorbs(self) -> None:
+        ser = self.chunk_len.astype(np.uint64) + np.uint64(8)  # scheme 0 (random) serialized size
+        self.xorb_of = np.asarray(_core.plan_xorbs(ser, self.max_xorb_bytes, MAX_XORB_CHUNKS), dtype=np.int64)
+        # offset of each chunk header inside its xorb
+        cum = np.cumsum(ser) - ser
+        first = np.concatenate([[True], self.xorb_of[1:] != self.xorb_of[:-1]])
+        xorb_start = np.maximum.accumulate(np.where(first, cum, 0).astype(np.uint64))
+        self.ser_off = (cum - xorb_start).astype(np.uint64)
+        self.ser_len = ser
+        self.n_xorbs = int(self.xorb_of[-1]) + 1 if len(self.xorb_of) else 0
+        self.xorb_chunk0 = np.flatnonzero(first).astype(np.int64)
+        # terms: maximal runs of consecutive chunks sharing (file, xorb)
+        brk = np.concatenate([[True], (self.xorb_of[1:] != self.xorb_of[:-1]) |
+                              (self.chunk_file[1:] != self.chunk_file[:-1])])
+        t0 = np.flatnonzero(brk)
+        t1 = np.concatenate([t0[1:], [self.n_chunks]])
+        T = np.zeros(len(t0), dtype=[("file", "<i4"), ("xorb", "<i8"), ("c0", "<i8"), ("c1", "<i8"),
+                                     ("local0", "<i8"), ("ser0", "<u8"), ("ser_len", "<u8"),
+                                     ("dst", "<u8"), ("ulen", "<u8")])
+        T["file"] = self.chunk_file[t0]
+        T["xorb"] = self.xorb_of[t0]
+        T["c0"] = t0
+        T["c1"] = t1
+        T["local0"] = t0 - self.xorb_chunk0[self.xorb_of[t0]]
+        T["ser0"] = self.ser_off[t0]
+        cs = np.concatenate([[0], np.cumsum(ser)]).astype(np.uint64)
+        T["ser_len"] = cs[t1] - cs[t0]
+        T["dst"] = self.chunk_off[t0]
+        cl = np.concatenate([[0], np.cumsum(self.chunk_len.astype(np.uint64))]).astype(np.uint64)
+        T["ulen"] = cl[t1] - cl[t0]
+        self.terms = T
+
+    # ------------------------------------------------------------------------------------------
+    def reconstruction(self, file_idx: int, cas_url: str) -> dict:
+        """Xet reconstruction JSON for one file (CAS /v1/reconstructions/{file_hash})."""
+        T = self.terms[self.terms["file"] == file_idx]
+        terms, fetch = [], {}
+        for t in T:
+            xh = self.xorb_hash_hex(int(t["xorb"]))
+            n = int(t["c1"] - t["c0"])
+            local0 = int(t["local0"])
+            terms.append({"hash": xh, "unpacked_length": int(t["ulen"]),
+                          "range": {"start": local0, "end": local0 + n}})
+            fetch.setdefault(xh, []).append({
+                "range": {"start": local0, "end": local0 + n},
+                "url": f"{cas_url}/xorbs/default/{xh}",
+                "url_range": {"start": int(t["ser0"]), "end": int(t["ser0"] + t["ser_len"]) - 1}})
+        return {"offset_into_first_range": 0, "terms": terms, "fetch_info": fetch}
+
+    def xorb_hash(self, x: int) -> bytes:
+        a = int(self.xorb_chunk0[x])
+        b = int(self.xorb_chunk0[x + 1]) if x + 1 < self.n_xorbs else self.n_chunks
+        leaves = [(self.chunk_hashes[j].tobytes(), int(self.chunk_len[j])) for j in range(a, b)]
+        return _core.merkle_root(leaves)
+
+    def xorb_hash_hex(self, x: int) -> str:
+        if not hasattr(self, "_xorb_hex"):
+            self._xorb_hex = {}
+        if x not in self._xorb_hex:
+            self._xorb_hex[x] = _core.xet_hex(self.xorb_hash(x))
+        return self._xorb_hex[x]
+
+    def xorb_bytes_host(self, x: int, contents: dict[str, bytes], policy: str = "none", footer: bool = True) -> bytes:
+        """Serialize xorb x from host file contents (CAS object bytes)."""
+        a = int(self.xorb_chunk0[x])
+        b = int(self.xorb_chunk0[x + 1]) if x + 1 < self.n_xorbs else self.n_chunks
+        bld = _core.XorbBuilder(policy)
+        for j in range(a, b):
+            f = self.xet_files[int(self.chunk_file[j])]
+            rel = int(self.chunk_off[j]) - f.arena_off
+            bld.add_chunk(contents[f.path][rel:rel + int(self.chunk_len[j])])
+        return bld.serialize(footer)
+
+
+def _host_fill(out: np.ndarray, seed: int, mode: int) -> None:
+    """numpy twin of the device generator (zest_amd.ops.fill_synthetic) for small files."""
+    n = out.size
+    if n == 0:
+        return
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def splitmix(x):
+        x = (x + np.uint64(0x9E3779B97F4A7C15)) & M
+        x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M
+        x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M
+        return x ^ (x >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        if mode == 0:
+            words = (n + 7) // 8
+            idx = np.arange(words, dtype=np.uint64)
+            w = splitmix(np.uint64(seed) ^ (idx * np.uint64(0xD1B54A32D192ED03)))
+            out[:] = w.view(np.uint8)[:n]
+        else:
+            ne = (n + 1) // 2
+            e = np.arange(ne, dtype=np.uint64)
+            h = splitmix(np.uint64(seed) ^ (e * np.uint64(0xA24BAED4963EE407)))
+            u1 = (((h >> np.uint64(40)) & np.uint64(0xFFFFFF)).astype(np.float32) + 0.5) / 16777216.0
+            u2 = ((h >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.float32) / 16777216.0
+            z = (np.sqrt(-2.0 * np.log(u1)) * np.cos(6.28318530718 * u2) * 0.02).astype(np.float32)
+            bits = z.view(np.uint32)
+            bf = ((bits + np.uint32(0x7FFF) + ((bits >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16)).astype(np.uint16)
+            out[:] = bf.view(np.uint8)[:n]
