@@ -1,0 +1,137 @@
+#include "bridge.h"
+
+#include <iomanip>
+
+#include "json.h"
+#include "xorb.h"
+
+namespace zest {
+
+void XetBridge::authenticate(const std::string& repo_id, const std::string& repo_type, const std::string& revision) {
+  hub::XetToken t = hub::xet_read_token(cfg_, repo_id, revision, repo_type);
+  set_cas(t.cas_url, t.access_token);
+}
+
+void XetBridge::set_cas(const std::string& cas_url, const std::string& token) {
+  cas_ = std::make_unique<cas::CasClient>(cas_url, token);
+}
+
+cas::Reconstruction XetBridge::get_reconstruction(const std::string& file_hash_hex) const {
+  if (!cas_) throw Error("NotAuthenticated");
+  return cas_->get_reconstruction(file_hash_hex);
+}
+
+namespace {
+// A cached / received run must contain the term's chunks.
+bool covers(const Bytes& data, uint32_t chunk_offset, uint64_t start, uint64_t end) {
+  if (start < chunk_offset) return false;
+  try {
+    auto idx = xet::index_chunks(data.data(), data.size());
+    return end - chunk_offset <= idx.size();
+  } catch (const Error&) {
+    return false;
+  }
+}
+}  // namespace
+
+XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p,
+                                      bool allow_cache) {
+  const std::string& hex = term.hash_hex;
+  auto it = recon.fetch_info.find(hex);
+  if (it == recon.fetch_info.end()) throw Error("NotAuthenticated", "no fetch_info for " + hex);
+  const cas::FetchInfo* fi = recon.match(hex, term.range.start, term.range.end);
+  if (!fi) throw Error("NoMatchingFetchInfo", hex);
+  XorbFetchResult out;
+  // 1. local xorb cache (full or partial entry)
+  if (allow_cache && cache_) {
+    if (auto hit = cache_->get_with_range(hex, uint32_t(fi->range.start))) {
+      if (covers(hit->data, hit->chunk_offset, term.range.start, term.range.end)) {
+        stats_.xorbs_from_cache++;
+        stats_.bytes_from_cache += hit->data.size();
+        if (swarm_) swarm_->stats().cached_xorbs++;
+        out.data = std::move(hit->data);
+        out.local_start = uint32_t(term.range.start - hit->chunk_offset);
+        out.local_end = uint32_t(term.range.end - hit->chunk_offset);
+        out.source = Source::Cache;
+        return out;
+      }
+    }
+  }
+  const bool whole = fi->range.start == 0 && it->second.size() == 1;
+  // 2. P2P swarm with the FetchInfo's chunk range
+  if (allow_p2p && swarm_ && swarm_->p2p_enabled()) {
+    if (auto r = swarm_->try_peers(term.hash, uint32_t(fi->range.start), uint32_t(fi->range.end))) {
+      if (covers(r->data, r->chunk_offset, term.range.start, term.range.end)) {
+        stats_.xorbs_from_peer++;
+        stats_.bytes_from_peer += r->data.size();
+        if (cache_) {
+          try {
+            if (r->chunk_offset == 0 && whole) cache_->put(hex, r->data.data(), r->data.size());
+            else cache_->put_partial(hex, r->chunk_offset, r->data.data(), r->data.size());
+          } catch (const Error&) {
+          }
+        }
+        out.local_start = uint32_t(term.range.start - r->chunk_offset);
+        out.local_end = uint32_t(term.range.end - r->chunk_offset);
+        out.data = std::move(r->data);
+        out.source = Source::Peer;
+        out.peer = r->peer;
+        return out;
+      }
+      swarm_->report_bad_peer(r->peer);  // served a run that does not even parse
+    }
+  }
+  // 3. CDN
+  if (!cas_) throw Error("NotAuthenticated");
+  out.data = cas_->fetch(*fi);
+  stats_.xorbs_from_cdn++;
+  stats_.bytes_from_cdn += out.data.size();
+  if (swarm_) {
+    swarm_->stats().cdn_xorbs++;
+    swarm_->stats().total_xorbs++;
+    swarm_->stats().total_bytes += out.data.size();
+  }
+  if (cache_) {
+    try {
+      if (whole) cache_->put(hex, out.data.data(), out.data.size());
+      else cache_->put_partial(hex, uint32_t(fi->range.start), out.data.data(), out.data.size());
+    } catch (const Error&) {
+    }
+  }
+  out.local_start = uint32_t(term.range.start - fi->range.start);
+  out.local_end = uint32_t(term.range.end - fi->range.start);
+  out.source = Source::Cdn;
+  return out;
+}
+
+void XetBridge::print_stats(std::ostream& w) const {
+  const uint64_t total = stats_.xorbs_from_cache + stats_.xorbs_from_peer + stats_.xorbs_from_cdn;
+  const uint64_t total_bytes = stats_.bytes_from_cache + stats_.bytes_from_peer + stats_.bytes_from_cdn;
+  w << "\nXorb fetch stats:\n";
+  w << "  Total xorbs:  " << total << "\n";
+  w << "  From cache:   " << stats_.xorbs_from_cache.load() << "\n";
+  w << "  From peers:   " << stats_.xorbs_from_peer.load() << "\n";
+  w << "  From CDN:     " << stats_.xorbs_from_cdn.load() << "\n";
+  w << "  Total bytes:  " << total_bytes << "\n";
+  if (total_bytes > 0) {
+    const double pct = double(stats_.bytes_from_peer.load()) / double(total_bytes) * 100.0;
+    w << "  P2P ratio:    " << std::fixed << std::setprecision(1) << pct << "%\n";
+  }
+  if (stats_.verify_failures.load())
+    w << "  Verify fails: " << stats_.verify_failures.load() << " (refetched " << stats_.refetches.load() << ")\n";
+}
+
+std::string XetBridge::stats_json() const {
+  const uint64_t total_bytes = stats_.bytes_from_cache + stats_.bytes_from_peer + stats_.bytes_from_cdn;
+  json::Writer w;
+  w.obj();
+  w.key("xorbs_from_cache").num_u(stats_.xorbs_from_cache).key("xorbs_from_peer").num_u(stats_.xorbs_from_peer);
+  w.key("xorbs_from_cdn").num_u(stats_.xorbs_from_cdn).key("bytes_from_cache").num_u(stats_.bytes_from_cache);
+  w.key("bytes_from_peer").num_u(stats_.bytes_from_peer).key("bytes_from_cdn").num_u(stats_.bytes_from_cdn);
+  w.key("p2p_ratio").num(total_bytes ? double(stats_.bytes_from_peer) / double(total_bytes) : 0.0, 4);
+  w.key("verify_failures").num_u(stats_.verify_failures).key("refetches").num_u(stats_.refetches);
+  w.end();
+  return w.out();
+}
+
+}  // namespace zest

@@ -1,0 +1,62 @@
+// XetBridge: the cache -> P2P -> CDN waterfall for one reconstruction term, plus fetch stats.
+//
+// Reference: src/xet_bridge.zig:1-307 — authenticate via xet-read-token (:76-130),
+// getReconstruction (:133-142), fetchXorbForTerm (:149-218) using the FetchInfo that covers the
+// term (:221-228), caching every CDN entry full/partial for seeding, returning local (rebased)
+// chunk indices; printStats strings (:267-281) are preserved verbatim.  Stats are atomics here
+// (the reference races on them from concurrent tasks, SURVEY §5.2 a).
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <ostream>
+#include <string>
+
+#include "config.h"
+#include "hub.h"
+#include "storage.h"
+#include "swarm.h"
+
+namespace zest {
+
+struct FetchStats {
+  std::atomic<uint64_t> xorbs_from_cache{0}, xorbs_from_peer{0}, xorbs_from_cdn{0};
+  std::atomic<uint64_t> bytes_from_cache{0}, bytes_from_peer{0}, bytes_from_cdn{0};
+  std::atomic<uint64_t> verify_failures{0}, refetches{0};
+};
+
+enum class Source { Cache, Peer, Cdn };
+
+struct XorbFetchResult {
+  Bytes data;
+  uint32_t local_start = 0, local_end = 0;  // chunk indices inside `data`
+  Source source = Source::Cdn;
+  std::string peer;
+};
+
+class XetBridge {
+ public:
+  XetBridge(const Config& cfg, storage::XorbCache* cache, SwarmDownloader* swarm)
+      : cfg_(cfg), cache_(cache), swarm_(swarm) {}
+  void authenticate(const std::string& repo_id, const std::string& repo_type, const std::string& revision);
+  void set_cas(const std::string& cas_url, const std::string& token);
+  bool authenticated() const { return cas_ != nullptr; }
+  cas::Reconstruction get_reconstruction(const std::string& file_hash_hex) const;
+  XorbFetchResult fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p = true,
+                             bool allow_cache = true);
+  FetchStats& stats() { return stats_; }
+  void print_stats(std::ostream& w) const;
+  std::string stats_json() const;
+  SwarmDownloader* swarm() { return swarm_; }
+
+ private:
+  const Config& cfg_;
+  storage::XorbCache* cache_;
+  SwarmDownloader* swarm_;
+  std::unique_ptr<cas::CasClient> cas_;
+  FetchStats stats_;
+};
+
+}  // namespace zest

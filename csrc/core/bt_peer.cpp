@@ -1,0 +1,154 @@
+#include "bt_peer.h"
+
+#include <cstring>
+
+namespace zest::bt {
+
+void PeerSession::read_frame(Bytes& frame, Message& m, int timeout_ms) {
+  sock_.set_timeout(timeout_ms);
+  uint8_t lenb[4];
+  sock_.read_exact(lenb, 4);
+  const uint32_t len = load_be32(lenb);
+  if (len > kMaxMessage) throw Error("InvalidMessageSize");
+  frame.resize(4 + size_t(len));
+  std::memcpy(frame.data(), lenb, 4);
+  if (len) sock_.read_exact(frame.data() + 4, len);
+  bytes_rx_ += 4 + len;
+  if (parse_message(frame.data(), frame.size(), m) == 0) throw Error("UnexpectedEnd");
+}
+
+std::shared_ptr<PeerSession> PeerSession::connect(const net::Addr& addr, const Sha1Digest& info_hash,
+                                                  const peer_id::PeerId& me, uint16_t listen_port, int timeout_ms) {
+  std::shared_ptr<PeerSession> s(new PeerSession());
+  s->addr_ = addr;
+  s->sock_ = net::Socket::connect_tcp(addr, timeout_ms);
+  s->sock_.set_timeout(timeout_ms);
+  s->sock_.set_buffers(8 << 20);
+  Bytes out;
+  write_handshake(out, info_hash, me);
+  s->sock_.write_all(out.data(), out.size());
+  uint8_t hs[kHandshakeLen];
+  s->sock_.read_exact(hs, kHandshakeLen);
+  Handshake h = parse_handshake(hs);
+  if (h.info_hash != info_hash) throw Error("InfoHashMismatch");
+  s->remote_id_ = h.peer_id;
+  if (!h.supports_bep10()) return s;
+  out.clear();
+  const std::string ext = bep_xet::make_ext_handshake(listen_port);
+  Bytes payload(1 + ext.size());
+  payload[0] = 0;  // ext_id 0 = extended handshake
+  std::memcpy(payload.data() + 1, ext.data(), ext.size());
+  write_message(out, kExtended, payload.data(), payload.size());
+  write_message(out, kUnchoke);
+  write_message(out, kInterested);
+  s->sock_.write_all(out.data(), out.size());
+  // Read until the peer's extended handshake (bounded).
+  Bytes frame;
+  for (int i = 0; i < 8; ++i) {
+    Message m;
+    s->read_frame(frame, m, timeout_ms);
+    if (m.keepalive || m.id != kExtended) continue;
+    Extended e = parse_extended(m.payload);
+    if (e.ext_id != 0) continue;
+    bep_xet::ExtCapabilities caps = bep_xet::parse_ext_handshake(e.data);
+    s->remote_xet_id_ = caps.ut_xet_id;
+    s->client_ = caps.client;
+    break;
+  }
+  return s;
+}
+
+ChunkResult PeerSession::request(const XetRequest& r, int timeout_ms) {
+  std::vector<std::string> errs;
+  auto res = request_many({r}, timeout_ms, &errs);
+  if (!errs[0].empty()) throw Error(errs[0]);
+  return std::move(res[0]);
+}
+
+std::vector<ChunkResult> PeerSession::request_many(const std::vector<XetRequest>& reqs, int timeout_ms,
+                                                   std::vector<std::string>* errors) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!supports_xet()) throw Error("PeerNoXet");
+  std::vector<ChunkResult> out(reqs.size());
+  std::vector<std::string> errs(reqs.size());
+  std::map<uint32_t, size_t> want;
+  Bytes msg;
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    const uint32_t id = next_req_++;
+    want[id] = i;
+    bep_xet::encode_chunk_request(msg, uint8_t(remote_xet_id_), id, reqs[i].xorb_hash.data(), reqs[i].range_start,
+                                  reqs[i].range_end);
+  }
+  try {
+    sock_.write_all(msg.data(), msg.size());
+    Bytes frame;
+    while (!want.empty()) {
+      Message m;
+      read_frame(frame, m, timeout_ms);
+      if (m.keepalive) continue;
+      if (m.id == kChoke || m.id == kUnchoke || m.id == kInterested || m.id == kNotInterested) continue;
+      if (m.id != kExtended) continue;
+      Extended e = parse_extended(m.payload);
+      if (e.ext_id == 0) continue;  // late/extra ext handshake
+      bep_xet::Message x = bep_xet::decode(e.data);
+      auto it = want.find(x.request_id);
+      if (it == want.end()) continue;  // stale reply for another request
+      const size_t i = it->second;
+      want.erase(it);
+      switch (x.type) {
+        case bep_xet::kChunkResponse:
+          out[i].data.assign(x.data.data, x.data.data + x.data.size);
+          out[i].chunk_offset = x.chunk_offset;
+          break;
+        case bep_xet::kChunkNotFound: errs[i] = "ChunkNotFound"; break;
+        case bep_xet::kChunkError: errs[i] = "ChunkError"; break;
+        default: errs[i] = "UnexpectedMessage"; break;
+      }
+    }
+  } catch (const Error&) {
+    healthy_ = false;
+    throw;
+  }
+  if (errors) *errors = std::move(errs);
+  return out;
+}
+
+std::shared_ptr<PeerSession> PeerPool::get_or_connect(const net::Addr& a, const Sha1Digest& info_hash) {
+  const std::string key = a.str();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = peers_.find(key);
+    if (it != peers_.end()) {
+      if (it->second->healthy()) return it->second;
+      peers_.erase(it);
+    }
+  }
+  // Connect + handshake outside the lock.
+  auto s = PeerSession::connect(a, info_hash, me_, listen_port_, timeout_);
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = peers_.find(key);
+  if (it != peers_.end() && it->second->healthy()) return it->second;  // lost the race: use the winner
+  if (peers_.size() >= max_) {
+    // Evict an idle session (only the pool holds it).
+    for (auto e = peers_.begin(); e != peers_.end(); ++e) {
+      if (e->second.use_count() == 1) {
+        peers_.erase(e);
+        break;
+      }
+    }
+  }
+  peers_[key] = s;
+  return s;
+}
+
+void PeerPool::remove(const net::Addr& a) {
+  std::lock_guard<std::mutex> g(mu_);
+  peers_.erase(a.str());
+}
+
+size_t PeerPool::count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return peers_.size();
+}
+
+}  // namespace zest::bt

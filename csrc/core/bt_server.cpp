@@ -1,0 +1,195 @@
+#include "bt_server.h"
+
+#include <chrono>
+#include <cstring>
+#include <random>
+
+#include "bt_wire.h"
+#include "xet_hash.h"
+#include "xorb.h"
+
+namespace zest::bt {
+
+FaultSpec FaultSpec::parse(const std::string& s) {
+  FaultSpec f;
+  size_t p = 0;
+  while (p < s.size()) {
+    size_t c = s.find(',', p);
+    std::string kv = s.substr(p, c == std::string::npos ? std::string::npos : c - p);
+    size_t colon = kv.find(':');
+    if (colon != std::string::npos) {
+      std::string k = kv.substr(0, colon), v = kv.substr(colon + 1);
+      if (k == "drop") f.drop = std::atof(v.c_str());
+      else if (k == "corrupt") f.corrupt = std::atof(v.c_str());
+      else if (k == "delay") f.delay_ms = std::atoi(v.c_str());
+    }
+    if (c == std::string::npos) break;
+    p = c + 1;
+  }
+  return f;
+}
+
+std::optional<storage::CacheHit> slice_chunks(const Bytes& data, uint32_t offset, uint32_t start, uint32_t end) {
+  if (start < offset) return std::nullopt;
+  auto idx = xet::index_chunks(data.data(), data.size());
+  const uint32_t a = start - offset;
+  if (a >= idx.size()) return std::nullopt;
+  uint32_t b = end > start ? end - offset : uint32_t(idx.size());
+  if (b > idx.size()) b = uint32_t(idx.size());
+  const uint64_t lo = idx[a].header_off;
+  const uint64_t hi = idx[b - 1].header_off + xet::kChunkHeaderLen + idx[b - 1].clen;
+  storage::CacheHit h;
+  h.data.assign(data.begin() + long(lo), data.begin() + long(hi));
+  h.chunk_offset = start;
+  return h;
+}
+
+BtServer::BtServer(const Config& cfg, storage::XorbCache* cache, PieceProvider provider, int port)
+    : cfg_(cfg), cache_(cache), provider_(std::move(provider)) {
+  listener_ = net::Socket::listen_tcp(net::Addr::any(port < 0 ? cfg.listen_port : uint16_t(port)));
+  port_ = listener_.local_addr().port();
+  if (!cfg.fault.empty()) fault_ = FaultSpec::parse(cfg.fault);
+}
+
+BtServer::~BtServer() { stop(); }
+
+void BtServer::start() {
+  stop_ = false;
+  acceptor_ = std::thread([this] { accept_loop(); });
+}
+
+void BtServer::stop() {
+  if (stop_.exchange(true)) return;
+  listener_.shutdown();
+  if (acceptor_.joinable()) acceptor_.join();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
+  }
+  for (auto& t : workers_)
+    if (t.joinable()) t.join();
+  listener_.close();  // closed exactly once (server.zig double-closes)
+}
+
+ServerStats BtServer::stats() const {
+  ServerStats s;
+  s.active_peers = active_.load();
+  s.total_peers = total_.load();
+  s.chunks_served = served_.load();
+  s.bytes_served = bytes_.load();
+  s.not_found = nf_.load();
+  return s;
+}
+
+void BtServer::accept_loop() {
+  while (!stop_) {
+    net::Addr peer;
+    net::Socket s;
+    try {
+      s = listener_.accept(200, &peer);
+    } catch (const Error&) {
+      if (stop_) return;
+      continue;
+    }
+    if (!s.valid()) continue;
+    std::lock_guard<std::mutex> g(mu_);
+    conns_.insert(s.fd());
+    workers_.emplace_back([this, sock = std::move(s), peer]() mutable {
+      const int fd = sock.fd();
+      try {
+        handle(std::move(sock), peer);
+      } catch (...) {
+      }
+      std::lock_guard<std::mutex> g2(mu_);
+      conns_.erase(fd);
+    });
+  }
+}
+
+std::optional<storage::CacheHit> BtServer::lookup(const std::array<uint8_t, 32>& hash, uint32_t start, uint32_t end) {
+  xet::Hash h;
+  std::memcpy(h.data(), hash.data(), 32);
+  const std::string hex = xet::to_hex(h);
+  if (provider_) {
+    if (auto hit = provider_(hash, hex, start, end)) return hit;
+  }
+  if (!cache_) return std::nullopt;
+  auto hit = cache_->get_with_range(hex, start);
+  if (!hit) return std::nullopt;
+  if (hit->chunk_offset == 0 && (start != 0 || end != 0)) {
+    try {
+      if (auto s = slice_chunks(hit->data, 0, start, end)) return s;
+    } catch (const Error&) {
+    }
+  }
+  return hit;
+}
+
+void BtServer::handle(net::Socket s, net::Addr peer) {
+  (void)peer;
+  active_++;
+  total_++;
+  struct Dec {
+    std::atomic<uint64_t>& a;
+    ~Dec() { a--; }
+  } dec{active_};
+  s.set_timeout(cfg_.io_timeout_ms);
+  s.set_buffers(8 << 20);
+  uint8_t hs[kHandshakeLen];
+  s.read_exact(hs, kHandshakeLen);
+  Handshake theirs = parse_handshake(hs);
+  Bytes out;
+  write_handshake(out, theirs.info_hash, cfg_.peer_id);
+  const std::string ext = bep_xet::make_ext_handshake(cfg_.listen_port);
+  Bytes p(1 + ext.size());
+  p[0] = 0;
+  std::memcpy(p.data() + 1, ext.data(), ext.size());
+  write_message(out, kExtended, p.data(), p.size());
+  write_message(out, kUnchoke);
+  write_message(out, kInterested);
+  s.write_all(out.data(), out.size());
+  int peer_xet = 1;  // until the peer tells us otherwise
+  std::mt19937_64 rng(std::random_device{}());
+  std::uniform_real_distribution<double> u01(0, 1);
+  Bytes frame;
+  while (!stop_) {
+    if (!s.wait_readable(200)) continue;
+    uint8_t lenb[4];
+    s.read_exact(lenb, 4);
+    const uint32_t len = load_be32(lenb);
+    if (len > kMaxMessage) return;
+    frame.resize(4 + size_t(len));
+    std::memcpy(frame.data(), lenb, 4);
+    if (len) s.read_exact(frame.data() + 4, len);
+    Message m;
+    parse_message(frame.data(), frame.size(), m);  // unknown ids throw -> connection closed
+    if (m.keepalive || m.id != kExtended) continue;
+    Extended e = parse_extended(m.payload);
+    if (e.ext_id == 0) {
+      auto caps = bep_xet::parse_ext_handshake(e.data);
+      if (caps.ut_xet_id > 0) peer_xet = caps.ut_xet_id;
+      continue;
+    }
+    bep_xet::Message x = bep_xet::decode(e.data);
+    if (x.type != bep_xet::kChunkRequest) continue;
+    if (fault_.delay_ms) std::this_thread::sleep_for(std::chrono::milliseconds(fault_.delay_ms));
+    if (fault_.drop > 0 && u01(rng) < fault_.drop) return;  // injected connection drop
+    auto hit = lookup(x.hash, x.range_start, x.range_end);
+    out.clear();
+    if (!hit) {
+      nf_++;
+      bep_xet::encode_chunk_not_found(out, uint8_t(peer_xet), x.request_id, x.hash.data());
+      s.write_all(out.data(), out.size());
+      continue;
+    }
+    if (fault_.corrupt > 0 && u01(rng) < fault_.corrupt && !hit->data.empty()) hit->data[hit->data.size() / 2] ^= 0x5A;
+    bep_xet::encode_chunk_response_header(out, uint8_t(peer_xet), x.request_id, hit->chunk_offset,
+                                          uint32_t(hit->data.size()));
+    iovec iov[2] = {{out.data(), out.size()}, {hit->data.data(), hit->data.size()}};
+    s.writev_all(iov, 2);
+    served_++;
+    bytes_ += hit->data.size();
+  }
+}
+
+}  // namespace zest::bt

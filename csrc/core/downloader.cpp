@@ -1,0 +1,202 @@
+#include "downloader.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "storage.h"
+#include "xorb.h"
+
+namespace zest {
+
+namespace {
+
+constexpr char kResumeMagic[4] = {'Z', 'R', 'S', '1'};
+
+struct Sidecar {
+  int fd = -1;
+  std::mutex mu;
+  ~Sidecar() {
+    if (fd >= 0) ::close(fd);
+  }
+  void append(uint32_t term, const std::vector<xet::HashSize>& hs) {
+    Bytes rec(8 + hs.size() * 40);
+    store_le32(rec.data(), term);
+    store_le32(rec.data() + 4, uint32_t(hs.size()));
+    for (size_t i = 0; i < hs.size(); ++i) {
+      std::memcpy(rec.data() + 8 + 40 * i, hs[i].hash.data(), 32);
+      store_le64(rec.data() + 8 + 40 * i + 32, hs[i].size);
+    }
+    std::lock_guard<std::mutex> g(mu);
+    if (::write(fd, rec.data(), rec.size()) != ssize_t(rec.size())) throw Error("IoError", "resume sidecar");
+  }
+};
+
+void pwrite_all(int fd, const uint8_t* p, size_t n, uint64_t off) {
+  while (n) {
+    ssize_t w = ::pwrite(fd, p, n, off_t(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw Error("IoError", std::string("pwrite: ") + std::strerror(errno));
+    }
+    p += w;
+    n -= size_t(w);
+    off += uint64_t(w);
+  }
+}
+
+}  // namespace
+
+FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const std::string& out_path, bool verify) {
+  const auto t0 = std::chrono::steady_clock::now();
+  cas::Reconstruction rec = bridge_.get_reconstruction(hex);
+  const size_t n = rec.terms.size();
+  std::vector<uint64_t> offs(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) offs[i + 1] = offs[i] + rec.terms[i].unpacked_length;
+  const uint64_t skip = rec.offset_into_first_range;
+  const uint64_t total = offs[n] - skip;
+  const size_t slash = out_path.rfind('/');
+  if (slash != std::string::npos) storage::ensure_dir(out_path.substr(0, slash));
+  const std::string tmp = out_path + ".incomplete";
+  const std::string side = out_path + ".zest-resume";
+
+  std::vector<std::vector<xet::HashSize>> hashes(n);
+  std::vector<uint8_t> done(n, 0);
+  size_t resumed = 0;
+  // ---- resume from sidecar
+  if (storage::exists(tmp) && storage::exists(side)) {
+    if (auto b = storage::read_file(side); b && b->size() >= 4 + 64 + 4 && std::memcmp(b->data(), kResumeMagic, 4) == 0 &&
+                                         std::string(reinterpret_cast<char*>(b->data()) + 4, 64) == hex &&
+                                         load_le32(b->data() + 68) == n) {
+      size_t p = 72;
+      while (p + 8 <= b->size()) {
+        const uint32_t t = load_le32(b->data() + p), k = load_le32(b->data() + p + 4);
+        if (t >= n || p + 8 + size_t(k) * 40 > b->size()) break;
+        std::vector<xet::HashSize> hs(k);
+        for (uint32_t i = 0; i < k; ++i) {
+          std::memcpy(hs[i].hash.data(), b->data() + p + 8 + 40 * i, 32);
+          hs[i].size = load_le64(b->data() + p + 8 + 40 * i + 32);
+        }
+        hashes[t] = std::move(hs);
+        if (!done[t]) ++resumed;
+        done[t] = 1;
+        p += 8 + size_t(k) * 40;
+      }
+    }
+  }
+  if (!resumed) storage::remove_file(side);
+  int fd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+  if (fd < 0) throw Error("IoError", tmp + ": " + std::strerror(errno));
+  if (::ftruncate(fd, off_t(total)) != 0) {
+    ::close(fd);
+    throw Error("IoError", "ftruncate");
+  }
+  Sidecar sc;
+  const bool fresh = !storage::exists(side);
+  sc.fd = ::open(side.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+  if (sc.fd >= 0 && fresh) {
+    Bytes h(72);
+    std::memcpy(h.data(), kResumeMagic, 4);
+    std::memcpy(h.data() + 4, hex.data(), 64);
+    store_le32(h.data() + 68, uint32_t(n));
+    if (::write(sc.fd, h.data(), h.size()) != 72) throw Error("IoError", "resume header");
+  }
+
+  std::vector<Source> src(n, Source::Cdn);
+  std::vector<std::string> peer(n);
+  std::atomic<size_t> next{0};
+  std::atomic<bool> failed{false};
+  std::string first_err;
+  std::mutex err_mu;
+
+  auto do_term = [&](size_t i, bool allow_p2p, bool allow_cache) {
+    const cas::Term& t = rec.terms[i];
+    XorbFetchResult f = bridge_.fetch_term(t, rec, allow_p2p, allow_cache);
+    Bytes out;
+    std::vector<xet::HashSize> hs;
+    xet::extract_chunk_range(f.data.data(), f.data.size(), f.local_start, f.local_end, out, &hs);
+    if (out.size() != t.unpacked_length) throw Error("SizeMismatch", "term " + std::to_string(i));
+    uint64_t off = offs[i], a = 0;
+    if (off < skip) {  // only the first term can straddle offset_into_first_range
+      a = std::min<uint64_t>(skip - off, out.size());
+      off = skip;
+    }
+    pwrite_all(fd, out.data() + a, out.size() - a, off - skip);
+    hashes[i] = std::move(hs);
+    src[i] = f.source;
+    peer[i] = f.peer;
+  };
+
+  auto worker = [&]() {
+    while (!failed.load()) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      if (done[i]) continue;
+      try {
+        do_term(i, true, true);
+        if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
+      } catch (const std::exception& e) {
+        // A peer/cache copy that does not decode: retry straight from the CDN once.
+        try {
+          if (src[i] != Source::Cdn && !peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
+          do_term(i, false, false);
+          if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
+        } catch (const std::exception& e2) {
+          std::lock_guard<std::mutex> g(err_mu);
+          if (first_err.empty()) first_err = e2.what();
+          failed = true;
+        }
+      }
+    }
+  };
+  const int nthreads = std::max(1, std::min<int>(concurrency_, int(n)));
+  std::vector<std::thread> ts;
+  for (int k = 0; k < nthreads; ++k) ts.emplace_back(worker);
+  for (auto& t : ts) t.join();
+  if (failed) {
+    ::close(fd);
+    throw Error("DownloadFailed", first_err);
+  }
+  bool ok = true;
+  if (verify) {
+    auto file_hash_now = [&]() {
+      std::vector<xet::HashSize> leaves;
+      for (auto& h : hashes) leaves.insert(leaves.end(), h.begin(), h.end());
+      return xet::to_hex(xet::file_hash(leaves));
+    };
+    ok = file_hash_now() == hex;
+    if (!ok) {
+      bridge_.stats().verify_failures++;
+      for (size_t i = 0; i < n; ++i) {
+        if (src[i] == Source::Cdn) continue;
+        if (!peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
+        do_term(i, false, false);
+        bridge_.stats().refetches++;
+      }
+      ok = file_hash_now() == hex;
+    }
+    if (!ok) {
+      ::close(fd);
+      storage::remove_file(side);
+      throw Error("HashMismatch", "file " + hex);
+    }
+  }
+  ::fdatasync(fd);
+  ::close(fd);
+  if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);
+  storage::remove_file(side);
+  FileResult r;
+  r.bytes = total;
+  r.terms = n;
+  r.resumed_terms = resumed;
+  r.verified = verify && ok;
+  r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+}  // namespace zest

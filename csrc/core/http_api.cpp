@@ -1,0 +1,211 @@
+#include "http_api.h"
+
+#include <dirent.h>
+
+#include <chrono>
+#include <sstream>
+
+#include "json.h"
+#include "pull.h"
+
+namespace zest {
+
+ApiServer::ApiServer(Config& cfg, bt::BtServer* bt, storage::XorbRegistry* registry, std::string self_exe)
+    : cfg_(cfg), bt_(bt), registry_(registry), self_exe_(std::move(self_exe)) {
+  started_ = std::chrono::steady_clock::now();
+  server_ = std::make_unique<http::Server>(net::Addr::loopback(cfg.http_port),
+                                           [this](const http::Request& r) { return route(r); }, 8);
+}
+
+ApiServer::~ApiServer() {
+  stop();
+  for (auto& t : job_threads_)
+    if (t.joinable()) t.join();
+}
+
+void ApiServer::start() { server_->start(); }
+
+void ApiServer::run_until_stopped() {
+  start();
+  while (!stop_.load()) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  server_->stop();
+}
+
+void ApiServer::stop() { stop_.store(true); }
+
+std::string ApiServer::status_json() const {
+  bt::ServerStats s = bt_ ? bt_->stats() : bt::ServerStats{};
+  json::Writer w;
+  w.obj();
+  w.key("version").str(kVersion);
+  w.key("bt_peers").num_u(s.active_peers);
+  w.key("chunks_served").num_u(s.chunks_served);
+  w.key("xorbs_cached").num_u(registry_ ? registry_->count() : 0);
+  w.key("http_requests").num_u(server_ ? server_->requests() : 0);
+  w.key("http_port").num(int64_t(cfg_.http_port));
+  w.key("bt_port").num(int64_t(bt_ ? bt_->port() : cfg_.listen_port));
+  w.key("bytes_served").num_u(s.bytes_served);
+  w.key("total_peers").num_u(s.total_peers);
+  w.key("not_found").num_u(s.not_found);
+  w.key("uptime_s").num(std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count(), 1);
+  w.key("peer_id").str(std::string(reinterpret_cast<const char*>(cfg_.peer_id.data()), 8));
+  if (extra_) w.key("device").raw(extra_());
+  w.end();
+  return w.out();
+}
+
+std::string ApiServer::models_json() const {
+  json::Writer w;
+  w.arr();
+  DIR* d = ::opendir(cfg_.hf_cache_dir.c_str());
+  if (d) {
+    while (dirent* e = ::readdir(d)) {
+      std::string name = e->d_name;
+      if (name.rfind("models--", 0) != 0 || name.size() == 8) continue;
+      std::string raw = name.substr(8);
+      size_t sep = raw.find("--");
+      std::string repo = sep == std::string::npos ? raw : raw.substr(0, sep) + "/" + raw.substr(sep + 2);
+      size_t files = 0;
+      std::string snaps = cfg_.hf_cache_dir + "/" + name + "/snapshots";
+      if (DIR* sd = ::opendir(snaps.c_str())) {
+        while (dirent* s = ::readdir(sd)) {
+          std::string sn = s->d_name;
+          if (sn == "." || sn == "..") continue;
+          if (DIR* fd = ::opendir((snaps + "/" + sn).c_str())) {
+            while (dirent* f = ::readdir(fd)) {
+              std::string fn = f->d_name;
+              if (fn != "." && fn != "..") ++files;
+            }
+            ::closedir(fd);
+          }
+          break;  // first snapshot, like the reference
+        }
+        ::closedir(sd);
+      }
+      w.obj().key("name").str(repo).key("files").num(int64_t(files)).end();
+    }
+    ::closedir(d);
+  }
+  w.end();
+  return w.out();
+}
+
+http::ServerResponse ApiServer::route(const http::Request& r) {
+  http::ServerResponse resp;
+  const std::string& p = r.path;
+  if (p == "/v1/health") {
+    resp.body = "{\"status\":\"ok\"}";
+  } else if (p == "/v1/status") {
+    resp.body = status_json();
+  } else if (p == "/v1/stop") {
+    resp.body = "{\"status\":\"shutting down\"}";
+    stop();
+    if (bt_) std::thread([bt = bt_] { bt->stop(); }).detach();
+  } else if (p == "/v1/models") {
+    resp.body = models_json();
+  } else if (p == "/v1/config") {
+    resp.body = cfg_.to_json();
+  } else if (p == "/v1/pull" && r.method == "POST") {
+    json::Value body = r.body.empty() ? json::Value() : json::Value::parse(r.body);
+    auto job = std::make_shared<PullJob>();
+    job->repo = body.str_or("repo", "");
+    job->revision = body.str_or("revision", "main");
+    if (job->repo.empty()) {
+      resp.status = 400;
+      resp.body = "{\"error\":\"missing repo\"}";
+      return resp;
+    }
+    PullOptions opt;
+    opt.repo_id = job->repo;
+    opt.revision = job->revision;
+    opt.p2p = !(body["no_p2p"].type() == json::Value::Type::Bool && body["no_p2p"].as_bool());
+    opt.autostart_server = false;
+    for (auto& pe : body["peers"].array())
+      if (pe.is_string()) opt.peers.push_back(pe.as_string());
+    {
+      std::lock_guard<std::mutex> g(jobs_mu_);
+      job->id = std::to_string(jobs_.size() + 1);
+      jobs_[job->id] = job;
+    }
+    job_threads_.emplace_back([this, job, opt] {
+      job->state = "running";
+      std::ostringstream out, err;
+      try {
+        Config c = cfg_;
+        PullSummary s = run_pull(c, opt, out, err);
+        job->snapshot = s.snapshot_dir;
+        job->stats_json = s.stats_json;
+        job->state = "done";
+        job->progress = 1.0;
+        if (registry_) registry_->scan(cfg_);
+      } catch (const std::exception& e) {
+        job->state = "error";
+        job->error = e.what();
+      }
+      job->log = out.str() + err.str();
+    });
+    resp.body = "{\"status\":\"started\",\"job\":\"" + job->id + "\"}";
+  } else if (p.rfind("/v1/pull", 0) == 0) {
+    std::string id = p.size() > 9 ? p.substr(9) : "";
+    std::shared_ptr<PullJob> job;
+    {
+      std::lock_guard<std::mutex> g(jobs_mu_);
+      auto it = jobs_.find(id);
+      if (it != jobs_.end()) job = it->second;
+    }
+    if (!job) {
+      resp.status = 404;
+      resp.body = "{\"error\":\"no such pull job\"}";
+    } else {
+      json::Writer w;
+      w.obj().key("job").str(job->id).key("repo").str(job->repo).key("revision").str(job->revision);
+      w.key("state").str(job->state).key("progress").num(job->progress, 2).key("snapshot").str(job->snapshot);
+      w.key("error").str(job->error).key("stats").raw(job->stats_json).key("log").str(job->log).end();
+      resp.body = w.out();
+    }
+  } else if (p == "/metrics") {
+    bt::ServerStats s = bt_ ? bt_->stats() : bt::ServerStats{};
+    std::ostringstream m;
+    m << "# TYPE zest_chunks_served_total counter\nzest_chunks_served_total " << s.chunks_served << "\n";
+    m << "# TYPE zest_bytes_served_total counter\nzest_bytes_served_total " << s.bytes_served << "\n";
+    m << "# TYPE zest_bt_peers gauge\nzest_bt_peers " << s.active_peers << "\n";
+    m << "# TYPE zest_xorbs_cached gauge\nzest_xorbs_cached " << (registry_ ? registry_->count() : 0) << "\n";
+    m << "# TYPE zest_http_requests_total counter\nzest_http_requests_total " << server_->requests() << "\n";
+    resp.content_type = "text/plain; version=0.0.4";
+    resp.body = m.str();
+  } else if (p == "/" || p == "/ui") {
+    resp.content_type = "text/html; charset=utf-8";
+    resp.body = kDashboardHtml;
+  } else {
+    resp.status = 404;
+    resp.body = "{\"error\":\"not found\"}";
+  }
+  return resp;
+}
+
+const char* kDashboardHtml = R"HTML(<!doctype html>
+<html><head><meta charset="utf-8"><title>zest (MI355X)</title>
+<style>
+body{font:14px system-ui,sans-serif;background:#0f1115;color:#e6e6e6;margin:2rem}
+h1{font-size:20px} .grid{display:grid;grid-template-columns:repeat(auto-fill,minmax(180px,1fr));gap:12px}
+.card{background:#1a1d24;border-radius:8px;padding:12px}.k{color:#8a93a6;font-size:12px}.v{font-size:22px}
+table{border-collapse:collapse;margin-top:1rem;width:100%}td,th{border-bottom:1px solid #2a2f3a;padding:6px;text-align:left}
+button{background:#c0392b;color:#fff;border:0;border-radius:6px;padding:6px 14px;cursor:pointer}
+</style></head><body>
+<h1>zest &mdash; P2P model distribution on AMD Instinct</h1>
+<div class="grid" id="cards"></div>
+<table><thead><tr><th>model</th><th>files</th></tr></thead><tbody id="models"></tbody></table>
+<p><button onclick="fetch('/v1/stop',{method:'POST'}).then(()=>document.title='stopped')">Stop server</button></p>
+<script>
+const keys=["version","bt_peers","chunks_served","bytes_served","xorbs_cached","http_requests","bt_port","uptime_s"];
+async function tick(){
+ try{const s=await (await fetch('/v1/status')).json();
+  document.getElementById('cards').innerHTML=keys.map(k=>`<div class="card"><div class="k">${k}</div><div class="v">${s[k]}</div></div>`).join('');
+  const m=await (await fetch('/v1/models')).json();
+  document.getElementById('models').innerHTML=m.map(x=>`<tr><td>${x.name}</td><td>${x.files}</td></tr>`).join('');
+ }catch(e){}
+}
+tick();setInterval(tick,2000);
+</script></body></html>)HTML";
+
+}  // namespace zest

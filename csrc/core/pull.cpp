@@ -1,0 +1,163 @@
+#include "pull.h"
+
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <iomanip>
+
+#include "bridge.h"
+#include "downloader.h"
+#include "http.h"
+#include "hub.h"
+#include "storage.h"
+#include "swarm.h"
+
+extern char** environ;
+
+namespace zest {
+
+bool server_healthy(uint16_t http_port, int timeout_ms) {
+  try {
+    http::RequestOptions o;
+    o.timeout_ms = timeout_ms;
+    o.max_redirects = 0;
+    auto r = http::get("http://127.0.0.1:" + std::to_string(http_port) + "/v1/health", {}, o);
+    return r.status == 200;
+  } catch (const Error&) {
+    return false;
+  }
+}
+
+bool spawn_background_server(const std::string& self_exe, uint16_t http_port) {
+  if (server_healthy(http_port, 300)) return true;
+  std::string port = std::to_string(http_port);
+  const char* argv[] = {self_exe.c_str(), "serve", "--http-port", port.c_str(), nullptr};
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+  posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);
+  posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
+  posix_spawnattr_t at;
+  posix_spawnattr_init(&at);
+  posix_spawnattr_setflags(&at, POSIX_SPAWN_SETSID);
+  pid_t pid = 0;
+  int rc = posix_spawn(&pid, self_exe.c_str(), &fa, &at, const_cast<char* const*>(argv), environ);
+  posix_spawn_file_actions_destroy(&fa);
+  posix_spawnattr_destroy(&at);
+  return rc == 0;
+}
+
+PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std::ostream& err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  PullSummary S;
+  out << "zest pull " << opt.repo_id << " (revision: " << opt.revision << ")\n";
+  if (!cfg.hf_token) err << "Warning: no HuggingFace token found. Set HF_TOKEN or run `huggingface-cli login`.\n";
+  if (opt.p2p) out << "P2P enabled (peer_id: " << peer_id::kClientPrefix << "...)\n";
+  else out << "P2P disabled (CDN only)\n";
+  out << "Fetching model info from HuggingFace Hub...\n" << std::flush;
+  std::vector<hub::RepoFile> files = hub::list_files(cfg, opt.repo_id, opt.revision, opt.repo_type);
+  if (!opt.include.empty()) {
+    std::vector<hub::RepoFile> keep;
+    for (auto& f : files)
+      for (auto& suf : opt.include)
+        if (f.path.size() >= suf.size() && f.path.compare(f.path.size() - suf.size(), suf.size(), suf) == 0) {
+          keep.push_back(f);
+          break;
+        }
+    files.swap(keep);
+  }
+  auto sha = hub::resolve_commit(cfg, opt.repo_id, opt.revision, opt.repo_type);
+  S.commit = sha ? *sha : opt.revision;
+  if (sha) out << "Found " << files.size() << " files (revision: " << opt.revision << " \xE2\x86\x92 " << S.commit << ")\n";
+  else out << "Found " << files.size() << " files (revision: " << opt.revision << ")\n";
+  out << "Detecting Xet-backed files...\n";
+  for (auto& f : files)
+    if (f.xet_hash) S.xet_files++;
+  out << "  " << S.xet_files << " Xet-backed files, " << files.size() << " total files\n";
+  S.files = files.size();
+
+  std::vector<net::Addr> boot;
+  for (auto& b : opt.dht_bootstrap) {
+    try {
+      boot.push_back(net::Addr::parse(b, 6881));
+    } catch (const Error&) {
+      err << "Warning: invalid DHT bootstrap node: " << b << "\n";
+    }
+  }
+  storage::XorbRegistry registry;
+  storage::XorbCache cache(cfg, &registry);
+  SwarmDownloader swarm(cfg, opt.tracker, opt.p2p, opt.dht && opt.p2p, boot);
+  for (auto& p : opt.peers) {
+    try {
+      swarm.add_direct_peer(net::Addr::parse(p, 6881));
+      out << "  Direct peer: " << p << "\n";
+    } catch (const Error&) {
+      err << "Warning: invalid peer address: " << p << "\n";
+    }
+  }
+  XetBridge bridge(cfg, &cache, &swarm);
+  if (S.xet_files > 0) {
+    out << "Authenticating with Xet CAS...\n" << std::flush;
+    try {
+      bridge.authenticate(opt.repo_id, opt.repo_type, opt.revision);
+    } catch (const Error& e) {
+      err << "Warning: Xet auth failed (" << e.what() << ")\n";
+    }
+  }
+  ParallelDownloader dl(bridge, opt.concurrency > 0 ? opt.concurrency : int(cfg.concurrency));
+  S.snapshot_dir = cfg.snapshot_dir(opt.repo_id, S.commit);
+  size_t k = 0;
+  for (auto& f : files) {
+    ++k;
+    out << "[" << k << "/" << files.size() << "] " << f.path;
+    const std::string dst = S.snapshot_dir + "/" + f.path;
+    if (storage::exists(dst) && (f.size == 0 || storage::file_size(dst) == f.size)) {
+      out << " (cached)\n";
+      S.cached_files++;
+      continue;
+    }
+    if (f.xet_hash) {
+      out << " [xet]\n" << std::flush;
+      if (!bridge.authenticated()) {
+        err << "  Error downloading via xet: not authenticated\n";
+        continue;
+      }
+      try {
+        FileResult r = dl.reconstruct_to_file(*f.xet_hash, dst, opt.verify);
+        S.bytes += r.bytes;
+        if (r.resumed_terms) out << "  resumed " << r.resumed_terms << "/" << r.terms << " terms\n";
+      } catch (const Error& e) {
+        err << "  Parallel download error (" << e.what() << ")\n";
+        continue;
+      }
+    } else {
+      out << " [regular]\n" << std::flush;
+      try {
+        S.bytes += hub::download_regular(cfg, opt.repo_id, S.commit == opt.revision ? opt.revision : S.commit, f.path, dst);
+      } catch (const Error& e) {
+        err << "  Error downloading: " << e.what() << "\n";
+        continue;
+      }
+    }
+  }
+  try {
+    storage::write_ref(cfg, opt.repo_id, opt.revision, S.commit);
+  } catch (const Error& e) {
+    err << "Warning: failed to write ref: " << e.what() << "\n";
+  }
+  bridge.print_stats(out);
+  swarm.print_stats(out);
+  S.bytes_from_peer = bridge.stats().bytes_from_peer;
+  S.bytes_from_cdn = bridge.stats().bytes_from_cdn;
+  S.bytes_from_cache = bridge.stats().bytes_from_cache;
+  S.stats_json = bridge.stats_json();
+  S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  out << "\nDone! Model available at:\n  " << S.snapshot_dir << "\n";
+  out << "\nRun: transformers.AutoModel.from_pretrained(\"" << opt.repo_id << "\")\n" << std::flush;
+  return S;
+}
+
+}  // namespace zest

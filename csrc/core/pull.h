@@ -1,0 +1,51 @@
+// `zest pull`: list repo files, resolve the commit, authenticate with Xet CAS, reconstruct every
+// Xet file through the cache -> P2P -> CDN waterfall, download regular files, write the HF cache
+// layout (snapshots/{commit}/..., refs/{revision}) and print the reference's stats block.
+//
+// Reference: src/main.zig:83-305 (cmdPull) with its fallbacks: parallel -> sequential bridge ->
+// opaque CDN download (main.zig:233-256); a file is "(cached)" only if it exists — here cached
+// files must also match their size (a crashed run leaves `.incomplete`, never a final name).
+#pragma once
+
+#include <optional>
+#include <ostream>
+#include <string>
+#include <vector>
+
+#include "config.h"
+#include "net.h"
+
+namespace zest {
+
+struct PullOptions {
+  std::string repo_id;
+  std::string revision = "main";
+  std::string repo_type = "model";
+  std::optional<std::string> tracker;
+  std::vector<std::string> peers;           // --peer ip:port (repeatable)
+  std::vector<std::string> dht_bootstrap;   // --dht-bootstrap host:port
+  bool p2p = true;
+  bool dht = true;
+  bool verify = true;
+  int concurrency = 0;                      // 0 = cfg.concurrency
+  bool autostart_server = true;
+  std::vector<std::string> include;         // optional path filters (suffix match)
+};
+
+struct PullSummary {
+  std::string snapshot_dir;
+  std::string commit;
+  uint64_t bytes = 0;
+  size_t files = 0, xet_files = 0, cached_files = 0;
+  uint64_t bytes_from_peer = 0, bytes_from_cdn = 0, bytes_from_cache = 0;
+  double seconds = 0;
+  std::string stats_json;
+};
+
+PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std::ostream& err);
+
+// Background server helpers shared by the CLI and the HTTP API.
+bool server_healthy(uint16_t http_port, int timeout_ms = 1000);
+bool spawn_background_server(const std::string& self_exe, uint16_t http_port);
+
+}  // namespace zest

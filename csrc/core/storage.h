@@ -1,0 +1,75 @@
+// Filesystem layer: atomic writes, HF cache layout (refs/snapshots), the content-addressed xorb
+// disk cache and the xorb registry (piece map of what this node can seed).
+//
+// Reference: src/storage.zig:1-228 and XorbCache in src/swarm.zig:46-148.  Same on-disk names
+// (xorbs/{hex[0..2]}/{hex} for full xorbs, {hex}.{range_start} for partial entries) but writes are
+// really atomic (tmp + fsync + rename; the reference's writeFileAtomic is not, storage.zig:29-41),
+// the registry is updated on every put (seed-while-downloading) and thread-safe.
+#pragma once
+
+#include <cstdint>
+#include <mutex>
+#include <optional>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "config.h"
+
+namespace zest::storage {
+
+void ensure_dir(const std::string& path);
+bool exists(const std::string& path);
+uint64_t file_size(const std::string& path);  // 0 if missing
+void write_file_atomic(const std::string& path, const uint8_t* data, size_t n);
+inline void write_file_atomic(const std::string& path, const std::string& s) {
+  write_file_atomic(path, reinterpret_cast<const uint8_t*>(s.data()), s.size());
+}
+std::optional<Bytes> read_file(const std::string& path);
+// Read [off, off+n) of a file into out (false if short/missing).
+bool read_range(const std::string& path, uint64_t off, uint64_t n, uint8_t* out);
+void remove_file(const std::string& path);
+
+// HF cache: models--org--name/refs/{ref} = commit
+void write_ref(const Config& cfg, const std::string& repo_id, const std::string& ref, const std::string& commit);
+std::optional<std::string> read_ref(const Config& cfg, const std::string& repo_id, const std::string& ref);
+
+// List 64-char xorb names in the 2-char prefix dirs (partials excluded).
+std::vector<std::string> list_cached_xorbs(const Config& cfg);
+
+struct CacheHit {
+  Bytes data;
+  uint32_t chunk_offset = 0;  // chunk index of data's first chunk inside the xorb
+};
+
+class XorbRegistry {
+ public:
+  void add(const std::string& key);
+  bool has(const std::string& key) const;
+  size_t count() const;
+  void scan(const Config& cfg);
+  std::vector<std::string> keys() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::set<std::string> keys_;
+};
+
+class XorbCache {
+ public:
+  explicit XorbCache(const Config& cfg, XorbRegistry* registry = nullptr) : cfg_(cfg), registry_(registry) {}
+  bool has(const std::string& hex) const;
+  std::optional<Bytes> get(const std::string& hex) const;
+  // Full xorb first (offset 0), then the partial entry {hex}.{range_start}.
+  std::optional<CacheHit> get_with_range(const std::string& hex, uint32_t range_start) const;
+  void put(const std::string& hex, const uint8_t* data, size_t n);
+  void put_partial(const std::string& hex, uint32_t range_start, const uint8_t* data, size_t n);
+  uint64_t bytes_on_disk() const;
+
+ private:
+  const Config& cfg_;
+  XorbRegistry* registry_;
+};
+
+}  // namespace zest::storage

@@ -1,0 +1,157 @@
+#include "swarm.h"
+
+#include <cstring>
+#include <iomanip>
+
+#include "tracker.h"
+
+namespace zest {
+
+SwarmDownloader::SwarmDownloader(const Config& cfg, std::optional<std::string> tracker_url, bool enable_p2p,
+                                 bool enable_dht, std::vector<net::Addr> dht_bootstrap)
+    : cfg_(cfg), enabled_(enable_p2p), tracker_(std::move(tracker_url)) {
+  pool_ = std::make_unique<bt::PeerPool>(cfg.peer_id, cfg.listen_port, cfg.max_peers, cfg.connect_timeout_ms);
+  if (enable_p2p && enable_dht) {
+    dht_ = std::make_unique<dht::Dht>(cfg.dht_port);
+    if (!dht_->has_socket()) dht_ = std::make_unique<dht::Dht>(0);  // port taken: ephemeral
+    dht_->start();
+    if (!dht_bootstrap.empty()) dht_->bootstrap(dht_bootstrap, 1500);
+  }
+}
+
+SwarmDownloader::~SwarmDownloader() {
+  if (dht_) dht_->stop();
+}
+
+void SwarmDownloader::add_direct_peer(const net::Addr& a) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& d : direct_)
+    if (d == a) return;
+  direct_.push_back(a);
+}
+
+std::vector<net::Addr> SwarmDownloader::discover(const Sha1Digest& ih) {
+  const std::string key(reinterpret_cast<const char*>(ih.data()), 20);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = discovered_.find(key);
+    if (it != discovered_.end() &&
+        std::chrono::steady_clock::now() - it->second.at < std::chrono::seconds(cfg_.discovery_ttl_s))
+      return it->second.peers;
+  }
+  std::lock_guard<std::mutex> dg(disc_mu_);  // one discovery at a time (swarm.zig:320-355)
+  std::vector<net::Addr> peers;
+  if (dht_ && dht_->table().size() > 0) {
+    stats_.dht_lookups++;
+    for (auto& p : dht_->get_peers(ih, 2000)) peers.push_back(p);
+  }
+  if (tracker_) {
+    try {
+      stats_.tracker_announces++;
+      auto r = tracker::announce(*tracker_, ih, cfg_.peer_id, cfg_.listen_port, tracker::Event::Started, 5000);
+      for (auto& p : r.peers) peers.push_back(p);
+    } catch (const Error&) {
+    }
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  discovered_[key] = {peers, std::chrono::steady_clock::now()};
+  return peers;
+}
+
+std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash, uint32_t start, uint32_t end) {
+  if (!enabled_) return std::nullopt;
+  const Sha1Digest ih = peer_id::info_hash(hash.data());
+  std::vector<net::Addr> cands;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    cands = direct_;
+  }
+  if (cands.empty() || dht_ || tracker_) {
+    for (auto& p : discover(ih)) {
+      bool dup = false;
+      for (auto& c : cands)
+        if (c == p) dup = true;
+      if (!dup) cands.push_back(p);
+    }
+  }
+  bt::XetRequest req;
+  std::memcpy(req.xorb_hash.data(), hash.data(), 32);
+  req.range_start = start;
+  req.range_end = end;
+  for (const auto& a : cands) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = score_.find(a.str());
+      if (it != score_.end() && it->second >= 3) continue;  // banned / repeatedly failing
+    }
+    try {
+      auto s = pool_->get_or_connect(a, ih);
+      if (!s->supports_xet()) continue;
+      stats_.peers_connected++;
+      bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
+      r.peer = a.str();
+      stats_.peer_xorbs++;
+      stats_.peer_bytes += r.data.size();
+      stats_.total_bytes += r.data.size();
+      stats_.total_xorbs++;
+      if (dht_) {
+        std::thread([this, ih] {
+          try {
+            dht_->announce_peer(ih, cfg_.listen_port, 1000);
+          } catch (...) {
+          }
+        }).detach();
+      }
+      return r;
+    } catch (const Error& e) {
+      stats_.peer_failures++;
+      if (e.code() != "ChunkNotFound" && e.code() != "ChunkError") {
+        pool_->remove(a);
+        std::lock_guard<std::mutex> g(mu_);
+        score_[a.str()]++;
+      }
+    }
+  }
+  return std::nullopt;
+}
+
+void SwarmDownloader::report_bad_peer(const std::string& addr) {
+  try {
+    pool_->remove(net::Addr::parse(addr));
+  } catch (const Error&) {
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  score_[addr] = 1000;
+  stats_.peers_banned++;
+}
+
+void SwarmDownloader::announce(const std::vector<xet::Hash>& xorbs) {
+  for (const auto& h : xorbs) {
+    const Sha1Digest ih = peer_id::info_hash(h.data());
+    if (dht_ && dht_->table().size() > 0) dht_->announce_peer(ih, cfg_.listen_port, 1000);
+    if (tracker_) {
+      try {
+        tracker::announce(*tracker_, ih, cfg_.peer_id, cfg_.listen_port, tracker::Event::Started, 5000);
+        stats_.tracker_announces++;
+      } catch (const Error&) {
+      }
+    }
+  }
+}
+
+void SwarmDownloader::print_stats(std::ostream& w) const {
+  w << "\nDownload stats:\n";
+  w << "  Total xorbs:     " << stats_.total_xorbs.load() << "\n";
+  w << "  From cache:      " << stats_.cached_xorbs.load() << "\n";
+  w << "  From peers:      " << stats_.peer_xorbs.load() << "\n";
+  w << "  From CDN:        " << stats_.cdn_xorbs.load() << "\n";
+  w << "  Total bytes:     " << stats_.total_bytes.load() << "\n";
+  w << "  Peers connected: " << stats_.peers_connected.load() << "\n";
+  w << "  DHT lookups:     " << stats_.dht_lookups.load() << "\n";
+  if (stats_.total_bytes.load() > 0) {
+    const double pct = double(stats_.peer_bytes.load()) / double(stats_.total_bytes.load()) * 100.0;
+    w << "  P2P ratio:       " << std::fixed << std::setprecision(1) << pct << "%\n";
+  }
+}
+
+}  // namespace zest

@@ -1,0 +1,72 @@
+// Swarm orchestration: peer discovery (DHT + tracker, TTL-cached), direct peers, pooled BEP XET
+// fetches, announce/seed bookkeeping and download statistics.
+//
+// Reference: src/swarm.zig:150-486 — SwarmDownloader with DHT, tracker, PeerPool, direct peers,
+// discovered-peer cache with a 30 s TTL (:182-254), discoverPeers (:320-355), sequential
+// tryBtPeerDownload over direct then cached peers (:363-394), tryPooledChunkDownload (:398-437),
+// announceToSwarm (:458-470), printStats (:472-485).  Differences: counters are atomics (the
+// reference mutates stats from concurrent tasks without a lock, SURVEY §5.2 a/b), the cached peer
+// list is copied under the lock before iteration (§5.2 c), peers that time out or serve corrupt
+// data are scored down and skipped, and candidates can be raced (`race` > 1).
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <ostream>
+#include <string>
+#include <vector>
+
+#include "bt_peer.h"
+#include "config.h"
+#include "dht.h"
+#include "storage.h"
+#include "xet_hash.h"
+
+namespace zest {
+
+struct DownloadStats {
+  std::atomic<uint64_t> total_xorbs{0}, cached_xorbs{0}, peer_xorbs{0}, cdn_xorbs{0};
+  std::atomic<uint64_t> total_bytes{0}, peer_bytes{0}, peers_connected{0}, dht_lookups{0}, tracker_announces{0};
+  std::atomic<uint64_t> peer_failures{0}, peers_banned{0};
+};
+
+class SwarmDownloader {
+ public:
+  SwarmDownloader(const Config& cfg, std::optional<std::string> tracker_url, bool enable_p2p,
+                  bool enable_dht = true, std::vector<net::Addr> dht_bootstrap = {});
+  ~SwarmDownloader();
+  void add_direct_peer(const net::Addr& a);
+  bool p2p_enabled() const { return enabled_; }
+  // Fetch chunks [start, end) of xorb `hash` from any peer; nullopt if no peer could serve it.
+  std::optional<bt::ChunkResult> try_peers(const xet::Hash& hash, uint32_t start, uint32_t end);
+  std::vector<net::Addr> discover(const Sha1Digest& info_hash);
+  void announce(const std::vector<xet::Hash>& xorbs);
+  // A peer served bytes that failed verification: ban it for the rest of the session.
+  void report_bad_peer(const std::string& addr);
+  DownloadStats& stats() { return stats_; }
+  void print_stats(std::ostream& os) const;
+  dht::Dht* dht() { return dht_.get(); }
+
+ private:
+  const Config& cfg_;
+  bool enabled_;
+  std::optional<std::string> tracker_;
+  std::unique_ptr<dht::Dht> dht_;
+  std::unique_ptr<bt::PeerPool> pool_;
+  std::vector<net::Addr> direct_;
+  std::mutex mu_;
+  struct Cached {
+    std::vector<net::Addr> peers;
+    std::chrono::steady_clock::time_point at;
+  };
+  std::map<std::string, Cached> discovered_;
+  std::map<std::string, int> score_;  // addr -> failures
+  std::mutex disc_mu_;
+  DownloadStats stats_;
+};
+
+}  // namespace zest
