@@ -1,4 +1,551 @@
-// Bindings for the BitTorrent / HTTP / storage stack (filled in as those layers land).
-#include "bind_extra.h"
+// pybind11 bindings for the native control plane: bencode, BT wire, BEP XET, SHA-1 info-hash,
+// tracker, DHT, BT server / peer client, xorb cache, pull and the synthetic benchmark.
+// Submodules of `zest_amd._core` so Python code reads `_core.bencode.decode(...)` etc.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
-void bind_extra(pybind11::module_& m) { (void)m; }
+#include <cstring>
+#include <memory>
+#include <sstream>
+
+#include "bench.h"
+#include "bencode.h"
+#include "bind_extra.h"
+#include "bt_peer.h"
+#include "bt_server.h"
+#include "bt_wire.h"
+#include "config.h"
+#include "dht.h"
+#include "pull.h"
+#include "sha1.h"
+#include "storage.h"
+#include "tracker.h"
+#include "xet_hash.h"
+
+namespace py = pybind11;
+using namespace zest;
+
+namespace {
+
+py::bytes pyb(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
+py::bytes pyb(const Bytes& b) { return pyb(b.data(), b.size()); }
+py::bytes pyb(std::string_view s) { return pyb(s.data(), s.size()); }
+py::bytes pyb(ByteSpan s) { return pyb(s.data, s.size); }
+
+template <size_t N>
+std::array<uint8_t, N> arr_of(const py::bytes& b, const char* what) {
+  std::string s = b;
+  if (s.size() != N) throw Error("InvalidLength", std::string(what) + " must be " + std::to_string(N) + " bytes");
+  std::array<uint8_t, N> a;
+  std::memcpy(a.data(), s.data(), N);
+  return a;
+}
+
+// ---- bencode <-> Python
+py::object bdecode_ref(bencode::Ref r) {
+  switch (r.type()) {
+    case bencode::Type::Int:
+      return py::int_(r.as_int());
+    case bencode::Type::Str:
+      return pyb(r.as_str());
+    case bencode::Type::List: {
+      py::list l;
+      for (auto& c : r.children()) l.append(bdecode_ref(c));
+      return l;
+    }
+    case bencode::Type::Dict: {
+      py::dict d;
+      for (auto& c : r.children()) d[pyb(c.key())] = bdecode_ref(c);
+      return d;
+    }
+  }
+  return py::none();
+}
+
+void bencode_obj(bencode::Encoder& e, const py::handle& o) {
+  if (py::isinstance<py::bool_>(o)) {
+    e.integer(o.cast<bool>() ? 1 : 0);
+  } else if (py::isinstance<py::int_>(o)) {
+    e.integer(o.cast<int64_t>());
+  } else if (py::isinstance<py::bytes>(o)) {
+    e.str(std::string(o.cast<py::bytes>()));
+  } else if (py::isinstance<py::str>(o)) {
+    e.str(o.cast<std::string>());
+  } else if (py::isinstance<py::list>(o) || py::isinstance<py::tuple>(o)) {
+    e.begin_list();
+    for (auto item : o) bencode_obj(e, item);
+    e.end();
+  } else if (py::isinstance<py::dict>(o)) {
+    std::vector<std::pair<std::string, py::handle>> items;
+    for (auto kv : o.cast<py::dict>()) {
+      std::string k = py::isinstance<py::bytes>(kv.first) ? std::string(kv.first.cast<py::bytes>())
+                                                         : kv.first.cast<std::string>();
+      items.emplace_back(std::move(k), kv.second);
+    }
+    std::sort(items.begin(), items.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    e.begin_dict();
+    for (auto& [k, v] : items) {
+      e.key(k);
+      bencode_obj(e, v);
+    }
+    e.end();
+  } else {
+    throw Error("InvalidFormat", "cannot bencode object of this type");
+  }
+}
+
+py::dict xet_msg_dict(const bep_xet::Message& m) {
+  py::dict d;
+  d["type"] = int(m.type);
+  d["request_id"] = m.request_id;
+  switch (m.type) {
+    case bep_xet::kChunkRequest:
+      d["hash"] = pyb(m.hash.data(), 32);
+      d["range_start"] = m.range_start;
+      d["range_end"] = m.range_end;
+      break;
+    case bep_xet::kChunkResponse:
+      d["chunk_offset"] = m.chunk_offset;
+      d["data"] = pyb(m.data);
+      break;
+    case bep_xet::kChunkNotFound:
+      d["hash"] = pyb(m.hash.data(), 32);
+      break;
+    case bep_xet::kChunkError:
+      d["error_code"] = m.error_code;
+      d["message"] = pyb(m.data);
+      break;
+  }
+  return d;
+}
+
+std::vector<std::string> addr_strs(const std::vector<net::Addr>& v) {
+  std::vector<std::string> out;
+  for (auto& a : v) out.push_back(a.str());
+  return out;
+}
+
+// Python-owned BT seeder: a cache + registry + server bundled together.
+struct PySeeder {
+  Config cfg;
+  storage::XorbRegistry registry;
+  std::unique_ptr<storage::XorbCache> cache;
+  std::unique_ptr<bt::BtServer> server;
+  PySeeder(int port, const std::string& fault) : cfg(Config::from_env()) {
+    registry.scan(cfg);
+    cache = std::make_unique<storage::XorbCache>(cfg, &registry);
+    server = std::make_unique<bt::BtServer>(cfg, cache.get(), bt::PieceProvider{}, port);
+    if (!fault.empty()) server->set_fault(bt::FaultSpec::parse(fault));
+    server->start();
+  }
+  ~PySeeder() { server->stop(); }
+};
+
+}  // namespace
+
+void bind_extra(py::module_& m) {
+  // ---------------- bencode ----------------
+  auto mb = m.def_submodule("bencode", "BEP 3 bencode (strict decoder, canonical encoder)");
+  mb.def("decode", [](py::bytes b) {
+    std::string s = b;
+    bencode::Document doc;
+    doc.parse(s);
+    return bdecode_ref(doc.root());
+  });
+  mb.def("decode_prefix", [](py::bytes b) {
+    std::string s = b;
+    bencode::Document doc;
+    size_t used = doc.parse(s);
+    return py::make_tuple(bdecode_ref(doc.root()), used);
+  });
+  mb.def("encode", [](py::object o) {
+    std::string out;
+    bencode::Encoder e(out);
+    bencode_obj(e, o);
+    return pyb(out);
+  });
+  mb.def("roundtrip", [](py::bytes b) {
+    std::string s = b;
+    bencode::Document doc;
+    doc.parse(s);
+    return pyb(bencode::encode(doc.root()));
+  });
+
+  // ---------------- SHA-1 / peer id ----------------
+  m.def("sha1", [](py::bytes b) {
+    std::string s = b;
+    auto d = Sha1::hash(s.data(), s.size());
+    return pyb(d.data(), d.size());
+  });
+  m.def("sha1_backend", []() { return std::string(Sha1::backend()); });
+  m.def("info_hash", [](py::bytes xorb_hash) {
+    auto h = arr_of<32>(xorb_hash, "xorb hash");
+    auto d = peer_id::info_hash(h.data());
+    return pyb(d.data(), d.size());
+  });
+  m.def("generate_peer_id", []() {
+    auto p = peer_id::generate();
+    return pyb(p.data(), p.size());
+  });
+  m.attr("CLIENT_PREFIX") = std::string(peer_id::kClientPrefix);
+  m.attr("VERSION") = std::string(kVersion);
+
+  // ---------------- BT wire ----------------
+  auto mw = m.def_submodule("bt", "BitTorrent wire protocol (BEP 3 + BEP 10)");
+  mw.attr("HANDSHAKE_LEN") = bt::kHandshakeLen;
+  mw.attr("MAX_MESSAGE") = bt::kMaxMessage;
+  mw.def("handshake", [](py::bytes ih, py::bytes pid) {
+    Bytes out;
+    bt::write_handshake(out, arr_of<20>(ih, "info_hash"), arr_of<20>(pid, "peer_id"));
+    return pyb(out);
+  });
+  mw.def("parse_handshake", [](py::bytes b) {
+    std::string s = b;
+    if (s.size() < bt::kHandshakeLen) throw Error("UnexpectedEnd", "handshake needs 68 bytes");
+    auto h = bt::parse_handshake(reinterpret_cast<const uint8_t*>(s.data()));
+    py::dict d;
+    d["reserved"] = pyb(h.reserved.data(), 8);
+    d["info_hash"] = pyb(h.info_hash.data(), 20);
+    d["peer_id"] = pyb(h.peer_id.data(), 20);
+    d["bep10"] = h.supports_bep10();
+    return d;
+  });
+  mw.def("message", [](int id, py::bytes payload) {
+    std::string p = payload;
+    Bytes out;
+    bt::write_message(out, uint8_t(id), reinterpret_cast<const uint8_t*>(p.data()), p.size());
+    return pyb(out);
+  }, py::arg("id"), py::arg("payload") = py::bytes());
+  mw.def("keepalive", []() {
+    Bytes out;
+    bt::write_keepalive(out);
+    return pyb(out);
+  });
+  mw.def("extended", [](int ext_id, py::bytes payload) {
+    std::string p = payload;
+    Bytes out;
+    bt::write_extended(out, uint8_t(ext_id), reinterpret_cast<const uint8_t*>(p.data()), p.size());
+    return pyb(out);
+  });
+  mw.def("parse_message", [](py::bytes b) -> py::object {
+    std::string s = b;
+    bt::Message msg;
+    size_t used = bt::parse_message(reinterpret_cast<const uint8_t*>(s.data()), s.size(), msg);
+    if (!used) return py::none();
+    py::dict d;
+    d["consumed"] = used;
+    d["keepalive"] = msg.keepalive;
+    d["id"] = int(msg.id);
+    d["payload"] = pyb(msg.payload);
+    return d;
+  });
+  mw.def("frame_length", [](py::bytes b) {
+    std::string s = b;
+    return bt::frame_length(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  mw.def("parse_extended", [](py::bytes b) {
+    std::string s = b;
+    auto e = bt::parse_extended(ByteSpan(s));
+    return py::make_tuple(int(e.ext_id), pyb(e.data));
+  });
+  mw.def("known_msg_id", [](int id) { return bt::known_msg_id(uint8_t(id)); });
+
+  // ---------------- BEP XET ----------------
+  auto mx = m.def_submodule("bep_xet", "ut_xet extension: chunk request/response over BT");
+  mx.attr("CHUNK_REQUEST") = int(bep_xet::kChunkRequest);
+  mx.attr("CHUNK_RESPONSE") = int(bep_xet::kChunkResponse);
+  mx.attr("CHUNK_NOT_FOUND") = int(bep_xet::kChunkNotFound);
+  mx.attr("CHUNK_ERROR") = int(bep_xet::kChunkError);
+  mx.def("chunk_request", [](int ext, uint32_t rid, py::bytes hash, uint32_t a, uint32_t b) {
+    Bytes out;
+    auto h = arr_of<32>(hash, "hash");
+    bep_xet::encode_chunk_request(out, uint8_t(ext), rid, h.data(), a, b);
+    return pyb(out);
+  });
+  mx.def("chunk_response", [](int ext, uint32_t rid, uint32_t off, py::bytes data) {
+    std::string d = data;
+    Bytes out;
+    bep_xet::encode_chunk_response(out, uint8_t(ext), rid, off, reinterpret_cast<const uint8_t*>(d.data()), d.size());
+    return pyb(out);
+  });
+  mx.def("chunk_not_found", [](int ext, uint32_t rid, py::bytes hash) {
+    Bytes out;
+    auto h = arr_of<32>(hash, "hash");
+    bep_xet::encode_chunk_not_found(out, uint8_t(ext), rid, h.data());
+    return pyb(out);
+  });
+  mx.def("chunk_error", [](int ext, uint32_t rid, uint32_t code, std::string msg) {
+    Bytes out;
+    bep_xet::encode_chunk_error(out, uint8_t(ext), rid, code, msg);
+    return pyb(out);
+  });
+  mx.def("decode", [](py::bytes b) {
+    std::string s = b;
+    return xet_msg_dict(bep_xet::decode(ByteSpan(s)));
+  });
+  mx.def("make_ext_handshake", [](uint16_t port, int id, std::string client) {
+    return pyb(bep_xet::make_ext_handshake(port, uint8_t(id), client));
+  }, py::arg("port"), py::arg("ut_xet_id") = 1, py::arg("client") = std::string(bep_xet::kClientVersion));
+  mx.def("parse_ext_handshake", [](py::bytes b) {
+    std::string s = b;
+    auto c = bep_xet::parse_ext_handshake(ByteSpan(s));
+    py::dict d;
+    d["ut_xet"] = c.ut_xet_id;
+    d["port"] = c.listen_port;
+    d["client"] = c.client;
+    return d;
+  });
+
+  // ---------------- tracker ----------------
+  auto mt = m.def_submodule("tracker", "BEP 3 HTTP tracker client");
+  mt.def("announce_url", [](std::string url, py::bytes ih, py::bytes pid, uint16_t port, std::string ev,
+                            uint64_t up, uint64_t down, uint64_t left) {
+    tracker::Event e = ev == "started" ? tracker::Event::Started
+                       : ev == "stopped" ? tracker::Event::Stopped
+                       : ev == "completed" ? tracker::Event::Completed
+                                           : tracker::Event::None;
+    return tracker::announce_url(url, arr_of<20>(ih, "info_hash"), arr_of<20>(pid, "peer_id"), port, e, up, down, left);
+  }, py::arg("url"), py::arg("info_hash"), py::arg("peer_id"), py::arg("port"), py::arg("event") = "started",
+     py::arg("uploaded") = 0, py::arg("downloaded") = 0, py::arg("left") = 0);
+  mt.def("parse_announce", [](py::bytes b) {
+    std::string s = b;
+    auto r = tracker::parse_announce(s);
+    py::dict d;
+    d["interval"] = r.interval;
+    d["peers"] = addr_strs(r.peers);
+    return d;
+  });
+  mt.def("announce", [](std::string url, py::bytes ih, uint16_t port, std::string ev, int timeout_ms) {
+    auto pid = peer_id::generate();
+    tracker::Event e = ev == "started" ? tracker::Event::Started
+                       : ev == "stopped" ? tracker::Event::Stopped
+                       : ev == "completed" ? tracker::Event::Completed
+                                           : tracker::Event::None;
+    auto ihb = arr_of<20>(ih, "info_hash");
+    tracker::AnnounceResponse r;
+    {
+      py::gil_scoped_release nogil;
+      r = tracker::announce(url, ihb, pid, port, e, timeout_ms);
+    }
+    return addr_strs(r.peers);
+  }, py::arg("url"), py::arg("info_hash"), py::arg("port"), py::arg("event") = "started", py::arg("timeout_ms") = 5000);
+  mt.def("parse_compact_peers", [](py::bytes b, bool v6) {
+    std::string s = b;
+    return addr_strs(tracker::parse_compact_peers(s, v6));
+  }, py::arg("data"), py::arg("v6") = false);
+  mt.def("encode_compact_peer", [](std::string a) { return pyb(tracker::encode_compact_peer(net::Addr::parse(a, 0))); });
+
+  // ---------------- DHT ----------------
+  auto md = m.def_submodule("dht", "BEP 5 Kademlia DHT");
+  md.def("xor_distance", [](py::bytes a, py::bytes b) {
+    auto d = dht::xor_distance(arr_of<20>(a, "id"), arr_of<20>(b, "id"));
+    return pyb(d.data(), 20);
+  });
+  md.def("bucket_index", [](py::bytes own, py::bytes other) {
+    return dht::bucket_index(arr_of<20>(own, "id"), arr_of<20>(other, "id"));
+  });
+  md.def("random_id", []() {
+    auto id = dht::random_id();
+    return pyb(id.data(), 20);
+  });
+  md.def("build_ping", [](py::bytes tid, py::bytes own) { return pyb(dht::build_ping(std::string(tid), arr_of<20>(own, "id"))); });
+  md.def("build_find_node", [](py::bytes tid, py::bytes own, py::bytes target) {
+    return pyb(dht::build_find_node(std::string(tid), arr_of<20>(own, "id"), arr_of<20>(target, "target")));
+  });
+  md.def("build_get_peers", [](py::bytes tid, py::bytes own, py::bytes ih) {
+    return pyb(dht::build_get_peers(std::string(tid), arr_of<20>(own, "id"), arr_of<20>(ih, "info_hash")));
+  });
+  md.def("build_announce_peer", [](py::bytes tid, py::bytes own, py::bytes ih, uint16_t port, py::bytes token, bool implied) {
+    return pyb(dht::build_announce_peer(std::string(tid), arr_of<20>(own, "id"), arr_of<20>(ih, "info_hash"), port,
+                                        std::string(token), implied));
+  }, py::arg("tid"), py::arg("own"), py::arg("info_hash"), py::arg("port"), py::arg("token"), py::arg("implied_port") = false);
+  md.def("parse_compact_nodes", [](py::bytes b) {
+    std::string s = b;
+    py::list out;
+    for (auto& n : dht::parse_compact_nodes(s)) out.append(py::make_tuple(pyb(n.id.data(), 20), n.addr.str()));
+    return out;
+  });
+  md.def("encode_compact_node", [](py::bytes id, std::string addr) {
+    dht::NodeInfo n;
+    n.id = arr_of<20>(id, "id");
+    n.addr = net::Addr::parse(addr, 0);
+    return pyb(dht::encode_compact_node(n));
+  });
+  py::class_<dht::RoutingTable>(md, "RoutingTable")
+      .def(py::init([](py::bytes own) { return new dht::RoutingTable(arr_of<20>(own, "id")); }))
+      .def("insert", [](dht::RoutingTable& t, py::bytes id, std::string addr) {
+        return t.insert({arr_of<20>(id, "id"), net::Addr::parse(addr, 0)});
+      })
+      .def("remove", [](dht::RoutingTable& t, py::bytes id) { t.remove(arr_of<20>(id, "id")); })
+      .def("closest", [](const dht::RoutingTable& t, py::bytes target, size_t k) {
+        py::list out;
+        for (auto& n : t.closest(arr_of<20>(target, "target"), k)) out.append(py::make_tuple(pyb(n.id.data(), 20), n.addr.str()));
+        return out;
+      }, py::arg("target"), py::arg("k") = size_t(dht::K))
+      .def("__len__", &dht::RoutingTable::size);
+  py::class_<dht::Dht>(md, "Node")
+      .def(py::init([](uint16_t port) {
+             auto* d = new dht::Dht(port);
+             d->start();
+             return d;
+           }), py::arg("port") = 0)
+      .def_property_readonly("port", &dht::Dht::port)
+      .def_property_readonly("id", [](const dht::Dht& d) { return pyb(d.id().data(), 20); })
+      .def("bootstrap", [](dht::Dht& d, std::vector<std::string> nodes, int timeout_ms) {
+        std::vector<net::Addr> a;
+        for (auto& s : nodes) a.push_back(net::Addr::parse(s, 6881));
+        py::gil_scoped_release nogil;
+        return d.bootstrap(a, timeout_ms);
+      }, py::arg("nodes"), py::arg("timeout_ms") = 2000)
+      .def("get_peers", [](dht::Dht& d, py::bytes ih, int timeout_ms) {
+        auto h = arr_of<20>(ih, "info_hash");
+        std::vector<net::Addr> r;
+        {
+          py::gil_scoped_release nogil;
+          r = d.get_peers(h, timeout_ms);
+        }
+        return addr_strs(r);
+      }, py::arg("info_hash"), py::arg("timeout_ms") = 3000)
+      .def("announce_peer", [](dht::Dht& d, py::bytes ih, uint16_t port, int timeout_ms) {
+        auto h = arr_of<20>(ih, "info_hash");
+        py::gil_scoped_release nogil;
+        return d.announce_peer(h, port, timeout_ms);
+      }, py::arg("info_hash"), py::arg("port"), py::arg("timeout_ms") = 3000)
+      .def("ping", [](dht::Dht& d, std::string addr, int timeout_ms) {
+        auto a = net::Addr::parse(addr, 6881);
+        py::gil_scoped_release nogil;
+        return d.ping(a, timeout_ms);
+      }, py::arg("addr"), py::arg("timeout_ms") = 1000)
+      .def("routing_size", [](dht::Dht& d) { return d.table().size(); })
+      .def("stored_peers", [](const dht::Dht& d, py::bytes ih) { return addr_strs(d.stored_peers(arr_of<20>(ih, "info_hash"))); })
+      .def("stats", [](const dht::Dht& d) {
+        auto s = d.stats();
+        py::dict r;
+        r["queries_sent"] = s.queries_sent;
+        r["responses"] = s.responses;
+        r["queries_answered"] = s.queries_answered;
+        r["timeouts"] = s.timeouts;
+        r["lookups"] = s.lookups;
+        return r;
+      })
+      .def("stop", [](dht::Dht& d) {
+        py::gil_scoped_release nogil;
+        d.stop();
+      });
+
+  // ---------------- config / cache ----------------
+  m.def("config_json", []() { return Config::from_env().to_json(); });
+  m.def("repo_folder_name", &repo_folder_name, py::arg("repo_id"), py::arg("type") = "model");
+  m.def("list_cached_xorbs", []() { return storage::list_cached_xorbs(Config::from_env()); });
+  m.def("cache_put_xorb", [](std::string hex, py::bytes data, int64_t range_start) {
+    Config cfg = Config::from_env();
+    storage::XorbCache c(cfg);
+    std::string d = data;
+    if (range_start < 0) c.put(hex, reinterpret_cast<const uint8_t*>(d.data()), d.size());
+    else c.put_partial(hex, uint32_t(range_start), reinterpret_cast<const uint8_t*>(d.data()), d.size());
+  }, py::arg("hex"), py::arg("data"), py::arg("range_start") = -1);
+
+  // ---------------- BT seeder / peer client ----------------
+  py::class_<PySeeder>(m, "Seeder", "BT listener serving the local xorb cache over ut_xet")
+      .def(py::init<int, std::string>(), py::arg("port") = 0, py::arg("fault") = "")
+      .def_property_readonly("port", [](const PySeeder& s) { return s.server->port(); })
+      .def("rescan", [](PySeeder& s) { s.registry.scan(s.cfg); })
+      .def("stats", [](const PySeeder& s) {
+        auto st = s.server->stats();
+        py::dict r;
+        r["active_peers"] = st.active_peers;
+        r["total_peers"] = st.total_peers;
+        r["chunks_served"] = st.chunks_served;
+        r["bytes_served"] = st.bytes_served;
+        r["not_found"] = st.not_found;
+        return r;
+      })
+      .def("stop", [](PySeeder& s) {
+        py::gil_scoped_release nogil;
+        s.server->stop();
+      });
+  m.def("peer_fetch", [](std::string addr, py::bytes xorb_hash, uint32_t start, uint32_t end, int timeout_ms) {
+    auto h = arr_of<32>(xorb_hash, "xorb hash");
+    auto a = net::Addr::parse(addr, 6881);
+    bt::ChunkResult r;
+    std::string client;
+    {
+      py::gil_scoped_release nogil;
+      auto me = peer_id::generate();
+      auto sess = bt::PeerSession::connect(a, peer_id::info_hash(h.data()), me, 0, timeout_ms);
+      if (!sess->supports_xet()) throw Error("PeerNoXet", addr);
+      bt::XetRequest req;
+      req.xorb_hash = h;
+      req.range_start = start;
+      req.range_end = end;
+      r = sess->request(req, timeout_ms);
+      client = sess->client();
+    }
+    return py::make_tuple(pyb(r.data), r.chunk_offset, client);
+  }, py::arg("addr"), py::arg("xorb_hash"), py::arg("start"), py::arg("end"), py::arg("timeout_ms") = 5000);
+
+  // ---------------- pull ----------------
+  m.def("pull", [](std::string repo, std::string revision, bool p2p, std::vector<std::string> peers,
+                   std::optional<std::string> tracker_url, bool dht, std::vector<std::string> dht_bootstrap,
+                   std::vector<std::string> include, bool verify, int concurrency, std::string repo_type) {
+    Config cfg = Config::from_env();
+    PullOptions o;
+    o.repo_id = repo;
+    o.revision = revision;
+    o.p2p = p2p;
+    o.peers = peers;
+    o.tracker = tracker_url;
+    o.dht = dht;
+    o.dht_bootstrap = dht_bootstrap;
+    o.include = include;
+    o.verify = verify;
+    o.concurrency = concurrency;
+    o.repo_type = repo_type;
+    o.autostart_server = false;
+    std::ostringstream out, err;
+    PullSummary s;
+    {
+      py::gil_scoped_release nogil;
+      s = run_pull(cfg, o, out, err);
+    }
+    py::dict d;
+    d["snapshot_dir"] = s.snapshot_dir;
+    d["commit"] = s.commit;
+    d["bytes"] = s.bytes;
+    d["files"] = s.files;
+    d["xet_files"] = s.xet_files;
+    d["cached_files"] = s.cached_files;
+    d["bytes_from_peer"] = s.bytes_from_peer;
+    d["bytes_from_cdn"] = s.bytes_from_cdn;
+    d["bytes_from_cache"] = s.bytes_from_cache;
+    d["seconds"] = s.seconds;
+    d["stats_json"] = s.stats_json;
+    d["stdout"] = out.str();
+    d["stderr"] = err.str();
+    return d;
+  }, py::arg("repo"), py::arg("revision") = "main", py::arg("p2p") = true, py::arg("peers") = std::vector<std::string>{},
+     py::arg("tracker") = std::nullopt, py::arg("dht") = true, py::arg("dht_bootstrap") = std::vector<std::string>{},
+     py::arg("include") = std::vector<std::string>{}, py::arg("verify") = true, py::arg("concurrency") = 0,
+     py::arg("repo_type") = "model");
+  m.def("server_healthy", &server_healthy, py::arg("http_port"), py::arg("timeout_ms") = 1000);
+
+  // ---------------- synthetic bench ----------------
+  m.def("bench_synthetic", [](bool extended) {
+    std::vector<bench::Result> r;
+    {
+      py::gil_scoped_release nogil;
+      r = bench::run_synthetic(extended);
+    }
+    py::list out;
+    for (auto& x : r) {
+      py::dict d;
+      d["name"] = x.name;
+      d["runs"] = x.runs;
+      d["median_ns"] = x.median_ns;
+      d["throughput_mbps"] = x.throughput_mbps();
+      d["bytes_processed"] = x.bytes_processed;
+      out.append(d);
+    }
+    return out;
+  }, py::arg("extended") = true);
+}

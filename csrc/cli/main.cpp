@@ -1,0 +1,436 @@
+// `zest` command-line tool: pull / seed / serve / start / stop / status / bench / version / help.
+//
+// Reference: src/main.zig:40-81 (dispatch), :83-305 (pull), :306-369 (seed), :371-391 (bench),
+// :404-468 (serve), :470-503 (start), :552-590 (stop + PID file), :730-776 (usage).  Flags and
+// user-visible strings are kept so scripts written against the reference keep working.
+// Differences: `seed` keeps serving after announcing (the reference announces and exits,
+// main.zig:361-369), re-announcing every `--reannounce` seconds; `serve` can also run a DHT node;
+// xorb hashes are parsed with the Xet word-order hex (the reference's seed parses bytewise,
+// main.zig:349-356, which yields info-hashes no puller computes).
+#include <signal.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <iostream>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bench.h"
+#include "bt_server.h"
+#include "config.h"
+#include "dht.h"
+#include "http.h"
+#include "http_api.h"
+#include "json.h"
+#include "pull.h"
+#include "storage.h"
+#include "swarm.h"
+#include "xet_hash.h"
+
+using namespace zest;
+
+namespace {
+
+std::atomic<bool> g_stop{false};
+void on_signal(int) { g_stop.store(true); }
+
+std::string self_exe(const char* argv0) {
+  char buf[4096];
+  ssize_t n = ::readlink("/proc/self/exe", buf, sizeof buf - 1);
+  if (n > 0) return std::string(buf, size_t(n));
+  return argv0;
+}
+
+void print_usage(std::ostream& w) {
+  w << "zest \xE2\x80\x94 P2P acceleration for ML model distribution (BitTorrent-compliant, AMD Instinct native)\n"
+       "\n"
+       "Usage:\n"
+       "  zest pull <repo_id> [options]    Download a model\n"
+       "  zest seed [options]              Seed cached xorbs to peers\n"
+       "  zest serve [options]             Run server (BT + HTTP API)\n"
+       "  zest start                       Start server in background\n"
+       "  zest stop                        Stop background server\n"
+       "  zest status                      Show background server status\n"
+       "  zest bench [options]             Run benchmarks\n"
+       "  zest version                     Show version\n"
+       "  zest help                        Show this help\n"
+       "\n"
+       "Pull options:\n"
+       "  --revision, -r <ref>     Git revision (default: main)\n"
+       "  --peer, -p <ip:port>     Direct peer address (repeatable)\n"
+       "  --tracker, -t <url>      BT tracker URL for peer discovery\n"
+       "  --dht-port <port>        DHT UDP port (default: 6881)\n"
+       "  --dht-bootstrap <h:p>    DHT bootstrap node (repeatable)\n"
+       "  --no-dht                 Disable DHT lookups\n"
+       "  --listen, -l <addr>      Listen address for P2P (default: 0.0.0.0:6881)\n"
+       "  --no-p2p                 Disable P2P, CDN only\n"
+       "  --include <suffix>       Only files ending in <suffix> (repeatable)\n"
+       "  --concurrency, -j <n>    Parallel term downloads (default: 16)\n"
+       "  --no-verify              Skip the Xet file-hash check\n"
+       "  --no-serve               Do not auto-start the background seeder\n"
+       "\n"
+       "Seed options:\n"
+       "  --tracker, -t <url>      BT tracker URL\n"
+       "  --dht-port <port>        DHT UDP port (default: 6881)\n"
+       "  --dht-bootstrap <h:p>    DHT bootstrap node (repeatable)\n"
+       "  --listen, -l <addr>      Listen address (default: 0.0.0.0:6881)\n"
+       "  --reannounce <sec>       Re-announce interval (default: 900)\n"
+       "  --announce-only          Announce and exit (reference behaviour)\n"
+       "\n"
+       "Serve options:\n"
+       "  --http-port <port>       HTTP API port (default: 9847)\n"
+       "  --listen-port <port>     BT listen port (default: 6881)\n"
+       "  --dht                    Also run a DHT node on --dht-port\n"
+       "  --fault <spec>           Fault injection, e.g. drop:0.1,corrupt:0.05,delay:20\n"
+       "\n"
+       "Bench options:\n"
+       "  --synthetic              Run synthetic benchmarks\n"
+       "  --json                   Output results as JSON\n"
+       "\n"
+       "Examples:\n"
+       "  zest pull meta-llama/Llama-3.1-8B\n"
+       "  zest pull Qwen/Qwen2-7B --revision v1.0 --no-p2p\n"
+       "  zest pull gpt2 --peer 10.0.0.5:6881\n"
+       "  zest seed --tracker http://tracker.example.com:6881\n"
+       "  zest serve --http-port 8080\n"
+       "  zest bench --synthetic --json\n";
+}
+
+bool parse_port(const std::string& s, uint16_t& out) {
+  try {
+    int v = std::stoi(s);
+    if (v < 0 || v > 65535) return false;
+    out = uint16_t(v);
+    return true;
+  } catch (...) {
+    return false;
+  }
+}
+
+// --listen accepts "port", ":port" or "host:port".
+void apply_listen(Config& cfg, const std::string& s) {
+  size_t c = s.rfind(':');
+  uint16_t p;
+  if (parse_port(c == std::string::npos ? s : s.substr(c + 1), p)) cfg.listen_port = p;
+}
+
+void write_pid_file(const Config& cfg) {
+  try {
+    storage::write_file_atomic(cfg.pid_file, std::to_string(::getpid()));
+  } catch (const Error&) {
+  }
+}
+
+std::vector<xet::Hash> cached_xorb_hashes(const Config& cfg) {
+  std::set<std::string> uniq;
+  for (auto& k : storage::list_cached_xorbs(cfg))
+    if (k.size() >= 64) uniq.insert(k.substr(0, 64));
+  std::vector<xet::Hash> out;
+  for (auto& h : uniq) {
+    try {
+      out.push_back(xet::from_hex(h));
+    } catch (const Error&) {
+    }
+  }
+  return out;
+}
+
+int cmd_pull(const std::string& exe, const std::vector<std::string>& a) {
+  if (a.empty() || a[0].rfind("-", 0) == 0) {
+    std::cerr << "Error: missing repository ID\n"
+              << "Usage: zest pull <repo_id> [--revision <ref>] [--tracker <url>] [--no-p2p]\n";
+    return 1;
+  }
+  Config cfg = Config::from_env();
+  PullOptions o;
+  o.repo_id = a[0];
+  for (size_t i = 1; i < a.size(); ++i) {
+    const std::string& f = a[i];
+    auto next = [&]() -> std::string { return i + 1 < a.size() ? a[++i] : std::string(); };
+    if (f == "--revision" || f == "-r") o.revision = next();
+    else if (f == "--tracker" || f == "-t") o.tracker = next();
+    else if (f == "--peer" || f == "-p") o.peers.push_back(next());
+    else if (f == "--dht-port") parse_port(next(), cfg.dht_port);
+    else if (f == "--dht-bootstrap") o.dht_bootstrap.push_back(next());
+    else if (f == "--no-dht") o.dht = false;
+    else if (f == "--listen" || f == "-l") apply_listen(cfg, next());
+    else if (f == "--no-p2p") o.p2p = false;
+    else if (f == "--include") o.include.push_back(next());
+    else if (f == "--concurrency" || f == "-j") o.concurrency = std::atoi(next().c_str());
+    else if (f == "--no-verify") o.verify = false;
+    else if (f == "--no-serve") o.autostart_server = false;
+    else if (f == "--repo-type") o.repo_type = next();
+    else std::cerr << "Warning: unknown option " << f << "\n";
+  }
+  try {
+    PullSummary s = run_pull(cfg, o, std::cout, std::cerr);
+    if (o.p2p && o.autostart_server && !std::getenv("ZEST_NO_AUTOSTART")) {
+      if (!server_healthy(cfg.http_port, 300) && spawn_background_server(exe, cfg.http_port)) {
+        std::cout << "Seeding in background (BT :" << cfg.listen_port << ", HTTP :" << cfg.http_port << ")\n";
+        std::cout << "Dashboard: http://localhost:" << cfg.http_port << "\n";
+      }
+    }
+    (void)s;
+    return 0;
+  } catch (const Error& e) {
+    std::cerr << "Error: " << e.what() << "\n";
+    return 1;
+  }
+}
+
+int cmd_seed(const std::vector<std::string>& a) {
+  Config cfg = Config::from_env();
+  std::optional<std::string> tracker;
+  std::vector<net::Addr> boot;
+  int reannounce = 900;
+  bool announce_only = false;
+  for (size_t i = 0; i < a.size(); ++i) {
+    const std::string& f = a[i];
+    auto next = [&]() -> std::string { return i + 1 < a.size() ? a[++i] : std::string(); };
+    if (f == "--tracker" || f == "-t") tracker = next();
+    else if (f == "--listen" || f == "-l") apply_listen(cfg, next());
+    else if (f == "--dht-port") parse_port(next(), cfg.dht_port);
+    else if (f == "--dht-bootstrap") {
+      try {
+        boot.push_back(net::Addr::parse(next(), 6881));
+      } catch (const Error&) {
+      }
+    } else if (f == "--reannounce") reannounce = std::max(5, std::atoi(next().c_str()));
+    else if (f == "--announce-only") announce_only = true;
+  }
+  std::cout << "Scanning local xorb cache...\n";
+  auto hashes = cached_xorb_hashes(cfg);
+  std::cout << "Found " << hashes.size() << " cached xorbs\n";
+  if (hashes.empty()) {
+    std::cout << "Nothing to seed. Run `zest pull` first.\n";
+    return 0;
+  }
+  storage::XorbRegistry registry;
+  registry.scan(cfg);
+  storage::XorbCache cache(cfg, &registry);
+  std::unique_ptr<bt::BtServer> server;
+  if (!announce_only) {
+    try {
+      server = std::make_unique<bt::BtServer>(cfg, &cache, bt::PieceProvider{}, cfg.listen_port);
+      if (!cfg.fault.empty()) server->set_fault(bt::FaultSpec::parse(cfg.fault));
+      server->start();
+      cfg.listen_port = server->port();
+    } catch (const Error& e) {
+      std::cerr << "Error: cannot listen on port " << cfg.listen_port << " (" << e.what() << ")\n";
+      return 1;
+    }
+  }
+  SwarmDownloader swarm(cfg, tracker, true, true, boot);
+  swarm.announce(hashes);
+  std::cout << "Announced " << hashes.size() << " xorbs via BT protocol\n";
+  std::cout << "  Peer ID: " << peer_id::kClientPrefix << "...\n";
+  std::cout << "  DHT port: " << cfg.dht_port << "\n";
+  std::cout << "  Listen port: " << cfg.listen_port << "\n";
+  if (tracker) std::cout << "  Tracker: " << *tracker << "\n";
+  std::cout << "Seeding...\n" << std::flush;
+  if (announce_only) return 0;
+  ::signal(SIGINT, on_signal);
+  ::signal(SIGTERM, on_signal);
+  auto last = std::chrono::steady_clock::now();
+  while (!g_stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    if (std::chrono::steady_clock::now() - last > std::chrono::seconds(reannounce)) {
+      swarm.announce(cached_xorb_hashes(cfg));
+      last = std::chrono::steady_clock::now();
+    }
+  }
+  server->stop();
+  auto st = server->stats();
+  std::cout << "\nSeeding stopped. Served " << st.chunks_served << " chunk ranges (" << st.bytes_served
+            << " bytes) to " << st.total_peers << " peers.\n";
+  return 0;
+}
+
+int cmd_bench(const std::vector<std::string>& a) {
+  bool json = false, synthetic = false, core_only = false;
+  for (auto& f : a) {
+    if (f == "--json") json = true;
+    else if (f == "--synthetic") synthetic = true;
+    else if (f == "--core") core_only = true;
+  }
+  if (!synthetic) {
+    std::cerr << "Usage: zest bench --synthetic [--json]\n"
+              << "  --synthetic  Run bencode/hash/wire benchmarks\n"
+              << "  --json       Output results as JSON\n"
+              << "  --core       Only the five reference rows\n";
+    return 0;
+  }
+  auto r = bench::run_synthetic(!core_only);
+  if (json) bench::write_json(std::cout, r);
+  else bench::write_text(std::cout, r);
+  return 0;
+}
+
+int cmd_serve(const std::vector<std::string>& a) {
+  Config cfg = Config::from_env();
+  bool run_dht = false;
+  std::vector<net::Addr> boot;
+  for (size_t i = 0; i < a.size(); ++i) {
+    const std::string& f = a[i];
+    auto next = [&]() -> std::string { return i + 1 < a.size() ? a[++i] : std::string(); };
+    if (f == "--http-port") parse_port(next(), cfg.http_port);
+    else if (f == "--listen-port") parse_port(next(), cfg.listen_port);
+    else if (f == "--dht") run_dht = true;
+    else if (f == "--dht-port") parse_port(next(), cfg.dht_port);
+    else if (f == "--dht-bootstrap") {
+      try {
+        boot.push_back(net::Addr::parse(next(), 6881));
+      } catch (const Error&) {
+      }
+    } else if (f == "--fault") cfg.fault = next();
+  }
+  storage::XorbRegistry registry;
+  registry.scan(cfg);
+  storage::XorbCache cache(cfg, &registry);
+  std::unique_ptr<bt::BtServer> bt;
+  try {
+    bt = std::make_unique<bt::BtServer>(cfg, &cache, bt::PieceProvider{}, cfg.listen_port);
+    if (!cfg.fault.empty()) bt->set_fault(bt::FaultSpec::parse(cfg.fault));
+  } catch (const Error& e) {
+    std::cerr << "Error: BT listen failed on port " << cfg.listen_port << ": " << e.what() << "\n";
+    return 1;
+  }
+  std::unique_ptr<ApiServer> api;
+  try {
+    api = std::make_unique<ApiServer>(cfg, bt.get(), &registry, "");
+  } catch (const Error& e) {
+    std::cerr << "HTTP API error: " << e.what() << "\n";
+    return 1;
+  }
+  std::cout << "zest server v" << kVersion << "\n";
+  std::cout << "  BT listen port: " << bt->port() << "\n";
+  std::cout << "  HTTP API port:  " << api->port() << "\n";
+  std::cout << "  Peer ID:        " << peer_id::kClientPrefix << "...\n";
+  std::cout << "  Cached xorbs:   " << registry.count() << "\n";
+  std::unique_ptr<dht::Dht> node;
+  if (run_dht) {
+    node = std::make_unique<dht::Dht>(cfg.dht_port);
+    node->start();
+    if (!boot.empty()) node->bootstrap(boot);
+    std::cout << "  DHT port:       " << node->port() << "\n";
+  }
+  std::cout << "\nServer running. Press Ctrl+C to stop.\n" << std::flush;
+  write_pid_file(cfg);
+  ::signal(SIGINT, on_signal);
+  ::signal(SIGTERM, on_signal);
+  ::signal(SIGPIPE, SIG_IGN);
+  bt->start();
+  api->start();
+  auto last_announce = std::chrono::steady_clock::now() - std::chrono::hours(1);
+  while (!g_stop.load() && !api->stopping()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (node && std::chrono::steady_clock::now() - last_announce > std::chrono::minutes(15)) {
+      for (auto& h : cached_xorb_hashes(cfg)) node->announce_peer(peer_id::info_hash(h.data()), bt->port(), 1000);
+      last_announce = std::chrono::steady_clock::now();
+    }
+  }
+  api->stop();
+  bt->stop();
+  if (node) node->stop();
+  api.reset();
+  storage::remove_file(cfg.pid_file);
+  std::cout << "\nServer stopped.\n";
+  return 0;
+}
+
+int cmd_start(const std::string& exe) {
+  Config cfg = Config::from_env();
+  if (server_healthy(cfg.http_port, 500)) {
+    std::cerr << "zest server is already running on port " << cfg.http_port << ".\n";
+    return 0;
+  }
+  if (!spawn_background_server(exe, cfg.http_port)) {
+    std::cerr << "Failed to start zest server.\n";
+    return 1;
+  }
+  for (int i = 0; i < 50 && !server_healthy(cfg.http_port, 200); ++i)
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  std::cout << "Seeding in background (BT :" << cfg.listen_port << ", HTTP :" << cfg.http_port << ")\n";
+  std::cout << "Dashboard: http://localhost:" << cfg.http_port << "\n";
+  return 0;
+}
+
+int cmd_stop() {
+  Config cfg = Config::from_env();
+  auto pid = storage::read_file(cfg.pid_file);
+  std::string pid_str = pid ? std::string(pid->begin(), pid->end()) : "";
+  while (!pid_str.empty() && std::isspace(uint8_t(pid_str.back()))) pid_str.pop_back();
+  if (pid_str.empty()) {
+    std::cerr << "No running zest server found.\n";
+    return 1;
+  }
+  try {
+    http::RequestOptions ro;
+    ro.timeout_ms = 3000;
+    auto r = http::request("POST", "http://127.0.0.1:" + std::to_string(cfg.http_port) + "/v1/stop", {}, "", ro);
+    if (r.status == 200) {
+      std::cout << "zest server stopped (was PID " << pid_str << ").\n";
+      return 0;
+    }
+    std::cerr << "Server returned status " << r.status << ".\n";
+    return 1;
+  } catch (const Error&) {
+    std::cerr << "Failed to connect to zest server. It may have already stopped.\n";
+    storage::remove_file(cfg.pid_file);
+    return 1;
+  }
+}
+
+int cmd_status() {
+  Config cfg = Config::from_env();
+  try {
+    http::RequestOptions ro;
+    ro.timeout_ms = 2000;
+    auto r = http::get("http://127.0.0.1:" + std::to_string(cfg.http_port) + "/v1/status", {}, ro);
+    std::cout << std::string(r.body.begin(), r.body.end()) << "\n";
+    return r.status == 200 ? 0 : 1;
+  } catch (const Error&) {
+    std::cerr << "No running zest server found.\n";
+    return 1;
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::ios::sync_with_stdio(true);
+  const std::string exe = self_exe(argv[0]);
+  if (argc < 2) {
+    print_usage(std::cout);
+    return 0;
+  }
+  const std::string cmd = argv[1];
+  std::vector<std::string> rest(argv + 2, argv + argc);
+  try {
+    if (cmd == "pull") return cmd_pull(exe, rest);
+    if (cmd == "seed") return cmd_seed(rest);
+    if (cmd == "bench") return cmd_bench(rest);
+    if (cmd == "serve") return cmd_serve(rest);
+    if (cmd == "start") return cmd_start(exe);
+    if (cmd == "stop") return cmd_stop();
+    if (cmd == "status") return cmd_status();
+    if (cmd == "version" || cmd == "--version" || cmd == "-V") {
+      std::cout << "zest " << kVersion << "\n";
+      return 0;
+    }
+    if (cmd == "help" || cmd == "--help" || cmd == "-h") {
+      print_usage(std::cout);
+      return 0;
+    }
+    std::cerr << "Unknown command: " << cmd << "\n\n";
+    print_usage(std::cout);
+    return 1;
+  } catch (const std::exception& e) {
+    std::cerr << "Error: " << e.what() << "\n";
+    return 1;
+  }
+}

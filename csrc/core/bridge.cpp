@@ -3,6 +3,7 @@
 #include <iomanip>
 
 #include "json.h"
+#include "trace.h"
 #include "xorb.h"
 
 namespace zest {
@@ -42,22 +43,19 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   const cas::FetchInfo* fi = recon.match(hex, term.range.start, term.range.end);
   if (!fi) throw Error("NoMatchingFetchInfo", hex);
   XorbFetchResult out;
-  // 1. local xorb cache (full or partial entry)
+  // 1. local xorb cache: any cached run covering the term's chunks
   if (allow_cache && cache_) {
-    if (auto hit = cache_->get_with_range(hex, uint32_t(fi->range.start))) {
-      if (covers(hit->data, hit->chunk_offset, term.range.start, term.range.end)) {
-        stats_.xorbs_from_cache++;
-        stats_.bytes_from_cache += hit->data.size();
-        if (swarm_) swarm_->stats().cached_xorbs++;
-        out.data = std::move(hit->data);
-        out.local_start = uint32_t(term.range.start - hit->chunk_offset);
-        out.local_end = uint32_t(term.range.end - hit->chunk_offset);
-        out.source = Source::Cache;
-        return out;
-      }
+    if (auto hit = cache_->find(hex, uint32_t(term.range.start), uint32_t(term.range.end))) {
+      stats_.xorbs_from_cache++;
+      stats_.bytes_from_cache += hit->data.size();
+      if (swarm_) swarm_->stats().cached_xorbs++;
+      out.data = std::move(hit->data);
+      out.local_start = uint32_t(term.range.start - hit->chunk_offset);
+      out.local_end = uint32_t(term.range.end - hit->chunk_offset);
+      out.source = Source::Cache;
+      return out;
     }
   }
-  const bool whole = fi->range.start == 0 && it->second.size() == 1;
   // 2. P2P swarm with the FetchInfo's chunk range
   if (allow_p2p && swarm_ && swarm_->p2p_enabled()) {
     if (auto r = swarm_->try_peers(term.hash, uint32_t(fi->range.start), uint32_t(fi->range.end))) {
@@ -66,8 +64,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         stats_.bytes_from_peer += r->data.size();
         if (cache_) {
           try {
-            if (r->chunk_offset == 0 && whole) cache_->put(hex, r->data.data(), r->data.size());
-            else cache_->put_partial(hex, r->chunk_offset, r->data.data(), r->data.size());
+            cache_->put_run(hex, r->chunk_offset, r->data.data(), r->data.size());
           } catch (const Error&) {
           }
         }
@@ -78,12 +75,16 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         out.peer = r->peer;
         return out;
       }
+      ZTRACE("bridge", "peer " << r->peer << " run for " << hex << " does not cover [" << term.range.start << ","
+                                << term.range.end << ") (offset " << r->chunk_offset << ")");
       swarm_->report_bad_peer(r->peer);  // served a run that does not even parse
     }
   }
   // 3. CDN
   if (!cas_) throw Error("NotAuthenticated");
+  trace::Span span("cdn", "fetch " + hex.substr(0, 12));
   out.data = cas_->fetch(*fi);
+  span.arg("\"bytes\":" + std::to_string(out.data.size()));
   stats_.xorbs_from_cdn++;
   stats_.bytes_from_cdn += out.data.size();
   if (swarm_) {
@@ -93,8 +94,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   }
   if (cache_) {
     try {
-      if (whole) cache_->put(hex, out.data.data(), out.data.size());
-      else cache_->put_partial(hex, uint32_t(fi->range.start), out.data.data(), out.data.size());
+      cache_->put_run(hex, uint32_t(fi->range.start), out.data.data(), out.data.size());
     } catch (const Error&) {
     }
   }

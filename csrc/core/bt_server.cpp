@@ -30,18 +30,7 @@ FaultSpec FaultSpec::parse(const std::string& s) {
 }
 
 std::optional<storage::CacheHit> slice_chunks(const Bytes& data, uint32_t offset, uint32_t start, uint32_t end) {
-  if (start < offset) return std::nullopt;
-  auto idx = xet::index_chunks(data.data(), data.size());
-  const uint32_t a = start - offset;
-  if (a >= idx.size()) return std::nullopt;
-  uint32_t b = end > start ? end - offset : uint32_t(idx.size());
-  if (b > idx.size()) b = uint32_t(idx.size());
-  const uint64_t lo = idx[a].header_off;
-  const uint64_t hi = idx[b - 1].header_off + xet::kChunkHeaderLen + idx[b - 1].clen;
-  storage::CacheHit h;
-  h.data.assign(data.begin() + long(lo), data.begin() + long(hi));
-  h.chunk_offset = start;
-  return h;
+  return storage::slice_run(data, offset, start, end);
 }
 
 BtServer::BtServer(const Config& cfg, storage::XorbCache* cache, PieceProvider provider, int port)
@@ -114,15 +103,9 @@ std::optional<storage::CacheHit> BtServer::lookup(const std::array<uint8_t, 32>&
     if (auto hit = provider_(hash, hex, start, end)) return hit;
   }
   if (!cache_) return std::nullopt;
-  auto hit = cache_->get_with_range(hex, start);
-  if (!hit) return std::nullopt;
-  if (hit->chunk_offset == 0 && (start != 0 || end != 0)) {
-    try {
-      if (auto s = slice_chunks(hit->data, 0, start, end)) return s;
-    } catch (const Error&) {
-    }
-  }
-  return hit;
+  // Only runs that really hold [start, end) are served; otherwise NOT_FOUND lets the requester
+  // move on to another peer or the CDN instead of receiving a run it cannot use.
+  return cache_->find(hex, start, end);
 }
 
 void BtServer::handle(net::Socket s, net::Addr peer) {

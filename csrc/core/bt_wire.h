@@ -11,6 +11,7 @@
 
 #include <array>
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <string_view>
 
@@ -49,6 +50,13 @@ void write_handshake(Bytes& out, const Sha1Digest& info_hash, const peer_id::Pee
 Handshake parse_handshake(const uint8_t* p68);  // throws Error("InvalidProtocolString")
 
 void write_message(Bytes& out, uint8_t id, const uint8_t* payload = nullptr, size_t n = 0);
+// Fixed-buffer variant (caller guarantees 5 + n bytes of room); returns bytes written.
+inline size_t write_message(uint8_t* out, uint8_t id, const uint8_t* payload, size_t n) {
+  store_be32(out, uint32_t(1 + n));
+  out[4] = id;
+  if (n) std::memcpy(out + 5, payload, n);
+  return 5 + n;
+}
 void write_keepalive(Bytes& out);
 void write_extended(Bytes& out, uint8_t ext_id, const uint8_t* payload, size_t n);
 

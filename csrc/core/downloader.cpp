@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "storage.h"
+#include "trace.h"
 #include "xorb.h"
 
 namespace zest {
@@ -117,6 +118,8 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   auto do_term = [&](size_t i, bool allow_p2p, bool allow_cache) {
     const cas::Term& t = rec.terms[i];
     XorbFetchResult f = bridge_.fetch_term(t, rec, allow_p2p, allow_cache);
+    src[i] = f.source;  // recorded before decoding so a bad peer copy can be attributed
+    peer[i] = f.peer;
     Bytes out;
     std::vector<xet::HashSize> hs;
     xet::extract_chunk_range(f.data.data(), f.data.size(), f.local_start, f.local_end, out, &hs);
@@ -128,8 +131,6 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     }
     pwrite_all(fd, out.data() + a, out.size() - a, off - skip);
     hashes[i] = std::move(hs);
-    src[i] = f.source;
-    peer[i] = f.peer;
   };
 
   auto worker = [&]() {
@@ -142,6 +143,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
         if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
       } catch (const std::exception& e) {
         // A peer/cache copy that does not decode: retry straight from the CDN once.
+        ZTRACE("download", "term " << i << " via " << int(src[i]) << " failed (" << e.what() << "), CDN retry");
         try {
           if (src[i] != Source::Cdn && !peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
           do_term(i, false, false);

@@ -1,5 +1,7 @@
 #include "hub.h"
 
+#include <algorithm>
+
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -75,7 +77,12 @@ std::optional<std::string> resolve_commit(const Config& cfg, const std::string& 
   try {
     http::Response r = http::get(api_base(cfg, repo_type) + repo_id + "/revision/" + revision, auth_headers(cfg));
     if (r.status != 200) return std::nullopt;
-    return extract_json_sha(r.body);
+    if (auto fast = extract_json_sha(r.body)) return fast;
+    // Not compact JSON: parse properly.
+    std::string sha = json::Value::parse(r.body).str_or("sha", "");
+    if (sha.size() == 40 && std::all_of(sha.begin(), sha.end(), [](char c) { return std::isxdigit(uint8_t(c)); }))
+      return sha;
+    return std::nullopt;
   } catch (const Error&) {
     return std::nullopt;
   }

@@ -5,10 +5,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cerrno>
 #include <cstring>
 #include <random>
+#include <set>
+
+#include "xorb.h"
 
 namespace zest::storage {
 
@@ -122,9 +127,9 @@ std::optional<std::string> read_ref(const Config& cfg, const std::string& repo_i
 }
 
 std::vector<std::string> list_cached_xorbs(const Config& cfg) {
-  std::vector<std::string> out;
+  std::set<std::string> out;
   DIR* d = ::opendir(cfg.xorb_cache_dir.c_str());
-  if (!d) return out;
+  if (!d) return {};
   while (dirent* e = ::readdir(d)) {
     std::string pfx = e->d_name;
     if (pfx.size() != 2) continue;
@@ -132,12 +137,13 @@ std::vector<std::string> list_cached_xorbs(const Config& cfg) {
     if (!sd) continue;
     while (dirent* f = ::readdir(sd)) {
       std::string n = f->d_name;
-      if (n.size() == 64 && n.compare(0, 2, pfx) == 0) out.push_back(n);
+      if (n.size() < 64 || n.compare(0, 2, pfx) != 0) continue;
+      if (n.size() == 64 || (n[64] == '.' && n.find(".tmp") == std::string::npos)) out.insert(n.substr(0, 64));
     }
     ::closedir(sd);
   }
   ::closedir(d);
-  return out;
+  return {out.begin(), out.end()};
 }
 
 void XorbRegistry::add(const std::string& key) {
@@ -166,6 +172,59 @@ bool XorbCache::has(const std::string& hex) const { return exists(cfg_.xorb_cach
 
 std::optional<Bytes> XorbCache::get(const std::string& hex) const { return read_file(cfg_.xorb_cache_path(hex)); }
 
+std::optional<CacheHit> slice_run(const Bytes& data, uint32_t offset, uint32_t start, uint32_t end) {
+  if (start < offset) return std::nullopt;
+  std::vector<xet::ChunkEntry> idx;
+  try {
+    idx = xet::index_chunks(data.data(), data.size());
+  } catch (const Error&) {
+    return std::nullopt;
+  }
+  const uint64_t a = start - offset;
+  const uint64_t b = end == 0 ? idx.size() : uint64_t(end) - offset;
+  if (a >= b || b > idx.size()) return std::nullopt;
+  const uint64_t lo = idx[a].header_off;
+  const uint64_t hi = idx[b - 1].header_off + xet::kChunkHeaderLen + idx[b - 1].clen;
+  CacheHit h;
+  h.chunk_offset = start;
+  if (lo == 0 && hi == data.size()) h.data = data;
+  else h.data.assign(data.begin() + long(lo), data.begin() + long(hi));
+  return h;
+}
+
+std::vector<uint32_t> XorbCache::run_offsets(const std::string& hex) const {
+  std::vector<uint32_t> out;
+  if (hex.size() != 64) return out;
+  const std::string dir = cfg_.xorb_cache_dir + "/" + hex.substr(0, 2);
+  DIR* d = ::opendir(dir.c_str());
+  if (!d) return out;
+  while (dirent* e = ::readdir(d)) {
+    std::string n = e->d_name;
+    if (n.compare(0, 64, hex) != 0) continue;
+    if (n.size() == 64) {
+      out.push_back(0);
+    } else if (n[64] == '.' && n.size() > 65 && std::all_of(n.begin() + 65, n.end(), ::isdigit)) {
+      out.push_back(uint32_t(std::stoul(n.substr(65))));
+    }
+  }
+  ::closedir(d);
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  return out;
+}
+
+std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, uint32_t end) const {
+  auto offs = run_offsets(hex);
+  // Closest preceding run first: most likely to be the one that was fetched for this range.
+  for (auto it = offs.rbegin(); it != offs.rend(); ++it) {
+    if (*it > start) continue;
+    auto data = read_file(cfg_.xorb_cache_path(*it == 0 ? hex : hex + "." + std::to_string(*it)));
+    if (!data) continue;
+    if (auto hit = slice_run(*data, *it, start, end)) return hit;
+  }
+  return std::nullopt;
+}
+
 std::optional<CacheHit> XorbCache::get_with_range(const std::string& hex, uint32_t range_start) const {
   if (auto full = read_file(cfg_.xorb_cache_path(hex))) return CacheHit{std::move(*full), 0};
   if (auto part = read_file(cfg_.xorb_cache_path(hex + "." + std::to_string(range_start))))
@@ -173,14 +232,12 @@ std::optional<CacheHit> XorbCache::get_with_range(const std::string& hex, uint32
   return std::nullopt;
 }
 
-void XorbCache::put(const std::string& hex, const uint8_t* data, size_t n) {
-  write_file_atomic(cfg_.xorb_cache_path(hex), data, n);
+void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+  const std::string key = chunk_offset == 0 ? hex : hex + "." + std::to_string(chunk_offset);
+  const std::string path = cfg_.xorb_cache_path(key);
+  if (exists(path) && file_size(path) >= n) return;  // keep the longer run
+  write_file_atomic(path, data, n);
   if (registry_) registry_->add(hex);
-}
-
-void XorbCache::put_partial(const std::string& hex, uint32_t range_start, const uint8_t* data, size_t n) {
-  write_file_atomic(cfg_.xorb_cache_path(hex + "." + std::to_string(range_start)), data, n);
-  if (registry_) registry_->add(hex + "." + std::to_string(range_start));
 }
 
 uint64_t XorbCache::bytes_on_disk() const {

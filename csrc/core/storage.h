@@ -35,13 +35,16 @@ void remove_file(const std::string& path);
 void write_ref(const Config& cfg, const std::string& repo_id, const std::string& ref, const std::string& commit);
 std::optional<std::string> read_ref(const Config& cfg, const std::string& repo_id, const std::string& ref);
 
-// List 64-char xorb names in the 2-char prefix dirs (partials excluded).
+// Distinct xorb hashes (hex) with any cached run: full `{hex}` or partial `{hex}.{chunk_offset}`.
 std::vector<std::string> list_cached_xorbs(const Config& cfg);
 
 struct CacheHit {
   Bytes data;
   uint32_t chunk_offset = 0;  // chunk index of data's first chunk inside the xorb
 };
+
+// Slice a run (first chunk = `offset`) to chunks [start, end); nullopt if it does not cover them.
+std::optional<CacheHit> slice_run(const Bytes& data, uint32_t offset, uint32_t start, uint32_t end);
 
 class XorbRegistry {
  public:
@@ -61,10 +64,22 @@ class XorbCache {
   explicit XorbCache(const Config& cfg, XorbRegistry* registry = nullptr) : cfg_(cfg), registry_(registry) {}
   bool has(const std::string& hex) const;
   std::optional<Bytes> get(const std::string& hex) const;
-  // Full xorb first (offset 0), then the partial entry {hex}.{range_start}.
+  // A cached run covering chunks [start, end) (end == 0: through the end of the run), sliced to
+  // exactly that range.  Every candidate is validated by walking its chunk headers, so a run
+  // stored under the "full" name that is really a prefix (what the reference's
+  // `range.start == 0 && one fetch entry` rule produces, xet_bridge.zig:189-217 — the source of
+  // its P2P RangeOutOfBounds failures) is never served for chunks it does not hold.
+  std::optional<CacheHit> find(const std::string& hex, uint32_t start, uint32_t end) const;
+  // Legacy lookup kept for callers that want the raw run at an exact offset.
   std::optional<CacheHit> get_with_range(const std::string& hex, uint32_t range_start) const;
-  void put(const std::string& hex, const uint8_t* data, size_t n);
-  void put_partial(const std::string& hex, uint32_t range_start, const uint8_t* data, size_t n);
+  // Store a run of serialized chunks starting at chunk `chunk_offset`: offset 0 goes to `{hex}`,
+  // others to `{hex}.{offset}`; an existing longer run under the same name is kept.
+  void put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  void put(const std::string& hex, const uint8_t* data, size_t n) { put_run(hex, 0, data, n); }
+  void put_partial(const std::string& hex, uint32_t range_start, const uint8_t* data, size_t n) {
+    put_run(hex, range_start, data, n);
+  }
+  std::vector<uint32_t> run_offsets(const std::string& hex) const;  // offsets of cached runs
   uint64_t bytes_on_disk() const;
 
  private:

@@ -3,6 +3,7 @@
 #include <cstring>
 #include <iomanip>
 
+#include "trace.h"
 #include "tracker.h"
 
 namespace zest {
@@ -16,11 +17,39 @@ SwarmDownloader::SwarmDownloader(const Config& cfg, std::optional<std::string> t
     if (!dht_->has_socket()) dht_ = std::make_unique<dht::Dht>(0);  // port taken: ephemeral
     dht_->start();
     if (!dht_bootstrap.empty()) dht_->bootstrap(dht_bootstrap, 1500);
+    aq_thread_ = std::thread([this] { announce_worker(); });
   }
 }
 
 SwarmDownloader::~SwarmDownloader() {
+  {
+    std::lock_guard<std::mutex> g(aq_mu_);
+    aq_stop_ = true;
+  }
+  aq_cv_.notify_all();
+  if (aq_thread_.joinable()) aq_thread_.join();
   if (dht_) dht_->stop();
+}
+
+void SwarmDownloader::announce_worker() {
+  std::unique_lock<std::mutex> lk(aq_mu_);
+  while (true) {
+    aq_cv_.wait(lk, [&] { return aq_stop_ || !announce_q_.empty(); });
+    if (aq_stop_) return;
+    std::vector<Sha1Digest> batch;
+    batch.swap(announce_q_);
+    lk.unlock();
+    for (auto& ih : batch) {
+      if (dht_->table().size() == 0) break;
+      try {
+        dht_->announce_peer(ih, cfg_.listen_port, 1000);
+      } catch (...) {
+      }
+      std::lock_guard<std::mutex> g(aq_mu_);
+      if (aq_stop_) return;
+    }
+    lk.lock();
+  }
 }
 
 void SwarmDownloader::add_direct_peer(const net::Addr& a) {
@@ -87,24 +116,30 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
     try {
       auto s = pool_->get_or_connect(a, ih);
       if (!s->supports_xet()) continue;
-      stats_.peers_connected++;
       bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
       r.peer = a.str();
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (served_by_.insert(r.peer).second) stats_.peers_connected++;
+      }
+      ZTRACE("swarm", "peer " << r.peer << " served " << xet::to_hex(hash) << " [" << start << "," << end
+                              << ") offset " << r.chunk_offset << " bytes " << r.data.size());
       stats_.peer_xorbs++;
       stats_.peer_bytes += r.data.size();
       stats_.total_bytes += r.data.size();
       stats_.total_xorbs++;
       if (dht_) {
-        std::thread([this, ih] {
-          try {
-            dht_->announce_peer(ih, cfg_.listen_port, 1000);
-          } catch (...) {
-          }
-        }).detach();
+        {
+          std::lock_guard<std::mutex> g(aq_mu_);
+          announce_q_.push_back(ih);
+        }
+        aq_cv_.notify_one();
       }
       return r;
     } catch (const Error& e) {
       stats_.peer_failures++;
+      ZTRACE("swarm", "peer " << a.str() << " failed " << xet::to_hex(hash) << " [" << start << "," << end
+                              << "): " << e.what());
       if (e.code() != "ChunkNotFound" && e.code() != "ChunkError") {
         pool_->remove(a);
         std::lock_guard<std::mutex> g(mu_);

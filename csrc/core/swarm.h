@@ -12,12 +12,15 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <set>
 #include <ostream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bt_peer.h"
@@ -65,8 +68,17 @@ class SwarmDownloader {
   };
   std::map<std::string, Cached> discovered_;
   std::map<std::string, int> score_;  // addr -> failures
+  std::set<std::string> served_by_;   // distinct peers that served data ("Peers connected")
   std::mutex disc_mu_;
   DownloadStats stats_;
+  // DHT re-announce of xorbs fetched from peers: queued and drained by an owned worker thread
+  // (never a detached thread holding `this`).
+  void announce_worker();
+  std::mutex aq_mu_;
+  std::condition_variable aq_cv_;
+  std::vector<Sha1Digest> announce_q_;
+  bool aq_stop_ = false;
+  std::thread aq_thread_;
 };
 
 }  // namespace zest
