@@ -1,0 +1,299 @@
+"""End-to-end tests of the native `zest` CLI against the offline fake Hub/CAS/tracker.
+
+Mirrors the reference's integration strategy (test/local/p2p-docker-test.sh: seeder + leecher,
+grep "P2P ratio", compare file hashes; test/integration/zest-p2p-test.sh) without Docker or the
+network: every "machine" is a separate cache root + port set on 127.0.0.1.
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import pytest
+
+from e2e_util import Node, ZEST, assert_snapshot, free_port, p2p_ratio, sample_files
+from zest_amd import _core
+from zest_amd.testing import FakeHub
+
+REPO_ID = "org/tiny"
+
+
+@pytest.fixture
+def hub():
+    h = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    h.start()
+    yield h
+    h.stop()
+
+
+@pytest.fixture
+def nodes(hub, tmp_path):
+    made = []
+
+    def make(name):
+        n = Node(hub, tmp_path, name)
+        made.append(n)
+        return n
+
+    yield make
+    for n in made:
+        n.close()
+
+
+def test_version_and_help(nodes):
+    n = nodes("a")
+    assert n.run("version").stdout.strip() == "zest " + _core.VERSION
+    h = n.run("help").stdout
+    for s in ("Usage:", "zest pull <repo_id>", "--no-p2p", "--http-port", "--synthetic"):
+        assert s in h
+    r = n.run("frobnicate", check=False)
+    assert r.returncode == 1 and "Unknown command: frobnicate" in r.stderr
+    r = n.run("pull", check=False)
+    assert r.returncode == 1 and "missing repository ID" in r.stderr
+
+
+def test_bench_synthetic_json(nodes):
+    n = nodes("a")
+    out = json.loads(n.run("bench", "--synthetic", "--json", "--core").stdout)
+    names = [r["name"] for r in out["results"]]
+    assert names == ["bencode_encode", "bencode_decode", "blake3_64kb", "sha1_info_hash", "bt_wire_frame"]
+    for r in out["results"]:
+        assert set(r) == {"name", "runs", "median_ns", "throughput_mbps", "bytes_processed"}
+        assert r["runs"] > 0 and r["throughput_mbps"] > 0 and r["bytes_processed"] > 0
+    txt = n.run("bench", "--synthetic").stdout
+    assert "zest benchmark results" in txt and "Median (ns)" in txt
+    r = n.run("bench")
+    assert "Usage: zest bench --synthetic [--json]" in r.stderr
+
+
+def test_pull_cdn_only(hub, nodes):
+    files = sample_files()
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("a")
+    r = a.run("pull", REPO_ID, "--no-p2p")
+    out = r.stdout
+    assert f"zest pull {REPO_ID} (revision: main)" in out
+    assert "P2P disabled (CDN only)" in out
+    assert f"Found 3 files (revision: main → {commit})" in out
+    assert "2 Xet-backed files, 3 total files" in out
+    for s in ("Xorb fetch stats:", "Total xorbs:", "From peers:", "From CDN:", "P2P ratio:", "Done! Model available at:"):
+        assert s in out
+    assert p2p_ratio(out) == 0.0
+    assert_snapshot(a, REPO_ID, commit, files)
+    ref = a.root / "hf" / "hub" / "models--org--tiny" / "refs" / "main"
+    assert ref.read_text().strip() == commit
+    # xorb cache populated in the reference layout: xorbs/{hex[0:2]}/{hex}[.{chunk_offset}]
+    xf = a.xorb_files()
+    assert xf and all(p.parent.name == p.name[:2] for p in xf)
+    # second pull: everything cached
+    out2 = a.run("pull", REPO_ID, "--no-p2p").stdout
+    assert out2.count("(cached)") == 3
+
+
+@pytest.mark.parametrize("policy", ["none", "lz4", "bg4"])
+def test_pull_compression_policies(policy, nodes, tmp_path):
+    h = FakeHub(policy=policy, max_xorb_bytes=1 << 20)
+    h.start()
+    try:
+        files = sample_files(seed=3)
+        files["weights.bin"] = (bytes(range(256)) * 4000)[:900_000]  # highly compressible
+        commit = h.add_repo(REPO_ID, files, xet_min_size=100_000)
+        n = Node(h, tmp_path, "p")
+        try:
+            n.run("pull", REPO_ID, "--no-p2p")
+            assert_snapshot(n, REPO_ID, commit, files)
+        finally:
+            n.close()
+    finally:
+        h.stop()
+
+
+def test_pull_revision_and_dedup(hub, nodes):
+    files = sample_files()
+    c1 = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    files2 = dict(files)
+    files2["model.safetensors"] = files["model.safetensors"][:1_000_000] + b"\x00" * 1000 + files["model.safetensors"][1_000_000:]
+    c2 = hub.add_repo(REPO_ID, files2, revision="v2", xet_min_size=100_000)
+    assert c1 != c2
+    a = nodes("a")
+    a.run("pull", REPO_ID, "--no-p2p")
+    gets = hub.counters.get("xorb_get", 0)
+    a.run("pull", REPO_ID, "--revision", "v2", "--no-p2p")
+    assert_snapshot(a, REPO_ID, c2, files2)
+    # v2 shares most chunks with main: most terms come from the local xorb cache
+    assert hub.counters.get("xorb_get", 0) - gets <= 3
+    assert (a.root / "hf/hub/models--org--tiny/refs/v2").read_text().strip() == c2
+
+
+def _seed_node(hub, nodes, files):
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("seeder")
+    a.run("pull", REPO_ID, "--no-p2p")
+    return a, commit
+
+
+def test_p2p_loopback_direct_peer(hub, nodes):
+    files = sample_files()
+    a, commit = _seed_node(hub, nodes, files)
+    srv = a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
+    a.wait_healthy()
+    b = nodes("leecher")
+    before = hub.counters.get("xorb_get", 0)
+    out = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{a.listen_port}", "--no-dht").stdout
+    assert f"Direct peer: 127.0.0.1:{a.listen_port}" in out
+    assert p2p_ratio(out) == 100.0
+    assert hub.counters.get("xorb_get", 0) == before, "leecher touched the CDN"
+    assert_snapshot(b, REPO_ID, commit, files)
+    st = json.loads(a.api("/v1/status")[1])
+    assert st["chunks_served"] > 0 and st["bytes_served"] > 0
+    # the leecher cached what it received and can itself seed a third node
+    srv_b = b.spawn("serve", "--listen-port", str(b.listen_port), "--http-port", str(b.http_port))
+    b.wait_healthy()
+    a.run("stop")
+    srv.wait(timeout=10)
+    c = nodes("third")
+    out = c.run("pull", REPO_ID, "--peer", f"127.0.0.1:{b.listen_port}", "--no-dht").stdout
+    assert p2p_ratio(out) == 100.0
+    assert_snapshot(c, REPO_ID, commit, files)
+    b.run("stop")
+    srv_b.wait(timeout=10)
+
+
+def test_p2p_corrupt_peer_falls_back_to_cdn(hub, nodes):
+    files = sample_files()
+    a, commit = _seed_node(hub, nodes, files)
+    a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port), "--fault", "corrupt:1.0")
+    a.wait_healthy()
+    b = nodes("leecher")
+    r = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{a.listen_port}", "--no-dht")
+    # every peer copy is corrupt: files are still exact, repaired from the CDN
+    assert_snapshot(b, REPO_ID, commit, files)
+    assert p2p_ratio(r.stdout) < 100.0
+    assert hub.counters.get("xorb_get", 0) > 0
+
+
+def test_p2p_dead_peer_falls_back_to_cdn(hub, nodes):
+    files = sample_files()
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    b = nodes("leecher")
+    out = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{free_port()}", "--no-dht").stdout
+    assert p2p_ratio(out) == 0.0
+    assert_snapshot(b, REPO_ID, commit, files)
+
+
+def test_tracker_discovery(hub, nodes):
+    files = sample_files()
+    a, commit = _seed_node(hub, nodes, files)
+    tracker = hub.url + "/announce"
+    seed = a.spawn("seed", "--tracker", tracker, "--listen", str(a.listen_port))
+    # wait until the seeder announced every cached xorb
+    t0 = time.time()
+    while hub.counters.get("announce", 0) < len(hub.xorbs) and time.time() - t0 < 20:
+        time.sleep(0.05)
+    assert hub.counters.get("announce", 0) >= len(hub.xorbs)
+    b = nodes("leecher")
+    out = b.run("pull", REPO_ID, "--tracker", tracker, "--no-dht").stdout
+    assert p2p_ratio(out) == 100.0
+    assert_snapshot(b, REPO_ID, commit, files)
+    seed.terminate()
+    seed.wait(timeout=10)
+    assert "Seeding..." in seed.stdout.read()
+
+
+def test_dht_discovery(hub, nodes):
+    files = sample_files()
+    a, commit = _seed_node(hub, nodes, files)
+    boot = _core.dht.Node(0)
+    try:
+        bs = f"127.0.0.1:{boot.port}"
+        seed = a.spawn("seed", "--dht-bootstrap", bs, "--dht-port", str(a.dht_port), "--listen", str(a.listen_port))
+        info_hashes = [_core.info_hash(_core.from_xet_hex(x.hash_hex)) for x in hub.xorbs]
+        t0 = time.time()
+        while time.time() - t0 < 20 and not all(boot.stored_peers(ih) for ih in info_hashes):
+            time.sleep(0.1)
+        assert all(boot.stored_peers(ih) for ih in info_hashes), "seeder did not announce via DHT"
+        b = nodes("leecher")
+        out = b.run("pull", REPO_ID, "--dht-bootstrap", bs).stdout
+        assert p2p_ratio(out) == 100.0
+        assert_snapshot(b, REPO_ID, commit, files)
+        seed.terminate()
+        seed.wait(timeout=10)
+    finally:
+        boot.stop()
+
+
+def test_resume_after_failed_term(hub, nodes):
+    files = {"model.safetensors": sample_files(big=6_000_000)["model.safetensors"]}
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=1)
+    assert len(hub.xorbs) >= 4
+    bad = hub.xorbs[-1].hash_hex
+    hub.fail_xorbs.add(bad)
+    a = nodes("a")
+    r = a.run("pull", REPO_ID, "--no-p2p", "--concurrency", "1", check=False)
+    assert "download error" in r.stderr
+    snap = a.snapshot(REPO_ID, commit)
+    assert (snap / "model.safetensors.incomplete").exists()
+    assert (snap / "model.safetensors.zest-resume").exists()
+    assert not (snap / "model.safetensors").exists()
+    hub.fail_xorbs.clear()
+    out = a.run("pull", REPO_ID, "--no-p2p").stdout
+    assert "resumed" in out
+    assert_snapshot(a, REPO_ID, commit, files)
+    assert not (snap / "model.safetensors.zest-resume").exists()
+
+
+def test_http_api_and_pull_job(hub, nodes):
+    files = sample_files()
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("a")
+    srv = a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
+    a.wait_healthy()
+    assert a.api("/v1/health") == (200, b'{"status":"ok"}')
+    st = json.loads(a.api("/v1/status")[1])
+    for k in ("version", "bt_peers", "chunks_served", "xorbs_cached", "http_requests", "http_port", "bt_port"):
+        assert k in st
+    assert st["http_port"] == a.http_port and st["bt_port"] == a.listen_port
+    assert a.api("/nope") == (404, b'{"error":"not found"}')
+    code, html = a.api("/")
+    assert code == 200 and b"<html" in html
+    code, body = a.api("/v1/pull", "POST", {"repo": REPO_ID, "no_p2p": True})
+    job = json.loads(body)["job"]
+    t0 = time.time()
+    while time.time() - t0 < 60:
+        js = json.loads(a.api(f"/v1/pull/{job}")[1])
+        if js["state"] in ("done", "error"):
+            break
+        time.sleep(0.1)
+    assert js["state"] == "done", js
+    assert_snapshot(a, REPO_ID, commit, files)
+    models = json.loads(a.api("/v1/models")[1])
+    assert {"name": REPO_ID, "files": 3} in models
+    assert json.loads(a.api("/v1/status")[1])["xorbs_cached"] > 0
+    assert b"zest_chunks_served_total" in a.api("/metrics")[1]
+    assert json.loads(a.api("/v1/stop", "POST")[1]) == {"status": "shutting down"}
+    srv.wait(timeout=10)
+    out = srv.stdout.read()
+    for s in ("BT listen port:", "HTTP API port:", "Cached xorbs:", "Server running. Press Ctrl+C to stop.",
+              "Server stopped."):
+        assert s in out
+
+
+def test_start_stop(nodes):
+    a = nodes("a")
+    r = a.run("stop", check=False)
+    assert "No running zest server found." in r.stderr
+    out = a.run("start").stdout
+    assert f"Dashboard: http://localhost:{a.http_port}" in out
+    a.wait_healthy()
+    assert "already running" in a.run("start").stderr
+    r = a.run("stop")
+    assert "zest server stopped (was PID" in r.stdout
+    t0 = time.time()
+    while time.time() - t0 < 10:
+        try:
+            a.api("/v1/health", timeout=0.5)
+        except OSError:
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("server still up after stop")
