@@ -520,6 +520,8 @@ void bind_extra(py::module_& m) {
     d["bytes_from_cache"] = s.bytes_from_cache;
     d["seconds"] = s.seconds;
     d["stats_json"] = s.stats_json;
+    d["files_json"] = s.files_json;
+    d["failed_files"] = s.failed_files;
     d["stdout"] = out.str();
     d["stderr"] = err.str();
     return d;

@@ -11,6 +11,7 @@
 #include "bridge.h"
 #include "downloader.h"
 #include "http.h"
+#include "json.h"
 #include "hub.h"
 #include "storage.h"
 #include "swarm.h"
@@ -110,8 +111,10 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
   ParallelDownloader dl(bridge, opt.concurrency > 0 ? opt.concurrency : int(cfg.concurrency));
   S.snapshot_dir = cfg.snapshot_dir(opt.repo_id, S.commit);
   size_t k = 0;
+  std::vector<uint8_t> ok(files.size(), 1);
   for (auto& f : files) {
     ++k;
+    uint8_t& file_ok = ok[k - 1];
     out << "[" << k << "/" << files.size() << "] " << f.path;
     const std::string dst = S.snapshot_dir + "/" + f.path;
     if (storage::exists(dst) && (f.size == 0 || storage::file_size(dst) == f.size)) {
@@ -123,6 +126,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
       out << " [xet]\n" << std::flush;
       if (!bridge.authenticated()) {
         err << "  Error downloading via xet: not authenticated\n";
+        file_ok = 0;
         continue;
       }
       try {
@@ -131,6 +135,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
         if (r.resumed_terms) out << "  resumed " << r.resumed_terms << "/" << r.terms << " terms\n";
       } catch (const Error& e) {
         err << "  Parallel download error (" << e.what() << ")\n";
+        file_ok = 0;
         continue;
       }
     } else {
@@ -139,6 +144,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
         S.bytes += hub::download_regular(cfg, opt.repo_id, S.commit == opt.revision ? opt.revision : S.commit, f.path, dst);
       } catch (const Error& e) {
         err << "  Error downloading: " << e.what() << "\n";
+        file_ok = 0;
         continue;
       }
     }
@@ -154,6 +160,17 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
   S.bytes_from_cdn = bridge.stats().bytes_from_cdn;
   S.bytes_from_cache = bridge.stats().bytes_from_cache;
   S.stats_json = bridge.stats_json();
+  json::Writer fw;
+  fw.arr();
+  for (size_t i = 0; i < files.size(); ++i) {
+    fw.obj().key("path").str(files[i].path).key("size").num_u(files[i].size).key("xet_hash");
+    if (files[i].xet_hash) fw.str(*files[i].xet_hash);
+    else fw.null();
+    fw.key("ok").boolean(ok[i] != 0).end();
+    if (!ok[i]) S.failed_files++;
+  }
+  fw.end();
+  S.files_json = fw.out();
   S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   out << "\nDone! Model available at:\n  " << S.snapshot_dir << "\n";
   out << "\nRun: transformers.AutoModel.from_pretrained(\"" << opt.repo_id << "\")\n" << std::flush;

@@ -40,6 +40,8 @@ struct PullSummary {
   uint64_t bytes_from_peer = 0, bytes_from_cdn = 0, bytes_from_cache = 0;
   double seconds = 0;
   std::string stats_json;
+  std::string files_json;  // [{"path","size","xet_hash"|null,"ok"}] for every listed file
+  size_t failed_files = 0;
 };
 
 PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std::ostream& err);

@@ -1,13 +1,106 @@
 """zest_amd — MI355X-native P2P model distribution (zest capabilities, rebuilt for AMD CDNA4).
 
+Usage (same API as the reference's `zest` package, python/zest/__init__.py:1-73):
+
+    import zest_amd as zest          # or: import zest  (compat shim)
+    zest.enable()                    # background seeder + huggingface_hub patch
+    path = zest.pull("meta-llama/Llama-3.1-8B")
+    weights = zest.pull("meta-llama/Llama-3.1-8B", device="cuda:0")   # HBM tensors, GPU-verified
+    print(zest.status()); zest.stop()
+
 Layers (see docs/ARCHITECTURE.md):
   zest_amd._core    C++17 host core: BLAKE3/Xet hashing, LZ4/BG4, CDC, xorbs, BT/DHT/HTTP stack
   zest_amd._hip     HIP/CDNA4 kernels for gfx950: xorb ingest (decode+verify), BLAKE3, Merkle, CDC
   zest_amd.ops      torch-facing wrappers of the HIP kernels
   zest_amd.parallel RCCL (torch.distributed "nccl") intra-node swarm: GPUs as BitTorrent peers
   zest_amd.models   synthetic model specs (gpt2, Llama-3.1-8B/70B, Qwen2-7B, Mixtral-8x7B)
-  zest_amd.utils    config, safetensors views, tracing, fault injection
+  zest_amd.utils    tracing, fault-injection spec, formatting helpers
 """
 from __future__ import annotations
 
+import os
+
 __version__ = "0.4.2"
+
+_server = None
+_client = None
+
+
+def _init():
+    global _server, _client
+    if _server is None:
+        from .client import ZestClient
+        from .server import ZestServer
+
+        _server = ZestServer()
+        _client = ZestClient()
+
+
+def enable() -> None:
+    """Start the background zest server (seeding) and route huggingface_hub downloads through zest."""
+    _init()
+    _server.ensure_running()
+    from .hf_backend import patch_hf_hub
+
+    patch_hf_hub(_client)
+
+
+def disable() -> None:
+    """Restore the original huggingface_hub functions."""
+    from .hf_backend import unpatch_hf_hub
+
+    unpatch_hf_hub()
+
+
+def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = False, verify: bool = True,
+         p2p: bool = True, peers=None, tracker=None, dht: bool = True, dht_bootstrap=None, include=None,
+         group=None, repo_type: str = "model", verbose: bool = False):
+    """Download `repo@revision` via zest.
+
+    * default: returns the HF-cache snapshot directory (reference behaviour).
+    * device="cuda:N" (or as_tensors=True): also loads every *.safetensors file into that GPU's HBM,
+      verifies each against its Xet file hash on the GPU, and returns {tensor_name: tensor}.
+    * device="all": collective over `group` (default WORLD) — every rank gets all tensors on its
+      own GPU while each file is read/pushed by one owner rank and replicated over xGMI (RCCL).
+    """
+    _init()
+    kw = dict(p2p=p2p, peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, include=include,
+              verify=verify, repo_type=repo_type, verbose=verbose)
+    if device is None and not as_tensors:
+        return _client.pull(repo, revision, **kw)
+    if device == "all":
+        import torch.distributed as dist
+
+        from .parallel import swarm_load
+
+        # rank 0 pulls (P2P/CDN), the others wait; then the snapshot is swarm-loaded into HBM.
+        res = _client.pull_detailed(repo, revision, **kw) if dist.get_rank(group) == 0 else None
+        obj = [None if res is None else (res.snapshot_dir, res.xet_hashes())]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        snap, hashes = obj[0]
+        return swarm_load(snap, group=group, xet_hashes=hashes if verify else None)
+    from .device import load_snapshot
+
+    res = _client.pull_detailed(repo, revision, **kw)
+    return load_snapshot(res.snapshot_dir, device or "cuda:0", res.xet_hashes() if verify else None)
+
+
+def status() -> dict:
+    """Status JSON of the background server (starting it if needed)."""
+    _init()
+    _server.ensure_running()
+    return _client.status()
+
+
+def stop() -> None:
+    """Stop the background server."""
+    _init()
+    _server.stop()
+
+
+# Auto-enable when ZEST=1 is set (reference python/zest/__init__.py:68-73).
+if os.environ.get("ZEST", "").strip().lower() in ("1", "true", "yes"):
+    try:
+        enable()
+    except Exception:
+        pass
