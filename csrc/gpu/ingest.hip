@@ -6,6 +6,9 @@
 // alignment-fixing loads read whole aligned dwords (and the LZ4 window reads 256-byte lines).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "blake3_dev.h"
 #include "zgpu.h"
 
@@ -156,206 +159,356 @@ __global__ void __launch_bounds__(256) k_place_raw(const uint8_t* __restrict__ s
 }
 
 // --------------------------------------------------------------------------------------------
-// K3b: LZ4-frame (+BG4) decode.  One wave per chunk, output assembled in LDS, then written to
-// HBM with the BG4 regroup fused into the store pass.  Token parsing reads a 256-byte window of
-// the compressed stream held one dword per lane (v_readlane_b32), literal bytes are fetched from
-// that window with ds_bpermute, match copies run lane-parallel in LDS (overlapping matches use
-// the periodic form out[op+i] = out[op-off+(i mod off)], so every source byte is final).
+// K3b: LZ4-frame (+BG4) decode.  One wave per chunk, 4 waves per 256-thread block, persistent
+// grid.  Decoded bytes go through a small per-wave LDS history ring (8 KiB) and are flushed to
+// HBM in 16-byte stores every 2 KiB, so occupancy is set by VGPRs (~20 waves/CU) instead of a
+// whole-chunk LDS buffer (which allowed one wave per CU).
+//
+//  * compressed stream: a 512-byte window held as two dwords per lane; token / length bytes are
+//    read with v_readlane (uniform), literal bytes lane-parallel with ds_bpermute; the window
+//    slides by 256 bytes so the next line's load overlaps the current line's parsing.
+//  * match copies: lane i of a 64-byte block reads source o - off*(1 + i/off) (the periodic form
+//    of an overlapping copy, always a final byte); distances <= 7872 come from the LDS ring,
+//    longer ones from HBM with L2-coherent loads (sc1, agent scope) after s_waitcnt vmcnt(0) —
+//    those bytes were flushed by this wave >= 5 KiB earlier.
+//  * BG4: the grouped stream is scattered to its interleaved position (4*j + g) on flush, and
+//    long-distance match reads use the same mapping, so no regroup pass or scratch is needed.
+//  * chunks clipped by [clip_lo, clip_hi) decode into a 128 KiB global scratch slot (one for the
+//    chunk straddling clip_lo, one for clip_hi), then the clipped range is copied out.
 // --------------------------------------------------------------------------------------------
-struct Window {
-  uintptr_t base;  // absolute, 4-byte aligned
-  uint32_t w;      // this lane's dword: bytes [base + 4*lane, +4)
+constexpr uint32_t kRing = 8192;
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kFlushAt = 2048;
+constexpr uint32_t kRingReach = kRing - 256 - 64;  // max match distance served from the ring
+
+__device__ uint8_t g_clip_scratch[2][kMaxChunk + 256];
+
+// Compressed-stream window: three dwords per lane = bytes [wofs, wofs + 768) of the payload,
+// addressed relative to the 4-byte-aligned payload base.  Reads stay inside [wofs, wofs + 320);
+// the window slides by 256 bytes as the stream advances, so w2 is a 256-byte-ahead prefetch whose
+// load latency overlaps parsing.  Offsets are 32-bit (a chunk payload is < 16 MiB).
+struct Win {
+  const uint32_t* pb;
+  uint32_t wofs;
+  uint32_t w0, w1, w2;
 };
 
-__device__ __forceinline__ void win_fill(Window& win, uintptr_t addr, uint32_t lane) {
-  win.base = addr & ~uintptr_t(3);
-  win.w = reinterpret_cast<const uint32_t*>(win.base)[lane];
+__device__ __forceinline__ void win_init(Win& w, const uint8_t* payload, uint32_t lane) {
+  w.pb = reinterpret_cast<const uint32_t*>(payload - (reinterpret_cast<uintptr_t>(payload) & 3));
+  w.wofs = 0;
+  w.w0 = w.pb[lane];
+  w.w1 = w.pb[kWave + lane];
+  w.w2 = w.pb[2 * kWave + lane];
 }
 
-// Ensure [a, a + need) is inside the window (need <= 252).
-__device__ __forceinline__ void win_ensure(Window& win, uintptr_t a, uint32_t need, uint32_t lane) {
-  if (a < win.base || a + need > win.base + 256) win_fill(win, a, lane);
+// Slide so that position a (relative to pb) is in the first 256 bytes of the window.  Callers
+// advance by < 256 bytes between seeks, so at most one slide happens (an `if`, not a loop: a loop
+// makes the compiler copy the freshly loaded prefetch register and wait for it immediately).
+__device__ __forceinline__ void win_seek(Win& w, uint32_t a, uint32_t lane) {
+  if (a >= w.wofs + 512) {  // long jump (raw block / checksum skip): reload
+    w.wofs = a & ~255u;
+    w.w0 = w.pb[(w.wofs >> 2) + lane];
+    w.w1 = w.pb[(w.wofs >> 2) + kWave + lane];
+    w.w2 = w.pb[(w.wofs >> 2) + 2 * kWave + lane];
+  } else if (a >= w.wofs + 256) {
+    w.wofs += 256;
+    w.w0 = w.w1;
+    w.w1 = w.w2;
+    w.w2 = w.pb[(w.wofs >> 2) + 2 * kWave + lane];
+  }
 }
 
-// Uniform byte read (a must be inside the window).
-__device__ __forceinline__ uint32_t win_byte(const Window& win, uintptr_t a) {
-  const uint32_t rel = uint32_t(a - win.base);
-  const uint32_t w = __builtin_amdgcn_readlane(win.w, int(rel >> 2));
-  return (w >> (8 * (rel & 3))) & 0xFF;
+// Uniform byte at a (a in [wofs, wofs + 512)).
+__device__ __forceinline__ uint32_t win_u8(const Win& w, uint32_t a) {
+  const uint32_t rel = a - w.wofs;
+  uint32_t d;
+  if (rel < 256) d = __builtin_amdgcn_readlane(w.w0, int(rel >> 2));
+  else d = __builtin_amdgcn_readlane(w.w1, int((rel >> 2) - 64));
+  return (d >> (8 * (rel & 3))) & 0xFF;
 }
 
-// Per-lane byte read: lane i gets the byte at a + i (a + 64 must be inside the window).
-__device__ __forceinline__ uint32_t win_lane_byte(const Window& win, uintptr_t a, uint32_t lane) {
-  const uint32_t rel = uint32_t(a - win.base) + lane;
-  const uint32_t w = __shfl(win.w, int(rel >> 2), kWave);
-  return (w >> (8 * (rel & 3))) & 0xFF;
+// Lane i gets the byte at a + i (a in [wofs, wofs + 256)).
+__device__ __forceinline__ uint32_t win_lane_u8(const Win& w, uint32_t a, uint32_t lane) {
+  const uint32_t r0 = a - w.wofs;
+  const uint32_t rel = r0 + lane;
+  uint32_t d;
+  if (r0 <= 192) {
+    d = __shfl(w.w0, int(rel >> 2), kWave);
+  } else {
+    const uint32_t v0 = __shfl(w.w0, int((rel >> 2) & 63), kWave);
+    const uint32_t v1 = __shfl(w.w1, int((rel >> 2) & 63), kWave);
+    d = rel < 256 ? v0 : v1;
+  }
+  return (d >> (8 * (rel & 3))) & 0xFF;
 }
 
-// Decode one LZ4 block (blk[0..blen)) into lds at op; returns new op, or ~0u on error.
-__device__ uint32_t lz4_block(Window& win, uintptr_t blk, uint32_t blen, uint8_t* lds, uint32_t op,
-                              uint32_t cap, uint32_t lane) {
-  uint32_t bp = 0;
+// L2-coherent byte load (bypasses this CU's L1, which never sees its own earlier stores).
+__device__ __forceinline__ uint32_t load_u8_coherent(const uint8_t* p) {
+  const uint32_t k = uint32_t(reinterpret_cast<uintptr_t>(p) & 3);
+  uint32_t* w = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(p - k));
+  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (v >> (8 * k)) & 0xFF;
+}
+
+// Optional decode profile (ZG_LZ4_PROF=1 selects the kProf instantiation).
+__device__ unsigned long long g_lz4_prof[10];
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+
+struct Sink {
+  uint8_t* ring;  // this wave's LDS ring (16-byte aligned)
+  uint8_t* out;   // chunk byte 0 in HBM (dst or scratch)
+  uint32_t tmod;  // ring index of stream byte p = (tmod + p) & kRingMask
+  uint32_t n;     // expected decoded size
+  uint32_t op;    // bytes produced
+  uint32_t fp;    // bytes flushed
+  uint32_t g1, g2, g3;
+  bool bg4;
+  // profile counters (kProf only)
+  uint64_t t_lit, t_match, t_flush, nseq, lit_bytes, match_bytes, nfar, nflush, nshort;
+};
+
+// Grouped-stream position -> byte offset in the chunk (identity unless BG4).
+__device__ __forceinline__ uint32_t out_pos(const Sink& s, uint32_t p) {
+  if (!s.bg4) return p;
+  const uint32_t g = uint32_t(p >= s.g1) + uint32_t(p >= s.g2) + uint32_t(p >= s.g3);
+  const uint32_t base = g == 0 ? 0u : g == 1 ? s.g1 : g == 2 ? s.g2 : s.g3;
+  return 4 * (p - base) + g;
+}
+
+__device__ void sink_flush(Sink& s, uint32_t upto, bool final, uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();
+  if (s.bg4) {
+    for (uint32_t i = s.fp + lane; i < upto; i += kWave) s.out[out_pos(s, i)] = s.ring[(s.tmod + i) & kRingMask];
+    s.fp = upto;
+    return;
+  }
+  uint32_t p = s.fp;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(s.out) + p;
+  uint32_t head = uint32_t((16 - (a & 15)) & 15);
+  if (head > upto - p) head = upto - p;
+  if (lane < head) s.out[p + lane] = s.ring[(s.tmod + p + lane) & kRingMask];
+  p += head;
+  const uint32_t nvec = (upto - p) >> 4;
+  for (uint32_t v = lane; v < nvec; v += kWave) {
+    const uint32_t q = p + 16 * v;
+    const uint4 x = *reinterpret_cast<const uint4*>(s.ring + ((s.tmod + q) & kRingMask));
+    *reinterpret_cast<uint4*>(s.out + q) = x;
+  }
+  p += 16 * nvec;
+  if (final) {
+    if (lane < upto - p) s.out[p + lane] = s.ring[(s.tmod + p + lane) & kRingMask];
+    p = upto;
+  }
+  s.fp = p;
+}
+
+template <bool kProf>
+__device__ __forceinline__ void sink_advance(Sink& s, uint32_t cnt, uint32_t lane) {
+  s.op += cnt;
+  if (s.op - s.fp >= kFlushAt) {
+    const uint64_t t0 = kProf ? clk() : 0;
+    sink_flush(s, s.op, false, lane);
+    if (kProf) {
+      s.t_flush += clk() - t0;
+      s.nflush++;
+    }
+  }
+}
+
+// Copy `len` literal bytes starting at stream position a.
+template <bool kProf>
+__device__ __forceinline__ void copy_literals(Sink& s, Win& w, uint32_t a, uint32_t len, uint32_t lane) {
+  for (uint32_t b = 0; b < len; b += kWave) {
+    const uint32_t cnt = len - b < kWave ? len - b : kWave;
+    win_seek(w, a + b, lane);
+    const uint32_t v = win_lane_u8(w, a + b, lane);
+    if (lane < cnt) s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(v);
+    sink_advance<kProf>(s, cnt, lane);
+  }
+}
+
+template <bool kProf>
+__device__ __forceinline__ void copy_match(Sink& s, uint32_t off, uint32_t ml, uint32_t lane) {
+  // lane i of each 64-byte block copies from distance back = off * (1 + i / off): the periodic form
+  // of an overlapping copy, so every source byte is already final.
+  uint32_t back = off;
+  if (off < kWave) {
+    const uint32_t magic = (65536u + off - 1) / off;  // exact floor(lane / off) for lane, off < 64
+    back = off * (1 + ((lane * magic) >> 16));
+  }
+  if (off <= kRingReach) {
+    for (uint32_t b = 0; b < ml; b += kWave) {
+      const uint32_t cnt = ml - b < kWave ? ml - b : kWave;
+      const uint32_t o = s.op + lane;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < cnt) s.ring[(s.tmod + o) & kRingMask] = s.ring[(s.tmod + o - back) & kRingMask];
+      sink_advance<kProf>(s, cnt, lane);
+    }
+  } else {
+    for (uint32_t b = 0; b < ml; b += kWave) {
+      const uint32_t cnt = ml - b < kWave ? ml - b : kWave;
+      const uint32_t o = s.op + lane;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < cnt) s.ring[(s.tmod + o) & kRingMask] = uint8_t(load_u8_coherent(s.out + out_pos(s, o - back)));
+      sink_advance<kProf>(s, cnt, lane);
+    }
+  }
+}
+
+// One LZ4 block at stream positions [blk, blk + blen). Returns false on malformed input.
+template <bool kProf>
+__device__ bool lz4_block(Sink& s, Win& w, uint32_t blk, uint32_t blen, uint32_t lane) {
+  const uint32_t end = blk + blen;
+  uint32_t ip = blk;
   while (true) {
-    if (bp >= blen) return ~0u;
-    win_ensure(win, blk + bp, 32, lane);
-    const uint32_t token = win_byte(win, blk + bp);
-    ++bp;
+    if (ip >= end) return false;
+    win_seek(w, ip, lane);
+    const uint32_t token = win_u8(w, ip);
+    ++ip;
     uint32_t lit = token >> 4;
     if (lit == 15) {
       uint32_t b;
       do {
-        if (bp >= blen) return ~0u;
-        win_ensure(win, blk + bp, 1, lane);
-        b = win_byte(win, blk + bp);
-        ++bp;
+        if (ip >= end) return false;
+        win_seek(w, ip, lane);
+        b = win_u8(w, ip);
+        ++ip;
         lit += b;
       } while (b == 255);
     }
-    if (lit > blen - bp || lit > cap - op) return ~0u;
-    for (uint32_t i = 0; i < lit; i += kWave) {
-      win_ensure(win, blk + bp + i, kWave, lane);
-      const uint32_t v = win_lane_byte(win, blk + bp + i, lane);
-      if (i + lane < lit) lds[op + i + lane] = uint8_t(v);
+    if (lit > end - ip || lit > s.n - s.op) return false;
+    if (kProf) s.nseq++;
+    if (lit) {
+      const uint64_t t0 = kProf ? clk() : 0;
+      copy_literals<kProf>(s, w, ip, lit, lane);
+      if (kProf) {
+        s.t_lit += clk() - t0;
+        s.lit_bytes += lit;
+      }
     }
-    bp += lit;
-    op += lit;
-    if (bp == blen) return op;
-    if (blen - bp < 2) return ~0u;
-    win_ensure(win, blk + bp, 32, lane);
-    const uint32_t off = win_byte(win, blk + bp) | (win_byte(win, blk + bp + 1) << 8);
-    bp += 2;
-    if (off == 0 || off > op) return ~0u;
+    ip += lit;
+    if (ip == end) return true;  // last sequence: literals only
+    if (end - ip < 2) return false;
+    win_seek(w, ip, lane);
+    const uint32_t off = win_u8(w, ip) | (win_u8(w, ip + 1) << 8);
+    ip += 2;
+    if (off == 0 || off > s.op) return false;
     uint32_t ml = token & 15;
     if (ml == 15) {
       uint32_t b;
       do {
-        if (bp >= blen) return ~0u;
-        win_ensure(win, blk + bp, 1, lane);
-        b = win_byte(win, blk + bp);
-        ++bp;
+        if (ip >= end) return false;
+        win_seek(w, ip, lane);
+        b = win_u8(w, ip);
+        ++ip;
         ml += b;
       } while (b == 255);
     }
     ml += 4;
-    if (ml > cap - op) return ~0u;
-    if (off >= ml) {
-      for (uint32_t i = lane; i < ml; i += kWave) lds[op + i] = lds[op - off + i];
-    } else {
-      for (uint32_t i = lane; i < ml; i += kWave) lds[op + i] = lds[op - off + (i % off)];
+    if (ml > s.n - s.op) return false;
+    const uint64_t t0 = kProf ? clk() : 0;
+    copy_match<kProf>(s, off, ml, lane);
+    if (kProf) {
+      s.t_match += clk() - t0;
+      s.match_bytes += ml;
+      s.nfar += off > kRingReach;
+      s.nshort += off < kWave;
     }
-    op += ml;
   }
 }
 
-// Returns decoded length or ~0u on malformed frame.
-__device__ uint32_t lz4_frame(const uint8_t* payload, uint32_t clen, uint8_t* lds, uint32_t cap, uint32_t lane) {
-  const uintptr_t p = reinterpret_cast<uintptr_t>(payload);
-  Window win;
-  win_fill(win, p, lane);
-  if (clen < 7) return ~0u;
-  const uint32_t magic = win_byte(win, p) | (win_byte(win, p + 1) << 8) | (win_byte(win, p + 2) << 16) |
-                         (win_byte(win, p + 3) << 24);
-  if (magic != 0x184D2204u) return ~0u;
-  const uint32_t flg = win_byte(win, p + 4);
-  if ((flg >> 6) != 1) return ~0u;
+// Decode an LZ4 frame of clen bytes; returns false on malformed input.
+template <bool kProf>
+__device__ bool lz4_frame(Sink& s, const uint8_t* payload, uint32_t clen, uint32_t lane) {
+  Win w;
+  win_init(w, payload, lane);
+  const uint32_t k = uint32_t(reinterpret_cast<uintptr_t>(payload) & 3);  // stream pos = k + byte index
+  if (clen < 7) return false;
+  const uint32_t magic = win_u8(w, k) | (win_u8(w, k + 1) << 8) | (win_u8(w, k + 2) << 16) | (win_u8(w, k + 3) << 24);
+  if (magic != 0x184D2204u) return false;
+  const uint32_t flg = win_u8(w, k + 4);
+  if ((flg >> 6) != 1) return false;
   uint32_t ip = 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
   const bool block_ck = flg & 0x10;
-  uint32_t op = 0;
   while (true) {
-    if (clen - ip < 4 || ip > clen) return ~0u;
-    win_ensure(win, p + ip, 4, lane);
-    const uint32_t bs = win_byte(win, p + ip) | (win_byte(win, p + ip + 1) << 8) |
-                        (win_byte(win, p + ip + 2) << 16) | (win_byte(win, p + ip + 3) << 24);
+    if (ip > clen || clen - ip < 4) return false;
+    win_seek(w, k + ip, lane);
+    const uint32_t bs = win_u8(w, k + ip) | (win_u8(w, k + ip + 1) << 8) | (win_u8(w, k + ip + 2) << 16) |
+                        (win_u8(w, k + ip + 3) << 24);
     ip += 4;
-    if (bs == 0) break;
+    if (bs == 0) return true;
     const uint32_t len = bs & 0x7FFFFFFFu;
-    if (len > clen - ip) return ~0u;
+    if (len > clen - ip) return false;
     if (bs & 0x80000000u) {
-      if (len > cap - op) return ~0u;
-      for (uint32_t i = 0; i < len; i += kWave) {
-        win_ensure(win, p + ip + i, kWave, lane);
-        const uint32_t v = win_lane_byte(win, p + ip + i, lane);
-        if (i + lane < len) lds[op + i + lane] = uint8_t(v);
-      }
-      op += len;
-    } else {
-      op = lz4_block(win, p + ip, len, lds, op, cap, lane);
-      if (op == ~0u) return ~0u;
+      if (len > s.n - s.op) return false;
+      copy_literals<kProf>(s, w, k + ip, len, lane);
+    } else if (!lz4_block<kProf>(s, w, k + ip, len, lane)) {
+      return false;
     }
     ip += len + (block_ck ? 4 : 0);
   }
-  return op;
 }
 
-// Store LDS chunk bytes to dst[lo, hi) (chunk-relative [lo - base, hi - base)), applying the
-// BG4 regroup when `bg4`: original byte j = grouped[goff[j & 3] + (j >> 2)].
-__device__ void store_from_lds(const uint8_t* lds, uint32_t ulen, bool bg4, uint8_t* dst_chunk, uint32_t lo,
-                               uint32_t hi, uint32_t lane) {
-  const uint32_t q = ulen >> 2, r = ulen & 3;
-  const uint32_t g1 = q + (r > 0 ? 1 : 0);
-  const uint32_t g2 = g1 + q + (r > 1 ? 1 : 0);
-  const uint32_t g3 = g2 + q + (r > 2 ? 1 : 0);
-  auto src_of = [&](uint32_t j) -> uint32_t {
-    if (!bg4) return j;
-    const uint32_t g = j & 3, i = j >> 2;
-    const uint32_t base = g == 0 ? 0 : g == 1 ? g1 : g == 2 ? g2 : g3;
-    return base + i;
-  };
-  // head bytes until dst 4-aligned
-  const uintptr_t da = reinterpret_cast<uintptr_t>(dst_chunk + lo);
-  uint32_t head = uint32_t((4 - (da & 3)) & 3);
-  if (head > hi - lo) head = hi - lo;
-  if (lane < head) dst_chunk[lo + lane] = lds[src_of(lo + lane)];
-  const uint32_t s = lo + head;
-  const uint32_t nw = (hi - s) >> 2;
-  uint32_t* dw = reinterpret_cast<uint32_t*>(dst_chunk + s);
-  for (uint32_t w = lane; w < nw; w += kWave) {
-    const uint32_t j = s + 4 * w;
-    uint32_t v;
-    if (!bg4) {
-      v = uint32_t(lds[j]) | (uint32_t(lds[j + 1]) << 8) | (uint32_t(lds[j + 2]) << 16) | (uint32_t(lds[j + 3]) << 24);
-    } else {
-      v = uint32_t(lds[src_of(j)]) | (uint32_t(lds[src_of(j + 1)]) << 8) | (uint32_t(lds[src_of(j + 2)]) << 16) |
-          (uint32_t(lds[src_of(j + 3)]) << 24);
-    }
-    dw[w] = v;
-  }
-  const uint32_t t = s + 4 * nw;
-  if (lane < hi - t) dst_chunk[t + lane] = lds[src_of(t + lane)];
-}
-
-__global__ void __launch_bounds__(64) k_decode_lz4(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                   const ZgChunk* __restrict__ chunks, int n_chunks,
-                                                   uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
-                                                   uint32_t lds_cap, uint64_t src_n, uint64_t dst_n) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+template <bool kProf>
+__global__ void __launch_bounds__(256) k_decode_lz4(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    const ZgChunk* __restrict__ chunks, int n_chunks,
+                                                    uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
+                                                    uint64_t src_n, uint64_t dst_n) {
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][kRing];
   const uint32_t lane = lane_id();
-  for (int c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+  const int wave = wave_uniform(int(threadIdx.x >> 6));
+  const int stride = int(gridDim.x) * kWavesPerBlock;
+  uint64_t prof[10] = {};
+  for (int c = wave_uniform(int(blockIdx.x) * kWavesPerBlock + wave); c < n_chunks; c += stride) {
     const ZgChunk ch = chunks[c];
     if (ch.scheme == 0) continue;
     if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
-      report(err, ZG_ERR_RANGE, uint32_t(c));
+      if (lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
       continue;
     }
-    const uint64_t lo = ch.dst > clip_lo ? ch.dst : clip_lo;
+    if (ch.ulen > kMaxChunk) {
+      if (lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      continue;
+    }
     const uint64_t end = ch.dst + ch.ulen;
+    const uint64_t lo = ch.dst > clip_lo ? ch.dst : clip_lo;
     const uint64_t hi = end < clip_hi ? end : clip_hi;
     if (lo >= hi) continue;
-    if (ch.ulen > lds_cap) {
-      report(err, ZG_ERR_CAPACITY, uint32_t(c));
+    const bool clipped = lo != ch.dst || hi != end;
+    const uint64_t t_start = kProf ? clk() : 0;
+    Sink s{};
+    s.ring = rings[wave];
+    s.out = clipped ? g_clip_scratch[ch.dst < clip_lo ? 0 : 1] : dst + ch.dst;
+    s.bg4 = ch.scheme == 2;
+    s.tmod = s.bg4 ? 0u : uint32_t(reinterpret_cast<uintptr_t>(s.out) & kRingMask);
+    s.n = ch.ulen;
+    const uint32_t q = ch.ulen >> 2, r = ch.ulen & 3;
+    s.g1 = q + (r > 0 ? 1u : 0u);
+    s.g2 = s.g1 + q + (r > 1 ? 1u : 0u);
+    s.g3 = s.g2 + q + (r > 2 ? 1u : 0u);
+    const bool ok = lz4_frame<kProf>(s, src + ch.src, ch.clen, lane);
+    if (!ok) {
+      if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
       continue;
     }
-    const uint32_t got = lz4_frame(src + ch.src, ch.clen, lds, ch.ulen, lane);
-    if (got == ~0u) {
-      report(err, ZG_ERR_LZ4, uint32_t(c));
+    if (s.op != ch.ulen) {
+      if (lane == 0) report(err, ZG_ERR_SIZE, uint32_t(c));
       continue;
     }
-    if (got != ch.ulen) {
-      report(err, ZG_ERR_SIZE, uint32_t(c));
-      continue;
+    sink_flush(s, s.op, true, lane);
+    if (kProf) {
+      const uint64_t v[10] = {s.t_lit, s.t_match, s.t_flush, clk() - t_start, s.nseq,
+                              s.lit_bytes, s.match_bytes, s.nfar, s.nflush, s.nshort};
+      for (int i = 0; i < 10; ++i) prof[i] += v[i];
     }
-    store_from_lds(lds, ch.ulen, ch.scheme == 2, dst + ch.dst, uint32_t(lo - ch.dst), uint32_t(hi - ch.dst), lane);
+    if (clipped) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t a = uint32_t(lo - ch.dst), len = uint32_t(hi - lo);
+      for (uint32_t i = lane; i < len; i += kWave) dst[lo + i] = uint8_t(load_u8_coherent(s.out + a + i));
+    }
   }
+  if (kProf && lane == 0)
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_lz4_prof[i], (unsigned long long)prof[i]);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -492,17 +645,34 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                      dst, chunks, n_chunks, clip_lo, clip_hi, src_n, dst_n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t cap = kMaxChunk;
-  const size_t lds = cap + 16;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_lz4), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        int(lds));
-    attr_set = true;
+  // Persistent grid: up to 5 blocks (20 waves) per CU on 256 CUs.
+  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int grid = blocks < 1280 ? blocks : 1280;
+  static const bool prof = [] {
+    const char* v = getenv("ZG_LZ4_PROF");
+    return v && *v && *v != '0';
+  }();
+  if (prof) {
+    unsigned long long zero[10] = {};
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lz4_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, stream);
   }
-  const int grid = n_chunks < 1024 ? n_chunks : 1024;
-  hipLaunchKernelGGL(k_decode_lz4, dim3(grid), dim3(64), lds, stream, src, dst, chunks, n_chunks, clip_lo, clip_hi,
-                     err, cap, src_n, dst_n);
+  if (prof)
+    hipLaunchKernelGGL(k_decode_lz4<true>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
+                       clip_hi, err, src_n, dst_n);
+  else
+    hipLaunchKernelGGL(k_decode_lz4<false>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
+                       clip_hi, err, src_n, dst_n);
+  if (prof) {
+    unsigned long long v[10];
+    hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lz4_prof), sizeof v, 0, hipMemcpyDeviceToHost, stream);
+    hipStreamSynchronize(stream);
+    if (v[4])
+      fprintf(stderr,
+              "{\"lz4_prof\": {\"chunks\": %d, \"t_lit\": %llu, \"t_match\": %llu, \"t_flush\": %llu, \"t_total\": %llu, "
+              "\"nseq\": %llu, \"lit_bytes\": %llu, \"match_bytes\": %llu, \"nfar\": %llu, \"nflush\": %llu, "
+              "\"nshort\": %llu}}\n",
+              n_chunks, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9]);
+  }
   return hipGetLastError();
 }
 

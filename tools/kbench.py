@@ -121,48 +121,73 @@ def main():
         emit(kernel="hash_chunks", bytes=n, ms=ms, gbps=n / ms / 1e6)
         del body, dst
 
+    def ingest_case(name, raw, policy, iters):
+        """Pack `raw` into xorb runs with `policy`, then time index+place/decode+hash on the GPU."""
+        m = len(raw)
+        ends = C.chunk_ends(raw)
+        b = C.XorbBuilder(policy)
+        prev, terms_l, bodies, src_off, cbase, schemes = 0, [], [], 0, 0, {}
+
+        def close():
+            nonlocal src_off, cbase
+            body_b = b.serialize(False)
+            for e in C.index_chunks(body_b):
+                schemes[e[2]] = schemes.get(e[2], 0) + 1
+            bodies.append(body_b)
+            terms_l.append((src_off, len(body_b), cbase, b.num_chunks(), b.unpacked_size()))
+            src_off += len(body_b)
+            cbase += b.num_chunks()
+            b.clear()
+
+        for e in ends:
+            if not b.fits(e - prev):
+                close()
+            b.add_chunk(raw[prev:e])
+            prev = e
+        close()
+        blob = b"".join(bodies)
+        terms = np.zeros(len(terms_l), dtype=ops.TERM_DTYPE)
+        uo = 0
+        for i, t in enumerate(terms_l):
+            terms[i] = (t[0], t[1], uo, t[2], t[3], t[4])
+            uo += t[4]
+        src = ops.padded_empty(len(blob), dev)
+        src.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+        dst = ops.padded_empty(m, dev)
+        nck2 = int(terms["n_chunks"].sum())
+        hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
+        ws = ops.IngestWorkspace(dev, len(terms), nck2)
+        ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
+        ops.raise_on_error(ws.err)
+        ok = dst[:m].cpu().numpy().tobytes() == raw
+        emit(kernel=f"ingest_{policy}({name})", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
+             chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
+        assert ok, name
+        del src, dst, hashes, ws
+
     if want("lz4"):
-        # bf16-like data, compressed on the host (LZ4 / BG4 frames), decoded on the GPU
+        # bf16-like weights, compressed on the host (LZ4 / BG4 frames), decoded on the GPU
         m = min(n, 256 << 20)
         w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
         raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
-        ends = C.chunk_ends(raw)
         for policy in ("lz4", "bg4"):
-            b = C.XorbBuilder(policy)
-            prev = 0
-            terms_l = []
-            bodies = []
-            src_off = 0
-            cbase = 0
-            for e in ends:
-                if not b.fits(e - prev):
-                    body_b = b.serialize(False)
-                    bodies.append(body_b)
-                    terms_l.append((src_off, len(body_b), 0, cbase, b.num_chunks(), b.unpacked_size()))
-                    src_off += len(body_b)
-                    cbase += b.num_chunks()
-                    b.clear()
-                b.add_chunk(raw[prev:e])
-                prev = e
-            body_b = b.serialize(False)
-            bodies.append(body_b)
-            terms_l.append((src_off, len(body_b), 0, cbase, b.num_chunks(), b.unpacked_size()))
-            blob = b"".join(bodies)
-            terms = np.zeros(len(terms_l), dtype=ops.TERM_DTYPE)
-            uo = 0
-            for i, t in enumerate(terms_l):
-                terms[i] = (t[0], t[1], uo, t[3], t[4], t[5])
-                uo += t[5]
-            src = ops.padded_empty(len(blob), dev)
-            src.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
-            dst = ops.padded_empty(m, dev)
-            nck2 = int(terms["n_chunks"].sum())
-            hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
-            ws = ops.IngestWorkspace(dev, len(terms), nck2)
-            ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), a.iters)
-            ops.raise_on_error(ws.err)
-            assert dst.cpu().numpy().tobytes() == raw[:m]
-            emit(kernel=f"ingest_{policy}(bf16)", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m)
+            ingest_case("bf16", raw, policy, a.iters)
+
+    if want("lz4paths"):
+        # one decoder path per data set: short matches, long literal runs, RLE, far matches
+        m = 64 << 20
+        rng = np.random.default_rng(1)
+        sets = {
+            "lowent": rng.integers(0, 8, m, dtype=np.uint8) * 31,
+            "sparse": np.where(rng.random(m) < 0.02, rng.integers(0, 256, m), 0).astype(np.uint8),
+            "mostly_random": np.where(rng.random(m) < 0.85, rng.integers(0, 256, m), 7).astype(np.uint8),
+        }
+        phrase = rng.integers(0, 256, 40_000, dtype=np.uint8)
+        far = np.resize(phrase, m).copy()
+        far[rng.integers(0, m, m // 64)] = rng.integers(0, 256, m // 64, dtype=np.uint8)
+        sets["far_repeats"] = far
+        for name, arr in sets.items():
+            ingest_case(name, arr.tobytes(), "lz4", a.iters)
 
     if want("merkle"):
         nl = 80_000
