@@ -16,6 +16,8 @@
 #include "bt_wire.h"
 #include "config.h"
 #include "dht.h"
+#include "http.h"
+#include "hub.h"
 #include "pull.h"
 #include "sha1.h"
 #include "storage.h"
@@ -432,6 +434,15 @@ void bind_extra(py::module_& m) {
         py::gil_scoped_release nogil;
         d.stop();
       });
+
+  // ---------------- small helpers (HTTP / hub) ----------------
+  m.def("percent_encode", [](py::bytes b) {
+    std::string s = b;
+    return http::percent_encode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  m.def("percent_decode", [](std::string s) { return pyb(http::percent_decode(s)); });
+  m.def("extract_json_sha", [](std::string s) { return hub::extract_json_sha(s); });
+  m.def("parse_reconstruction", [](std::string s) { return cas::reconstruction_to_json(cas::parse_reconstruction(s)); });
 
   // ---------------- config / cache ----------------
   m.def("config_json", []() { return Config::from_env().to_json(); });

@@ -97,7 +97,8 @@ std::string Config::to_json() const {
   json::Writer w;
   w.obj();
   w.key("version").str(kVersion).key("hub_url").str(hub_url).key("hf_cache_dir").str(hf_cache_dir);
-  w.key("cache_dir").str(cache_dir).key("dht_port").num(int64_t(dht_port)).key("listen_port").num(int64_t(listen_port));
+  w.key("cache_dir").str(cache_dir).key("xorb_cache_dir").str(xorb_cache_dir).key("chunk_cache_dir").str(chunk_cache_dir);
+  w.key("pid_file").str(pid_file).key("dht_port").num(int64_t(dht_port)).key("listen_port").num(int64_t(listen_port));
   w.key("http_port").num(int64_t(http_port)).key("max_peers").num(int64_t(max_peers));
   w.key("concurrency").num(int64_t(concurrency)).key("has_token").boolean(hf_token.has_value());
   w.key("gpus").num(int64_t(gpus)).key("hbm_cache_gb").num(hbm_cache_gb, 1);
