@@ -197,7 +197,8 @@ class FakeHub:
         f = self.file_index.get(file_hash)
         if f is None:
             return None
-        terms_out, fetch = [], {}
+        terms_out = []
+        ranges: dict[int, list[list[int]]] = {}
         pos = 0
         offset_into_first = 0
         for (x, c0, c1) in f.terms:
@@ -212,14 +213,33 @@ class FakeHub:
                 if not terms_out:
                     offset_into_first = max(0, a - t_start)
             terms_out.append({"hash": xb.hash_hex, "unpacked_length": ulen, "range": {"start": c0, "end": c1}})
-            lo = xb.boundaries[c0 - 1] if c0 > 0 else 0
-            hi = xb.boundaries[c1 - 1] - 1
-            ent = {"range": {"start": c0, "end": c1}, "url": f"{self.url}/xorbs/default/{xb.hash_hex}",
-                   "url_range": {"start": lo, "end": hi}}
-            lst = fetch.setdefault(xb.hash_hex, [])
-            if ent not in lst:
-                lst.append(ent)
+            ranges.setdefault(x, []).append([c0, c1])
+        # Like the real CAS: per xorb, one fetch entry per maximal union of the terms' chunk ranges,
+        # so every term lies inside exactly one entry (hf_xet relies on this).
+        fetch = {}
+        for x, rs in ranges.items():
+            rs.sort()
+            merged = [rs[0][:]]
+            for a, b in rs[1:]:
+                if a <= merged[-1][1]:
+                    merged[-1][1] = max(merged[-1][1], b)
+                else:
+                    merged.append([a, b])
+            xb = self.xorbs[x]
+            fetch[xb.hash_hex] = [{"range": {"start": a, "end": b}, "url": self._presign(xb.hash_hex),
+                                   "url_range": {"start": xb.boundaries[a - 1] if a > 0 else 0,
+                                                 "end": xb.boundaries[b - 1] - 1}} for a, b in merged]
         return {"offset_into_first_range": offset_into_first, "terms": terms_out, "fetch_info": fetch}
+
+    def _presign(self, hx: str) -> str:
+        # Like S3 presigned URLs, the xorb URL carries its own authorization (clients such as hf_xet
+        # fetch it without the CAS bearer token).
+        sig = hashlib.sha256(f"{self.token}:{hx}".encode()).hexdigest()[:32]
+        return f"{self.url}/xorbs/default/{hx}?X-Zest-Signature={sig}"
+
+    def _presign_ok(self, hx: str, query: dict) -> bool:
+        want = hashlib.sha256(f"{self.token}:{hx}".encode()).hexdigest()[:32]
+        return query.get("X-Zest-Signature", [""])[0] == want
 
     def file(self, repo_id: str, path: str, repo_type: str = "model") -> bytes:
         return self.repos[(repo_type, repo_id)].files[path].data
@@ -339,7 +359,7 @@ class FakeHub:
         if parts[0] == "reconstruction" and len(parts) == 2:
             return self._json(h, {"error": "not found"}, 404)
         if parts[0] == "xorbs" and len(parts) == 3:
-            return self._xorb(h, parts[2])
+            return self._xorb(h, parts[2], q)
         # ---- hub API
         if parts[0] == "api" and len(parts) >= 5 and parts[1] in ("models", "datasets", "spaces"):
             kind = parts[1][:-1]
@@ -412,8 +432,8 @@ class FakeHub:
             return self._send(h, 200, data, "application/octet-stream", hdr)
         return self._json(h, {"error": "not found"}, 404)
 
-    def _xorb(self, h, hx: str) -> None:
-        if not self._cas_authorized(h):
+    def _xorb(self, h, hx: str, query: dict | None = None) -> None:
+        if not self._cas_authorized(h) and not self._presign_ok(hx, query or {}):
             return self._json(h, {"error": "unauthorized"}, 401)
         idx = self.xorb_index.get(hx)
         if idx is None:
