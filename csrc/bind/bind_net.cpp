@@ -495,6 +495,52 @@ void bind_extra(py::module_& m) {
     return py::make_tuple(pyb(r.data), r.chunk_offset, client);
   }, py::arg("addr"), py::arg("xorb_hash"), py::arg("start"), py::arg("end"), py::arg("timeout_ms") = 5000);
 
+  // Persistent BEP XET client connection (pipelined requests; any xorb over one connection).
+  py::class_<bt::PeerSession, std::shared_ptr<bt::PeerSession>>(m, "PeerConnection")
+      .def(py::init([](std::string addr, py::bytes first_xorb, int timeout_ms) {
+             auto a = net::Addr::parse(addr, 6881);
+             auto h = arr_of<32>(first_xorb, "xorb hash");
+             py::gil_scoped_release nogil;
+             return bt::PeerSession::connect(a, peer_id::info_hash(h.data()), peer_id::generate(), 0, timeout_ms);
+           }),
+           py::arg("addr"), py::arg("xorb_hash"), py::arg("timeout_ms") = 5000)
+      .def_property_readonly("supports_xet", &bt::PeerSession::supports_xet)
+      .def_property_readonly("client", &bt::PeerSession::client)
+      .def("fetch", [](bt::PeerSession& s, py::bytes xorb_hash, uint32_t a, uint32_t b, int timeout_ms) {
+        bt::XetRequest r;
+        r.xorb_hash = arr_of<32>(xorb_hash, "xorb hash");
+        r.range_start = a;
+        r.range_end = b;
+        bt::ChunkResult res;
+        {
+          py::gil_scoped_release nogil;
+          res = s.request(r, timeout_ms);
+        }
+        return py::make_tuple(pyb(res.data), res.chunk_offset);
+      }, py::arg("xorb_hash"), py::arg("start"), py::arg("end"), py::arg("timeout_ms") = 30000)
+      .def("fetch_many_bytes", [](bt::PeerSession& s, std::vector<py::bytes> hashes, std::vector<uint32_t> starts,
+                                  std::vector<uint32_t> ends, int timeout_ms) {
+        // Pipelined; returns total payload bytes (the data is discarded: for load generation).
+        std::vector<bt::XetRequest> reqs(hashes.size());
+        for (size_t i = 0; i < hashes.size(); ++i) {
+          reqs[i].xorb_hash = arr_of<32>(hashes[i], "xorb hash");
+          reqs[i].range_start = starts.at(i);
+          reqs[i].range_end = ends.at(i);
+        }
+        uint64_t total = 0;
+        size_t failed = 0;
+        {
+          py::gil_scoped_release nogil;
+          std::vector<std::string> errs;
+          auto res = s.request_many(reqs, timeout_ms, &errs);
+          for (size_t i = 0; i < res.size(); ++i) {
+            total += res[i].data.size();
+            if (i < errs.size() && !errs[i].empty()) failed++;
+          }
+        }
+        return py::make_tuple(total, failed);
+      }, py::arg("hashes"), py::arg("starts"), py::arg("ends"), py::arg("timeout_ms") = 60000);
+
   // ---------------- pull ----------------
   m.def("pull", [](std::string repo, std::string revision, bool p2p, std::vector<std::string> peers,
                    std::optional<std::string> tracker_url, bool dht, std::vector<std::string> dht_bootstrap,

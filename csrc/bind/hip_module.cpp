@@ -12,6 +12,8 @@
 
 namespace py = pybind11;
 
+void bind_hip_seed(py::module_& m);  // hip_seed.cpp
+
 namespace {
 
 template <typename T>
@@ -32,6 +34,7 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("CHUNK_BYTES") = sizeof(ZgChunk);
   m.attr("MERKLE_JOB_BYTES") = sizeof(ZgMerkleJob);
   m.attr("ARCH") = "gfx950";
+  bind_hip_seed(m);
 
   m.def("device_count", &zg_device_count);
   // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host

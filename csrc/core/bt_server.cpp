@@ -67,6 +67,7 @@ ServerStats BtServer::stats() const {
   s.chunks_served = served_.load();
   s.bytes_served = bytes_.load();
   s.not_found = nf_.load();
+  s.chunk_units = units_.load();
   return s;
 }
 
@@ -165,13 +166,17 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
       s.write_all(out.data(), out.size());
       continue;
     }
-    if (fault_.corrupt > 0 && u01(rng) < fault_.corrupt && !hit->data.empty()) hit->data[hit->data.size() / 2] ^= 0x5A;
+    if (fault_.corrupt > 0 && u01(rng) < fault_.corrupt && hit->size()) {
+      hit->materialize();
+      hit->data[hit->data.size() / 2] ^= 0x5A;
+    }
     bep_xet::encode_chunk_response_header(out, uint8_t(peer_xet), x.request_id, hit->chunk_offset,
-                                          uint32_t(hit->data.size()));
-    iovec iov[2] = {{out.data(), out.size()}, {hit->data.data(), hit->data.size()}};
+                                          uint32_t(hit->size()));
+    iovec iov[2] = {{out.data(), out.size()}, {const_cast<uint8_t*>(hit->bytes()), hit->size()}};
     s.writev_all(iov, 2);
     served_++;
-    bytes_ += hit->data.size();
+    bytes_ += hit->size();
+    if (x.range_end > x.range_start) units_ += x.range_end - x.range_start;
   }
 }
 

@@ -35,6 +35,7 @@ struct ServerStats {
   uint64_t chunks_served = 0;
   uint64_t bytes_served = 0;
   uint64_t not_found = 0;
+  uint64_t chunk_units = 0;  // Xet chunks delivered (sum of requested range lengths)
 };
 
 struct FaultSpec {
@@ -68,7 +69,7 @@ class BtServer {
   std::mutex mu_;
   std::set<int> conns_;
   std::vector<std::thread> workers_;
-  std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0};
+  std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0};
   FaultSpec fault_;
 };
 

@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <optional>
 #include <set>
@@ -41,6 +42,21 @@ std::vector<std::string> list_cached_xorbs(const Config& cfg);
 struct CacheHit {
   Bytes data;
   uint32_t chunk_offset = 0;  // chunk index of data's first chunk inside the xorb
+  // Zero-copy alternative to `data` (e.g. a pinned staging buffer filled from HBM), valid while
+  // `keep` is held.
+  const uint8_t* ext = nullptr;
+  size_t ext_len = 0;
+  std::shared_ptr<void> keep;
+  const uint8_t* bytes() const { return ext ? ext : data.data(); }
+  size_t size() const { return ext ? ext_len : data.size(); }
+  void materialize() {  // copy an external view into `data`
+    if (ext) {
+      data.assign(ext, ext + ext_len);
+      ext = nullptr;
+      ext_len = 0;
+      keep.reset();
+    }
+  }
 };
 
 // Slice a run (first chunk = `offset`) to chunks [start, end); nullopt if it does not cover them.

@@ -121,7 +121,7 @@ def build(only: str | None = None, jobs: int | None = None, debug: bool = False,
     core_objs = b.compile(core_sources(), "core")
     ssl_libs = ["-lssl", "-lcrypto"]
     if only in (None, "core"):
-        bind_srcs = sorted(p for p in (CSRC / "bind").glob("*.cpp") if p.name != "hip_module.cpp")
+        bind_srcs = sorted(p for p in (CSRC / "bind").glob("*.cpp") if not p.name.startswith("hip_"))
         bind = b.compile(bind_srcs, "bind",
                          extra=[f"-I{_pybind_include()}", f"-I{_py_include()}", "-fvisibility=hidden"])
         out = PKG / f"_core{EXT}"
@@ -130,7 +130,7 @@ def build(only: str | None = None, jobs: int | None = None, debug: bool = False,
     if only in (None, "hip"):
         gpu_srcs = sorted((CSRC / "gpu").glob("*.hip"))
         gpu_objs = b.compile(gpu_srcs, "gpu", hip=True)
-        hbind = b.compile([CSRC / "bind" / "hip_module.cpp"], "hbind", hip=True,
+        hbind = b.compile(sorted((CSRC / "bind").glob("hip_*.cpp")), "hbind", hip=True,
                           extra=[f"-I{_pybind_include()}", f"-I{_py_include()}", "-fvisibility=hidden"])
         out = PKG / f"_hip{EXT}"
         b.link(gpu_objs + hbind + core_objs, out, shared=True,

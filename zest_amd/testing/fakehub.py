@@ -31,6 +31,8 @@ import urllib.parse
 from dataclasses import dataclass, field
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
+import numpy as np
+
 from .. import _core
 
 MAX_XORB_BYTES = 64 << 20
@@ -123,11 +125,43 @@ class FakeHub:
         self.repos[key].revisions[commit] = commit
         return commit
 
-    def add_world(self, world, revision: str = "main") -> str:
-        """Publish a zest_amd.synthetic.SyntheticWorld (host-generated bytes)."""
+    def add_world(self, world, revision: str = "main", exact: bool = False) -> str:
+        """Publish a zest_amd.synthetic.SyntheticWorld (host-generated bytes).
+
+        exact=True reuses the world's own xorb layout (so xorb hashes match what a device-built
+        world / HBM seeder holds); otherwise the files are re-packed by this hub like any upload."""
         files = {f.path: world.file_bytes_host(f) for f in world.files}
-        return self.add_repo(world.spec.repo_id, files, revision=revision,
-                             xet_suffixes=(".safetensors",), commit=world.commit)
+        if not exact:
+            return self.add_repo(world.spec.repo_id, files, revision=revision,
+                                 xet_suffixes=(".safetensors",), commit=world.commit)
+        if world.terms is None:
+            world.build_on_host()
+        contents = {f.path: files[f.path] for f in world.xet_files}
+        base = len(self.xorbs)
+        with self.lock:
+            for x in range(world.n_xorbs):
+                data = world.xorb_bytes_host(x, contents, policy="none", footer=True)
+                a = int(world.xorb_chunk0[x])
+                b = int(world.xorb_chunk0[x + 1]) if x + 1 < world.n_xorbs else world.n_chunks
+                ser = world.chunk_len[a:b].astype(np.int64) + 8
+                hx = world.xorb_hash_hex(x)
+                self.xorbs.append(_Xorb(data, hx, np.cumsum(ser).tolist(), world.chunk_len[a:b].tolist()))
+                self.xorb_index[hx] = base + x
+            out = {}
+            for i, f in enumerate(world.files):
+                ff = _File(f.path, files[f.path])
+                if f.xet:
+                    fi = world.xet_files.index(f)
+                    T = world.terms[world.terms["file"] == fi]
+                    ff.xet_hash = world.file_hash_hex(fi)
+                    ff.terms = [(base + int(t["xorb"]), int(t["local0"]), int(t["local0"] + t["c1"] - t["c0"]))
+                                for t in T]
+                    self.file_index[ff.xet_hash] = ff
+                out[f.path] = ff
+        key = ("model", world.spec.repo_id)
+        self.repos[key] = _Repo(world.spec.repo_id, "model", world.commit, out,
+                                {revision: world.commit, world.commit: world.commit})
+        return world.commit
 
     def _ingest(self, f: _File) -> None:
         data = f.data
