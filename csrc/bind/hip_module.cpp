@@ -98,6 +98,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fill_synthetic", [](uintptr_t dst, uint64_t n, uint64_t seed, uint64_t off, int mode, uintptr_t st) {
     check(zg_fill_synthetic(P<uint8_t>(dst), n, seed, off, mode, S(st)), "zg_fill_synthetic");
   });
+  m.def("sha1_info_hash", [](uintptr_t hashes, int n, uintptr_t out, uintptr_t st) {
+    check(zg_sha1_info_hash(P<const uint8_t>(hashes), n, P<uint8_t>(out), S(st)), "zg_sha1_info_hash");
+  });
   m.def("pack_chunks", [](uintptr_t data, uintptr_t data_off, uintptr_t lens, uintptr_t out_off, int n, uintptr_t out,
                           uintptr_t st) {
     check(zg_pack_chunks(P<const uint8_t>(data), P<const uint64_t>(data_off), P<const uint32_t>(lens),

@@ -234,3 +234,14 @@ def test_fill_synthetic_deterministic():
     ops.fill_synthetic(f, 7, 0, 1)
     v = f.view(torch.bfloat16).float()
     assert abs(v.std().item() - 0.02) < 0.002 and abs(v.mean().item()) < 0.002
+
+
+def test_sha1_info_hash_kernel():
+    import hashlib
+
+    g = torch.Generator().manual_seed(3)
+    hs = torch.randint(0, 256, (1000, 32), dtype=torch.uint8, generator=g)
+    got = ops.sha1_info_hash(hs.cuda()).cpu().numpy()
+    for i in range(0, 1000, 37):
+        assert got[i].tobytes() == hashlib.sha1(b"zest-xet-v1:" + hs[i].numpy().tobytes()).digest()
+    assert ops.sha1_info_hash(hs[:0].cuda()).shape == (0, 20)

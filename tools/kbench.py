@@ -189,6 +189,23 @@ def main():
         for name, arr in sets.items():
             ingest_case(name, arr.tobytes(), "lz4", a.iters)
 
+    if want("sha1"):
+        # K6 parity row: sha1_info_hash over many xorb hashes at once (reference: 1 hash, 55 ns on a CPU core)
+        nh = 1 << 22
+        hs = torch.randint(0, 256, (nh, 32), dtype=torch.uint8, device=dev)
+        ms = timed(lambda: ops.sha1_info_hash(hs), a.iters)
+        emit(kernel="sha1_info_hash_gpu", hashes=nh, ms=ms, ns_per_hash=ms * 1e6 / nh,
+             mbps=nh * 44 / (ms / 1e3) / 2**20)
+        del hs
+
+    if want("blake3_64kb"):
+        # parity row blake3_64kb_gpu: plain BLAKE3 of many 64 KiB buffers
+        nb = 1 << 15
+        offs = np.arange(nb, dtype=np.uint64) * 65536
+        lens = np.full(nb, 65536, dtype=np.uint32)
+        ms = timed(lambda: ops.hash_ranges(arena, offs, lens, key_mode=2), a.iters)
+        emit(kernel="blake3_64kb_gpu", bytes=nb * 65536, ms=ms, mbps=nb * 65536 / (ms / 1e3) / 2**20)
+
     if want("merkle"):
         nl = 80_000
         hs = torch.randint(0, 256, (nl * 8, 32), dtype=torch.uint8, device=dev)

@@ -330,6 +330,19 @@ def fill_synthetic(t: torch.Tensor, seed: int, stream_offset: int = 0, mode: int
     H.fill_synthetic(u8.data_ptr(), u8.numel(), seed & 0xFFFFFFFFFFFFFFFF, stream_offset, mode, _stream(t.device))
 
 
+def sha1_info_hash(xorb_hashes: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, 32] xorb hashes -> uint8 [n, 20] BitTorrent info-hashes (K6)."""
+    n = xorb_hashes.shape[0]
+    if xorb_hashes.device.type != "cuda":
+        hs = xorb_hashes.numpy()
+        return torch.from_numpy(np.stack([np.frombuffer(_core.info_hash(hs[i].tobytes()), dtype=np.uint8)
+                                          for i in range(n)]) if n else np.zeros((0, 20), np.uint8))
+    src = xorb_hashes.contiguous()
+    out = torch.empty((n, 20), dtype=torch.uint8, device=src.device)
+    hip().sha1_info_hash(src.data_ptr(), n, out.data_ptr(), _stream(src.device))
+    return out
+
+
 def pack_chunks(data: torch.Tensor, data_off: np.ndarray, lens: np.ndarray, out_off: np.ndarray,
                 out: torch.Tensor) -> None:
     """Serialize uncompressed chunks (8-byte header + payload) into `out` at out_off."""
