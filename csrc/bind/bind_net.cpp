@@ -21,6 +21,7 @@
 #include "pull.h"
 #include "sha1.h"
 #include "storage.h"
+#include "trace.h"
 #include "tracker.h"
 #include "xet_hash.h"
 
@@ -587,6 +588,21 @@ void bind_extra(py::module_& m) {
      py::arg("include") = std::vector<std::string>{}, py::arg("verify") = true, py::arg("concurrency") = 0,
      py::arg("repo_type") = "model");
   m.def("server_healthy", &server_healthy, py::arg("http_port"), py::arg("timeout_ms") = 1000);
+
+  // ---------------- tracing (shared with the C++ spans) ----------------
+  auto mtr = m.def_submodule("trace", "host tracing: ZEST_TRACE=1 (log) or ZEST_TRACE=file.json (Chrome trace)");
+  mtr.def("enabled", &trace::enabled);
+  mtr.def("mode", &trace::mode);
+  mtr.def("now_us", &trace::now_us);
+  mtr.def("log", [](const std::string& cat, const std::string& msg) { trace::log(cat.c_str(), msg); });
+  mtr.def("complete", [](const std::string& cat, const std::string& name, uint64_t ts, uint64_t dur,
+                         const std::string& args) {
+    // cat must outlive the call only; complete() copies it into the event string
+    trace::complete(cat.c_str(), name, ts, dur, args);
+  }, py::arg("cat"), py::arg("name"), py::arg("ts_us"), py::arg("dur_us"), py::arg("args_json") = "");
+  mtr.def("counter", &trace::counter);
+  mtr.def("flush", &trace::flush);
+  mtr.def("set_output", &trace::set_output);
 
   // ---------------- synthetic bench ----------------
   m.def("bench_synthetic", [](bool extended) {
