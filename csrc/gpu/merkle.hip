@@ -11,8 +11,9 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr uint32_t kMsgBytes = 1024;  // 9 children * (64 + 3 + 20 + 1) = 792 < 1024
+constexpr int kThreads = 1024;
+constexpr uint32_t kMsgBytes = 1024;
+constexpr uint32_t kLdsFlagWords = 4096;  // cut flags of levels with <= 131072 nodes live in LDS  // 9 children * (64 + 3 + 20 + 1) = 792 < 1024
 
 struct JobScratch {
   uint8_t* hash_a;   // [n][32]
@@ -52,6 +53,15 @@ __device__ inline JobScratch carve(uint8_t* base, uint64_t n) {
   return s;
 }
 
+__device__ inline uint32_t ndigits(uint64_t v) {
+  uint32_t d = 1;
+  while (v >= 10) {
+    v /= 10;
+    ++d;
+  }
+  return d;
+}
+
 __device__ inline uint32_t put_line(uint8_t* m, uint32_t pos, const uint8_t* h, uint64_t size) {
   const char* hex = "0123456789abcdef";
   for (int w = 0; w < 4; ++w) {
@@ -82,6 +92,11 @@ __global__ void __launch_bounds__(kThreads) k_merkle(const uint8_t* __restrict__
                                                      const ZgMerkleJob* __restrict__ jobs, uint8_t* __restrict__ roots,
                                                      uint8_t* __restrict__ scratch, uint64_t per_job) {
   __shared__ uint32_t s_ngroups;
+  __shared__ uint8_t s_exit[kThreads][9];
+  __shared__ uint8_t s_entry[kThreads];
+  __shared__ uint32_t s_scan[kThreads];
+  __shared__ uint32_t s_blk[kThreads * 17];
+  __shared__ uint32_t s_flags[kLdsFlagWords];
   const ZgMerkleJob job = jobs[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   uint8_t* out = roots + 32 * size_t(blockIdx.x);
@@ -106,49 +121,124 @@ __global__ void __launch_bounds__(kThreads) k_merkle(const uint8_t* __restrict__
           if ((hw[6] & 3u) == 0) word |= 1u << b;
         }
       }
-      s.flags[i] = word;
+      if (nwords <= kLdsFlagWords) s_flags[i] = word;
+      else s.flags[i] = word;
     }
     __syncthreads();
-    if (tid == 0) {
-      uint64_t p = 0;
-      uint32_t g = 0;
-      while (p < n) {
-        s.starts[g++] = uint32_t(p);
+    const uint32_t* flags = nwords <= kLdsFlagWords ? s_flags : s.flags;
+    // Group boundaries in parallel.  The rule (close after the first flagged child at index >= 2,
+    // at most 9 children) is a chain p -> p + cut(p); thread t owns positions [t*B, (t+1)*B).  A
+    // group that starts before a block ends at most 8 positions into it, so (A) each thread walks
+    // its block from all 9 possible entry offsets, (B) one thread chains the 1024 exit offsets,
+    // (C) each thread re-walks from its true entry counting starts, and after a block scan (D)
+    // writes them.  O(n/T) dependent steps per thread instead of O(n) on one thread.
+    {
+      const uint64_t B = (n + kThreads - 1) / kThreads;
+      const uint64_t lo = uint64_t(tid) * B;
+      const uint64_t hi = lo + B < n ? lo + B : n;
+      auto cut_at = [&](uint64_t p) -> uint64_t {
         const uint64_t rem = n - p;
-        uint64_t cut;
-        if (rem <= 2) {
-          cut = rem;
-        } else {
-          const uint64_t end = rem < 9 ? rem : 9;
-          cut = end;
-          for (uint64_t i = 2; i < end; ++i) {
-            const uint64_t j = p + i;
-            if ((s.flags[j >> 5] >> (j & 31)) & 1u) {
-              cut = i + 1;
-              break;
-            }
-          }
+        if (rem <= 2) return rem;
+        const uint64_t end = rem < 9 ? rem : 9;
+        for (uint64_t i = 2; i < end; ++i) {
+          const uint64_t j = p + i;
+          if ((flags[j >> 5] >> (j & 31)) & 1u) return i + 1;
         }
-        p += cut;
+        return end;
+      };
+      if (lo < hi) {
+        for (uint32_t e = 0; e < 9; ++e) {
+          uint64_t p = lo + e;
+          while (p < hi) p += cut_at(p);
+          s_exit[tid][e] = uint8_t(p >= hi ? p - hi : 0);
+        }
       }
-      s.starts[g] = uint32_t(n);
-      s_ngroups = g;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t entry = 0;
+        for (uint32_t t = 0; t < uint32_t(kThreads) && uint64_t(t) * B < n; ++t) {
+          s_entry[t] = uint8_t(entry);
+          entry = s_exit[t][entry];
+        }
+      }
+      __syncthreads();
+      uint32_t cnt = 0;
+      if (lo < hi) {
+        for (uint64_t p = lo + s_entry[tid]; p < hi; p += cut_at(p)) ++cnt;
+      }
+      // block-wide exclusive scan of cnt (Hillis-Steele in LDS)
+      s_scan[tid] = cnt;
+      __syncthreads();
+      for (uint32_t d = 1; d < uint32_t(kThreads); d <<= 1) {
+        const uint32_t v = tid >= d ? s_scan[tid - d] : 0;
+        __syncthreads();
+        s_scan[tid] += v;
+        __syncthreads();
+      }
+      const uint32_t base = s_scan[tid] - cnt;
+      if (lo < hi) {
+        uint32_t g = base;
+        for (uint64_t p = lo + s_entry[tid]; p < hi; p += cut_at(p)) s.starts[g++] = uint32_t(p);
+      }
+      if (tid == kThreads - 1) {
+        s.starts[s_scan[tid]] = uint32_t(n);
+        s_ngroups = s_scan[tid];
+      }
     }
     __syncthreads();
     const uint32_t ng = s_ngroups;
     uint8_t* nxt_h = into_a ? s.hash_a : s.hash_b;
     uint64_t* nxt_s = into_a ? s.size_a : s.size_b;
-    uint8_t* msg = s.msg + size_t(tid) * kMsgBytes;
+    // Node hashes: each thread streams its group's lines "{xet_hex} : {size}\n" byte by byte into
+    // a private 64-byte LDS block (stride 68 B: conflict-free banks) and compresses every full
+    // block; the message (<= 9 lines, < 1 KiB) is a single BLAKE3 chunk, so its total length is
+    // known up front for the CHUNK_END/ROOT flags.
+    uint8_t* blk = reinterpret_cast<uint8_t*>(&s_blk[tid * 17]);
     for (uint32_t g = tid; g < ng; g += kThreads) {
       const uint32_t a = s.starts[g], b = s.starts[g + 1];
-      uint32_t pos = 0;
       uint64_t total = 0;
-      for (uint32_t j = a; j < b; ++j) {
-        pos = put_line(msg, pos, cur_h + 32 * size_t(j), cur_s[j]);
-        total += cur_s[j];
-      }
+      uint32_t msg_len = 0;
+      for (uint32_t j = a; j < b; ++j) msg_len += 68 + ndigits(cur_s[j]);
       uint32_t cv[8];
-      zg::hash_chunk(msg, pos, 0, zg::kNodeKeyW, zg::KEYED_HASH, true, cv);
+      zg::load_key(cv, zg::kNodeKeyW);
+      uint32_t fill = 0, done = 0;  // bytes in the current block / bytes already compressed
+      auto put = [&](uint32_t byte) {
+        blk[fill++] = uint8_t(byte);
+        if (fill == 64 && done + 64 < msg_len) {
+          uint32_t m[16];
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(blk);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) m[i] = w[i];
+          zg::compress(cv, m, 0, 64, zg::KEYED_HASH | (done == 0 ? zg::CHUNK_START : 0u));
+          done += 64;
+          fill = 0;
+        }
+      };
+      for (uint32_t j = a; j < b; ++j) {
+        const uint64_t* hw = reinterpret_cast<const uint64_t*>(cur_h + 32 * size_t(j));
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t v = hw[q];
+          for (int d = 60; d >= 0; d -= 4) {
+            const uint32_t nib = uint32_t(v >> d) & 15u;
+            put(nib < 10 ? '0' + nib : 'a' + nib - 10);
+          }
+        }
+        put(' ');
+        put(':');
+        put(' ');
+        const uint64_t sz = cur_s[j];
+        total += sz;
+        uint64_t pw = 1;
+        while (pw <= sz / 10) pw *= 10;
+        for (; pw; pw /= 10) put('0' + uint32_t((sz / pw) % 10));
+        put('\n');
+      }
+      for (uint32_t i = fill; i < 64; ++i) blk[i] = 0;
+      uint32_t m[16];
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(blk);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = w[i];
+      zg::compress(cv, m, 0, fill, zg::KEYED_HASH | zg::CHUNK_END | zg::ROOT | (done == 0 ? zg::CHUNK_START : 0u));
       uint32_t* dst = reinterpret_cast<uint32_t*>(nxt_h + 32 * size_t(g));
       for (int k = 0; k < 8; ++k) dst[k] = cv[k];
       nxt_s[g] = total;
