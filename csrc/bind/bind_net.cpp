@@ -587,6 +587,25 @@ void bind_extra(py::module_& m) {
      py::arg("tracker") = std::nullopt, py::arg("dht") = true, py::arg("dht_bootstrap") = std::vector<std::string>{},
      py::arg("include") = std::vector<std::string>{}, py::arg("verify") = true, py::arg("concurrency") = 0,
      py::arg("repo_type") = "model");
+  m.def("list_repo_files", [](std::string repo, std::string revision, std::string repo_type) {
+    Config cfg = Config::from_env();
+    std::vector<hub::RepoFile> files;
+    std::optional<std::string> sha;
+    {
+      py::gil_scoped_release nogil;
+      files = hub::list_files(cfg, repo, revision, repo_type);
+      sha = hub::resolve_commit(cfg, repo, revision, repo_type);
+    }
+    py::list out;
+    for (auto& f : files) {
+      py::dict d;
+      d["path"] = f.path;
+      d["size"] = f.size;
+      d["xet_hash"] = f.xet_hash ? py::object(py::str(*f.xet_hash)) : py::object(py::none());
+      out.append(d);
+    }
+    return py::make_tuple(sha ? py::object(py::str(*sha)) : py::object(py::none()), out);
+  }, py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model");
   m.def("server_healthy", &server_healthy, py::arg("http_port"), py::arg("timeout_ms") = 1000);
 
   // ---------------- tracing (shared with the C++ spans) ----------------

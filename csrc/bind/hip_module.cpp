@@ -13,6 +13,7 @@
 namespace py = pybind11;
 
 void bind_hip_seed(py::module_& m);  // hip_seed.cpp
+void bind_hip_pull(py::module_& m);  // hip_pull.cpp
 
 namespace {
 
@@ -35,6 +36,7 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("MERKLE_JOB_BYTES") = sizeof(ZgMerkleJob);
   m.attr("ARCH") = "gfx950";
   bind_hip_seed(m);
+  bind_hip_pull(m);
 
   m.def("device_count", &zg_device_count);
   // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host

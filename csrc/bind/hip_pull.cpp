@@ -1,0 +1,275 @@
+// Device-direct pull: fetch a Xet file's reconstruction terms through the native cache -> P2P ->
+// CDN waterfall into pinned staging buffers and ingest them on the GPU (header walk, LZ4/BG4
+// decode, BLAKE3 chunk hashes) straight into a caller-provided HBM buffer, then verify the file's
+// Xet hash with the Merkle kernel.  The host only moves compressed bytes; decompression and
+// verification never touch the CPU (the host pull path, csrc/core/downloader.cpp, does both on
+// the CPU).  North-star path for `zest_amd.pull(..., device=...)`.
+//
+// Pipeline per file: batches of terms fill one of two pinned buffers (fetch threads) while the
+// previous batch's H2D + kernels run on a private HIP stream; a buffer is reused only after its
+// stream event completed.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../gpu/zgpu.h"
+#include "bridge.h"
+#include "config.h"
+#include "storage.h"
+#include "swarm.h"
+#include "xet_hash.h"
+#include "xorb.h"
+
+namespace py = pybind11;
+using namespace zest;
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error("HipError", std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void ensure(size_t count) {
+    if (count <= n) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    hip_check(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T) + 4096), "hipMalloc");
+    n = count;
+  }
+};
+
+struct Slot {
+  uint8_t* host = nullptr;  // pinned
+  DevBuf<uint8_t> dev;      // device staging (padded)
+  std::vector<ZgTerm> terms;
+  DevBuf<ZgTerm> terms_dev;
+  DevBuf<ZgChunk> chunks_dev;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+};
+
+class DeviceXetPull {
+ public:
+  DeviceXetPull(const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
+                std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
+                std::vector<std::string> dht_bootstrap, int device, size_t staging_bytes, int threads)
+      : cfg_(Config::from_env()), device_(device), cap_(staging_bytes), threads_(threads > 0 ? threads : 16) {
+    registry_.scan(cfg_);
+    cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
+    std::vector<net::Addr> boot;
+    for (auto& b : dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
+    swarm_ = std::make_unique<SwarmDownloader>(cfg_, tracker, p2p, dht && p2p, boot);
+    for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
+    bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
+    bridge_->authenticate(repo, repo_type, revision);
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    for (auto& s : slots_) {
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cap_ + 4096, hipHostMallocDefault), "hipHostMalloc");
+      s.dev.ensure(cap_);
+      hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+    }
+    err_.ensure(1);
+  }
+
+  ~DeviceXetPull() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& s : slots_) {
+      if (s.host) (void)hipHostFree(s.host);
+      if (s.done) (void)hipEventDestroy(s.done);
+    }
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  py::dict pull_file(const std::string& hex, uintptr_t dst_ptr, uint64_t dst_size) {
+    const auto t0 = std::chrono::steady_clock::now();
+    cas::Reconstruction rec;
+    {
+      py::gil_scoped_release nogil;
+      rec = bridge_->get_reconstruction(hex);
+    }
+    if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
+    const size_t n = rec.terms.size();
+    std::vector<uint64_t> dst_off(n + 1, 0), cbase(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) {
+      dst_off[i + 1] = dst_off[i] + rec.terms[i].unpacked_length;
+      cbase[i + 1] = cbase[i] + (rec.terms[i].range.end - rec.terms[i].range.start);
+    }
+    if (dst_off[n] != dst_size) throw Error("SizeMismatch", "file is " + std::to_string(dst_off[n]) + " bytes");
+    const uint64_t nck = cbase[n];
+    hashes_.ensure(nck ? nck * 32 : 32);
+    sizes_.ensure(nck ? nck : 1);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(dst_ptr);
+    hip_check(hipMemsetAsync(err_.p, 0, sizeof(unsigned long long), stream_), "hipMemset");
+    uint64_t fetched = 0;
+    std::string fetch_err;
+    {
+      py::gil_scoped_release nogil;
+      size_t next = 0;
+      int slot = 0;
+      while (next < n && fetch_err.empty()) {
+        Slot& s = slots_[slot];
+        if (s.busy) {
+          hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
+          s.busy = false;
+        }
+        // choose the batch [next, end): terms fetched in parallel into this pinned buffer
+        const size_t end = std::min(n, next + size_t(4 * threads_));
+        std::vector<XorbFetchResult> res(end - next);
+        std::vector<std::pair<uint64_t, uint64_t>> span(end - next);  // byte range of the term's chunks
+        std::atomic<size_t> k{next};
+        std::mutex em;
+        auto worker = [&]() {
+          while (true) {
+            const size_t i = k.fetch_add(1);
+            if (i >= end) return;
+            try {
+              XorbFetchResult r = bridge_->fetch_term(rec.terms[i], rec);
+              auto idx = xet::index_chunks(r.data.data(), r.data.size());
+              if (r.local_end > idx.size() || r.local_start >= r.local_end) throw Error("RangeOutOfBounds", hex);
+              const uint64_t a = idx[r.local_start].header_off;
+              const uint64_t b = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
+              span[i - next] = {a, b};
+              res[i - next] = std::move(r);
+            } catch (const std::exception& e) {
+              std::lock_guard<std::mutex> g(em);
+              if (fetch_err.empty()) fetch_err = e.what();
+            }
+          }
+        };
+        std::vector<std::thread> ts;
+        const int nt = int(std::min<size_t>(size_t(threads_), end - next));
+        for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
+        for (auto& t : ts) t.join();
+        if (!fetch_err.empty()) break;
+        // pack into the pinned buffer; a batch that does not fit is cut short (>= 1 term always fits)
+        s.terms.clear();
+        uint64_t pos = 0;
+        size_t used = 0;
+        for (size_t i = next; i < end; ++i) {
+          const auto [a, b] = span[i - next];
+          if (pos + (b - a) > cap_ && used) break;
+          if (b - a > cap_) {
+            fetch_err = "term larger than staging buffer";
+            break;
+          }
+          std::memcpy(s.host + pos, res[i - next].data.data() + a, b - a);
+          ZgTerm t{};
+          t.src = pos;
+          t.src_len = b - a;
+          t.dst = dst_off[i];
+          t.chunk_base = uint32_t(cbase[i] - cbase[next]);
+          t.n_chunks = uint32_t(cbase[i + 1] - cbase[i]);
+          t.ulen = rec.terms[i].unpacked_length;
+          s.terms.push_back(t);
+          pos += b - a;
+          fetched += b - a;
+          ++used;
+        }
+        if (!fetch_err.empty()) break;
+        const int nterms = int(used);
+        const uint64_t c0 = cbase[next], c1 = cbase[next + used];
+        const int nchunks = int(c1 - c0);
+        s.terms_dev.ensure(size_t(nterms));
+        s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
+        hip_check(hipMemcpyAsync(s.dev.p, s.host, pos, hipMemcpyHostToDevice, stream_), "H2D");
+        hip_check(hipMemcpyAsync(s.terms_dev.p, s.terms.data(), sizeof(ZgTerm) * size_t(nterms),
+                                 hipMemcpyHostToDevice, stream_),
+                  "H2D terms");
+        hip_check(hipMemsetAsync(s.chunks_dev.p, 0, sizeof(ZgChunk) * size_t(nchunks), stream_), "memset");
+        hip_check(zg_index_terms(s.dev.p, s.terms_dev.p, nterms, s.chunks_dev.p, err_.p, stream_), "index");
+        hip_check(zg_place_chunks(s.dev.p, pos, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, err_.p, stream_),
+                  "place");
+        hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
+                                 stream_),
+                  "hash");
+        hip_check(hipEventRecord(s.done, stream_), "event");
+        s.busy = true;
+        next += used;
+        slot ^= 1;
+      }
+      hip_check(hipStreamSynchronize(stream_), "sync");
+      for (auto& s : slots_) s.busy = false;
+    }
+    if (!fetch_err.empty()) throw Error("DownloadFailed", fetch_err);
+    unsigned long long e = 0;
+    hip_check(hipMemcpy(&e, err_.p, sizeof e, hipMemcpyDeviceToHost), "err D2H");
+    if (e) throw Error("IngestError", "code " + std::to_string(e >> 32) + " at " + std::to_string(e & 0xFFFFFFFFu));
+    // Merkle verify of the whole file on the GPU
+    ZgMerkleJob job{0, nck, 1, 0};
+    merkle_job_.ensure(1);
+    hip_check(hipMemcpyAsync(merkle_job_.p, &job, sizeof job, hipMemcpyHostToDevice, stream_), "job H2D");
+    const size_t sb = zg_merkle_scratch_bytes(nck ? nck : 1, 1);
+    merkle_scratch_.ensure(sb);
+    root_.ensure(32);
+    hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, 1, root_.p, merkle_scratch_.p, sb, stream_), "merkle");
+    uint8_t root[32];
+    hip_check(hipMemcpyAsync(root, root_.p, 32, hipMemcpyDeviceToHost, stream_), "root D2H");
+    hip_check(hipStreamSynchronize(stream_), "sync");
+    const std::string got = xet::to_hex(*reinterpret_cast<xet::Hash*>(root));
+    if (got != hex) throw Error("HashMismatch", "device bytes hash " + got + " != " + hex);
+    py::dict d;
+    d["bytes"] = dst_size;
+    d["fetched_bytes"] = fetched;
+    d["terms"] = n;
+    d["chunks"] = nck;
+    d["seconds"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return d;
+  }
+
+  std::string stats_json() const { return bridge_->stats_json(); }
+
+ private:
+  Config cfg_;
+  int device_;
+  size_t cap_;
+  int threads_;
+  storage::XorbRegistry registry_;
+  std::unique_ptr<storage::XorbCache> cache_;
+  std::unique_ptr<SwarmDownloader> swarm_;
+  std::unique_ptr<XetBridge> bridge_;
+  hipStream_t stream_ = nullptr;
+  Slot slots_[2];
+  DevBuf<unsigned long long> err_;
+  DevBuf<uint8_t> hashes_;
+  DevBuf<uint64_t> sizes_;
+  DevBuf<ZgMerkleJob> merkle_job_;
+  DevBuf<uint8_t> merkle_scratch_;
+  DevBuf<uint8_t> root_;
+};
+
+}  // namespace
+
+void bind_hip_pull(py::module_& m) {
+  py::class_<DeviceXetPull>(m, "DeviceXetPull", "Xet pull with GPU ingest + verification into HBM")
+      .def(py::init([](const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
+                       std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
+                       std::vector<std::string> boot, int device, size_t staging, int threads) {
+             // Authentication talks HTTP: release the GIL (the hub may be served from this process).
+             py::gil_scoped_release nogil;
+             return new DeviceXetPull(repo, revision, repo_type, p2p, std::move(peers), std::move(tracker), dht,
+                                      std::move(boot), device, staging, threads);
+           }),
+           py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model", py::arg("p2p") = true,
+           py::arg("peers") = std::vector<std::string>{}, py::arg("tracker") = std::nullopt, py::arg("dht") = true,
+           py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("device") = 0,
+           py::arg("staging_bytes") = size_t(256) << 20, py::arg("threads") = 16)
+      .def("pull_file", &DeviceXetPull::pull_file, py::arg("xet_hash"), py::arg("dst_ptr"), py::arg("dst_size"))
+      .def("stats_json", &DeviceXetPull::stats_json);
+}

@@ -58,3 +58,41 @@ def test_pull_to_device(tmp_path, monkeypatch):
             zdev.load_snapshot(snap, "cuda:0", res.xet_hashes())
     finally:
         hub.stop()
+
+
+@pytest.mark.parametrize("policy", ["none", "lz4", "bg4", "auto"])
+def test_direct_pull_to_device(tmp_path, monkeypatch, policy):
+    """Network -> HBM with GPU decode + Merkle verify (no disk), incl. P2P from a local seeder."""
+    import zest_amd
+    from e2e_util import Node
+
+    world = SyntheticWorld(models.get("llama-tiny"), seed=12, mode="bf16")
+    hub = FakeHub(policy=policy, max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path / "a")).items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+        got = zest_amd.pull(world.spec.repo_id, device="cuda:0", direct=True, p2p=False)
+        host = zdev.load_snapshot(zest_amd.pull(world.spec.repo_id, p2p=False), "cpu")
+        assert set(got) == set(host)
+        for k, t in got.items():
+            assert t.device.type == "cuda" and torch.equal(t.cpu().view(torch.uint8), host[k].view(torch.uint8))
+        # P2P: node "a" (which now has the xorbs cached) seeds, a fresh node pulls to HBM from it
+        seeder = Node(hub, tmp_path, "seed-a")
+        seeder.env.update(hub.env(str(tmp_path / "a")))
+        seeder.env["ZEST_LISTEN_PORT"] = str(seeder.listen_port)
+        seeder.spawn("serve", "--listen-port", str(seeder.listen_port), "--http-port", str(seeder.http_port))
+        seeder.wait_healthy()
+        for k, v in hub.env(str(tmp_path / "b")).items():
+            monkeypatch.setenv(k, v)
+        before = hub.counters.get("xorb_get", 0)
+        got2 = zest_amd.pull(world.spec.repo_id, device="cuda:0", direct=True, peers=[f"127.0.0.1:{seeder.listen_port}"],
+                             dht=False)
+        assert hub.counters.get("xorb_get", 0) == before
+        for k, t in got2.items():
+            assert torch.equal(t.cpu().view(torch.uint8), host[k].view(torch.uint8))
+        seeder.close()
+    finally:
+        hub.stop()

@@ -54,7 +54,8 @@ def disable() -> None:
 
 def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = False, verify: bool = True,
          p2p: bool = True, peers=None, tracker=None, dht: bool = True, dht_bootstrap=None, include=None,
-         group=None, repo_type: str = "model", verbose: bool = False):
+         group=None, repo_type: str = "model", verbose: bool = False, direct: bool = False,
+         save_snapshot: bool = False):
     """Download `repo@revision` via zest.
 
     * default: returns the HF-cache snapshot directory (reference behaviour).
@@ -62,6 +63,8 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
       verifies each against its Xet file hash on the GPU, and returns {tensor_name: tensor}.
     * device="all": collective over `group` (default WORLD) — every rank gets all tensors on its
       own GPU while each file is read/pushed by one owner rank and replicated over xGMI (RCCL).
+    * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
+      cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct).
     """
     _init()
     kw = dict(p2p=p2p, peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, include=include,
@@ -79,6 +82,11 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         snap, hashes = obj[0]
         return swarm_load(snap, group=group, xet_hashes=hashes if verify else None)
+    if direct:
+        from .direct import pull_to_device
+
+        return pull_to_device(repo, revision, device or "cuda:0", p2p=p2p, peers=peers, tracker=tracker, dht=dht,
+                              dht_bootstrap=dht_bootstrap, repo_type=repo_type, save_snapshot=save_snapshot)
     from .device import load_snapshot
 
     res = _client.pull_detailed(repo, revision, **kw)
