@@ -46,6 +46,9 @@ def main() -> None:
     ap.add_argument("--slots", type=int, default=3)
     ap.add_argument("--verify-received", action="store_true", help="re-hash bytes received from peers")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--seeders", type=int, default=0,
+                    help="ranks that pull from the origin (default all); the rest leech everything from "
+                         "them over xGMI (BASELINE config 2: --gpus 2 --seeders 1)")
     a = ap.parse_args()
 
     from zest_amd import models, ops
@@ -88,8 +91,9 @@ def main() -> None:
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         assert int(lo.item()) == int(hi.item()), "ranks disagree on the synthetic repository"
+    seeders = a.seeders if a.seeders > 0 else world_size
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
-                          verify_received=a.verify_received)
+                          verify_received=a.verify_received, seeders=seeders)
     puller.build_origin()
     torch.cuda.synchronize()
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
@@ -145,7 +149,8 @@ def main() -> None:
         "p2p_ratio": round(p2p_ratio, 4),
         "ingest_GBps": round(float(ing.item()) / step_s / 1e9, 3),
         "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,
-                   "parallelism": f"swarm{world_size}", "model_bytes": model_b, "files": len(world.xet_files),
+                   "parallelism": (f"swarm{world_size}" if seeders == world_size
+                                   else f"seed{seeders}-leech{world_size - seeders}"), "model_bytes": model_b, "files": len(world.xet_files),
                    "chunks": world.n_chunks, "xorbs": world.n_xorbs, "terms": int(len(world.terms)),
                    "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": "rccl_p2p" if world_size > 1 else "none",
                    "verify": "merkle_file_hash" + ("+received" if a.verify_received else "")},

@@ -72,7 +72,7 @@ class HbmSeeder {
   void add_xorb(const std::string& hex, uint64_t dev_off, std::vector<uint64_t> ends, uint32_t first) {
     if (ends.empty() || dev_off + ends.back() > arena_n_) throw Error("InvalidRange", "xorb outside arena");
     std::unique_lock<std::shared_mutex> g(mu_);
-    index_[hex] = XorbLoc{dev_off, std::move(ends), first};
+    index_[hex].push_back(XorbLoc{dev_off, std::move(ends), first});  // several runs per xorb allowed
   }
   size_t count() const {
     std::shared_lock<std::shared_mutex> g(mu_);
@@ -92,13 +92,21 @@ class HbmSeeder {
       std::shared_lock<std::shared_mutex> g(mu_);
       auto it = index_.find(hex);
       if (it == index_.end()) return std::nullopt;
-      const XorbLoc& x = it->second;
-      const uint32_t n = x.first + uint32_t(x.ends.size());
-      if (b == 0) b = n;
-      if (a < x.first || a >= b || b > n) return std::nullopt;
-      const uint32_t ra = a - x.first, rb = b - x.first;
-      lo = x.dev_off + (ra ? x.ends[ra - 1] : 0);
-      hi = x.dev_off + x.ends[rb - 1];
+      const XorbLoc* hit = nullptr;
+      uint32_t bb = b;
+      for (const XorbLoc& x : it->second) {  // first run covering [a, b)
+        const uint32_t n = x.first + uint32_t(x.ends.size());
+        const uint32_t want_end = b == 0 ? n : b;
+        if (a >= x.first && a < want_end && want_end <= n) {
+          hit = &x;
+          bb = want_end;
+          break;
+        }
+      }
+      if (!hit) return std::nullopt;
+      const uint32_t ra = a - hit->first, rb = bb - hit->first;
+      lo = hit->dev_off + (ra ? hit->ends[ra - 1] : 0);
+      hi = hit->dev_off + hit->ends[rb - 1];
     }
     thread_local std::shared_ptr<Staging> st;
     if (!st) {
@@ -128,7 +136,7 @@ class HbmSeeder {
   std::unique_ptr<storage::XorbCache> cache_;
   std::unique_ptr<bt::BtServer> server_;
   mutable std::shared_mutex mu_;
-  std::unordered_map<std::string, XorbLoc> index_;
+  std::unordered_map<std::string, std::vector<XorbLoc>> index_;
 };
 
 }  // namespace

@@ -47,3 +47,37 @@ def test_pull_from_hbm_seeder(tmp_path):
     finally:
         srv.stop()
         hub.stop()
+
+
+def test_warm_seeding_from_disk_cache(tmp_path, monkeypatch):
+    """`python -m zest_amd.seed`: the disk xorb cache (full and partial runs) is uploaded to HBM and
+    served from there; a leecher gets everything from the GPU seeder."""
+    from e2e_util import sample_files
+    from zest_amd.seed import HbmCacheArena, HbmCacheSeedServer
+
+    hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        files = sample_files(seed=4)
+        commit = hub.add_repo("org/warm", files, xet_min_size=100_000)
+        a = Node(hub, tmp_path, "a")
+        a.run("pull", "org/warm", "--no-p2p")
+        for k, v in a.env.items():
+            if k.startswith(("ZEST_", "HF_", "HOME")):
+                monkeypatch.setenv(k, v)
+        arena = HbmCacheArena("cuda:0")
+        assert arena.runs and arena.used > 0
+        srv = HbmCacheSeedServer(arena)
+        try:
+            b = Node(hub, tmp_path, "b")
+            before = hub.counters.get("xorb_get", 0)
+            out = b.run("pull", "org/warm", "--peer", f"127.0.0.1:{srv.port}", "--no-dht").stdout
+            assert p2p_ratio(out) == 100.0 and hub.counters.get("xorb_get", 0) == before
+            assert_snapshot(b, "org/warm", commit, files)
+            assert srv.stats()["chunks_served"] > 0
+            b.close()
+        finally:
+            srv.stop()
+        a.close()
+    finally:
+        hub.stop()

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _worker(rank, world_size, port, model, result_q):
+def _worker(rank, world_size, port, model, result_q, seeders=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
@@ -22,7 +22,7 @@ def _worker(rank, world_size, port, model, result_q):
         w = SyntheticWorld(model, seed=3, mode="random", max_xorb_bytes=256 << 10)
         contents = w.build_on_host()
         arena = torch.zeros(w.arena_bytes + 4096, dtype=torch.uint8)[: w.arena_bytes]
-        p = DevicePuller(w, arena, rank, world_size, round_bytes=512 << 10)
+        p = DevicePuller(w, arena, rank, world_size, round_bytes=512 << 10, seeders=seeders)
         p.build_origin_host(contents)
         for _ in range(2):
             arena.zero_()
@@ -53,3 +53,23 @@ def test_cpu_swarm_full_replication(world_size):
     assert total_in < model * 1.01 + 8 * 4096
     for _, _, recv, ing, m in res:
         assert recv > 0 and recv < m
+
+
+def test_cpu_seeder_leecher():
+    """BASELINE config 2 shape: 1 seeder ingests everything from the origin, the leechers receive
+    the whole model from it (P2P ratio 100 % for them)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 100
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, "llama-tiny", q, 1)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, *_ in res)
+    model = res[0][4]
+    assert res[0][2] == 0 and res[0][3] > 0            # seeder: everything from the origin
+    for _, _, recv, ing, m in res[1:]:
+        assert ing == 0 and recv == m                   # leechers: everything from the seeder

@@ -69,9 +69,14 @@ class OriginStore:
             pass
 
 
-def plan_rank_terms(world: SyntheticWorld, n_ranks: int) -> list[tuple[int, int]]:
-    """Contiguous, byte-balanced split of the term list among ranks."""
+def plan_rank_terms(world: SyntheticWorld, n_ranks: int, seeders: int | None = None) -> list[tuple[int, int]]:
+    """Contiguous, byte-balanced split of the term list among the first `seeders` ranks (default:
+    all); the remaining ranks own nothing and receive the whole model from peers (leechers)."""
     T = world.terms
+    k = n_ranks if seeders is None else max(1, min(seeders, n_ranks))
+    if k < n_ranks:
+        own = plan_rank_terms(world, k)
+        return own + [(len(T), len(T))] * (n_ranks - k)
     cu = np.cumsum(T["ulen"].astype(np.float64))
     total = cu[-1] if len(cu) else 0.0
     bounds = [0]
@@ -99,7 +104,7 @@ def split_rounds(world: SyntheticWorld, a: int, b: int, n_rounds: int) -> list[t
 class DevicePuller:
     def __init__(self, world: SyntheticWorld, arena: torch.Tensor, rank: int = 0, n_ranks: int = 1,
                  round_bytes: int = 1 << 30, slots: int = 3, group=None, verify_received: bool = False,
-                 exchange: str = "p2p"):
+                 exchange: str = "p2p", seeders: int | None = None):
         self.world = world
         self.arena = arena
         self.device = arena.device
@@ -109,7 +114,7 @@ class DevicePuller:
         self.exchange = exchange
         self.is_cuda = self.device.type == "cuda"
         T = world.terms
-        self.rank_terms = plan_rank_terms(world, n_ranks)
+        self.rank_terms = plan_rank_terms(world, n_ranks, seeders)
         max_share = max((int(T["ulen"][a:b].sum()) for a, b in self.rank_terms), default=0)
         self.n_rounds = max(1, -(-max_share // round_bytes))
         # rounds[k][r] = (a, b) term range for rank r in round k

@@ -65,3 +65,105 @@ class HbmSeedServer:
 
     def stop(self) -> None:
         self.seeder.stop()
+
+
+class HbmCacheArena:
+    """Warm seeding: every run of the local xorb disk cache (`{hex}` / `{hex}.{chunk_offset}`)
+    uploaded once into one HBM buffer (restore the arena from the disk cache at serve
+    start)."""
+
+    def __init__(self, device="cuda:0", max_bytes: int | None = None):
+        import json
+        import os
+
+        import numpy as np
+
+        cfg = json.loads(_core.config_json())
+        root = cfg["xorb_cache_dir"]
+        runs = []
+        total = 0
+        for pfx in sorted(os.listdir(root)) if os.path.isdir(root) else []:
+            d = os.path.join(root, pfx)
+            if len(pfx) != 2 or not os.path.isdir(d):
+                continue
+            for name in sorted(os.listdir(d)):
+                hx, _, off = name.partition(".")
+                if len(hx) != 64 or (off and not off.isdigit()):
+                    continue
+                path = os.path.join(d, name)
+                size = os.path.getsize(path)
+                if max_bytes is not None and total + size > max_bytes:
+                    break
+                runs.append((hx, int(off or 0), path, size))
+                total += size
+        dev = torch.device(device)
+        self.nbytes = total
+        self.buf = ops.padded_empty(max(total, 1), dev)
+        self.runs = []  # (hex, dev_off, chunk_ends, first_chunk)
+        pos = 0
+        for hx, first, path, size in runs:
+            data = np.fromfile(path, dtype=np.uint8)
+            try:
+                idx = _core.index_chunks(data)
+            except Exception:
+                continue  # not a chunk run (corrupt file): skip
+            if not idx:
+                continue
+            ends = [e[0] + 8 + e[1] for e in idx]
+            n = ends[-1]
+            self.buf[pos:pos + n].copy_(torch.from_numpy(data[:n]), non_blocking=False)
+            self.runs.append((hx, pos, ends, first))
+            pos += n
+        self.used = pos
+
+
+class HbmCacheSeedServer:
+    """BEP XET seeder over an HbmCacheArena (falls back to the disk cache for anything else)."""
+
+    def __init__(self, arena: HbmCacheArena, port: int = 0):
+        H = ops.hip()
+        dev = arena.buf.device
+        self.arena = arena
+        self.seeder = H.HbmSeeder(arena.buf.data_ptr(), max(arena.used, 1), dev.index or 0, port, True)
+        for hx, off, ends, first in arena.runs:
+            self.seeder.add_xorb(hx, int(off), ends, int(first))
+        self.seeder.start()
+
+    @property
+    def port(self) -> int:
+        return self.seeder.port
+
+    def stats(self) -> dict:
+        return self.seeder.stats()
+
+    def stop(self) -> None:
+        self.seeder.stop()
+
+
+def main(argv=None) -> int:
+    """`python -m zest_amd.seed [--port P] [--device cuda:0] [--max-gb G]`: seed the local xorb cache
+    from HBM until interrupted."""
+    import argparse
+    import signal
+    import threading
+
+    ap = argparse.ArgumentParser(description="seed the local xorb cache from GPU memory")
+    ap.add_argument("--port", type=int, default=6881)
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--max-gb", type=float, default=None)
+    a = ap.parse_args(argv)
+    arena = HbmCacheArena(a.device, None if a.max_gb is None else int(a.max_gb * 1e9))
+    srv = HbmCacheSeedServer(arena, a.port)
+    print(f"HBM seeder: {len(arena.runs)} cached runs, {arena.used / 1e9:.2f} GB on {a.device}, "
+          f"BT listen port {srv.port}", flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    stop.wait()
+    srv.stop()
+    print("stats:", srv.stats(), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
