@@ -118,6 +118,15 @@ def build(only: str | None = None, jobs: int | None = None, debug: bool = False,
     jobs = jobs or min(16, os.cpu_count() or 4)
     b = Builder(jobs, debug, asan)
     built = {}
+    if asan:
+        # Host-only sanitizer build (ASan + UBSan) of the core, CLI and native unit tests, kept out
+        # of the package (build/asan/): python tools/build.py --asan && build/asan/core_tests
+        core_objs = b.compile(core_sources(), "asan/core")
+        t_objs = b.compile(sorted((ROOT / "tests" / "cpp").glob("*.cpp")), "asan/tests")
+        b.link(t_objs + core_objs, BUILD / "asan" / "core_tests", shared=False, libs=["-lssl", "-lcrypto"])
+        cli_objs = b.compile(sorted((CSRC / "cli").glob("*.cpp")), "asan/cli")
+        b.link(cli_objs + core_objs, BUILD / "asan" / "zest", shared=False, libs=["-lssl", "-lcrypto", "-ldl"])
+        return {"asan_tests": BUILD / "asan" / "core_tests", "asan_cli": BUILD / "asan" / "zest"}
     core_objs = b.compile(core_sources(), "core")
     ssl_libs = ["-lssl", "-lcrypto"]
     if only in (None, "core"):
@@ -143,6 +152,12 @@ def build(only: str | None = None, jobs: int | None = None, debug: bool = False,
             out = PKG / "_bin" / "zest"
             b.link(cli_objs + core_objs, out, shared=False, libs=ssl_libs + ["-ldl"])
             built["cli"] = out
+    if only in (None, "tests"):
+        t_objs = b.compile(sorted((ROOT / "tests" / "cpp").glob("*.cpp")), "tests")
+        if t_objs:
+            out = BUILD / "tests" / "core_tests"
+            b.link(t_objs + core_objs, out, shared=False, libs=ssl_libs)
+            built["tests"] = out
     return built
 
 
@@ -150,7 +165,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--clean", action="store_true")
-    ap.add_argument("--only", choices=["core", "hip", "cli"], default=None)
+    ap.add_argument("--only", choices=["core", "hip", "cli", "tests"], default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host-only ASan/UBSan build of core + cli")
     a = ap.parse_args()
