@@ -587,6 +587,11 @@ void bind_extra(py::module_& m) {
      py::arg("tracker") = std::nullopt, py::arg("dht") = true, py::arg("dht_bootstrap") = std::vector<std::string>{},
      py::arg("include") = std::vector<std::string>{}, py::arg("verify") = true, py::arg("concurrency") = 0,
      py::arg("repo_type") = "model");
+  m.def("write_ref", [](std::string repo, std::string ref, std::string commit, std::string repo_type) {
+    Config cfg = Config::from_env();
+    (void)repo_type;
+    storage::write_ref(cfg, repo, ref, commit);
+  }, py::arg("repo"), py::arg("ref"), py::arg("commit"), py::arg("repo_type") = "model");
   m.def("list_repo_files", [](std::string repo, std::string revision, std::string repo_type) {
     Config cfg = Config::from_env();
     std::vector<hub::RepoFile> files;

@@ -8,7 +8,11 @@
 // xorb hashes are parsed with the Xet word-order hex (the reference's seed parses bytewise,
 // main.zig:349-356, which yields info-hashes no puller computes).
 #include <signal.h>
+#include <spawn.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+#include <cerrno>
 
 #include <atomic>
 #include <chrono>
@@ -32,6 +36,8 @@
 #include "xet_hash.h"
 
 using namespace zest;
+
+extern char** environ;
 
 namespace {
 
@@ -72,6 +78,7 @@ void print_usage(std::ostream& w) {
        "  --concurrency, -j <n>    Parallel term downloads (default: 16)\n"
        "  --no-verify              Skip the Xet file-hash check\n"
        "  --no-serve               Do not auto-start the background seeder\n"
+       "  --gpus <n>               Decode + verify on n GPUs (one worker per GPU, RCCL)\n"
        "\n"
        "Seed options:\n"
        "  --tracker, -t <url>      BT tracker URL\n"
@@ -139,7 +146,47 @@ std::vector<xet::Hash> cached_xorb_hashes(const Config& cfg) {
   return out;
 }
 
+// `zest pull <repo> --gpus N`: run N GPU workers (python -m torch.distributed.run ... -m
+// zest_amd.multigpu) as child processes of this CLI and return their exit status.
+int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int gpus) {
+  // exe = <pkg>/_bin/zest -> PYTHONPATH = parent of the package directory
+  std::string pkg_parent = exe;
+  for (int i = 0; i < 3; ++i) {
+    const size_t s = pkg_parent.rfind('/');
+    pkg_parent = s == std::string::npos ? "." : pkg_parent.substr(0, s);
+  }
+  const char* py = std::getenv("ZEST_PYTHON");
+  std::vector<std::string> args = {py ? py : "python3", "-m", "torch.distributed.run", "--nnodes", "1",
+                                   "--nproc-per-node", std::to_string(gpus), "--master-addr", "127.0.0.1",
+                                   "--master-port", std::to_string(29400 + (::getpid() % 2000)), "-m",
+                                   "zest_amd.multigpu"};
+  for (size_t i = 0; i < a.size(); ++i) {
+    if (a[i] == "--gpus") {
+      ++i;
+      continue;
+    }
+    args.push_back(a[i]);
+  }
+  std::string pp = pkg_parent;
+  if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
+  ::setenv("PYTHONPATH", pp.c_str(), 1);
+  std::vector<char*> argv;
+  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
+  argv.push_back(nullptr);
+  pid_t pid = 0;
+  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
+    std::cerr << "Error: cannot start " << argv[0] << " for --gpus\n";
+    return 1;
+  }
+  int status = 0;
+  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  }
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 1;
+}
+
 int cmd_pull(const std::string& exe, const std::vector<std::string>& a) {
+  for (size_t i = 0; i + 1 < a.size(); ++i)
+    if (a[i] == "--gpus" && std::atoi(a[i + 1].c_str()) > 0) return pull_on_gpus(exe, a, std::atoi(a[i + 1].c_str()));
   if (a.empty() || a[0].rfind("-", 0) == 0) {
     std::cerr << "Error: missing repository ID\n"
               << "Usage: zest pull <repo_id> [--revision <ref>] [--tracker <url>] [--no-p2p]\n";

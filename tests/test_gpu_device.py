@@ -96,3 +96,23 @@ def test_direct_pull_to_device(tmp_path, monkeypatch, policy):
         seeder.close()
     finally:
         hub.stop()
+
+
+def test_cli_pull_gpus(tmp_path):
+    """`zest pull <repo> --gpus 1`: CLI spawns a torchrun GPU worker that decodes + verifies every Xet
+    file on the GPU and writes the HF snapshot (single-command multi-GPU UX)."""
+    from e2e_util import Node, assert_snapshot, sample_files
+
+    hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        files = sample_files(seed=6)
+        commit = hub.add_repo("org/gpus", files, xet_min_size=100_000)
+        n = Node(hub, tmp_path, "a")
+        r = n.run("pull", "org/gpus", "--gpus", "1", "--no-p2p", timeout=300)
+        assert "verified on 1 GPU(s)" in r.stdout and "Done! Model available at:" in r.stdout
+        assert_snapshot(n, "org/gpus", commit, files)
+        assert (n.root / "hf/hub/models--org--gpus/refs/main").read_text().strip() == commit
+        n.close()
+    finally:
+        hub.stop()

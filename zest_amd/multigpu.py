@@ -1,0 +1,104 @@
+"""`zest pull <repo> --gpus N`: pull a repository with N GPUs as decode/verify engines.
+
+Launched by the CLI as `python -m torch.distributed.run --nproc-per-node N -m zest_amd.multigpu ...`
+(one process per GPU, SURVEY §7.3 item 6: single-command UX over per-rank workers).  Xet files are
+assigned to ranks by size (LPT); each rank fetches its files' compressed runs through the native
+cache -> P2P -> CDN waterfall, decodes and verifies them on its own GPU (`_hip.DeviceXetPull`) and
+writes them into the HF-cache snapshot; rank 0 fetches the regular files and writes the ref.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from . import _core, ops
+from .parallel import assign_owners, init_from_env
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="zest pull --gpus N")
+    ap.add_argument("repo")
+    ap.add_argument("--revision", "-r", default="main")
+    ap.add_argument("--peer", "-p", action="append", default=[])
+    ap.add_argument("--tracker", "-t", default=None)
+    ap.add_argument("--no-p2p", action="store_true")
+    ap.add_argument("--no-dht", action="store_true")
+    ap.add_argument("--dht-bootstrap", action="append", default=[])
+    ap.add_argument("--repo-type", default="model")
+    a = ap.parse_args(argv)
+    rank, world, local, dev = init_from_env()
+    t0 = time.time()
+    commit, files = _core.list_repo_files(a.repo, a.revision, a.repo_type)
+    commit = commit or a.revision
+    cfg = json.loads(_core.config_json())
+    snap = os.path.join(cfg["hf_cache_dir"], _core.repo_folder_name(a.repo, a.repo_type), "snapshots", commit)
+    xet = [f for f in files if f["xet_hash"]]
+    regular = [f["path"] for f in files if not f["xet_hash"]]
+    owners = assign_owners([f["size"] for f in xet], world)
+    mine = [f for f, o in zip(xet, owners) if o == rank]
+    if rank == 0:
+        print(f"zest pull {a.repo} (revision: {a.revision}) on {world} GPU(s)", flush=True)
+        print(f"Found {len(files)} files ({len(xet)} Xet-backed), snapshot {commit}", flush=True)
+    p2p = not a.no_p2p
+    done_bytes = 0
+    failed = 0
+    if mine:
+        dp = ops.hip().DeviceXetPull(a.repo, a.revision, a.repo_type, p2p, a.peer, a.tracker, not a.no_dht,
+                                     a.dht_bootstrap, dev.index or 0, 256 << 20, 16)
+        for f in mine:
+            dst = os.path.join(snap, f["path"])
+            if os.path.exists(dst) and os.path.getsize(dst) == f["size"]:
+                print(f"[rank {rank}] {f['path']} (cached)", flush=True)
+                continue
+            buf = ops.padded_empty(f["size"], dev)[:f["size"]]
+            torch.cuda.synchronize(dev)
+            try:
+                st = dp.pull_file(f["xet_hash"], buf.data_ptr(), f["size"])
+            except Exception as e:  # keep going with the other files, like the host pull
+                print(f"[rank {rank}] {f['path']}: error {e}", file=sys.stderr, flush=True)
+                failed += 1
+                continue
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            tmp = dst + ".incomplete"
+            buf.cpu().numpy().tofile(tmp)
+            os.replace(tmp, dst)
+            done_bytes += f["size"]
+            print(f"[rank {rank}] {f['path']} [xet, gpu {dev.index}] {f['size'] / 1e6:.1f} MB "
+                  f"verified in {st['seconds']:.2f}s", flush=True)
+            del buf
+        stats = json.loads(dp.stats_json())
+    else:
+        stats = {}
+    if rank == 0 and regular:
+        r = _core.pull(a.repo, a.revision, p2p, a.peer, a.tracker, not a.no_dht, a.dht_bootstrap, regular, True, 0,
+                       a.repo_type)
+        failed += r["failed_files"]
+    if rank == 0:
+        _core.write_ref(a.repo, a.revision, commit, a.repo_type)
+    tot = torch.tensor([float(done_bytes), float(failed), float(stats.get("bytes_from_peer", 0)),
+                        float(stats.get("bytes_from_cdn", 0)), float(stats.get("bytes_from_cache", 0))],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    dt = time.time() - t0
+    if rank == 0:
+        b, f_, peer, cdn, cache = tot.tolist()
+        src = peer + cdn + cache
+        print(f"\nXorb fetch stats:\n  From peers:   {peer / 1e6:.1f} MB\n  From CDN:     {cdn / 1e6:.1f} MB\n"
+              f"  From cache:   {cache / 1e6:.1f} MB\n  P2P ratio:    {100 * peer / src if src else 0:.1f}%", flush=True)
+        print(f"\n{b / 1e9:.2f} GB verified on {world} GPU(s) in {dt:.1f}s ({b / dt / 1e9:.2f} GB/s)", flush=True)
+        print(f"\nDone! Model available at:\n  {snap}", flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 1 if int(tot[1].item()) else 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
