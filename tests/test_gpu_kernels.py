@@ -70,8 +70,16 @@ def _make_runs(policy, seed=0):
     return data, ends, b
 
 
+@pytest.fixture(params=[1, 2], ids=["wave_decoder", "lane_decoder"])
+def lz4_decoder(request):
+    """Run the test with the wave-per-chunk (K3b) and the thread-per-chunk (K3c) LZ4 decoder."""
+    prev = ops.hip().set_lz4_decoder(request.param)
+    yield request.param
+    ops.hip().set_lz4_decoder(prev)
+
+
 @pytest.mark.parametrize("policy", ["none", "lz4", "bg4", "auto"])
-def test_ingest_matches_cpu(policy):
+def test_ingest_matches_cpu(policy, lz4_decoder):
     data, ends, b = _make_runs(policy)
     body = b.serialize(False)
     nck = len(ends)
@@ -106,7 +114,7 @@ def test_ingest_matches_cpu(policy):
     assert hashes.cpu().numpy().tobytes() == want
 
 
-def test_ingest_clip_window():
+def test_ingest_clip_window(lz4_decoder):
     data, ends, b = _make_runs("auto", seed=3)
     body = b.serialize(False)
     nck = len(ends)
@@ -144,7 +152,24 @@ def test_ingest_detects_corruption():
         ops.ingest_terms(src, dst, terms, hashes)
 
 
-def test_ingest_real_hf_xet_xorbs(tmp_path):
+def test_ingest_detects_bad_lz4_frame(lz4_decoder):
+    data, ends, b = _make_runs("lz4", seed=6)
+    body = bytearray(b.serialize(False))
+    idx = C.index_chunks(bytes(body))
+    comp = [e for e in idx if e[2] != 0]
+    assert comp
+    body[comp[len(comp) // 2][0] + 8] ^= 0xFF  # LZ4 frame magic of a compressed chunk
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(body, dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, len(ends), len(data))
+    dst = ops.padded_empty(len(data), DEV)
+    hashes = torch.zeros((len(ends), 32), dtype=torch.uint8, device=DEV)
+    with pytest.raises(ops.IngestError):
+        ops.ingest_terms(src, dst, terms, hashes)
+
+
+def test_ingest_real_hf_xet_xorbs(tmp_path, lz4_decoder):
     hf_xet = pytest.importorskip("hf_xet")
     import glob
     import time

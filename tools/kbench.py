@@ -157,12 +157,16 @@ def main():
         nck2 = int(terms["n_chunks"].sum())
         hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
         ws = ops.IngestWorkspace(dev, len(terms), nck2)
-        ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
-        ops.raise_on_error(ws.err)
-        ok = dst[:m].cpu().numpy().tobytes() == raw
-        emit(kernel=f"ingest_{policy}({name})", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
-             chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
-        assert ok, name
+        for mode, dec in ((1, "wave"), (2, "lane")) if policy != "none" else ((0, "auto"),):
+            prev = H.set_lz4_decoder(mode)
+            dst.zero_()
+            ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
+            H.set_lz4_decoder(prev)
+            ops.raise_on_error(ws.err)
+            ok = dst[:m].cpu().numpy().tobytes() == raw
+            emit(kernel=f"ingest_{policy}({name})", decoder=dec, bytes=m, ms=ms, gbps=m / ms / 1e6,
+                 ratio=len(blob) / m, chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
+            assert ok, (name, dec)
         del src, dst, hashes, ws
 
     if want("lz4"):
@@ -172,6 +176,15 @@ def main():
         raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
         for policy in ("lz4", "bg4"):
             ingest_case("bf16", raw, policy, a.iters)
+
+    if want("lz4big"):
+        # a bench-sized round: 1 GiB of bf16 weights = ~16k chunks (enough for the thread-per-chunk decoder)
+        m = 1 << 30
+        w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
+        raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+        del w
+        ingest_case("bf16_1g", raw, "bg4", max(3, a.iters // 4))
+        del raw
 
     if want("lz4paths"):
         # one decoder path per data set: short matches, long literal runs, RLE, far matches
