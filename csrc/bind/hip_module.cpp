@@ -39,8 +39,6 @@ PYBIND11_MODULE(_hip, m) {
   bind_hip_pull(m);
 
   m.def("device_count", &zg_device_count);
-  m.def("set_lz4_decoder", &zg_set_lz4_decoder, py::arg("mode"),
-        "LZ4 decoder: 0 auto, 1 wave-per-chunk, 2 thread-per-chunk; returns the previous mode");
   // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host
   // allocator) and raw async copies on a caller-provided stream.
   m.def("host_malloc", [](size_t n) {

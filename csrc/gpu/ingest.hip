@@ -8,8 +8,6 @@
 
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
-#include <atomic>
 
 #include "blake3_dev.h"
 #include "zgpu.h"
@@ -19,8 +17,6 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kMaxChunk = 128u * 1024u;  // Xet CDC maximum chunk size
-constexpr int kLaneMinChunks = 8192;            // K3c (thread-per-chunk LZ4) from this many chunks
-constexpr bool kLaneAuto = false;               // K3c is opt-in until it beats K3b (ARCHITECTURE.md §8)
 
 __device__ __forceinline__ void report(unsigned long long* err, uint32_t code, uint32_t idx) {
   if (err) atomicCAS(err, 0ull, (static_cast<unsigned long long>(code) << 32) | idx);
@@ -516,336 +512,6 @@ __global__ void __launch_bounds__(256) k_decode_lz4(const uint8_t* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------------------
-// K3c: LZ4-frame (+BG4) decode, one THREAD per chunk.  LZ4 is a serial dependency chain (each
-// token's position depends on the previous sequence's lengths), so a wave-per-chunk decoder keeps
-// ~16 chains in flight per CU and spends its time waiting on them.  Here every lane runs its own
-// chain: a wave decodes 64 chunks at once and the per-sequence latency is paid once per 64
-// chunks.  Used when a launch has enough chunks to fill the chip (a 1 GiB round of 64 KiB chunks
-// is 16k chains = one wave per CU); small launches keep the wave-per-chunk kernel above.
-//
-//  * per-lane LDS history ring of R bytes (stride R+4 so lanes start on different banks); a
-//    lane flushes its ring to HBM with dword stores (byte scatter for BG4) when it is full;
-//  * matches with distance <= R read the ring; longer ones read the flushed bytes from HBM with
-//    L2-coherent (sc1) loads after s_waitcnt vmcnt(0), like K3b;
-//  * the compressed stream is read 16 bytes at a time with a one-line prefetch;
-//  * clipped chunks (<= 2 per launch) decode into K3b's scratch slots and are copied out.
-// --------------------------------------------------------------------------------------------
-struct LIn {
-  const uint4* p;  // 16-byte-aligned base; stream position 0 = p's first byte
-  uint32_t ci;     // index of the cached line
-  uint4 cur, nxt;  // lines ci and ci + 1
-};
-
-__device__ __forceinline__ void lin_init(LIn& in, const uint8_t* payload, uint32_t& k) {
-  k = uint32_t(reinterpret_cast<uintptr_t>(payload) & 15);
-  in.p = reinterpret_cast<const uint4*>(payload - k);
-  in.ci = 0;
-  in.cur = in.p[0];
-  in.nxt = in.p[1];
-}
-
-__device__ __forceinline__ uint32_t lin_u8(LIn& in, uint32_t pos) {
-  const uint32_t i = pos >> 4;
-  if (i != in.ci) {
-    if (i == in.ci + 1) {
-      in.cur = in.nxt;
-    } else {
-      in.cur = in.p[i];
-    }
-    in.ci = i;
-    in.nxt = in.p[i + 1];
-  }
-  const uint32_t w = (pos >> 2) & 3;
-  const uint32_t d = w == 0 ? in.cur.x : w == 1 ? in.cur.y : w == 2 ? in.cur.z : in.cur.w;
-  return (d >> (8 * (pos & 3))) & 0xFF;
-}
-
-template <uint32_t R>
-struct LSink {
-  uint8_t* ring;  // this lane's LDS ring
-  uint8_t* out;   // chunk byte 0 in HBM
-  uint32_t tmod;  // ring slot of stream byte p = (tmod + p) & (R - 1); tmod == out & 3 (dword-aligned flushes)
-  uint32_t n, op, fp;
-  uint32_t g1, g2, g3;
-  bool bg4;
-};
-
-template <uint32_t R>
-__device__ __forceinline__ uint32_t lpos(const LSink<R>& s, uint32_t p) {
-  if (!s.bg4) return p;
-  const uint32_t g = uint32_t(p >= s.g1) + uint32_t(p >= s.g2) + uint32_t(p >= s.g3);
-  const uint32_t base = g == 0 ? 0u : g == 1 ? s.g1 : g == 2 ? s.g2 : s.g3;
-  return 4 * (p - base) + g;
-}
-
-// Write this lane's pending bytes [fp, op) to HBM.  Called wave-uniformly, so the 64 lanes' store
-// loops run side by side (a per-lane flush inside divergent code serialises them: measured 50x
-// slower).  Non-final flushes leave < 4 bytes pending to keep the dword stores aligned.
-template <uint32_t R>
-__device__ void lsink_flush(LSink<R>& s, bool final) {
-  uint32_t p = s.fp;
-  const uint32_t upto = s.op;
-  if (s.bg4) {
-    for (; p < upto; ++p) s.out[lpos(s, p)] = s.ring[(s.tmod + p) & (R - 1)];
-    s.fp = upto;
-    return;
-  }
-  for (; p < upto && ((s.tmod + p) & 3); ++p) s.out[p] = s.ring[(s.tmod + p) & (R - 1)];
-  for (; p + 4 <= upto; p += 4)
-    *reinterpret_cast<uint32_t*>(s.out + p) = *reinterpret_cast<const uint32_t*>(s.ring + ((s.tmod + p) & (R - 1)));
-  if (final)
-    for (; p < upto; ++p) s.out[p] = s.ring[(s.tmod + p) & (R - 1)];
-  s.fp = p;
-}
-
-template <uint32_t R>
-__device__ __forceinline__ void lput(LSink<R>& s, uint32_t b) {
-  s.ring[(s.tmod + s.op) & (R - 1)] = uint8_t(b);
-  ++s.op;
-}
-
-// n bytes of a match at distance off.  Pending bytes never exceed R, so distances <= R are still in
-// the ring and longer ones were flushed by this lane.
-template <uint32_t R>
-__device__ __forceinline__ void lcopy_match(LSink<R>& s, uint32_t off, uint32_t n) {
-  uint32_t j = 0;
-  if (off <= R) {
-    if (off >= 4) {
-      for (; j + 4 <= n; j += 4) {  // 4 reads, then 4 writes: sources are all older than the writes
-        const uint32_t q = s.tmod + s.op - off;
-        const uint32_t b0 = s.ring[q & (R - 1)], b1 = s.ring[(q + 1) & (R - 1)];
-        const uint32_t b2 = s.ring[(q + 2) & (R - 1)], b3 = s.ring[(q + 3) & (R - 1)];
-        lput(s, b0);
-        lput(s, b1);
-        lput(s, b2);
-        lput(s, b3);
-      }
-    }
-    for (; j < n; ++j) lput(s, s.ring[(s.tmod + s.op - off) & (R - 1)]);
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (; j < n; ++j) lput(s, load_u8_coherent(s.out + lpos(s, s.op - off)));
-  }
-}
-
-// Per-lane LZ4 frame state machine; a step produces at most kLStep bytes so the wave can flush
-// between steps with every lane's pending bytes bounded.
-constexpr uint32_t kLStep = 256;
-enum : uint32_t { kLBlockHdr = 0, kLSeq = 1, kLCopy = 2, kLDone = 3, kLFail = 4 };
-
-struct LDec {
-  uint32_t ip;       // next stream position to parse
-  uint32_t end;      // end of the frame
-  uint32_t blk_end;  // end of the current compressed block
-  uint32_t lit_pos, lit_rem, off, ml_rem;
-  uint32_t after;  // phase once the current copy is done
-  uint32_t phase;
-  uint32_t ck;  // block checksum bytes (0 or 4)
-};
-
-__device__ __forceinline__ uint32_t lin_u32(LIn& in, uint32_t a) {
-  return lin_u8(in, a) | (lin_u8(in, a + 1) << 8) | (lin_u8(in, a + 2) << 16) | (lin_u8(in, a + 3) << 24);
-}
-
-__device__ __forceinline__ void ldec_init(LDec& d, LIn& in, uint32_t k, uint32_t clen) {
-  d = LDec{};
-  d.phase = kLFail;
-  if (clen < 7 || lin_u32(in, k) != 0x184D2204u) return;
-  const uint32_t flg = lin_u8(in, k + 4);
-  if ((flg >> 6) != 1) return;
-  d.ip = k + 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
-  d.end = k + clen;
-  d.ck = (flg & 0x10) ? 4 : 0;
-  d.phase = kLBlockHdr;
-}
-
-// Parse a block header or a sequence header.  `op` = bytes produced so far.
-__device__ __forceinline__ void ldec_parse(LDec& d, LIn& in, uint32_t op, uint32_t n) {
-  if (d.phase == kLBlockHdr) {
-    if (d.ip > d.end || d.end - d.ip < 4) {
-      d.phase = kLFail;
-      return;
-    }
-    const uint32_t bs = lin_u32(in, d.ip);
-    d.ip += 4;
-    if (bs == 0) {
-      d.phase = kLDone;
-      return;
-    }
-    const uint32_t len = bs & 0x7FFFFFFFu;
-    if (len > d.end - d.ip) {
-      d.phase = kLFail;
-      return;
-    }
-    if (bs & 0x80000000u) {  // stored block: literals only
-      if (len > n - op) {
-        d.phase = kLFail;
-        return;
-      }
-      d.lit_pos = d.ip;
-      d.lit_rem = len;
-      d.ml_rem = 0;
-      d.ip += len + d.ck;
-      d.after = kLBlockHdr;
-      d.phase = kLCopy;
-      return;
-    }
-    d.blk_end = d.ip + len;
-    d.phase = kLSeq;
-  }
-  const uint32_t end = d.blk_end;
-  uint32_t ip = d.ip;
-  d.phase = kLFail;
-  if (ip >= end) return;
-  const uint32_t token = lin_u8(in, ip++);
-  uint32_t lit = token >> 4;
-  if (lit == 15) {
-    uint32_t b;
-    do {
-      if (ip >= end) return;
-      b = lin_u8(in, ip++);
-      lit += b;
-    } while (b == 255);
-  }
-  if (lit > end - ip || lit > n - op) return;
-  d.lit_pos = ip;
-  d.lit_rem = lit;
-  ip += lit;
-  if (ip == end) {  // last sequence of the block
-    d.ml_rem = 0;
-    d.ip = end + d.ck;
-    d.after = kLBlockHdr;
-    d.phase = kLCopy;
-    return;
-  }
-  if (end - ip < 2) return;
-  const uint32_t off = lin_u8(in, ip) | (lin_u8(in, ip + 1) << 8);
-  ip += 2;
-  if (off == 0 || off > op + lit) return;
-  uint32_t ml = token & 15;
-  if (ml == 15) {
-    uint32_t b;
-    do {
-      if (ip >= end) return;
-      b = lin_u8(in, ip++);
-      ml += b;
-    } while (b == 255);
-  }
-  ml += 4;
-  if (ml > n - op - lit) return;
-  d.off = off;
-  d.ml_rem = ml;
-  d.ip = ip;
-  d.after = kLSeq;
-  d.phase = kLCopy;
-}
-
-// One step: produce up to kLStep bytes (whole sequences while they fit, then a partial copy).
-// kProf: pr[0..] = cycles in parse / literals / matches, inner iterations, far-match bytes.
-template <uint32_t R, bool kProf>
-__device__ __forceinline__ void ldec_step(LSink<R>& s, LDec& d, LIn& in, uint64_t* pr) {
-  uint32_t budget = kLStep;
-  while (budget) {
-    uint64_t t0 = kProf ? clk() : 0;
-    if (d.phase < kLCopy) ldec_parse(d, in, s.op, s.n);
-    if (d.phase != kLCopy) return;
-    uint64_t t1 = kProf ? clk() : 0;
-    uint32_t n = d.lit_rem < budget ? d.lit_rem : budget;
-    for (uint32_t j = 0; j < n; ++j) lput(s, lin_u8(in, d.lit_pos + j));
-    d.lit_pos += n;
-    d.lit_rem -= n;
-    budget -= n;
-    uint64_t t2 = kProf ? clk() : 0;
-    n = d.ml_rem < budget ? d.ml_rem : budget;
-    if (n) lcopy_match(s, d.off, n);
-    if (kProf) {
-      const uint64_t t3 = clk();
-      pr[0] += t1 - t0;
-      pr[1] += t2 - t1;
-      pr[2] += t3 - t2;
-      pr[3] += 1;
-      pr[4] += d.off > R ? n : 0;
-    }
-    d.ml_rem -= n;
-    budget -= n;
-    if (d.lit_rem == 0 && d.ml_rem == 0) d.phase = d.after;
-  }
-}
-
-template <uint32_t R, bool kProf>
-__global__ void __launch_bounds__(64) k_decode_lz4_lane(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                        const ZgChunk* __restrict__ chunks, int n_chunks,
-                                                        uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
-                                                        uint64_t src_n, uint64_t dst_n) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int c = int(blockIdx.x) * kWave + int(threadIdx.x);
-  if (c >= n_chunks) return;
-  const ZgChunk ch = chunks[c];
-  if (ch.scheme == 0) return;
-  if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
-    report(err, ZG_ERR_RANGE, uint32_t(c));
-    return;
-  }
-  if (ch.ulen > kMaxChunk) {
-    report(err, ZG_ERR_CAPACITY, uint32_t(c));
-    return;
-  }
-  const uint64_t end = ch.dst + ch.ulen;
-  const uint64_t lo = ch.dst > clip_lo ? ch.dst : clip_lo;
-  const uint64_t hi = end < clip_hi ? end : clip_hi;
-  if (lo >= hi) return;
-  const bool clipped = lo != ch.dst || hi != end;
-  LSink<R> s{};
-  s.ring = lds + threadIdx.x * (R + 4);
-  s.out = clipped ? g_clip_scratch[ch.dst < clip_lo ? 0 : 1] : dst + ch.dst;
-  s.bg4 = ch.scheme == 2;
-  s.tmod = uint32_t(reinterpret_cast<uintptr_t>(s.out) & 3);
-  s.n = ch.ulen;
-  const uint32_t q = ch.ulen >> 2, r = ch.ulen & 3;
-  s.g1 = q + (r > 0 ? 1u : 0u);
-  s.g2 = s.g1 + q + (r > 1 ? 1u : 0u);
-  s.g3 = s.g2 + q + (r > 2 ? 1u : 0u);
-  LIn in;
-  uint32_t k;
-  lin_init(in, src + ch.src, k);
-  LDec d;
-  ldec_init(d, in, k, ch.clen);
-  uint64_t pr[8] = {};
-  const uint64_t t_start = kProf ? clk() : 0;
-  while (true) {
-    const bool active = d.phase < kLDone;
-    if (__ballot(active) == 0) break;
-    const uint64_t t0 = kProf ? clk() : 0;
-    if (__ballot(s.op - s.fp > R - kLStep)) lsink_flush(s, false);
-    if (kProf) {
-      pr[5] += clk() - t0;
-      pr[6] += 1;
-    }
-    if (active) ldec_step<R, kProf>(s, d, in, pr);
-  }
-  if (kProf) {
-    pr[7] = clk() - t_start;
-    // g_lz4_prof layout: t_parse t_lit t_match inner far_bytes t_flush outer t_total (lane sums)
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_lz4_prof[i], (unsigned long long)pr[i]);
-    atomicAdd(&g_lz4_prof[8], 1ull);
-  }
-  if (d.phase == kLFail) {
-    report(err, ZG_ERR_LZ4, uint32_t(c));
-    return;
-  }
-  if (s.op != ch.ulen) {
-    report(err, ZG_ERR_SIZE, uint32_t(c));
-    return;
-  }
-  lsink_flush(s, true);
-  if (clipped) {  // at most two lanes per launch
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t a = uint32_t(lo - ch.dst), len = uint32_t(hi - lo);
-    for (uint32_t i = 0; i < len; ++i) dst[lo + i] = uint8_t(load_u8_coherent(s.out + a + i));
-  }
-}
-
-// --------------------------------------------------------------------------------------------
 // K1: keyed BLAKE3 chunk hashes.  One wave per Xet chunk (4 per 256-thread block); lane l owns
 // BLAKE3 chunks l, l+64 (<= 128 for a 128 KiB Xet chunk); chaining values are merged pairwise
 // in LDS (pairwise-with-carry == BLAKE3's left-complete tree).
@@ -962,20 +628,7 @@ __global__ void k_compare(const uint8_t* __restrict__ got, const uint8_t* __rest
 
 }  // namespace
 
-// 0 auto, 1 wave-per-chunk (K3b), 2 thread-per-chunk (K3c); initial value from ZG_LZ4_DECODER.
-std::atomic<int> g_lz4_mode{[] {
-  const char* v = getenv("ZG_LZ4_DECODER");
-  if (v && !strcmp(v, "wave")) return 1;
-  if (v && !strcmp(v, "lane")) return 2;
-  return 0;
-}()};
-
 extern "C" {
-
-int zg_set_lz4_decoder(int mode) {
-  if (mode < 0 || mode > 2) return -1;
-  return g_lz4_mode.exchange(mode);
-}
 
 hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
                           unsigned long long* err, hipStream_t stream) {
@@ -992,57 +645,28 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                      dst, chunks, n_chunks, clip_lo, clip_hi, src_n, dst_n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // Decoder choice: thread-per-chunk (K3c) when the launch has enough chunks to give every CU a
-  // wave, wave-per-chunk (K3b) otherwise (see ARCHITECTURE.md §8 for the measurements).
-  const int mode = g_lz4_mode.load(std::memory_order_relaxed);
-  static const int lane_ring = [] {
-    const char* v = getenv("ZG_LZ4_LANE_RING");
-    return v && atoi(v) == 1024 ? 1024 : 2048;
-  }();
-  const bool use_lane = mode == 2 || (mode == 0 && kLaneAuto && n_chunks >= kLaneMinChunks);
+  // Persistent grid: up to 5 blocks (20 waves) per CU on 256 CUs.
+  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int grid = blocks < 1280 ? blocks : 1280;
   static const bool prof = [] {
     const char* v = getenv("ZG_LZ4_PROF");
     return v && *v && *v != '0';
   }();
   if (prof) {
     unsigned long long zero[10] = {};
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lz4_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, stream);
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lz4_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, stream);
   }
-  if (use_lane) {
-    const int lgrid = (n_chunks + kWave - 1) / kWave;
-    auto go = [&](auto kern, uint32_t ring) {
-      const size_t lds = 64 * (ring + 4);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                int(lds));
-      hipLaunchKernelGGL(kern, dim3(lgrid), dim3(64), lds, stream, src, dst, chunks, n_chunks, clip_lo, clip_hi, err,
-                         src_n, dst_n);
-    };
-    if (lane_ring == 1024)
-      prof ? go(k_decode_lz4_lane<1024, true>, 1024) : go(k_decode_lz4_lane<1024, false>, 1024);
-    else
-      prof ? go(k_decode_lz4_lane<2048, true>, 2048) : go(k_decode_lz4_lane<2048, false>, 2048);
-  } else {
-    // Persistent grid: up to 5 blocks (20 waves) per CU on 256 CUs.
-    const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int grid = blocks < 1280 ? blocks : 1280;
-    if (prof)
-      hipLaunchKernelGGL(k_decode_lz4<true>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
-                         clip_hi, err, src_n, dst_n);
-    else
-      hipLaunchKernelGGL(k_decode_lz4<false>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
-                         clip_hi, err, src_n, dst_n);
-  }
+  if (prof)
+    hipLaunchKernelGGL(k_decode_lz4<true>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
+                       clip_hi, err, src_n, dst_n);
+  else
+    hipLaunchKernelGGL(k_decode_lz4<false>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
+                       clip_hi, err, src_n, dst_n);
   if (prof) {
     unsigned long long v[10];
-    (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lz4_prof), sizeof v, 0, hipMemcpyDeviceToHost, stream);
-    (void)hipStreamSynchronize(stream);
-    if (use_lane && v[8])
-      fprintf(stderr,
-              "{\"lz4_lane_prof\": {\"chunks\": %d, \"lanes\": %llu, \"t_parse\": %llu, \"t_lit\": %llu, "
-              "\"t_match\": %llu, \"inner\": %llu, \"far_bytes\": %llu, \"t_flush\": %llu, \"outer\": %llu, "
-              "\"t_total\": %llu}}\n",
-              n_chunks, v[8], v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-    else if (!use_lane && v[4])
+    hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lz4_prof), sizeof v, 0, hipMemcpyDeviceToHost, stream);
+    hipStreamSynchronize(stream);
+    if (v[4])
       fprintf(stderr,
               "{\"lz4_prof\": {\"chunks\": %d, \"t_lit\": %llu, \"t_match\": %llu, \"t_flush\": %llu, \"t_total\": %llu, "
               "\"nseq\": %llu, \"lit_bytes\": %llu, \"match_bytes\": %llu, \"nfar\": %llu, \"nflush\": %llu, "

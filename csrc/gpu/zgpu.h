@@ -84,8 +84,6 @@ hipError_t zg_pack_chunks(const uint8_t* data, const uint64_t* data_off, const u
                           const uint64_t* out_off, int n, uint8_t* out, hipStream_t stream);
 
 int zg_device_count(void);
-// LZ4 decoder selection: 0 auto, 1 wave-per-chunk, 2 thread-per-chunk; returns the previous mode.
-int zg_set_lz4_decoder(int mode);
 // K6: out[i] (20 B) = SHA1("zest-xet-v1:" || hashes[i] (32 B)); out must be 4-byte aligned.
 hipError_t zg_sha1_info_hash(const uint8_t* hashes, int n, uint8_t* out, hipStream_t stream);
 

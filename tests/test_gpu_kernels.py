@@ -70,16 +70,8 @@ def _make_runs(policy, seed=0):
     return data, ends, b
 
 
-@pytest.fixture(params=[1, 2], ids=["wave_decoder", "lane_decoder"])
-def lz4_decoder(request):
-    """Run the test with the wave-per-chunk (K3b) and the thread-per-chunk (K3c) LZ4 decoder."""
-    prev = ops.hip().set_lz4_decoder(request.param)
-    yield request.param
-    ops.hip().set_lz4_decoder(prev)
-
-
 @pytest.mark.parametrize("policy", ["none", "lz4", "bg4", "auto"])
-def test_ingest_matches_cpu(policy, lz4_decoder):
+def test_ingest_matches_cpu(policy):
     data, ends, b = _make_runs(policy)
     body = b.serialize(False)
     nck = len(ends)
@@ -114,7 +106,7 @@ def test_ingest_matches_cpu(policy, lz4_decoder):
     assert hashes.cpu().numpy().tobytes() == want
 
 
-def test_ingest_clip_window(lz4_decoder):
+def test_ingest_clip_window():
     data, ends, b = _make_runs("auto", seed=3)
     body = b.serialize(False)
     nck = len(ends)
@@ -152,7 +144,7 @@ def test_ingest_detects_corruption():
         ops.ingest_terms(src, dst, terms, hashes)
 
 
-def test_ingest_detects_bad_lz4_frame(lz4_decoder):
+def test_ingest_detects_bad_lz4_frame():
     data, ends, b = _make_runs("lz4", seed=6)
     body = bytearray(b.serialize(False))
     idx = C.index_chunks(bytes(body))
@@ -169,7 +161,7 @@ def test_ingest_detects_bad_lz4_frame(lz4_decoder):
         ops.ingest_terms(src, dst, terms, hashes)
 
 
-def test_ingest_real_hf_xet_xorbs(tmp_path, lz4_decoder):
+def test_ingest_real_hf_xet_xorbs(tmp_path):
     hf_xet = pytest.importorskip("hf_xet")
     import glob
     import time

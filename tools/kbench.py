@@ -157,16 +157,12 @@ def main():
         nck2 = int(terms["n_chunks"].sum())
         hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
         ws = ops.IngestWorkspace(dev, len(terms), nck2)
-        for mode, dec in ((1, "wave"), (2, "lane")) if policy != "none" else ((0, "auto"),):
-            prev = H.set_lz4_decoder(mode)
-            dst.zero_()
-            ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
-            H.set_lz4_decoder(prev)
-            ops.raise_on_error(ws.err)
-            ok = dst[:m].cpu().numpy().tobytes() == raw
-            emit(kernel=f"ingest_{policy}({name})", decoder=dec, bytes=m, ms=ms, gbps=m / ms / 1e6,
-                 ratio=len(blob) / m, chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
-            assert ok, (name, dec)
+        ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
+        ops.raise_on_error(ws.err)
+        ok = dst[:m].cpu().numpy().tobytes() == raw
+        emit(kernel=f"ingest_{policy}({name})", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
+             chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
+        assert ok, name
         del src, dst, hashes, ws
 
     if want("lz4"):
@@ -178,7 +174,7 @@ def main():
             ingest_case("bf16", raw, policy, a.iters)
 
     if want("lz4big"):
-        # a bench-sized round: 1 GiB of bf16 weights = ~16k chunks (enough for the thread-per-chunk decoder)
+        # a bench-sized round: 1 GiB of bf16 weights = ~16.7k chunks
         m = 1 << 30
         w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
         raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
