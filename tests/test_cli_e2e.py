@@ -7,13 +7,18 @@ network: every "machine" is a separate cache root + port set on 127.0.0.1.
 from __future__ import annotations
 
 import json
+import os
+import subprocess
 import time
+from pathlib import Path
 
 import pytest
 
 from e2e_util import Node, ZEST, assert_snapshot, free_port, p2p_ratio, sample_files
 from zest_amd import _core
 from zest_amd.testing import FakeHub
+
+ROOT = Path(__file__).resolve().parents[1]
 
 REPO_ID = "org/tiny"
 
@@ -297,3 +302,19 @@ def test_start_stop(nodes):
         time.sleep(0.1)
     else:
         raise AssertionError("server still up after stop")
+
+
+def test_p2p_cluster_script_local(tmp_path):
+    """scripts/p2p_cluster_test.sh --local 3 (the reference's hetzner / docker P2P suites): CDN-only
+    baseline, two seeders, pulls from both and from one — each snapshot identical, 100 % P2P."""
+    import shutil
+    if shutil.which("curl") is None:
+        pytest.skip("curl not installed")
+    env = dict(os.environ, TMPDIR=str(tmp_path), PYTHONPATH=str(ROOT))
+    base = 20000 + (os.getpid() % 500) * 40
+    r = subprocess.run(["bash", str(ROOT / "scripts" / "p2p_cluster_test.sh"), "--local", "3", "--bt-port", str(base),
+                        "--http-port", str(base + 5)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "all scenarios passed" in r.stdout
+    assert r.stdout.count("P2P ratio 100.0%") == 2

@@ -1,0 +1,110 @@
+"""End-to-end model check (the reference's test/local/verify-model.sh, offline): a GPT-2 checkpoint
+is published on the fake Hub, pulled with `zest pull` and with `zest.enable()` +
+`AutoModelForCausalLM.from_pretrained(repo_id)`, loaded with transformers and run.  Its logits
+and greedy continuation must match the model that was uploaded.
+
+The reference pulls openai-community/gpt2 from the real Hub; without network the checkpoint is a
+randomly initialised GPT-2 with a small config, saved by transformers itself (safetensors)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+from e2e_util import Node, free_port
+from zest_amd.testing import FakeHub
+
+transformers = pytest.importorskip("transformers")
+
+REPO = "openai-community/gpt2-zest-test"
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def gpt2_checkpoint(tmp_path_factory):
+    torch.manual_seed(0)
+    cfg = transformers.GPT2Config(n_layer=2, n_head=4, n_embd=128, vocab_size=2048, n_positions=128)
+    model = transformers.GPT2LMHeadModel(cfg).eval()
+    d = tmp_path_factory.mktemp("gpt2")
+    model.save_pretrained(d, safe_serialization=True)
+    files = {p.name: p.read_bytes() for p in d.iterdir() if p.is_file()}
+    assert "model.safetensors" in files and "config.json" in files
+    ids = torch.randint(0, cfg.vocab_size, (2, 16))
+    with torch.no_grad():
+        logits = model(ids).logits
+        gen = model.generate(ids[:1], max_new_tokens=8, do_sample=False, pad_token_id=0)
+    return files, ids, logits, gen
+
+
+@pytest.fixture
+def hub_with_gpt2(gpt2_checkpoint):
+    files = gpt2_checkpoint[0]
+    hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    hub.start()
+    commit = hub.add_repo(REPO, files, xet_min_size=100_000)
+    yield hub, commit
+    hub.stop()
+
+
+def _check(model_dir_or_id, gpt2_checkpoint):
+    _, ids, logits, gen = gpt2_checkpoint
+    model = transformers.AutoModelForCausalLM.from_pretrained(model_dir_or_id, torch_dtype=torch.float32).eval()
+    assert sum(p.numel() for p in model.parameters()) > 300_000
+    with torch.no_grad():
+        assert torch.equal(model(ids).logits, logits)
+        assert torch.equal(model.generate(ids[:1], max_new_tokens=8, do_sample=False, pad_token_id=0), gen)
+
+
+def test_cli_pull_then_transformers_inference(hub_with_gpt2, gpt2_checkpoint, tmp_path):
+    hub, commit = hub_with_gpt2
+    node = Node(hub, tmp_path, "verify")
+    try:
+        out = node.run("pull", REPO, "--no-p2p").stdout
+        assert "Done!" in out
+        snap = node.snapshot(REPO, commit)
+        assert (snap / "model.safetensors").is_file()
+        _check(str(snap), gpt2_checkpoint)
+    finally:
+        node.close()
+
+
+_ENABLE_SCRIPT = r"""
+import os, sys, torch
+import zest_amd as zest
+zest.enable()                                   # before transformers is imported, like a user script
+from transformers import AutoModelForCausalLM
+ids, logits, gen = torch.load(sys.argv[1], weights_only=True)
+m = AutoModelForCausalLM.from_pretrained(sys.argv[2], torch_dtype=torch.float32).eval()
+with torch.no_grad():
+    assert torch.equal(m(ids).logits, logits)
+    assert torch.equal(m.generate(ids[:1], max_new_tokens=8, do_sample=False, pad_token_id=0), gen)
+st = zest.status()
+zest.disable()
+zest.stop()
+print("OK", st.get("version"))
+"""
+
+
+def test_enable_from_pretrained_repo_id(hub_with_gpt2, gpt2_checkpoint, tmp_path):
+    """`import zest; zest.enable(); AutoModelForCausalLM.from_pretrained(repo)`, in a
+    fresh interpreter so huggingface_hub reads HF_ENDPOINT / HF_HUB_CACHE from this environment."""
+    hub, commit = hub_with_gpt2
+    _, ids, logits, gen = gpt2_checkpoint
+    ref = tmp_path / "ref.pt"
+    torch.save((ids, logits, gen), ref)
+    env = dict(os.environ, **hub.env(str(tmp_path)), ZEST_HTTP_PORT=str(free_port()),
+               ZEST_LISTEN_PORT=str(free_port()), PYTHONPATH=str(ROOT))
+    env.pop("ZEST_NO_AUTOSTART")
+    for k in ("HF_HUB_OFFLINE", "TRANSFORMERS_OFFLINE"):  # the "Hub" is the local fake
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", _ENABLE_SCRIPT, str(ref), REPO], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    snap = tmp_path / "hf" / "hub" / ("models--" + REPO.replace("/", "--")) / "snapshots" / commit
+    assert (snap / "model.safetensors").is_file()
+    assert "falling back to huggingface_hub" not in r.stderr, r.stderr[-4000:]  # zest served every file
+    assert hub.counters.get("xorb_get", 0) > 0

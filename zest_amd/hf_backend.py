@@ -9,16 +9,44 @@ on any failure, and unpatch restores exactly what was replaced.
 """
 from __future__ import annotations
 
+import logging
 import os
 import sys
+import threading
+import time
 from typing import Any
 
+log = logging.getLogger("zest")
 _originals: dict[tuple[str, str], Any] = {}
 _client = None
+_listings: dict[tuple[str, str, str], tuple[float, frozenset]] = {}
+_listings_lock = threading.Lock()
+_LISTING_TTL = 30.0
+
+
+def _repo_paths(repo_id: str, revision: str, repo_type: str) -> frozenset | None:
+    """Paths in the repo at `revision` (cached briefly: transformers probes many optional files)."""
+    key = (repo_id, revision, repo_type)
+    now = time.monotonic()
+    with _listings_lock:
+        hit = _listings.get(key)
+        if hit and now - hit[0] < _LISTING_TTL:
+            return hit[1]
+    try:
+        from . import _core
+
+        _, files = _core.list_repo_files(repo_id, revision, repo_type)
+    except Exception:
+        return None
+    paths = frozenset(f["path"] for f in files)
+    with _listings_lock:
+        _listings[key] = (now, paths)
+    return paths
 
 # (module, attribute) pairs that may hold the functions we wrap.
 _SNAPSHOT_SITES = [("huggingface_hub", "snapshot_download"),
-                   ("huggingface_hub._snapshot_download", "snapshot_download")]
+                   ("huggingface_hub._snapshot_download", "snapshot_download"),
+                   ("transformers.utils.hub", "snapshot_download")]
 _FILE_SITES = [("huggingface_hub", "hf_hub_download"),
                ("huggingface_hub.file_download", "hf_hub_download"),
                ("transformers.utils.hub", "hf_hub_download")]
@@ -41,8 +69,8 @@ def _wrap_snapshot(orig):
                                             include=_suffixes(include))
                 if res.snapshot_dir and os.path.isdir(res.snapshot_dir):
                     return res.snapshot_dir
-            except Exception:
-                pass
+            except Exception as e:  # fall back to huggingface_hub
+                log.warning("zest: snapshot_download(%s) falling back to huggingface_hub: %s", repo_id, e)
         return orig(repo_id, *args, revision=revision, **kwargs)
 
     zest_snapshot_download.__wrapped__ = orig
@@ -53,15 +81,24 @@ def _wrap_snapshot(orig):
 def _wrap_file(orig):
     def zest_hf_hub_download(repo_id, filename, *args, subfolder=None, revision=None, **kwargs):
         if not args and not _unsupported(kwargs):
+            path = f"{subfolder}/{filename}" if subfolder else filename
+            rt = kwargs.get("repo_type") or "model"
+            paths = _repo_paths(repo_id, revision or "main", rt)
+            if paths is not None and path not in paths:
+                # transformers probes optional files (adapter_config.json, ...): answer like the Hub does
+                from huggingface_hub.errors import EntryNotFoundError
+
+                raise EntryNotFoundError(f"{path} is not in {repo_id}@{revision or 'main'}")
             try:
-                path = f"{subfolder}/{filename}" if subfolder else filename
                 res = _client.pull_detailed(repo_id, revision or "main", repo_type=kwargs.get("repo_type") or "model",
                                             include=[path])
                 full = os.path.join(res.snapshot_dir, path)
                 if os.path.isfile(full):
                     return full
-            except Exception:
-                pass
+                log.warning("zest: %s missing from snapshot %s; falling back to huggingface_hub", path,
+                            res.snapshot_dir)
+            except Exception as e:
+                log.warning("zest: hf_hub_download(%s, %s) falling back to huggingface_hub: %s", repo_id, path, e)
         return orig(repo_id, filename, *args, subfolder=subfolder, revision=revision, **kwargs)
 
     zest_hf_hub_download.__wrapped__ = orig

@@ -514,3 +514,57 @@ class FakeHub:
             peers = [p for p in swarm if p != me]
         compact = b"".join(_core.tracker.encode_compact_peer(p) for p in peers)
         self._send(h, 200, _core.bencode.encode({"interval": 60, "peers": compact}), "text/plain")
+
+
+def main(argv=None) -> int:
+    """`python -m zest_amd.testing.fakehub`: serve a directory or a synthetic model as an offline Hub.
+
+    Prints one JSON line {"url", "token", "repo", "commit", "tracker"} and serves until SIGTERM /
+    Ctrl-C (scripts/p2p_cluster_test.sh uses it for air-gapped runs)."""
+    import argparse
+    import os
+    import signal
+
+    ap = argparse.ArgumentParser(prog="python -m zest_amd.testing.fakehub")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--repo", default="zest-test/model")
+    ap.add_argument("--dir", help="publish the files under this directory as --repo")
+    ap.add_argument("--model", default="llama-tiny", help="synthetic model spec (zest_amd.models) when --dir is absent")
+    ap.add_argument("--policy", default="auto", choices=["none", "lz4", "bg4", "auto"])
+    ap.add_argument("--max-xorb-bytes", type=int, default=64 << 20)
+    a = ap.parse_args(argv)
+    hub = FakeHub(policy=a.policy, max_xorb_bytes=a.max_xorb_bytes)
+    if a.dir:
+        files = {}
+        for root, _, names in os.walk(a.dir):
+            for n in names:
+                p = os.path.join(root, n)
+                with open(p, "rb") as fh:
+                    files[os.path.relpath(p, a.dir)] = fh.read()
+        commit = hub.add_repo(a.repo, files)
+        repo = a.repo
+    else:
+        from .. import models
+        from ..synthetic import SyntheticWorld
+
+        world = SyntheticWorld(models.get(a.model), seed=0, max_xorb_bytes=a.max_xorb_bytes)
+        commit = hub.add_world(world)
+        repo = world.spec.repo_id
+    hub.host = a.host
+    url = hub.start(a.port)
+    print(json.dumps({"url": url, "token": hub.token, "repo": repo, "commit": commit, "tracker": f"{url}/announce"}),
+          flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    hub.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
