@@ -53,6 +53,25 @@ class _File:
     data: bytes
     xet_hash: str | None = None
     terms: list[tuple[int, int, int]] = field(default_factory=list)  # (xorb_idx, c0, c1)
+    _oid: str | None = None
+    _sha256: str | None = None
+
+    def digests(self) -> tuple[str, str]:
+        """(git blob oid, sha256), computed once: tree listings of multi-GB repos stay fast."""
+        if self._oid is None:
+            h = hashlib.sha1(b"blob %d\0" % len(self.data))
+            h.update(self.data)
+            self._oid = h.hexdigest()
+            self._sha256 = hashlib.sha256(self.data).hexdigest()
+        return self._oid, self._sha256
+
+
+class _LazyFile(_File):
+    """Xet file published without host bytes (add_world(payload=False)); only its size is known."""
+
+    def __init__(self, path: str, data: bytes, size: int):
+        super().__init__(path, data)
+        self.size = size
 
 
 @dataclass
@@ -114,6 +133,8 @@ class FakeHub:
             for f in out.values():
                 if f.terms is not None and f.xet_hash is not None:
                     self.file_index[f.xet_hash] = f
+        for f in out.values():
+            f.digests()
         key = (repo_type, repo_id)
         if key in self.repos:
             repo = self.repos[key]
@@ -125,11 +146,17 @@ class FakeHub:
         self.repos[key].revisions[commit] = commit
         return commit
 
-    def add_world(self, world, revision: str = "main", exact: bool = False) -> str:
+    def add_world(self, world, revision: str = "main", exact: bool = False, payload: bool = True) -> str:
         """Publish a zest_amd.synthetic.SyntheticWorld (host-generated bytes).
 
         exact=True reuses the world's own xorb layout (so xorb hashes match what a device-built
-        world / HBM seeder holds); otherwise the files are re-packed by this hub like any upload."""
+        world / HBM seeder holds); otherwise the files are re-packed by this hub like any upload.
+        payload=False (exact only) publishes metadata without generating any Xet bytes on the host:
+        listings, reconstructions and hashes are real, xorb GETs answer 404 (counted as
+        `xorb_missing`), so every byte has to come from peers — used for multi-GB benches where the
+        content lives in an HBM seeder."""
+        if not payload:
+            return self._add_world_metadata(world, revision)
         files = {f.path: world.file_bytes_host(f) for f in world.files}
         if not exact:
             return self.add_repo(world.spec.repo_id, files, revision=revision,
@@ -157,6 +184,42 @@ class FakeHub:
                     ff.terms = [(base + int(t["xorb"]), int(t["local0"]), int(t["local0"] + t["c1"] - t["c0"]))
                                 for t in T]
                     self.file_index[ff.xet_hash] = ff
+                out[f.path] = ff
+        for ff in out.values():
+            ff.digests()
+        key = ("model", world.spec.repo_id)
+        self.repos[key] = _Repo(world.spec.repo_id, "model", world.commit, out,
+                                {revision: world.commit, world.commit: world.commit})
+        return world.commit
+
+    def _add_world_metadata(self, world, revision: str) -> str:
+        if world.terms is None:
+            raise ValueError("build the world (build_on_device / build_on_host) first")
+        base = len(self.xorbs)
+        with self.lock:
+            for x in range(world.n_xorbs):
+                a = int(world.xorb_chunk0[x])
+                b = int(world.xorb_chunk0[x + 1]) if x + 1 < world.n_xorbs else world.n_chunks
+                ser = world.chunk_len[a:b].astype(np.int64) + 8
+                hx = world.xorb_hash_hex(x)
+                self.xorbs.append(_Xorb(None, hx, np.cumsum(ser).tolist(), world.chunk_len[a:b].tolist()))
+                self.xorb_index[hx] = base + x
+            out = {}
+            for f in world.files:
+                if f.xet:
+                    fi = world.xet_files.index(f)
+                    ff = _LazyFile(f.path, b"", size=f.size)
+                    ff.xet_hash = world.file_hash_hex(fi)
+                    T = world.terms[world.terms["file"] == fi]
+                    ff.terms = [(base + int(t["xorb"]), int(t["local0"]), int(t["local0"] + t["c1"] - t["c0"]))
+                                for t in T]
+                    # no bytes on the host: stand-in digests derived from the Xet hash
+                    ff._oid = hashlib.sha1(ff.xet_hash.encode()).hexdigest()
+                    ff._sha256 = hashlib.sha256(ff.xet_hash.encode()).hexdigest()
+                    self.file_index[ff.xet_hash] = ff
+                else:
+                    ff = _File(f.path, f.content)
+                    ff.digests()
                 out[f.path] = ff
         key = ("model", world.spec.repo_id)
         self.repos[key] = _Repo(world.spec.repo_id, "model", world.commit, out,
@@ -425,12 +488,12 @@ class FakeHub:
                 self._count("hub_tree")
                 entries = []
                 for f in repo.files.values():
-                    e = {"type": "file", "path": f.path, "size": len(f.data),
-                         "oid": hashlib.sha1(b"blob %d\0" % len(f.data) + f.data).hexdigest()}
+                    oid, sha = f.digests()
+                    size = f.size if isinstance(f, _LazyFile) else len(f.data)
+                    e = {"type": "file", "path": f.path, "size": size, "oid": oid}
                     if f.xet_hash:
                         e["xetHash"] = f.xet_hash
-                        e["lfs"] = {"oid": hashlib.sha256(f.data).hexdigest(), "size": len(f.data),
-                                    "pointerSize": 134}
+                        e["lfs"] = {"oid": sha, "size": size, "pointerSize": 134}
                     entries.append(e)
                 entries.sort(key=lambda e: e["path"])
                 start = int(q.get("cursor", ["0"])[0])
@@ -460,7 +523,7 @@ class FakeHub:
                 return self._json(h, {"error": "unauthorized"}, 401)
             self._count("resolve")
             data = repo.files[fpath].data
-            hdr = {"X-Repo-Commit": repo.revisions[rev], "ETag": f'"{hashlib.sha256(data).hexdigest()}"'}
+            hdr = {"X-Repo-Commit": repo.revisions[rev], "ETag": f'"{repo.files[fpath].digests()[1]}"'}
             if repo.files[fpath].xet_hash:
                 hdr["X-Xet-Hash"] = repo.files[fpath].xet_hash
             return self._send(h, 200, data, "application/octet-stream", hdr)
@@ -476,6 +539,9 @@ class FakeHub:
             self._count("xorb_fail")
             return self._json(h, {"error": "injected failure"}, 500)
         data = self.xorbs[idx].data
+        if data is None:  # metadata-only world: the bytes live with the peers
+            self._count("xorb_missing")
+            return self._json(h, {"error": "xorb payload not published"}, 404)
         rng = None if self.ignore_range else self._parse_range(h)
         status = 200
         if rng is not None:
