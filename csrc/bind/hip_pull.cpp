@@ -124,15 +124,29 @@ class DeviceXetPull {
       size_t next = 0;
       int slot = 0;
       while (next < n && fetch_err.empty()) {
+        // Batch [next, end) by an upper bound of each term's fetched size, so every term fetched
+        // in the batch has a reserved region of the pinned buffer (no refetch, no second copy
+        // pass): workers memcpy their run straight into place.
+        std::vector<uint64_t> off;
+        uint64_t pos = 0;
+        size_t end = next;
+        while (end < n) {
+          const uint64_t bound = term_bound(rec.terms[end], cbase[end + 1] - cbase[end]);
+          if (bound > cap_) {
+            if (end > next) break;
+            grow_staging(bound);  // one huge term: enlarge both slots (waits for them)
+          }
+          if (pos + bound > cap_ && end > next) break;
+          off.push_back(pos);
+          pos += bound;
+          ++end;
+        }
         Slot& s = slots_[slot];
         if (s.busy) {
           hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
           s.busy = false;
         }
-        // choose the batch [next, end): terms fetched in parallel into this pinned buffer
-        const size_t end = std::min(n, next + size_t(4 * threads_));
-        std::vector<XorbFetchResult> res(end - next);
-        std::vector<std::pair<uint64_t, uint64_t>> span(end - next);  // byte range of the term's chunks
+        std::vector<uint64_t> len(end - next, 0);
         std::atomic<size_t> k{next};
         std::mutex em;
         auto worker = [&]() {
@@ -145,8 +159,10 @@ class DeviceXetPull {
               if (r.local_end > idx.size() || r.local_start >= r.local_end) throw Error("RangeOutOfBounds", hex);
               const uint64_t a = idx[r.local_start].header_off;
               const uint64_t b = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
-              span[i - next] = {a, b};
-              res[i - next] = std::move(r);
+              const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
+              if (b - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
+              std::memcpy(s.host + off[i - next], r.data.data() + a, b - a);
+              len[i - next] = b - a;
             } catch (const std::exception& e) {
               std::lock_guard<std::mutex> g(em);
               if (fetch_err.empty()) fetch_err = e.what();
@@ -158,50 +174,39 @@ class DeviceXetPull {
         for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
         for (auto& t : ts) t.join();
         if (!fetch_err.empty()) break;
-        // pack into the pinned buffer; a batch that does not fit is cut short (>= 1 term always fits)
         s.terms.clear();
-        uint64_t pos = 0;
-        size_t used = 0;
+        uint64_t top = 0;
         for (size_t i = next; i < end; ++i) {
-          const auto [a, b] = span[i - next];
-          if (pos + (b - a) > cap_ && used) break;
-          if (b - a > cap_) {
-            fetch_err = "term larger than staging buffer";
-            break;
-          }
-          std::memcpy(s.host + pos, res[i - next].data.data() + a, b - a);
           ZgTerm t{};
-          t.src = pos;
-          t.src_len = b - a;
+          t.src = off[i - next];
+          t.src_len = len[i - next];
           t.dst = dst_off[i];
           t.chunk_base = uint32_t(cbase[i] - cbase[next]);
           t.n_chunks = uint32_t(cbase[i + 1] - cbase[i]);
           t.ulen = rec.terms[i].unpacked_length;
           s.terms.push_back(t);
-          pos += b - a;
-          fetched += b - a;
-          ++used;
+          fetched += t.src_len;
+          top = t.src + t.src_len;
         }
-        if (!fetch_err.empty()) break;
-        const int nterms = int(used);
-        const uint64_t c0 = cbase[next], c1 = cbase[next + used];
+        const int nterms = int(end - next);
+        const uint64_t c0 = cbase[next], c1 = cbase[end];
         const int nchunks = int(c1 - c0);
         s.terms_dev.ensure(size_t(nterms));
         s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
-        hip_check(hipMemcpyAsync(s.dev.p, s.host, pos, hipMemcpyHostToDevice, stream_), "H2D");
+        hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
         hip_check(hipMemcpyAsync(s.terms_dev.p, s.terms.data(), sizeof(ZgTerm) * size_t(nterms),
                                  hipMemcpyHostToDevice, stream_),
                   "H2D terms");
         hip_check(hipMemsetAsync(s.chunks_dev.p, 0, sizeof(ZgChunk) * size_t(nchunks), stream_), "memset");
         hip_check(zg_index_terms(s.dev.p, s.terms_dev.p, nterms, s.chunks_dev.p, err_.p, stream_), "index");
-        hip_check(zg_place_chunks(s.dev.p, pos, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, err_.p, stream_),
+        hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, err_.p, stream_),
                   "place");
         hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
                                  stream_),
                   "hash");
         hip_check(hipEventRecord(s.done, stream_), "event");
         s.busy = true;
-        next += used;
+        next = end;
         slot ^= 1;
       }
       hip_check(hipStreamSynchronize(stream_), "sync");
@@ -235,7 +240,29 @@ class DeviceXetPull {
 
   std::string stats_json() const { return bridge_->stats_json(); }
 
+  size_t staging_bytes() const { return cap_; }
+
  private:
+  // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does
+  // not help, so the payload is <= its unpacked size plus LZ4 frame overhead; + 8-byte headers.
+  static uint64_t term_bound(const cas::Term& t, uint64_t nchunks) {
+    return t.unpacked_length + t.unpacked_length / 128 + 80 * nchunks + 4096;
+  }
+
+  void grow_staging(uint64_t bytes) {
+    for (auto& s : slots_) {
+      if (s.busy) {
+        hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
+        s.busy = false;
+      }
+      if (s.host) (void)hipHostFree(s.host);
+      s.host = nullptr;
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), bytes + 4096, hipHostMallocDefault), "hipHostMalloc");
+      s.dev.ensure(bytes);
+    }
+    cap_ = bytes;
+  }
+
   Config cfg_;
   int device_;
   size_t cap_;
@@ -269,7 +296,8 @@ void bind_hip_pull(py::module_& m) {
            py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model", py::arg("p2p") = true,
            py::arg("peers") = std::vector<std::string>{}, py::arg("tracker") = std::nullopt, py::arg("dht") = true,
            py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("device") = 0,
-           py::arg("staging_bytes") = size_t(256) << 20, py::arg("threads") = 16)
+           py::arg("staging_bytes") = size_t(1) << 30, py::arg("threads") = 16)
       .def("pull_file", &DeviceXetPull::pull_file, py::arg("xet_hash"), py::arg("dst_ptr"), py::arg("dst_size"))
-      .def("stats_json", &DeviceXetPull::stats_json);
+      .def("stats_json", &DeviceXetPull::stats_json)
+      .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

@@ -1,3 +1,4 @@
+#include <algorithm>
 #include "bt_peer.h"
 
 #include <cstring>
@@ -113,32 +114,56 @@ std::vector<ChunkResult> PeerSession::request_many(const std::vector<XetRequest>
   return out;
 }
 
+std::shared_ptr<PeerSession> PeerPool::lease(const std::shared_ptr<PeerSession>& s) {
+  struct Lease {
+    std::shared_ptr<PeerSession> s;
+    ~Lease() { s->users_.fetch_sub(1, std::memory_order_relaxed); }
+  };
+  s->users_.fetch_add(1, std::memory_order_relaxed);
+  auto l = std::make_shared<Lease>(Lease{s});
+  return std::shared_ptr<PeerSession>(l, s.get());  // aliasing: lives as long as the lease
+}
+
+size_t PeerPool::total_locked() const {
+  size_t n = 0;
+  for (const auto& [k, v] : peers_) n += v.size();
+  return n;
+}
+
+void PeerPool::evict_idle_locked(const std::string& keep) {
+  for (auto it = peers_.begin(); it != peers_.end() && total_locked() >= max_;) {
+    auto& v = it->second;
+    if (it->first != keep)
+      v.erase(std::remove_if(v.begin(), v.end(), [](const auto& s) { return s->users() == 0 && s.use_count() == 1; }),
+              v.end());
+    it = v.empty() ? peers_.erase(it) : std::next(it);
+  }
+}
+
 std::shared_ptr<PeerSession> PeerPool::get_or_connect(const net::Addr& a, const Sha1Digest& info_hash) {
   const std::string key = a.str();
   {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = peers_.find(key);
-    if (it != peers_.end()) {
-      if (it->second->healthy()) return it->second;
-      peers_.erase(it);
-    }
+    auto& v = peers_[key];
+    v.erase(std::remove_if(v.begin(), v.end(), [](const auto& s) { return !s->healthy(); }), v.end());
+    std::shared_ptr<PeerSession> best;
+    for (auto& s : v)
+      if (!best || s->users() < best->users()) best = s;
+    if (best && (best->users() == 0 || v.size() >= per_peer_)) return lease(best);
   }
-  // Connect + handshake outside the lock.
+  // Every session to this peer is busy (or there is none): connect + handshake outside the lock.
   auto s = PeerSession::connect(a, info_hash, me_, listen_port_, timeout_);
   std::lock_guard<std::mutex> g(mu_);
-  auto it = peers_.find(key);
-  if (it != peers_.end() && it->second->healthy()) return it->second;  // lost the race: use the winner
-  if (peers_.size() >= max_) {
-    // Evict an idle session (only the pool holds it).
-    for (auto e = peers_.begin(); e != peers_.end(); ++e) {
-      if (e->second.use_count() == 1) {
-        peers_.erase(e);
-        break;
-      }
-    }
+  auto& v = peers_[key];
+  if (v.size() >= per_peer_) {  // others connected meanwhile: use the least-used one
+    std::shared_ptr<PeerSession> best;
+    for (auto& x : v)
+      if (x->healthy() && (!best || x->users() < best->users())) best = x;
+    if (best) return lease(best);
   }
-  peers_[key] = s;
-  return s;
+  if (total_locked() >= max_) evict_idle_locked(key);
+  peers_[key].push_back(s);
+  return lease(s);
 }
 
 void PeerPool::remove(const net::Addr& a) {
@@ -148,7 +173,13 @@ void PeerPool::remove(const net::Addr& a) {
 
 size_t PeerPool::count() const {
   std::lock_guard<std::mutex> g(mu_);
-  return peers_.size();
+  return total_locked();
+}
+
+size_t PeerPool::count(const net::Addr& a) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = peers_.find(a.str());
+  return it == peers_.end() ? 0 : it->second.size();
 }
 
 }  // namespace zest::bt

@@ -10,6 +10,7 @@
 #pragma once
 
 #include <array>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -48,6 +49,7 @@ class PeerSession {
                                         std::vector<std::string>* errors = nullptr);
   bool healthy() const { return healthy_; }
   uint64_t bytes_received() const { return bytes_rx_; }
+  int users() const { return users_.load(std::memory_order_relaxed); }
 
  private:
   PeerSession() = default;
@@ -61,24 +63,38 @@ class PeerSession {
   bool healthy_ = true;
   uint64_t bytes_rx_ = 0;
   std::mutex mu_;  // one conversation at a time per connection
+  std::atomic<int> users_{0};  // pool leases currently holding this session
+  friend class PeerPool;
 };
 
+// Up to `per_peer` connections per peer address (the reference keeps one per peer and holds its
+// mutex for a whole round trip, so one peer serves one request at a time — SURVEY §2.E P4).  A
+// caller gets a lease: the returned pointer keeps the session's user count raised until the last
+// copy is dropped, and get_or_connect hands out the least-used session, opening another
+// connection while every existing one is busy.
 class PeerPool {
  public:
-  PeerPool(const peer_id::PeerId& me, uint16_t listen_port, size_t max_peers, int connect_timeout_ms)
-      : me_(me), listen_port_(listen_port), max_(max_peers), timeout_(connect_timeout_ms) {}
+  PeerPool(const peer_id::PeerId& me, uint16_t listen_port, size_t max_peers, int connect_timeout_ms,
+           size_t per_peer = 8)
+      : me_(me), listen_port_(listen_port), max_(max_peers), timeout_(connect_timeout_ms),
+        per_peer_(per_peer ? per_peer : 1) {}
   // Connection reuse across info_hashes, like the reference (peer_pool.zig:4-6).
   std::shared_ptr<PeerSession> get_or_connect(const net::Addr& a, const Sha1Digest& info_hash);
   void remove(const net::Addr& a);
-  size_t count() const;
+  size_t count() const;                         // open sessions
+  size_t count(const net::Addr& a) const;       // open sessions to one peer
 
  private:
+  std::shared_ptr<PeerSession> lease(const std::shared_ptr<PeerSession>& s);
+  void evict_idle_locked(const std::string& keep);
+  size_t total_locked() const;
   peer_id::PeerId me_;
   uint16_t listen_port_;
   size_t max_;
   int timeout_;
+  size_t per_peer_;
   mutable std::mutex mu_;
-  std::map<std::string, std::shared_ptr<PeerSession>> peers_;
+  std::map<std::string, std::vector<std::shared_ptr<PeerSession>>> peers_;
 };
 
 }  // namespace zest::bt

@@ -11,7 +11,8 @@ namespace zest {
 SwarmDownloader::SwarmDownloader(const Config& cfg, std::optional<std::string> tracker_url, bool enable_p2p,
                                  bool enable_dht, std::vector<net::Addr> dht_bootstrap)
     : cfg_(cfg), enabled_(enable_p2p), tracker_(std::move(tracker_url)) {
-  pool_ = std::make_unique<bt::PeerPool>(cfg.peer_id, cfg.listen_port, cfg.max_peers, cfg.connect_timeout_ms);
+  pool_ = std::make_unique<bt::PeerPool>(cfg.peer_id, cfg.listen_port, cfg.max_peers, cfg.connect_timeout_ms,
+                                         cfg.peer_connections);
   if (enable_p2p && enable_dht) {
     dht_ = std::make_unique<dht::Dht>(cfg.dht_port);
     if (!dht_->has_socket()) dht_ = std::make_unique<dht::Dht>(0);  // port taken: ephemeral

@@ -116,3 +116,30 @@ def test_cli_pull_gpus(tmp_path):
         n.close()
     finally:
         hub.stop()
+
+
+@pytest.mark.parametrize("staging", [64 << 10, 3 << 20])
+def test_direct_pull_staging_sizes(tmp_path, monkeypatch, staging):
+    """Batches are cut by a per-term byte bound; a term larger than the staging buffer grows it."""
+    from zest_amd.direct import pull_to_device
+
+    world = SyntheticWorld(models.get("llama-tiny"), seed=13, mode="bf16")
+    hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        got = pull_to_device(world.spec.repo_id, device="cuda:0", p2p=False, staging_bytes=staging, threads=4)
+        host = zdev.load_snapshot(zest_amd_pull_cpu(world.spec.repo_id), "cpu")
+        assert set(got) == set(host)
+        for k, t in got.items():
+            assert torch.equal(t.cpu().view(torch.uint8), host[k].view(torch.uint8))
+    finally:
+        hub.stop()
+
+
+def zest_amd_pull_cpu(repo):
+    import zest_amd
+
+    return zest_amd.pull(repo, p2p=False)

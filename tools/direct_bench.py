@@ -57,7 +57,7 @@ def main() -> int:
     print(f"[setup] {spec.repo_id}: {total / 1e9:.2f} GB, {world.n_chunks} chunks, {world.n_xorbs} xorbs in HBM "
           f"({time.time() - t0:.1f}s)", flush=True)
     work = Path(tempfile.mkdtemp(prefix="zest-direct-"))
-    os.environ.update(hub.env(str(work)))
+    os.environ.update(hub.env(str(work / "direct")))  # separate caches: the host pull must not hit them
     peer = f"127.0.0.1:{srv.port}"
     res = {"model": a.model, "repo": spec.repo_id, "bytes": total, "chunks": world.n_chunks, "xorbs": world.n_xorbs,
            "source": "HBM seeder over BEP XET (loopback TCP)",
@@ -78,14 +78,14 @@ def main() -> int:
         del out
         torch.cuda.empty_cache()
         if not a.skip_host:
-            env = dict(os.environ)
+            env = dict(os.environ, **hub.env(str(work / "host")))
             t0 = time.time()
             r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
                                 "--no-dht"], env=env, capture_output=True, text=True, timeout=3600)
             t1 = time.time()
             if r.returncode != 0:
                 raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
-            snap = work / "hf" / "hub" / ("models--" + spec.repo_id.replace("/", "--")) / "snapshots" / commit
+            snap = work / "host" / "hf" / "hub" / ("models--" + spec.repo_id.replace("/", "--")) / "snapshots" / commit
             hashes = {f.path: world.file_hash_hex(i) for i, f in enumerate(world.xet_files)}
             tensors = zdev.load_snapshot(str(snap), dev, hashes)
             torch.cuda.synchronize()

@@ -20,7 +20,7 @@ from . import device as zdev
 
 def pull_to_device(repo: str, revision: str = "main", device="cuda:0", *, p2p: bool = True, peers=None,
                    tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
-                   save_snapshot: bool = False, staging_bytes: int = 256 << 20, threads: int = 16):
+                   save_snapshot: bool = False, staging_bytes: int = 1 << 30, threads: int = 16):
     dev = torch.device(device)
     if dev.type != "cuda":
         raise ValueError("pull_to_device needs a GPU device")

@@ -50,7 +50,7 @@ def main(argv=None) -> int:
     failed = 0
     if mine:
         dp = ops.hip().DeviceXetPull(a.repo, a.revision, a.repo_type, p2p, a.peer, a.tracker, not a.no_dht,
-                                     a.dht_bootstrap, dev.index or 0, 256 << 20, 16)
+                                     a.dht_bootstrap, dev.index or 0, 1 << 30, 16)
         for f in mine:
             dst = os.path.join(snap, f["path"])
             if os.path.exists(dst) and os.path.getsize(dst) == f["size"]:
