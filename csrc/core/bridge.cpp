@@ -45,10 +45,12 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   XorbFetchResult out;
   // 1. local xorb cache: any cached run covering the term's chunks
   if (allow_cache && cache_) {
+    trace::Span sp("cache", "find");
     if (auto hit = cache_->find(hex, uint32_t(term.range.start), uint32_t(term.range.end))) {
       stats_.xorbs_from_cache++;
-      stats_.bytes_from_cache += hit->data.size();
+      stats_.bytes_from_cache += hit->size();
       if (swarm_) swarm_->stats().cached_xorbs++;
+      hit->materialize();  // the hit views a file mapping; the caller owns its bytes
       out.data = std::move(hit->data);
       out.local_start = uint32_t(term.range.start - hit->chunk_offset);
       out.local_end = uint32_t(term.range.end - hit->chunk_offset);
@@ -64,6 +66,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         stats_.bytes_from_peer += r->data.size();
         if (cache_) {
           try {
+            trace::Span sp("cache", "put_run");
             cache_->put_run(hex, r->chunk_offset, r->data.data(), r->data.size());
           } catch (const Error&) {
           }

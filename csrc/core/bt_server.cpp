@@ -1,5 +1,7 @@
 #include "bt_server.h"
 
+#include "trace.h"
+
 #include <chrono>
 #include <cstring>
 #include <random>
@@ -158,7 +160,11 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
     if (x.type != bep_xet::kChunkRequest) continue;
     if (fault_.delay_ms) std::this_thread::sleep_for(std::chrono::milliseconds(fault_.delay_ms));
     if (fault_.drop > 0 && u01(rng) < fault_.drop) return;  // injected connection drop
-    auto hit = lookup(x.hash, x.range_start, x.range_end);
+    std::optional<storage::CacheHit> hit;
+    {
+      trace::Span sp("serve", "lookup");
+      hit = lookup(x.hash, x.range_start, x.range_end);
+    }
     out.clear();
     if (!hit) {
       nf_++;
@@ -173,7 +179,11 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
     bep_xet::encode_chunk_response_header(out, uint8_t(peer_xet), x.request_id, hit->chunk_offset,
                                           uint32_t(hit->size()));
     iovec iov[2] = {{out.data(), out.size()}, {const_cast<uint8_t*>(hit->bytes()), hit->size()}};
-    s.writev_all(iov, 2);
+    {
+      trace::Span sp("serve", "send");
+      sp.arg("\"bytes\":" + std::to_string(hit->size()));
+      s.writev_all(iov, 2);
+    }
     served_++;
     bytes_ += hit->size();
     if (x.range_end > x.range_start) units_ += x.range_end - x.range_start;

@@ -1,14 +1,17 @@
 #include "downloader.h"
 
 #include <fcntl.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
 #include <mutex>
 #include <thread>
 
+#include "lz4.h"
 #include "storage.h"
 #include "trace.h"
 #include "xorb.h"
@@ -48,6 +51,26 @@ void pwrite_all(int fd, const uint8_t* p, size_t n, uint64_t off) {
     p += w;
     n -= size_t(w);
     off += uint64_t(w);
+  }
+}
+
+// pwritev of the whole list (IOV_MAX-sized batches, partial writes resumed).
+void pwritev_all(int fd, std::vector<iovec>& iov, uint64_t off) {
+  size_t k = 0;
+  while (k < iov.size()) {
+    const int cnt = int(std::min<size_t>(iov.size() - k, 1024));
+    ssize_t w = ::pwritev(fd, iov.data() + k, cnt, off_t(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw Error("IoError", std::string("pwritev: ") + std::strerror(errno));
+    }
+    off += uint64_t(w);
+    size_t left = size_t(w);
+    while (k < iov.size() && left >= iov[k].iov_len) left -= iov[k++].iov_len;
+    if (k < iov.size() && left) {
+      iov[k].iov_base = static_cast<uint8_t*>(iov[k].iov_base) + left;
+      iov[k].iov_len -= left;
+    }
   }
 }
 
@@ -120,16 +143,56 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     XorbFetchResult f = bridge_.fetch_term(t, rec, allow_p2p, allow_cache);
     src[i] = f.source;  // recorded before decoding so a bad peer copy can be attributed
     peer[i] = f.peer;
-    Bytes out;
+    // Uncompressed chunks are hashed and written straight from the fetched run (no decode
+    // buffer); compressed ones are decoded into one buffer for the term.
     std::vector<xet::HashSize> hs;
-    xet::extract_chunk_range(f.data.data(), f.data.size(), f.local_start, f.local_end, out, &hs);
-    if (out.size() != t.unpacked_length) throw Error("SizeMismatch", "term " + std::to_string(i));
-    uint64_t off = offs[i], a = 0;
+    std::vector<iovec> iov;
+    Bytes dec;
+    uint64_t total = 0;
+    {
+      trace::Span sp("download", "decode+hash");
+      const auto idx = xet::index_chunks(f.data.data(), f.data.size());
+      if (f.local_start > f.local_end || f.local_end > idx.size()) throw Error("RangeOutOfBounds");
+      uint64_t dec_bytes = 0;
+      for (uint32_t c = f.local_start; c < f.local_end; ++c)
+        if (idx[c].scheme != xet::Scheme::None) dec_bytes += idx[c].ulen;
+      dec.resize(dec_bytes);
+      uint8_t* dp = dec.data();
+      hs.reserve(f.local_end - f.local_start);
+      iov.reserve(f.local_end - f.local_start);
+      for (uint32_t c = f.local_start; c < f.local_end; ++c) {
+        const xet::ChunkEntry& e = idx[c];
+        const uint8_t* payload = f.data.data() + e.header_off + xet::kChunkHeaderLen;
+        const uint8_t* p = payload;
+        if (e.scheme != xet::Scheme::None) {
+          xet::decompress_chunk(e.scheme, payload, e.clen, dp, e.ulen);
+          p = dp;
+          dp += e.ulen;
+        } else if (e.clen != e.ulen) {
+          throw Error("CorruptChunk", "stored chunk length mismatch");
+        }
+        hs.push_back({xet::chunk_hash(p, e.ulen), e.ulen});
+        iov.push_back({const_cast<uint8_t*>(p), e.ulen});
+        total += e.ulen;
+      }
+    }
+    if (total != t.unpacked_length) throw Error("SizeMismatch", "term " + std::to_string(i));
+    uint64_t off = offs[i];
     if (off < skip) {  // only the first term can straddle offset_into_first_range
-      a = std::min<uint64_t>(skip - off, out.size());
+      uint64_t drop = std::min<uint64_t>(skip - off, total);
+      size_t k = 0;
+      while (k < iov.size() && drop >= iov[k].iov_len) drop -= iov[k++].iov_len;
+      iov.erase(iov.begin(), iov.begin() + long(k));
+      if (!iov.empty() && drop) {
+        iov[0].iov_base = static_cast<uint8_t*>(iov[0].iov_base) + drop;
+        iov[0].iov_len -= drop;
+      }
       off = skip;
     }
-    pwrite_all(fd, out.data() + a, out.size() - a, off - skip);
+    {
+      trace::Span sp("download", "pwrite");
+      pwritev_all(fd, iov, off - skip);
+    }
     hashes[i] = std::move(hs);
   };
 

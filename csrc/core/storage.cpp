@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -49,7 +50,7 @@ uint64_t file_size(const std::string& path) {
   return uint64_t(st.st_size);
 }
 
-void write_file_atomic(const std::string& path, const uint8_t* data, size_t n) {
+void write_file_atomic(const std::string& path, const uint8_t* data, size_t n, bool durable) {
   const size_t slash = path.rfind('/');
   if (slash != std::string::npos) ensure_dir(path.substr(0, slash));
   static std::atomic<uint64_t> counter{0};
@@ -67,7 +68,7 @@ void write_file_atomic(const std::string& path, const uint8_t* data, size_t n) {
     }
     off += size_t(w);
   }
-  ::fdatasync(fd);
+  if (durable) ::fdatasync(fd);
   ::close(fd);
   if (::rename(tmp.c_str(), path.c_str()) != 0) {
     ::unlink(tmp.c_str());
@@ -213,14 +214,62 @@ std::vector<uint32_t> XorbCache::run_offsets(const std::string& hex) const {
   return out;
 }
 
+namespace {
+struct Mapping {
+  void* p = MAP_FAILED;
+  size_t n = 0;
+  ~Mapping() {
+    if (p != MAP_FAILED) ::munmap(p, n);
+  }
+};
+
+// Map a cache file read-only; nullptr when missing / empty.
+std::shared_ptr<Mapping> map_file(const std::string& path) {
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return nullptr;
+  struct stat st;
+  if (::fstat(fd, &st) != 0 || st.st_size <= 0) {
+    ::close(fd);
+    return nullptr;
+  }
+  auto m = std::make_shared<Mapping>();
+  m->n = size_t(st.st_size);
+  m->p = ::mmap(nullptr, m->n, PROT_READ, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (m->p == MAP_FAILED) return nullptr;
+  ::madvise(m->p, m->n, MADV_SEQUENTIAL);
+  return m;
+}
+}  // namespace
+
+// Zero-copy: the hit views the page-cache mapping of the run file (cache files are only ever
+// replaced by rename, never truncated in place, so a live mapping stays valid).  Only the chunk
+// headers are touched to validate coverage.
 std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, uint32_t end) const {
   auto offs = run_offsets(hex);
   // Closest preceding run first: most likely to be the one that was fetched for this range.
   for (auto it = offs.rbegin(); it != offs.rend(); ++it) {
     if (*it > start) continue;
-    auto data = read_file(cfg_.xorb_cache_path(*it == 0 ? hex : hex + "." + std::to_string(*it)));
-    if (!data) continue;
-    if (auto hit = slice_run(*data, *it, start, end)) return hit;
+    auto m = map_file(cfg_.xorb_cache_path(*it == 0 ? hex : hex + "." + std::to_string(*it)));
+    if (!m) continue;
+    const uint8_t* base = static_cast<const uint8_t*>(m->p);
+    std::vector<xet::ChunkEntry> idx;
+    try {
+      idx = xet::index_chunks(base, m->n);
+    } catch (const Error&) {
+      continue;
+    }
+    const uint64_t a = start - *it;
+    const uint64_t b = end == 0 ? idx.size() : uint64_t(end) - *it;
+    if (a >= b || b > idx.size()) continue;
+    const uint64_t lo = idx[a].header_off;
+    const uint64_t hi = idx[b - 1].header_off + xet::kChunkHeaderLen + idx[b - 1].clen;
+    CacheHit h;
+    h.chunk_offset = start;
+    h.ext = base + lo;
+    h.ext_len = hi - lo;
+    h.keep = m;
+    return h;
   }
   return std::nullopt;
 }
@@ -236,7 +285,7 @@ void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uin
   const std::string key = chunk_offset == 0 ? hex : hex + "." + std::to_string(chunk_offset);
   const std::string path = cfg_.xorb_cache_path(key);
   if (exists(path) && file_size(path) >= n) return;  // keep the longer run
-  write_file_atomic(path, data, n);
+  write_file_atomic(path, data, n, /*durable=*/false);
   if (registry_) registry_->add(hex);
 }
 

@@ -23,7 +23,10 @@ namespace zest::storage {
 void ensure_dir(const std::string& path);
 bool exists(const std::string& path);
 uint64_t file_size(const std::string& path);  // 0 if missing
-void write_file_atomic(const std::string& path, const uint8_t* data, size_t n);
+// Write to a temp file and rename over `path`.  durable=false skips fdatasync (cache files: they
+// are re-validated on read and content-verified by hash, so losing one on a crash only costs a
+// refetch, while syncing every 64 MiB xorb serialises the pull on disk writeback).
+void write_file_atomic(const std::string& path, const uint8_t* data, size_t n, bool durable = true);
 inline void write_file_atomic(const std::string& path, const std::string& s) {
   write_file_atomic(path, reinterpret_cast<const uint8_t*>(s.data()), s.size());
 }

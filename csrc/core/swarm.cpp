@@ -117,6 +117,7 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
     try {
       auto s = pool_->get_or_connect(a, ih);
       if (!s->supports_xet()) continue;
+      trace::Span sp("peer", "request");
       bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
       r.peer = a.str();
       {

@@ -302,7 +302,12 @@ TEST(xorb_cache_runs) {
   CHECK(cache.find(hx, 0, 2).has_value());
   CHECK(!cache.find(hx, 0, 3).has_value());  // the prefix must not be served as the whole xorb
   auto h = cache.find(hx, 4, 6);
-  CHECK(h.has_value() && h->chunk_offset == 4 && xet::index_chunks(h->data.data(), h->data.size()).size() == 2);
+  CHECK(h.has_value() && h->chunk_offset == 4 && xet::index_chunks(h->bytes(), h->size()).size() == 2);
+  // zero-copy view of the file mapping, equal to the original bytes of chunks [4, 6)
+  CHECK(h.has_value() && h->size() == body.size() - idx[4].header_off &&
+        std::memcmp(h->bytes(), body.data() + idx[4].header_off, h->size()) == 0);
+  h->materialize();
+  CHECK(h->data.size() == body.size() - idx[4].header_off);
   CHECK(!cache.find(hx, 2, 4).has_value());
   CHECK(storage::list_cached_xorbs(cfg).size() == 1);
 }
