@@ -146,7 +146,7 @@ class DeviceXetPull {
           hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
           s.busy = false;
         }
-        std::vector<uint64_t> len(end - next, 0);
+        std::vector<uint64_t> len(end - next, 0), src_at(end - next, 0);
         std::atomic<size_t> k{next};
         std::mutex em;
         auto worker = [&]() {
@@ -154,14 +154,23 @@ class DeviceXetPull {
             const size_t i = k.fetch_add(1);
             if (i >= end) return;
             try {
-              XorbFetchResult r = bridge_->fetch_term(rec.terms[i], rec);
-              auto idx = xet::index_chunks(r.data.data(), r.data.size());
+              // The run is received straight into this term's region of the pinned buffer when it
+              // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
+              uint8_t* region = s.host + off[i - next];
+              const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
+              auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
+              XorbFetchResult r = bridge_->fetch_term(rec.terms[i], rec, true, true, sink);
+              auto idx = xet::index_chunks(r.bytes(), r.size());
               if (r.local_end > idx.size() || r.local_start >= r.local_end) throw Error("RangeOutOfBounds", hex);
               const uint64_t a = idx[r.local_start].header_off;
               const uint64_t b = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
-              const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
-              if (b - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
-              std::memcpy(s.host + off[i - next], r.data.data() + a, b - a);
+              if (r.ext) {
+                src_at[i - next] = off[i - next] + a;  // already in place
+              } else {
+                if (b - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
+                std::memcpy(region, r.data.data() + a, b - a);
+                src_at[i - next] = off[i - next];
+              }
               len[i - next] = b - a;
             } catch (const std::exception& e) {
               std::lock_guard<std::mutex> g(em);
@@ -178,7 +187,7 @@ class DeviceXetPull {
         uint64_t top = 0;
         for (size_t i = next; i < end; ++i) {
           ZgTerm t{};
-          t.src = off[i - next];
+          t.src = src_at[i - next];
           t.src_len = len[i - next];
           t.dst = dst_off[i];
           t.chunk_base = uint32_t(cbase[i] - cbase[next]);
@@ -186,7 +195,7 @@ class DeviceXetPull {
           t.ulen = rec.terms[i].unpacked_length;
           s.terms.push_back(t);
           fetched += t.src_len;
-          top = t.src + t.src_len;
+          top = std::max<uint64_t>(top, t.src + t.src_len);
         }
         const int nterms = int(end - next);
         const uint64_t c0 = cbase[next], c1 = cbase[end];

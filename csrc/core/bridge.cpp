@@ -1,5 +1,6 @@
 #include "bridge.h"
 
+#include <cstring>
 #include <iomanip>
 
 #include "json.h"
@@ -24,10 +25,10 @@ cas::Reconstruction XetBridge::get_reconstruction(const std::string& file_hash_h
 
 namespace {
 // A cached / received run must contain the term's chunks.
-bool covers(const Bytes& data, uint32_t chunk_offset, uint64_t start, uint64_t end) {
+bool covers(const uint8_t* data, size_t n, uint32_t chunk_offset, uint64_t start, uint64_t end) {
   if (start < chunk_offset) return false;
   try {
-    auto idx = xet::index_chunks(data.data(), data.size());
+    auto idx = xet::index_chunks(data, n);
     return end - chunk_offset <= idx.size();
   } catch (const Error&) {
     return false;
@@ -36,7 +37,19 @@ bool covers(const Bytes& data, uint32_t chunk_offset, uint64_t start, uint64_t e
 }  // namespace
 
 XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p,
-                                      bool allow_cache) {
+                                      bool allow_cache, const bt::PayloadSink& sink) {
+  // Copy a run into sink memory when the caller provided room for it; else keep it in `data`.
+  auto land = [&](XorbFetchResult& out, const uint8_t* p, size_t n, Bytes* owned) {
+    if (uint8_t* d = sink ? sink(n) : nullptr) {
+      std::memcpy(d, p, n);
+      out.ext = d;
+      out.ext_len = n;
+    } else if (owned) {
+      out.data = std::move(*owned);
+    } else {
+      out.data.assign(p, p + n);
+    }
+  };
   const std::string& hex = term.hash_hex;
   auto it = recon.fetch_info.find(hex);
   if (it == recon.fetch_info.end()) throw Error("NotAuthenticated", "no fetch_info for " + hex);
@@ -50,8 +63,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
       stats_.xorbs_from_cache++;
       stats_.bytes_from_cache += hit->size();
       if (swarm_) swarm_->stats().cached_xorbs++;
-      hit->materialize();  // the hit views a file mapping; the caller owns its bytes
-      out.data = std::move(hit->data);
+      land(out, hit->bytes(), hit->size(), hit->ext ? nullptr : &hit->data);  // hits view a file mapping
       out.local_start = uint32_t(term.range.start - hit->chunk_offset);
       out.local_end = uint32_t(term.range.end - hit->chunk_offset);
       out.source = Source::Cache;
@@ -60,20 +72,25 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   }
   // 2. P2P swarm with the FetchInfo's chunk range
   if (allow_p2p && swarm_ && swarm_->p2p_enabled()) {
-    if (auto r = swarm_->try_peers(term.hash, uint32_t(fi->range.start), uint32_t(fi->range.end))) {
-      if (covers(r->data, r->chunk_offset, term.range.start, term.range.end)) {
+    if (auto r = swarm_->try_peers(term.hash, uint32_t(fi->range.start), uint32_t(fi->range.end), sink)) {
+      if (covers(r->bytes(), r->size(), r->chunk_offset, term.range.start, term.range.end)) {
         stats_.xorbs_from_peer++;
-        stats_.bytes_from_peer += r->data.size();
+        stats_.bytes_from_peer += r->size();
         if (cache_) {
           try {
             trace::Span sp("cache", "put_run");
-            cache_->put_run(hex, r->chunk_offset, r->data.data(), r->data.size());
+            cache_->put_run(hex, r->chunk_offset, r->bytes(), r->size());
           } catch (const Error&) {
           }
         }
         out.local_start = uint32_t(term.range.start - r->chunk_offset);
         out.local_end = uint32_t(term.range.end - r->chunk_offset);
-        out.data = std::move(r->data);
+        if (r->ext) {
+          out.ext = r->ext;
+          out.ext_len = r->ext_len;
+        } else {
+          out.data = std::move(r->data);
+        }
         out.source = Source::Peer;
         out.peer = r->peer;
         return out;
@@ -86,21 +103,22 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   // 3. CDN
   if (!cas_) throw Error("NotAuthenticated");
   trace::Span span("cdn", "fetch " + hex.substr(0, 12));
-  out.data = cas_->fetch(*fi);
-  span.arg("\"bytes\":" + std::to_string(out.data.size()));
+  Bytes body = cas_->fetch(*fi);
+  span.arg("\"bytes\":" + std::to_string(body.size()));
   stats_.xorbs_from_cdn++;
-  stats_.bytes_from_cdn += out.data.size();
+  stats_.bytes_from_cdn += body.size();
   if (swarm_) {
     swarm_->stats().cdn_xorbs++;
     swarm_->stats().total_xorbs++;
-    swarm_->stats().total_bytes += out.data.size();
+    swarm_->stats().total_bytes += body.size();
   }
   if (cache_) {
     try {
-      cache_->put_run(hex, uint32_t(fi->range.start), out.data.data(), out.data.size());
+      cache_->put_run(hex, uint32_t(fi->range.start), body.data(), body.size());
     } catch (const Error&) {
     }
   }
+  land(out, body.data(), body.size(), &body);
   out.local_start = uint32_t(term.range.start - fi->range.start);
   out.local_end = uint32_t(term.range.end - fi->range.start);
   out.source = Source::Cdn;

@@ -31,9 +31,14 @@ enum class Source { Cache, Peer, Cdn };
 
 struct XorbFetchResult {
   Bytes data;
-  uint32_t local_start = 0, local_end = 0;  // chunk indices inside `data`
+  uint32_t local_start = 0, local_end = 0;  // chunk indices inside the fetched run
   Source source = Source::Cdn;
   std::string peer;
+  // With a sink: the run was written to sink memory instead of `data`.
+  uint8_t* ext = nullptr;
+  size_t ext_len = 0;
+  const uint8_t* bytes() const { return ext ? ext : data.data(); }
+  size_t size() const { return ext ? ext_len : data.size(); }
 };
 
 class XetBridge {
@@ -44,8 +49,10 @@ class XetBridge {
   void set_cas(const std::string& cas_url, const std::string& token);
   bool authenticated() const { return cas_ != nullptr; }
   cas::Reconstruction get_reconstruction(const std::string& file_hash_hex) const;
+  // `sink` (optional) supplies destination memory for the fetched run (e.g. a pinned staging
+  // region); when it returns nullptr the run lands in XorbFetchResult::data as usual.
   XorbFetchResult fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p = true,
-                             bool allow_cache = true);
+                             bool allow_cache = true, const bt::PayloadSink& sink = {});
   FetchStats& stats() { return stats_; }
   void print_stats(std::ostream& w) const;
   std::string stats_json() const;

@@ -112,8 +112,15 @@ std::vector<ChunkResult> PeerSession::request_many(const std::vector<XetRequest>
           const size_t i = it->second;
           want.erase(it);
           trace::Span sp("peer", "read_payload");
-          out[i].data.resize(dlen);
-          if (dlen) sock_.read_exact(out[i].data.data(), dlen);
+          uint8_t* dst = reqs[i].sink ? reqs[i].sink(dlen) : nullptr;
+          if (dst) {
+            out[i].ext = dst;
+            out[i].ext_len = dlen;
+          } else {
+            out[i].data.resize(dlen);
+            dst = out[i].data.data();
+          }
+          if (dlen) sock_.read_exact(dst, dlen);
           out[i].chunk_offset = load_be32(pre + 7);
           continue;
         }

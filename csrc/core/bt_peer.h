@@ -10,6 +10,7 @@
 #pragma once
 
 #include <array>
+#include <functional>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -23,15 +24,23 @@
 
 namespace zest::bt {
 
+// Caller-provided destination for a response payload of n bytes (nullptr = use `data`).
+using PayloadSink = std::function<uint8_t*(size_t n)>;
+
 struct ChunkResult {
   Bytes data;
-  uint32_t chunk_offset = 0;  // first chunk index of `data` inside the xorb
+  uint32_t chunk_offset = 0;  // first chunk index of the payload inside the xorb
   std::string peer;           // address of the serving peer (for scoring / banning)
+  uint8_t* ext = nullptr;     // payload landed in the request's sink instead of `data`
+  size_t ext_len = 0;
+  const uint8_t* bytes() const { return ext ? ext : data.data(); }
+  size_t size() const { return ext ? ext_len : data.size(); }
 };
 
 struct XetRequest {
   std::array<uint8_t, 32> xorb_hash{};
   uint32_t range_start = 0, range_end = 0;
+  PayloadSink sink;  // optional: receive the payload straight into caller memory (e.g. pinned)
 };
 
 class PeerSession {

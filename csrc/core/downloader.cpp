@@ -151,7 +151,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     uint64_t total = 0;
     {
       trace::Span sp("download", "decode+hash");
-      const auto idx = xet::index_chunks(f.data.data(), f.data.size());
+      const auto idx = xet::index_chunks(f.bytes(), f.size());
       if (f.local_start > f.local_end || f.local_end > idx.size()) throw Error("RangeOutOfBounds");
       uint64_t dec_bytes = 0;
       for (uint32_t c = f.local_start; c < f.local_end; ++c)
@@ -162,7 +162,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       iov.reserve(f.local_end - f.local_start);
       for (uint32_t c = f.local_start; c < f.local_end; ++c) {
         const xet::ChunkEntry& e = idx[c];
-        const uint8_t* payload = f.data.data() + e.header_off + xet::kChunkHeaderLen;
+        const uint8_t* payload = f.bytes() + e.header_off + xet::kChunkHeaderLen;
         const uint8_t* p = payload;
         if (e.scheme != xet::Scheme::None) {
           xet::decompress_chunk(e.scheme, payload, e.clen, dp, e.ulen);

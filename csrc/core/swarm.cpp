@@ -1,6 +1,7 @@
 #include "swarm.h"
 
 #include <cstring>
+#include <set>
 #include <iomanip>
 
 #include "trace.h"
@@ -88,68 +89,78 @@ std::vector<net::Addr> SwarmDownloader::discover(const Sha1Digest& ih) {
   return peers;
 }
 
-std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash, uint32_t start, uint32_t end) {
+// Peers are tried in two rounds: first the direct peers plus every peer that already served this
+// session (one seeder usually holds the whole repo, so its address is reused for the next xorb),
+// then — only if none of them had the range — the per-xorb DHT / tracker discovery.  The reference
+// runs discovery for every xorb (swarm.zig:363-394), serialised behind one lock.
+std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash, uint32_t start, uint32_t end,
+                                                          const bt::PayloadSink& sink) {
   if (!enabled_) return std::nullopt;
   const Sha1Digest ih = peer_id::info_hash(hash.data());
-  std::vector<net::Addr> cands;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    cands = direct_;
-  }
-  if (cands.empty() || dht_ || tracker_) {
-    for (auto& p : discover(ih)) {
-      bool dup = false;
-      for (auto& c : cands)
-        if (c == p) dup = true;
-      if (!dup) cands.push_back(p);
-    }
-  }
   bt::XetRequest req;
   std::memcpy(req.xorb_hash.data(), hash.data(), 32);
   req.range_start = start;
   req.range_end = end;
-  for (const auto& a : cands) {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      auto it = score_.find(a.str());
-      if (it != score_.end() && it->second >= 3) continue;  // banned / repeatedly failing
-    }
-    try {
-      auto s = pool_->get_or_connect(a, ih);
-      if (!s->supports_xet()) continue;
-      trace::Span sp("peer", "request");
-      bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
-      r.peer = a.str();
+  req.sink = sink;
+  std::set<std::string> tried;
+  auto attempt = [&](const std::vector<net::Addr>& cands) -> std::optional<bt::ChunkResult> {
+    for (const auto& a : cands) {
+      const std::string key = a.str();
+      if (!tried.insert(key).second) continue;
       {
         std::lock_guard<std::mutex> g(mu_);
-        if (served_by_.insert(r.peer).second) stats_.peers_connected++;
+        auto it = score_.find(key);
+        if (it != score_.end() && it->second >= 3) continue;  // banned / repeatedly failing
       }
-      ZTRACE("swarm", "peer " << r.peer << " served " << xet::to_hex(hash) << " [" << start << "," << end
-                              << ") offset " << r.chunk_offset << " bytes " << r.data.size());
-      stats_.peer_xorbs++;
-      stats_.peer_bytes += r.data.size();
-      stats_.total_bytes += r.data.size();
-      stats_.total_xorbs++;
-      if (dht_) {
+      try {
+        auto s = pool_->get_or_connect(a, ih);
+        if (!s->supports_xet()) continue;
+        trace::Span sp("peer", "request");
+        bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
+        r.peer = key;
         {
-          std::lock_guard<std::mutex> g(aq_mu_);
-          announce_q_.push_back(ih);
+          std::lock_guard<std::mutex> g(mu_);
+          if (served_by_.insert(r.peer).second) {
+            stats_.peers_connected++;
+            known_.push_back(a);
+          }
         }
-        aq_cv_.notify_one();
-      }
-      return r;
-    } catch (const Error& e) {
-      stats_.peer_failures++;
-      ZTRACE("swarm", "peer " << a.str() << " failed " << xet::to_hex(hash) << " [" << start << "," << end
-                              << "): " << e.what());
-      if (e.code() != "ChunkNotFound" && e.code() != "ChunkError") {
-        pool_->remove(a);
-        std::lock_guard<std::mutex> g(mu_);
-        score_[a.str()]++;
+        ZTRACE("swarm", "peer " << r.peer << " served " << xet::to_hex(hash) << " [" << start << "," << end
+                                << ") offset " << r.chunk_offset << " bytes " << r.size());
+        stats_.peer_xorbs++;
+        stats_.peer_bytes += r.size();
+        stats_.total_bytes += r.size();
+        stats_.total_xorbs++;
+        if (dht_) {
+          {
+            std::lock_guard<std::mutex> g(aq_mu_);
+            announce_q_.push_back(ih);
+          }
+          aq_cv_.notify_one();
+        }
+        return r;
+      } catch (const Error& e) {
+        stats_.peer_failures++;
+        ZTRACE("swarm", "peer " << key << " failed " << xet::to_hex(hash) << " [" << start << "," << end
+                                << "): " << e.what());
+        if (e.code() != "ChunkNotFound" && e.code() != "ChunkError") {
+          pool_->remove(a);
+          std::lock_guard<std::mutex> g(mu_);
+          score_[key]++;
+        }
       }
     }
+    return std::nullopt;
+  };
+  std::vector<net::Addr> first;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    first = direct_;
+    first.insert(first.end(), known_.begin(), known_.end());
   }
-  return std::nullopt;
+  if (auto r = attempt(first)) return r;
+  if (!dht_ && !tracker_) return std::nullopt;
+  return attempt(discover(ih));
 }
 
 void SwarmDownloader::report_bad_peer(const std::string& addr) {

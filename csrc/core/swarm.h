@@ -45,7 +45,8 @@ class SwarmDownloader {
   void add_direct_peer(const net::Addr& a);
   bool p2p_enabled() const { return enabled_; }
   // Fetch chunks [start, end) of xorb `hash` from any peer; nullopt if no peer could serve it.
-  std::optional<bt::ChunkResult> try_peers(const xet::Hash& hash, uint32_t start, uint32_t end);
+  std::optional<bt::ChunkResult> try_peers(const xet::Hash& hash, uint32_t start, uint32_t end,
+                                           const bt::PayloadSink& sink = {});
   std::vector<net::Addr> discover(const Sha1Digest& info_hash);
   void announce(const std::vector<xet::Hash>& xorbs);
   // A peer served bytes that failed verification: ban it for the rest of the session.
@@ -69,6 +70,7 @@ class SwarmDownloader {
   std::map<std::string, Cached> discovered_;
   std::map<std::string, int> score_;  // addr -> failures
   std::set<std::string> served_by_;   // distinct peers that served data ("Peers connected")
+  std::vector<net::Addr> known_;      // the same peers, tried before per-xorb discovery
   std::mutex disc_mu_;
   DownloadStats stats_;
   // DHT re-announce of xorbs fetched from peers: queued and drained by an owned worker thread
