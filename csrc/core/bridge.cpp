@@ -76,7 +76,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
       if (covers(r->bytes(), r->size(), r->chunk_offset, term.range.start, term.range.end)) {
         stats_.xorbs_from_peer++;
         stats_.bytes_from_peer += r->size();
-        if (cache_) {
+        if (cache_ && cfg_.cache_writes) {
           try {
             trace::Span sp("cache", "put_run");
             cache_->put_run(hex, r->chunk_offset, r->bytes(), r->size());
@@ -112,7 +112,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
     swarm_->stats().total_xorbs++;
     swarm_->stats().total_bytes += body.size();
   }
-  if (cache_) {
+  if (cache_ && cfg_.cache_writes) {
     try {
       cache_->put_run(hex, uint32_t(fi->range.start), body.data(), body.size());
     } catch (const Error&) {

@@ -73,6 +73,7 @@ Config Config::from_env() {
   if (const char* v = env("ZEST_HBM_CACHE_GB")) c.hbm_cache_gb = std::atof(v);
   if (env("ZEST_TRACE")) c.trace = true;
   if (const char* v = env("ZEST_FAULT")) c.fault = v;
+  if (const char* v = env("ZEST_CACHE_WRITES")) c.cache_writes = std::string(v) != "0";
   if (const char* v = env("ZEST_CONNECT_TIMEOUT_MS")) c.connect_timeout_ms = std::atoi(v);
   c.peer_id = peer_id::generate();
   return c;
@@ -101,7 +102,7 @@ std::string Config::to_json() const {
   w.key("cache_dir").str(cache_dir).key("xorb_cache_dir").str(xorb_cache_dir).key("chunk_cache_dir").str(chunk_cache_dir);
   w.key("pid_file").str(pid_file).key("dht_port").num(int64_t(dht_port)).key("listen_port").num(int64_t(listen_port));
   w.key("http_port").num(int64_t(http_port)).key("max_peers").num(int64_t(max_peers));
-  w.key("peer_connections").num(int64_t(peer_connections));
+  w.key("peer_connections").num(int64_t(peer_connections)).key("cache_writes").boolean(cache_writes);
   w.key("concurrency").num(int64_t(concurrency)).key("has_token").boolean(hf_token.has_value());
   w.key("gpus").num(int64_t(gpus)).key("hbm_cache_gb").num(hbm_cache_gb, 1);
   w.end();

@@ -52,6 +52,7 @@ struct Config {
   double hbm_cache_gb = 0;  // ZEST_HBM_CACHE_GB
   bool trace = false;       // ZEST_TRACE
   std::string fault;        // ZEST_FAULT ("drop:p,corrupt:p,delay:ms")
+  bool cache_writes = true; // ZEST_CACHE_WRITES=0: do not keep fetched runs in the xorb cache
 
   static Config from_env();
   std::string repo_dir(const std::string& repo_id) const;  // models--org--name

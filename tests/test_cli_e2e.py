@@ -320,3 +320,13 @@ def test_p2p_cluster_script_local(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "all scenarios passed" in r.stdout
     assert r.stdout.count("P2P ratio 100.0%") == 2
+
+
+def test_cache_writes_off(hub, nodes):
+    """ZEST_CACHE_WRITES=0: the pull verifies and writes the snapshot but keeps no xorb runs."""
+    files = sample_files(seed=3)
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("nocache")
+    a.run("pull", REPO_ID, "--no-p2p", env={"ZEST_CACHE_WRITES": "0"})
+    assert_snapshot(a, REPO_ID, commit, files)
+    assert a.xorb_files() == []

@@ -77,6 +77,18 @@ def main() -> int:
               f"({dt:.1f}s, {len(out)} tensors)", flush=True)
         del out
         torch.cuda.empty_cache()
+        # same, without keeping the fetched runs in the disk xorb cache (pure network -> HBM)
+        os.environ.update(hub.env(str(work / "direct_nocache")))
+        os.environ["ZEST_CACHE_WRITES"] = "0"
+        t0 = time.time()
+        out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        os.environ.pop("ZEST_CACHE_WRITES")
+        res.update(direct_nocache_s=round(dt, 3), direct_nocache_gbps=round(total / dt / 1e9, 3))
+        print(f"[direct, ZEST_CACHE_WRITES=0] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
+        del out
+        torch.cuda.empty_cache()
         if not a.skip_host:
             env = dict(os.environ, **hub.env(str(work / "host")))
             t0 = time.time()
