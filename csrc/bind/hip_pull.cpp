@@ -98,24 +98,73 @@ class DeviceXetPull {
   }
 
   py::dict pull_file(const std::string& hex, uintptr_t dst_ptr, uint64_t dst_size) {
+    py::list r = pull_files({std::make_tuple(hex, dst_ptr, dst_size)});
+    return r[0].cast<py::dict>();
+  }
+
+  // Pull several Xet files (hash, device pointer, size) through ONE pipeline: staging batches
+  // cross file boundaries, so there is no per-file drain; every file's Merkle hash is checked in a
+  // single kernel launch at the end.  Term destinations are device addresses relative to the
+  // lowest destination pointer.
+  py::list pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
     const auto t0 = std::chrono::steady_clock::now();
-    cas::Reconstruction rec;
+    const size_t nf = files.size();
+    std::vector<cas::Reconstruction> recs(nf);
     {
       py::gil_scoped_release nogil;
-      rec = bridge_->get_reconstruction(hex);
+      std::vector<std::string> errs(nf);
+      std::atomic<size_t> k{0};
+      auto w = [&]() {
+        for (size_t f; (f = k.fetch_add(1)) < nf;) {
+          try {
+            recs[f] = bridge_->get_reconstruction(std::get<0>(files[f]));
+          } catch (const std::exception& e) {
+            errs[f] = e.what();
+          }
+        }
+      };
+      std::vector<std::thread> ts;
+      for (size_t t = 0; t < std::min<size_t>(nf, 8); ++t) ts.emplace_back(w);
+      for (auto& t : ts) t.join();
+      for (size_t f = 0; f < nf; ++f)
+        if (!errs[f].empty()) throw Error("DownloadFailed", std::get<0>(files[f]) + ": " + errs[f]);
     }
-    if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
-    const size_t n = rec.terms.size();
-    std::vector<uint64_t> dst_off(n + 1, 0), cbase(n + 1, 0);
-    for (size_t i = 0; i < n; ++i) {
-      dst_off[i + 1] = dst_off[i] + rec.terms[i].unpacked_length;
-      cbase[i + 1] = cbase[i] + (rec.terms[i].range.end - rec.terms[i].range.start);
+    // Global term list in file order; chunk indices are global (one hash array for all files).
+    struct GTerm {
+      size_t file, term;
+      uint64_t dst;    // device address offset from `base`
+      uint64_t chunk;  // global index of the term's first chunk
+      uint32_t nchunks;
+      uint64_t ulen;
+    };
+    std::vector<GTerm> gt;
+    std::vector<uint64_t> file_chunk0(nf + 1, 0);
+    uintptr_t base = UINTPTR_MAX, top_addr = 0;
+    for (size_t f = 0; f < nf; ++f) {
+      base = std::min(base, std::get<1>(files[f]));
+      top_addr = std::max<uintptr_t>(top_addr, std::get<1>(files[f]) + std::get<2>(files[f]));
     }
-    if (dst_off[n] != dst_size) throw Error("SizeMismatch", "file is " + std::to_string(dst_off[n]) + " bytes");
-    const uint64_t nck = cbase[n];
+    for (size_t f = 0; f < nf; ++f) {
+      const auto& rec = recs[f];
+      if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
+      uint64_t off = 0, c = file_chunk0[f];
+      for (size_t i = 0; i < rec.terms.size(); ++i) {
+        const auto& t = rec.terms[i];
+        const uint32_t n = uint32_t(t.range.end - t.range.start);
+        gt.push_back({f, i, std::get<1>(files[f]) - base + off, c, n, t.unpacked_length});
+        off += t.unpacked_length;
+        c += n;
+      }
+      if (off != std::get<2>(files[f]))
+        throw Error("SizeMismatch", std::get<0>(files[f]) + " is " + std::to_string(off) + " bytes");
+      file_chunk0[f + 1] = c;
+    }
+    const uint64_t nck = file_chunk0[nf];
+    const size_t n = gt.size();
     hashes_.ensure(nck ? nck * 32 : 32);
     sizes_.ensure(nck ? nck : 1);
-    uint8_t* dst = reinterpret_cast<uint8_t*>(dst_ptr);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(base);
+    const uint64_t dst_size = nf ? uint64_t(top_addr - base) : 0;
     hip_check(hipMemsetAsync(err_.p, 0, sizeof(unsigned long long), stream_), "hipMemset");
     uint64_t fetched = 0;
     std::string fetch_err;
@@ -126,12 +175,12 @@ class DeviceXetPull {
       while (next < n && fetch_err.empty()) {
         // Batch [next, end) by an upper bound of each term's fetched size, so every term fetched
         // in the batch has a reserved region of the pinned buffer (no refetch, no second copy
-        // pass): workers memcpy their run straight into place.
+        // pass): workers receive / copy their run straight into place.
         std::vector<uint64_t> off;
         uint64_t pos = 0;
         size_t end = next;
         while (end < n) {
-          const uint64_t bound = term_bound(rec.terms[end], cbase[end + 1] - cbase[end]);
+          const uint64_t bound = term_bound(gt[end].ulen, gt[end].nchunks);
           if (bound > cap_) {
             if (end > next) break;
             grow_staging(bound);  // one huge term: enlarge both slots (waits for them)
@@ -154,14 +203,16 @@ class DeviceXetPull {
             const size_t i = k.fetch_add(1);
             if (i >= end) return;
             try {
+              const auto& rec = recs[gt[i].file];
               // The run is received straight into this term's region of the pinned buffer when it
               // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
               uint8_t* region = s.host + off[i - next];
               const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
               auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-              XorbFetchResult r = bridge_->fetch_term(rec.terms[i], rec, true, true, sink);
+              XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, true, true, sink);
               auto idx = xet::index_chunks(r.bytes(), r.size());
-              if (r.local_end > idx.size() || r.local_start >= r.local_end) throw Error("RangeOutOfBounds", hex);
+              if (r.local_end > idx.size() || r.local_start >= r.local_end)
+                throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
               const uint64_t a = idx[r.local_start].header_off;
               const uint64_t b = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
               if (r.ext) {
@@ -189,16 +240,17 @@ class DeviceXetPull {
           ZgTerm t{};
           t.src = src_at[i - next];
           t.src_len = len[i - next];
-          t.dst = dst_off[i];
-          t.chunk_base = uint32_t(cbase[i] - cbase[next]);
-          t.n_chunks = uint32_t(cbase[i + 1] - cbase[i]);
-          t.ulen = rec.terms[i].unpacked_length;
+          t.dst = gt[i].dst;
+          t.chunk_base = uint32_t(gt[i].chunk - gt[next].chunk);
+          t.n_chunks = gt[i].nchunks;
+          t.ulen = gt[i].ulen;
           s.terms.push_back(t);
           fetched += t.src_len;
           top = std::max<uint64_t>(top, t.src + t.src_len);
         }
         const int nterms = int(end - next);
-        const uint64_t c0 = cbase[next], c1 = cbase[end];
+        const uint64_t c0 = gt[next].chunk;
+        const uint64_t c1 = end < n ? gt[end].chunk : nck;
         const int nchunks = int(c1 - c0);
         s.terms_dev.ensure(size_t(nterms));
         s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
@@ -225,26 +277,43 @@ class DeviceXetPull {
     unsigned long long e = 0;
     hip_check(hipMemcpy(&e, err_.p, sizeof e, hipMemcpyDeviceToHost), "err D2H");
     if (e) throw Error("IngestError", "code " + std::to_string(e >> 32) + " at " + std::to_string(e & 0xFFFFFFFFu));
-    // Merkle verify of the whole file on the GPU
-    ZgMerkleJob job{0, nck, 1, 0};
-    merkle_job_.ensure(1);
-    hip_check(hipMemcpyAsync(merkle_job_.p, &job, sizeof job, hipMemcpyHostToDevice, stream_), "job H2D");
-    const size_t sb = zg_merkle_scratch_bytes(nck ? nck : 1, 1);
-    merkle_scratch_.ensure(sb);
-    root_.ensure(32);
-    hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, 1, root_.p, merkle_scratch_.p, sb, stream_), "merkle");
-    uint8_t root[32];
-    hip_check(hipMemcpyAsync(root, root_.p, 32, hipMemcpyDeviceToHost, stream_), "root D2H");
-    hip_check(hipStreamSynchronize(stream_), "sync");
-    const std::string got = xet::to_hex(*reinterpret_cast<xet::Hash*>(root));
-    if (got != hex) throw Error("HashMismatch", "device bytes hash " + got + " != " + hex);
-    py::dict d;
-    d["bytes"] = dst_size;
-    d["fetched_bytes"] = fetched;
-    d["terms"] = n;
-    d["chunks"] = nck;
-    d["seconds"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    return d;
+    // Merkle verify of every file in one launch
+    std::vector<ZgMerkleJob> jobs(nf);
+    uint64_t max_leaves = 1;
+    for (size_t f = 0; f < nf; ++f) {
+      jobs[f] = ZgMerkleJob{file_chunk0[f], file_chunk0[f + 1] - file_chunk0[f], 1, 0};
+      max_leaves = std::max<uint64_t>(max_leaves, jobs[f].n_leaves);
+    }
+    std::vector<uint8_t> roots(32 * std::max<size_t>(nf, 1));
+    if (nf) {
+      merkle_job_.ensure(nf);
+      hip_check(hipMemcpyAsync(merkle_job_.p, jobs.data(), sizeof(ZgMerkleJob) * nf, hipMemcpyHostToDevice, stream_),
+                "job H2D");
+      const size_t sb = zg_merkle_scratch_bytes(max_leaves, int(nf));
+      merkle_scratch_.ensure(sb);
+      root_.ensure(32 * nf);
+      hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, int(nf), root_.p, merkle_scratch_.p, sb, stream_),
+                "merkle");
+      hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
+      hip_check(hipStreamSynchronize(stream_), "sync");
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    py::list out;
+    for (size_t f = 0; f < nf; ++f) {
+      xet::Hash h;
+      std::memcpy(h.data(), roots.data() + 32 * f, 32);
+      const std::string got = xet::to_hex(h);
+      if (got != std::get<0>(files[f]))
+        throw Error("HashMismatch", "device bytes hash " + got + " != " + std::get<0>(files[f]));
+      py::dict d;
+      d["bytes"] = std::get<2>(files[f]);
+      d["terms"] = recs[f].terms.size();
+      d["chunks"] = file_chunk0[f + 1] - file_chunk0[f];
+      d["seconds"] = secs;
+      d["fetched_bytes"] = fetched;  // for the whole call
+      out.append(d);
+    }
+    return out;
   }
 
   std::string stats_json() const { return bridge_->stats_json(); }
@@ -254,8 +323,8 @@ class DeviceXetPull {
  private:
   // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does
   // not help, so the payload is <= its unpacked size plus LZ4 frame overhead; + 8-byte headers.
-  static uint64_t term_bound(const cas::Term& t, uint64_t nchunks) {
-    return t.unpacked_length + t.unpacked_length / 128 + 80 * nchunks + 4096;
+  static uint64_t term_bound(uint64_t unpacked, uint64_t nchunks) {
+    return unpacked + unpacked / 128 + 80 * nchunks + 4096;
   }
 
   void grow_staging(uint64_t bytes) {
@@ -307,6 +376,8 @@ void bind_hip_pull(py::module_& m) {
            py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("device") = 0,
            py::arg("staging_bytes") = size_t(1) << 30, py::arg("threads") = 16)
       .def("pull_file", &DeviceXetPull::pull_file, py::arg("xet_hash"), py::arg("dst_ptr"), py::arg("dst_size"))
+      .def("pull_files", &DeviceXetPull::pull_files, py::arg("files"),
+           "[(xet_hash, dst_ptr, size), ...] through one pipeline; returns one stats dict per file")
       .def("stats_json", &DeviceXetPull::stats_json)
       .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

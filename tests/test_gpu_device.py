@@ -143,3 +143,34 @@ def zest_amd_pull_cpu(repo):
     import zest_amd
 
     return zest_amd.pull(repo, p2p=False)
+
+
+def test_pull_files_multi_file_pipeline(tmp_path, monkeypatch):
+    """DeviceXetPull.pull_files: several files through one pipeline (tiny staging so batches cross
+    file boundaries); a wrong expected hash is reported as a mismatch."""
+    from zest_amd import _core, ops as zops
+
+    files = {f"model-{i:05d}.safetensors": bytes(np.random.default_rng(i).integers(0, 256, 300_000 + 7919 * i,
+                                                                                   dtype=np.uint8))
+             for i in range(4)}
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    try:
+        hub.add_repo("org/multi", files, xet_min_size=1)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        commit, listing = _core.list_repo_files("org/multi", "main", "model")
+        listing = sorted((f for f in listing if f["xet_hash"]), key=lambda f: f["path"])
+        dp = zops.hip().DeviceXetPull("org/multi", "main", "model", False, [], None, False, [], 0, 128 << 10, 4)
+        bufs = [zops.padded_empty(f["size"], "cuda:0")[:f["size"]] for f in listing]
+        torch.cuda.synchronize()
+        st = dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing, bufs)])
+        assert len(st) == 4
+        for f, b in zip(listing, bufs):
+            assert b.cpu().numpy().tobytes() == files[f["path"]]
+        wrong = listing[1]["xet_hash"][::-1]
+        with pytest.raises(Exception):
+            dp.pull_files([(listing[0]["xet_hash"], bufs[0].data_ptr(), listing[0]["size"]),
+                           (wrong, bufs[1].data_ptr(), listing[1]["size"])])
+    finally:
+        hub.stop()

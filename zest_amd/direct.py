@@ -32,10 +32,11 @@ def pull_to_device(repo: str, revision: str = "main", device="cuda:0", *, p2p: b
     if xet:
         dp = ops.hip().DeviceXetPull(repo, revision, repo_type, p2p, list(peers or []), tracker, dht,
                                      list(dht_bootstrap or []), dev.index or 0, staging_bytes, threads)
-        for f in xet:
-            buf = ops.padded_empty(f["size"], dev)[:f["size"]]
-            torch.cuda.synchronize(dev)  # allocation visible to the pull's private stream
-            dp.pull_file(f["xet_hash"], buf.data_ptr(), f["size"])
+        bufs = [ops.padded_empty(f["size"], dev)[:f["size"]] for f in xet]
+        torch.cuda.synchronize(dev)  # allocations visible to the pull's private stream
+        # one pipeline for all files: staging batches cross file boundaries
+        dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(xet, bufs)])
+        for f, buf in zip(xet, bufs):
             _add_views(out, buf, f["path"])
             if save_snapshot:
                 _save(repo, commit or revision, f["path"], buf)

@@ -51,27 +51,39 @@ def main(argv=None) -> int:
     if mine:
         dp = ops.hip().DeviceXetPull(a.repo, a.revision, a.repo_type, p2p, a.peer, a.tracker, not a.no_dht,
                                      a.dht_bootstrap, dev.index or 0, 1 << 30, 16)
+        todo = []
         for f in mine:
             dst = os.path.join(snap, f["path"])
             if os.path.exists(dst) and os.path.getsize(dst) == f["size"]:
                 print(f"[rank {rank}] {f['path']} (cached)", flush=True)
                 continue
-            buf = ops.padded_empty(f["size"], dev)[:f["size"]]
-            torch.cuda.synchronize(dev)
-            try:
-                st = dp.pull_file(f["xet_hash"], buf.data_ptr(), f["size"])
-            except Exception as e:  # keep going with the other files, like the host pull
-                print(f"[rank {rank}] {f['path']}: error {e}", file=sys.stderr, flush=True)
-                failed += 1
+            todo.append(f)
+        bufs = [ops.padded_empty(f["size"], dev)[:f["size"]] for f in todo]
+        torch.cuda.synchronize(dev)
+        try:  # one pipeline for all of this rank's files
+            st = dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(todo, bufs)]) if todo else []
+        except Exception as e:  # fall back to file by file so one bad file does not sink the rest
+            print(f"[rank {rank}] batch pull failed ({e}); retrying file by file", file=sys.stderr, flush=True)
+            st = []
+            for f, b in zip(todo, bufs):
+                try:
+                    st.append(dp.pull_file(f["xet_hash"], b.data_ptr(), f["size"]))
+                except Exception as e2:
+                    print(f"[rank {rank}] {f['path']}: error {e2}", file=sys.stderr, flush=True)
+                    failed += 1
+                    st.append(None)
+        for f, buf, s_ in zip(todo, bufs, st):
+            if s_ is None:
                 continue
+            dst = os.path.join(snap, f["path"])
             os.makedirs(os.path.dirname(dst), exist_ok=True)
             tmp = dst + ".incomplete"
             buf.cpu().numpy().tofile(tmp)
             os.replace(tmp, dst)
             done_bytes += f["size"]
             print(f"[rank {rank}] {f['path']} [xet, gpu {dev.index}] {f['size'] / 1e6:.1f} MB "
-                  f"verified in {st['seconds']:.2f}s", flush=True)
-            del buf
+                  f"verified ({s_['seconds']:.2f}s for this rank's batch)", flush=True)
+        del bufs
         stats = json.loads(dp.stats_json())
     else:
         stats = {}
