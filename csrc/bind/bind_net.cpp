@@ -592,6 +592,16 @@ void bind_extra(py::module_& m) {
     (void)repo_type;
     storage::write_ref(cfg, repo, ref, commit);
   }, py::arg("repo"), py::arg("ref"), py::arg("commit"), py::arg("repo_type") = "model");
+  m.def("write_verified_marker", [](std::string repo, std::string commit, std::string path, std::string xet_hex,
+                                    std::string file) {
+    Config cfg = Config::from_env();
+    storage::write_verified_marker(cfg, repo, commit, path, xet_hex, file);
+  }, py::arg("repo"), py::arg("commit"), py::arg("path"), py::arg("xet_hash"), py::arg("file"),
+     "Record that `file` (snapshot path) was verified against its Xet hash");
+  m.def("xet_hash_of_file", [](std::string file, int threads) {
+    py::gil_scoped_release nogil;
+    return storage::xet_hash_of_file(file, threads);
+  }, py::arg("file"), py::arg("threads") = 0, "Xet file hash of a file on disk (CDC + BLAKE3 + Merkle)");
   m.def("list_repo_files", [](std::string repo, std::string revision, std::string repo_type) {
     Config cfg = Config::from_env();
     std::vector<hub::RepoFile> files;

@@ -118,9 +118,25 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
     out << "[" << k << "/" << files.size() << "] " << f.path;
     const std::string dst = S.snapshot_dir + "/" + f.path;
     if (storage::exists(dst) && (f.size == 0 || storage::file_size(dst) == f.size)) {
-      out << " (cached)\n";
-      S.cached_files++;
-      continue;
+      // Xet files must also match their verified marker (or re-hash to the published hash):
+      // size alone would keep a corrupted or truncated-then-extended copy forever.
+      bool good = true;
+      if (f.xet_hash && opt.verify &&
+          !storage::check_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, dst)) {
+        try {
+          good = storage::xet_hash_of_file(dst) == *f.xet_hash;
+        } catch (const Error&) {
+          good = false;
+        }
+        if (good) storage::write_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, dst);
+      }
+      if (good) {
+        out << " (cached)\n";
+        S.cached_files++;
+        continue;
+      }
+      out << " (cached copy failed verification, downloading again)";
+      storage::remove_file(dst);
     }
     if (f.xet_hash) {
       out << " [xet]\n" << std::flush;
@@ -132,6 +148,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
       try {
         FileResult r = dl.reconstruct_to_file(*f.xet_hash, dst, opt.verify);
         S.bytes += r.bytes;
+        if (r.verified) storage::write_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, dst);
         if (r.resumed_terms) out << "  resumed " << r.resumed_terms << "/" << r.terms << " terms\n";
       } catch (const Error& e) {
         err << "  Parallel download error (" << e.what() << ")\n";

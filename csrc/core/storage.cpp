@@ -1,4 +1,7 @@
 #include "storage.h"
+#include "xet_hash.h"
+#include "cdc.h"
+#include <thread>
 
 #include <dirent.h>
 #include <fcntl.h>
@@ -293,6 +296,80 @@ uint64_t XorbCache::bytes_on_disk() const {
   uint64_t t = 0;
   for (auto& k : list_cached_xorbs(cfg_)) t += file_size(cfg_.xorb_cache_path(k));
   return t;
+}
+
+std::string verified_marker_path(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                                 const std::string& path) {
+  const std::string repo = cfg.repo_dir(repo_id);
+  const size_t slash = repo.rfind('/');
+  return cfg.cache_dir + "/verified/" + (slash == std::string::npos ? repo : repo.substr(slash + 1)) + "/" + commit +
+         "/" + path;
+}
+
+namespace {
+bool stat_file(const std::string& file, uint64_t& size, uint64_t& mtime_ns) {
+  struct stat st;
+  if (::stat(file.c_str(), &st) != 0) return false;
+  size = uint64_t(st.st_size);
+  mtime_ns = uint64_t(st.st_mtim.tv_sec) * 1000000000ull + uint64_t(st.st_mtim.tv_nsec);
+  return true;
+}
+}  // namespace
+
+void write_verified_marker(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                           const std::string& path, const std::string& xet_hex, const std::string& file) {
+  uint64_t size = 0, mtime = 0;
+  if (!stat_file(file, size, mtime)) return;
+  write_file_atomic(verified_marker_path(cfg, repo_id, commit, path),
+                    xet_hex + " " + std::to_string(size) + " " + std::to_string(mtime) + "\n", false);
+}
+
+bool check_verified_marker(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                           const std::string& path, const std::string& xet_hex, const std::string& file) {
+  uint64_t size = 0, mtime = 0;
+  if (!stat_file(file, size, mtime)) return false;
+  auto b = read_file(verified_marker_path(cfg, repo_id, commit, path));
+  if (!b) return false;
+  const std::string want = xet_hex + " " + std::to_string(size) + " " + std::to_string(mtime) + "\n";
+  return std::string(b->begin(), b->end()) == want;
+}
+
+std::string xet_hash_of_file(const std::string& file, int threads) {
+  int fd = ::open(file.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) throw Error("IoError", "open " + file);
+  struct stat st;
+  if (::fstat(fd, &st) != 0) {
+    ::close(fd);
+    throw Error("IoError", "stat " + file);
+  }
+  const size_t n = size_t(st.st_size);
+  const uint8_t* data = nullptr;
+  void* m = MAP_FAILED;
+  if (n) {
+    m = ::mmap(nullptr, n, PROT_READ, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) {
+      ::close(fd);
+      throw Error("IoError", "mmap " + file);
+    }
+    ::madvise(m, n, MADV_SEQUENTIAL);
+    data = static_cast<const uint8_t*>(m);
+  }
+  ::close(fd);
+  std::vector<uint64_t> ends = n ? xet::chunk_ends(data, n) : std::vector<uint64_t>{};
+  std::vector<xet::HashSize> leaves(ends.size());
+  const int nt = threads > 0 ? threads : int(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < ends.size();) {
+      const uint64_t a = i ? ends[i - 1] : 0;
+      leaves[i] = {xet::chunk_hash(data + a, size_t(ends[i] - a)), ends[i] - a};
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nt; ++t) ts.emplace_back(work);
+  for (auto& t : ts) t.join();
+  if (m != MAP_FAILED) ::munmap(m, n);
+  return xet::to_hex(xet::file_hash(leaves));
 }
 
 }  // namespace zest::storage

@@ -27,8 +27,8 @@ uint64_t file_size(const std::string& path);  // 0 if missing
 // are re-validated on read and content-verified by hash, so losing one on a crash only costs a
 // refetch, while syncing every 64 MiB xorb serialises the pull on disk writeback).
 void write_file_atomic(const std::string& path, const uint8_t* data, size_t n, bool durable = true);
-inline void write_file_atomic(const std::string& path, const std::string& s) {
-  write_file_atomic(path, reinterpret_cast<const uint8_t*>(s.data()), s.size());
+inline void write_file_atomic(const std::string& path, const std::string& s, bool durable = true) {
+  write_file_atomic(path, reinterpret_cast<const uint8_t*>(s.data()), s.size(), durable);
 }
 std::optional<Bytes> read_file(const std::string& path);
 // Read [off, off+n) of a file into out (false if short/missing).
@@ -64,6 +64,18 @@ struct CacheHit {
 
 // Slice a run (first chunk = `offset`) to chunks [start, end); nullopt if it does not cover them.
 std::optional<CacheHit> slice_run(const Bytes& data, uint32_t offset, uint32_t start, uint32_t end);
+
+// Verified-file markers: `{cache_dir}/verified/{repo folder}/{commit}/{path}` holds
+// "<xet hash> <size> <mtime ns>".  A snapshot file counts as cached only when its marker matches
+// (the reference trusts existence alone, so a truncated file from a crash stays "cached" forever).
+std::string verified_marker_path(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                                 const std::string& path);
+void write_verified_marker(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                           const std::string& path, const std::string& xet_hex, const std::string& file);
+bool check_verified_marker(const Config& cfg, const std::string& repo_id, const std::string& commit,
+                           const std::string& path, const std::string& xet_hex, const std::string& file);
+// Xet file hash of a file on disk (CDC + keyed BLAKE3 chunk hashes + Merkle), multi-threaded.
+std::string xet_hash_of_file(const std::string& file, int threads = 0);
 
 class XorbRegistry {
  public:

@@ -330,3 +330,30 @@ def test_cache_writes_off(hub, nodes):
     a.run("pull", REPO_ID, "--no-p2p", env={"ZEST_CACHE_WRITES": "0"})
     assert_snapshot(a, REPO_ID, commit, files)
     assert a.xorb_files() == []
+
+
+def test_cached_file_is_verified(hub, nodes):
+    """A snapshot file of the right size but wrong content is re-downloaded (the reference keeps any
+    file whose path exists); an intact one is reported cached without refetching."""
+    files = sample_files(seed=4)
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("verify-cached")
+    a.run("pull", REPO_ID, "--no-p2p")
+    big = max(files, key=lambda k: len(files[k]))
+    path = a.snapshot(REPO_ID, commit) / big
+    before = hub.counters.get("xorb_get", 0)
+    out = a.run("pull", REPO_ID, "--no-p2p").stdout
+    assert f"{big} (cached)" in out and hub.counters.get("xorb_get", 0) == before
+    data = bytearray(path.read_bytes())
+    data[len(data) // 2] ^= 0xFF
+    path.write_bytes(bytes(data))  # same size, new mtime, wrong bytes
+    out = a.run("pull", REPO_ID, "--no-p2p").stdout
+    assert "failed verification" in out
+    assert_snapshot(a, REPO_ID, commit, files)
+    # a copy without a marker (e.g. written by another tool) is re-hashed once and then trusted
+    marker_root = a.root / "zest" / "verified"
+    import shutil
+    shutil.rmtree(marker_root)
+    out = a.run("pull", REPO_ID, "--no-p2p").stdout
+    assert f"{big} (cached)" in out
+    assert any(marker_root.rglob("*"))

@@ -80,6 +80,7 @@ def main(argv=None) -> int:
             tmp = dst + ".incomplete"
             buf.cpu().numpy().tofile(tmp)
             os.replace(tmp, dst)
+            _core.write_verified_marker(a.repo, commit, f["path"], f["xet_hash"], dst)  # verified on the GPU
             done_bytes += f["size"]
             print(f"[rank {rank}] {f['path']} [xet, gpu {dev.index}] {f['size'] / 1e6:.1f} MB "
                   f"verified ({s_['seconds']:.2f}s for this rank's batch)", flush=True)
