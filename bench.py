@@ -7,7 +7,10 @@ in its HBM arena:
 
   origin (pinned host, = the CDN bytes of this rank's 1/N of the reconstruction terms)
     --hipMemcpyAsync--> HBM staging ring --HIP index/place/BLAKE3--> arena
-    --RCCL p2p over xGMI--> every other GPU; chunk-hash all-reduce; GPU Merkle file-hash check.
+    --RCCL over xGMI--> every other GPU; chunk-hash all-reduce; GPU Merkle file-hash check.
+
+The replication strategy (batched p2p sends, coalesced broadcasts, or equal-slab all-gather) is
+picked during setup by timing each one on the machine (--exchange auto, DevicePuller.autotune_exchange).
 
 value      = N * model_bytes / step_time   (bytes made resident + verified across all GPUs, GB/s)
 p2p_ratio  = fraction of each GPU's model bytes that arrived from peers rather than the origin
@@ -49,6 +52,8 @@ def main() -> None:
     ap.add_argument("--seeders", type=int, default=0,
                     help="ranks that pull from the origin (default all); the rest leech everything from "
                          "them over xGMI (BASELINE config 2: --gpus 2 --seeders 1)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "bcast", "allgather"],
+                    help="intra-node replication strategy; auto = time each on this machine during setup")
     a = ap.parse_args()
 
     from zest_amd import models, ops
@@ -98,6 +103,13 @@ def main() -> None:
     torch.cuda.synchronize()
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
+    if world_size > 1:
+        if a.exchange == "auto":
+            t_x = puller.autotune_exchange()
+            log(rank, "exchange autotune (s over the first rounds): "
+                + ", ".join(f"{m}={v:.3f}" for m, v in t_x.items()) + f" -> {puller.exchange}")
+        else:
+            puller.exchange = a.exchange
 
     def barrier():
         if dist is not None:
@@ -152,7 +164,8 @@ def main() -> None:
                    "parallelism": (f"swarm{world_size}" if seeders == world_size
                                    else f"seed{seeders}-leech{world_size - seeders}"), "model_bytes": model_b, "files": len(world.xet_files),
                    "chunks": world.n_chunks, "xorbs": world.n_xorbs, "terms": int(len(world.terms)),
-                   "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": "rccl_p2p" if world_size > 1 else "none",
+                   "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": puller.exchange if world_size > 1 else "none",
+                   "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
                    "verify": "merkle_file_hash" + ("+received" if a.verify_received else "")},
     }
     if rank == 0:

@@ -647,7 +647,13 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
   if (e != hipSuccess) return e;
   // Persistent grid: up to 5 blocks (20 waves) per CU on 256 CUs.
   const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int grid = blocks < 1280 ? blocks : 1280;
+  // ZG_LZ4_GRID caps the persistent grid (occupancy experiments: 256 = one wave per SIMD).
+  static const int grid_cap = [] {
+    const char* v = getenv("ZG_LZ4_GRID");
+    const int g = v ? atoi(v) : 0;
+    return g > 0 && g < 1280 ? g : 1280;
+  }();
+  const int grid = blocks < grid_cap ? blocks : grid_cap;
   static const bool prof = [] {
     const char* v = getenv("ZG_LZ4_PROF");
     return v && *v && *v != '0';

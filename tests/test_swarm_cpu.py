@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _worker(rank, world_size, port, model, result_q, seeders=None):
+def _worker(rank, world_size, port, model, result_q, seeders=None, exchange="p2p"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
@@ -24,12 +24,16 @@ def _worker(rank, world_size, port, model, result_q, seeders=None):
         arena = torch.zeros(w.arena_bytes + 4096, dtype=torch.uint8)[: w.arena_bytes]
         p = DevicePuller(w, arena, rank, world_size, round_bytes=512 << 10, seeders=seeders)
         p.build_origin_host(contents)
+        if exchange == "auto":
+            p.autotune_exchange()
+        else:
+            p.exchange = exchange
         for _ in range(2):
             arena.zero_()
             p.step()
             p.check()
         ok = all(arena[f.arena_off:f.arena_off + f.size].numpy().tobytes() == contents[f.path] for f in w.xet_files)
-        result_q.put((rank, ok, p.bytes_received, p.bytes_ingested, w.model_bytes))
+        result_q.put((rank, ok, p.bytes_received, p.bytes_ingested, w.model_bytes, p.exchange))
     finally:
         dist.destroy_process_group()
 
@@ -51,7 +55,7 @@ def test_cpu_swarm_full_replication(world_size):
     model = res[0][4]
     # every rank ingests ~1/N from the origin and receives the rest from peers
     assert total_in < model * 1.01 + 8 * 4096
-    for _, _, recv, ing, m in res:
+    for _, _, recv, ing, m, _x in res:
         assert recv > 0 and recv < m
 
 
@@ -71,5 +75,26 @@ def test_cpu_seeder_leecher():
     assert all(ok for _, ok, *_ in res)
     model = res[0][4]
     assert res[0][2] == 0 and res[0][3] > 0            # seeder: everything from the origin
-    for _, _, recv, ing, m in res[1:]:
+    for _, _, recv, ing, m, _x in res[1:]:
         assert ing == 0 and recv == m                   # leechers: everything from the seeder
+
+
+@pytest.mark.parametrize("exchange", ["bcast", "allgather", "auto"])
+def test_cpu_swarm_exchange_modes(exchange):
+    """The alternative replication strategies (coalesced broadcasts, equal-slab all-gather +
+    unpack) and the setup-time autotuner give the same fully verified replica on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + 11 * ["bcast", "allgather", "auto"].index(exchange) + os.getpid() % 100
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, "llama-tiny", q, None, exchange)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, *_ in res)
+    chosen = {r[5] for r in res}
+    assert len(chosen) == 1, chosen  # all ranks agree
+    if exchange != "auto":
+        assert chosen == {exchange}

@@ -29,6 +29,19 @@ import torch
 from . import ops
 from .synthetic import SyntheticWorld
 
+EXCHANGE_MODES = ("p2p", "bcast", "allgather")
+
+
+class _StreamJoin:
+    """Work-like handle: wait() orders the current stream after everything queued on `stream`."""
+
+    def __init__(self, stream):
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
 
 @dataclass
 class RoundWork:
@@ -112,6 +125,8 @@ class DevicePuller:
         self.group = group
         self.verify_received = verify_received
         self.exchange = exchange
+        self.exchange_times: dict = {}
+        self._gather_bufs = None
         self.is_cuda = self.device.type == "cuda"
         T = world.terms
         self.rank_terms = plan_rank_terms(world, n_ranks, seeders)
@@ -231,7 +246,22 @@ class DevicePuller:
                 pos += 8 + n
 
     # ------------------------------------------------------------------------------------------
-    def _exchange(self, k: int):
+    def _exchange(self, k: int, mode: str | None = None):
+        """Replicate round k's regions to every rank.  Three strategies, picked at
+        setup by `autotune_exchange` on the real hardware because their relative speed depends on
+        RCCL's channel/link mapping over the xGMI mesh:
+
+        * ``p2p``       batch_isend_irecv: each owner sends its region to every peer (N-1 pairs).
+        * ``bcast``     uneven all_gather straight into the arena views (RCCL: one group of N
+                        broadcasts, zero copy).
+        * ``allgather`` equal-size slabs through all_gather_into_tensor into a double-buffered
+                        gather buffer, then D2D unpack on a side stream (RCCL's ring/mesh allgather).
+        """
+        mode = mode or self.exchange
+        if mode == "bcast":
+            return self._exchange_bcast(k)
+        if mode == "allgather":
+            return self._exchange_allgather(k)
         import torch.distributed as dist
         lo_me, hi_me = self.regions[k][self.rank]
         p2p = []
@@ -246,6 +276,117 @@ class DevicePuller:
         if not p2p:
             return []
         return dist.batch_isend_irecv(p2p)
+
+    def _backend(self) -> str:
+        import torch.distributed as dist
+        return str(dist.get_backend(self.group)).lower()
+
+    def _global_rank(self, r: int) -> int:
+        import torch.distributed as dist
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _exchange_bcast(self, k: int):
+        import torch.distributed as dist
+        regs = self.regions[k]
+        if all(hi <= lo for lo, hi in regs):
+            return []
+        outs = [self.arena[lo:hi] for lo, hi in regs]
+        if self._backend() == "nccl":
+            # ProcessGroupNCCL turns an uneven all_gather into one coalesced group of broadcasts.
+            return [dist.all_gather(outs, outs[self.rank], group=self.group, async_op=True)]
+        works = []
+        for r, t in enumerate(outs):
+            if t.numel():
+                works.append(dist.broadcast(t, src=self._global_rank(r), group=self.group, async_op=True))
+        return works
+
+    def _slab_plan(self, k: int):
+        """Equal-size slab per rank for round k; a region near the arena end starts earlier so the
+        slab stays inside the arena (receivers use only [lo, hi) of it)."""
+        regs = self.regions[k]
+        slab = max(hi - lo for lo, hi in regs)
+        n = self.arena.numel()
+        return slab, [max(0, min(lo, n - slab)) for lo, _ in regs]
+
+    def _exchange_allgather(self, k: int):
+        import torch.distributed as dist
+        slab, starts = self._slab_plan(k)
+        if slab == 0:
+            return []
+        if self._gather_bufs is None:
+            cap = max(self._slab_plan(j)[0] for j in range(self.n_rounds))
+            self._gather_bufs = [torch.empty(self.n_ranks * cap, dtype=torch.uint8, device=self.device)
+                                 for _ in range(2)]
+            self._gather_used = [False, False]
+            if self.is_cuda:
+                self._unpack_stream = torch.cuda.Stream(self.device)
+                self._unpacked = [torch.cuda.Event() for _ in range(2)]
+        b = k % 2
+        buf = self._gather_bufs[b][: self.n_ranks * slab]
+        if self.is_cuda and self._gather_used[b]:
+            # the collective may overwrite this buffer only after its previous round was unpacked
+            torch.cuda.current_stream(self.device).wait_event(self._unpacked[b])
+        me = starts[self.rank]
+        inp = self.arena[me:me + slab]
+        if self._backend() == "nccl":
+            work = dist.all_gather_into_tensor(buf, inp, group=self.group, async_op=True)
+        else:
+            work = dist.all_gather(list(buf.view(self.n_ranks, slab).unbind(0)), inp, group=self.group,
+                                   async_op=True)
+        regs = self.regions[k]
+
+        def unpack():
+            for p, (lo, hi) in enumerate(regs):
+                if p != self.rank and hi > lo:
+                    o = p * slab + lo - starts[p]
+                    self.arena[lo:hi].copy_(buf[o:o + hi - lo])
+
+        if not self.is_cuda:
+            work.wait()
+            unpack()
+            return []
+        with torch.cuda.stream(self._unpack_stream):
+            work.wait()  # the unpack stream waits for the collective, the compute stream does not
+            unpack()
+            self._unpacked[b].record(self._unpack_stream)
+        self._gather_used[b] = True
+        return [_StreamJoin(self._unpack_stream)]
+
+    def autotune_exchange(self, modes=EXCHANGE_MODES, max_rounds: int = 4) -> dict:
+        """Time each exchange strategy on this machine and keep the fastest (setup, untimed).
+
+        Per mode: one pass over the first rounds that also sets up RCCL's connections and buffers,
+        then a timed pass.  Timings are MAX-reduced, so every rank picks the same mode."""
+        import torch.distributed as dist
+        if self.n_ranks == 1:
+            return {}
+        modes = tuple(modes)
+        rounds = range(min(self.n_rounds, max_rounds))
+        times = {}
+        for mode in modes:
+            for _ in range(2):
+                self._sync()
+                dist.barrier(group=self.group)
+                t0 = time.perf_counter()
+                works = []
+                for k in rounds:
+                    works += self._exchange(k, mode)
+                for w in works:
+                    w.wait()
+                self._sync()
+                dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                                  device=self.device if self.is_cuda else "cpu")
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
+                times[mode] = float(dt.item())
+        self.exchange = min(modes, key=lambda m: times[m])
+        self.exchange_times = times
+        if self.exchange != "allgather":
+            self._gather_bufs = None
+        return times
+
+    def _sync(self):
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
 
     def step(self) -> dict:
         """One full pull of the model onto every rank.  Returns per-step stats."""
