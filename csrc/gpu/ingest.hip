@@ -227,19 +227,12 @@ __device__ __forceinline__ uint32_t win_u8(const Win& w, uint32_t a) {
   return (d >> (8 * (rel & 3))) & 0xFF;
 }
 
-// Lane i gets the byte at a + i (a in [wofs, wofs + 256)).
+// Lane i gets the byte at a + i (a in [wofs, wofs + 256)): two gathers and a select, no branch.
 __device__ __forceinline__ uint32_t win_lane_u8(const Win& w, uint32_t a, uint32_t lane) {
-  const uint32_t r0 = a - w.wofs;
-  const uint32_t rel = r0 + lane;
-  uint32_t d;
-  if (r0 <= 192) {
-    d = __shfl(w.w0, int(rel >> 2), kWave);
-  } else {
-    const uint32_t v0 = __shfl(w.w0, int((rel >> 2) & 63), kWave);
-    const uint32_t v1 = __shfl(w.w1, int((rel >> 2) & 63), kWave);
-    d = rel < 256 ? v0 : v1;
-  }
-  return (d >> (8 * (rel & 3))) & 0xFF;
+  const uint32_t rel = a - w.wofs + lane;  // < 320: inside w0 | w1
+  const uint32_t idx = (rel >> 2) & 63;
+  const uint32_t d0 = __shfl(w.w0, int(idx), kWave), d1 = __shfl(w.w1, int(idx), kWave);
+  return ((rel < 256 ? d0 : d1) >> (8 * (rel & 3))) & 0xFF;
 }
 
 // L2-coherent byte load (bypasses this CU's L1, which never sees its own earlier stores).
@@ -270,9 +263,12 @@ struct Sink {
 // Grouped-stream position -> byte offset in the chunk (identity unless BG4).
 __device__ __forceinline__ uint32_t out_pos(const Sink& s, uint32_t p) {
   if (!s.bg4) return p;
-  const uint32_t g = uint32_t(p >= s.g1) + uint32_t(p >= s.g2) + uint32_t(p >= s.g3);
-  const uint32_t base = g == 0 ? 0u : g == 1 ? s.g1 : g == 2 ? s.g2 : s.g3;
-  return 4 * (p - base) + g;
+  const uint32_t a1 = p >= s.g1, a2 = p >= s.g2, a3 = p >= s.g3;
+  uint32_t base = 0;  // selects, not branches: the lanes of one flush straddle group boundaries
+  base = a1 ? s.g1 : base;
+  base = a2 ? s.g2 : base;
+  base = a3 ? s.g3 : base;
+  return 4 * (p - base) + a1 + a2 + a3;
 }
 
 __device__ void sink_flush(Sink& s, uint32_t upto, bool final, uint32_t lane) {
@@ -322,7 +318,8 @@ __device__ __forceinline__ void copy_literals(Sink& s, Win& w, uint32_t a, uint3
     const uint32_t cnt = len - b < kWave ? len - b : kWave;
     win_seek(w, a + b, lane);
     const uint32_t v = win_lane_u8(w, a + b, lane);
-    if (lane < cnt) s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(v);
+    // unconditional: lanes past the literal write ring slots ahead of op (see lz4_fast)
+    s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(v);
     sink_advance<kProf>(s, cnt, lane);
   }
 }
@@ -379,23 +376,29 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
         sink_flush(s, s.op, false, lane);
         op_lim = op_room < s.fp + kFlushAt ? op_room : s.fp + kFlushAt;
       }
-      const uint32_t rel = ip - w.wofs + lane;  // < 320: inside w0 | w1
-      const uint32_t idx = (rel >> 2) & 63;
-      const uint32_t d0 = __shfl(w.w0, int(idx), kWave), d1 = __shfl(w.w1, int(idx), kWave);
-      const uint32_t v = ((rel < 256 ? d0 : d1) >> (8 * (rel & 3))) & 0xFF;
+      const uint32_t v = win_lane_u8(w, ip, lane);  // lane l: stream byte ip + l
       const uint32_t token = __builtin_amdgcn_readfirstlane(v);
       const uint32_t lit = token >> 4, mlc = token & 15;
-      if (lit == 15 || mlc == 15) return;
       const uint32_t off = __builtin_amdgcn_readlane(v, int(lit + 1)) | (__builtin_amdgcn_readlane(v, int(lit + 2)) << 8);
-      const uint32_t reach = s.op + lit < kRingReach ? s.op + lit : kRingReach;
-      if (off - 1 >= reach) return;  // off == 0, before the chunk start, or beyond the ring
+      // one exit test: a length-extension nibble, or an offset of 0 / before the chunk start (the
+      // general path then decodes the sequence, or reports it)
+      if (uint32_t(lit == 15) | uint32_t(mlc == 15) | uint32_t(off - 1 >= s.op + lit)) return;
       const uint32_t litv = __shfl_down(v, 1, kWave);  // lane l: stream byte ip + 1 + l
       s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(litv);
       const uint32_t mo = s.op + lit;
-      uint32_t back = off;
-      if (off < kWave) back = off * (1 + ((lane * ((65536u + off - 1) / off)) >> 16));
-      __builtin_amdgcn_wave_barrier();
-      const uint8_t m = s.ring[(s.tmod + mo + lane - back) & kRingMask];
+      uint8_t m;
+      if (off <= kRingReach) {
+        uint32_t back = off;
+        if (off < kWave) back = off * (1 + ((lane * ((65536u + off - 1) / off)) >> 16));
+        __builtin_amdgcn_wave_barrier();
+        m = s.ring[(s.tmod + mo + lane - back) & kRingMask];
+      } else {
+        // Far match (off > kRingReach >= 64, so no overlap): the source was flushed >= kRingReach -
+        // kFlushAt bytes ago; wait for this wave's stores, then read it back through L2.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        m = uint8_t(load_u8_coherent(s.out + out_pos(s, mo + lane - off)));
+        if (kProf) s.nfar++;
+      }
       __builtin_amdgcn_wave_barrier();
       s.ring[(s.tmod + mo + lane) & kRingMask] = m;
       __builtin_amdgcn_wave_barrier();
