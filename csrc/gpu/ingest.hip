@@ -160,26 +160,30 @@ __global__ void __launch_bounds__(256) k_place_raw(const uint8_t* __restrict__ s
 
 // --------------------------------------------------------------------------------------------
 // K3b: LZ4-frame (+BG4) decode.  One wave per chunk, 4 waves per 256-thread block, persistent
-// grid.  Decoded bytes go through a small per-wave LDS history ring (8 KiB) and are flushed to
-// HBM in 16-byte stores every 2 KiB, so occupancy is set by VGPRs (~20 waves/CU) instead of a
-// whole-chunk LDS buffer (which allowed one wave per CU).
+// grid.  Decoded bytes go through a small per-wave LDS history ring (4 KiB by default, so 8 waves
+// per SIMD stay resident) and are flushed to HBM in 16-byte stores every 2 KiB.
 //
 //  * compressed stream: a 512-byte window held as two dwords per lane; token / length bytes are
 //    read with v_readlane (uniform), literal bytes lane-parallel with ds_bpermute; the window
 //    slides by 256 bytes so the next line's load overlaps the current line's parsing.
+//  * lz4_fast takes the common short sequence (no length-extension bytes) with every check folded
+//    into loop bounds and unconditional ring writes; the general path handles the rest.
 //  * match copies: lane i of a 64-byte block reads source o - off*(1 + i/off) (the periodic form
-//    of an overlapping copy, always a final byte); distances <= 7872 come from the LDS ring,
-//    longer ones from HBM with L2-coherent loads (sc1, agent scope) after s_waitcnt vmcnt(0) —
-//    those bytes were flushed by this wave >= 5 KiB earlier.
+//    of an overlapping copy, always a final byte); distances <= ring - 320 come from the LDS ring,
+//    longer ones from HBM with L2-coherent loads (sc1, agent scope) after s_waitcnt vmcnt(0) --
+//    those bytes were flushed by this wave at least ring - 320 - 2 KiB earlier.
 //  * BG4: the grouped stream is scattered to its interleaved position (4*j + g) on flush, and
 //    long-distance match reads use the same mapping, so no regroup pass or scratch is needed.
 //  * chunks clipped by [clip_lo, clip_hi) decode into a 128 KiB global scratch slot (one for the
 //    chunk straddling clip_lo, one for clip_hi), then the clipped range is copied out.
 // --------------------------------------------------------------------------------------------
-constexpr uint32_t kRing = 8192;
-constexpr uint32_t kRingMask = kRing - 1;
+// Ring geometry (bytes per wave) is a template parameter RB: a larger ring keeps more match
+// sources in LDS (fewer L2 read-backs) at the price of fewer resident waves per CU.
+template <uint32_t RB> struct RingGeo {
+  static constexpr uint32_t kMask = RB - 1;
+  static constexpr uint32_t kReach = RB - 256 - 64;  // max match distance served from the ring
+};
 constexpr uint32_t kFlushAt = 2048;
-constexpr uint32_t kRingReach = kRing - 256 - 64;  // max match distance served from the ring
 
 __device__ uint8_t g_clip_scratch[2][kMaxChunk + 256];
 
@@ -271,10 +275,11 @@ __device__ __forceinline__ uint32_t out_pos(const Sink& s, uint32_t p) {
   return 4 * (p - base) + a1 + a2 + a3;
 }
 
+template <uint32_t RB>
 __device__ void sink_flush(Sink& s, uint32_t upto, bool final, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
   if (s.bg4) {
-    for (uint32_t i = s.fp + lane; i < upto; i += kWave) s.out[out_pos(s, i)] = s.ring[(s.tmod + i) & kRingMask];
+    for (uint32_t i = s.fp + lane; i < upto; i += kWave) s.out[out_pos(s, i)] = s.ring[(s.tmod + i) & RingGeo<RB>::kMask];
     s.fp = upto;
     return;
   }
@@ -282,28 +287,28 @@ __device__ void sink_flush(Sink& s, uint32_t upto, bool final, uint32_t lane) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(s.out) + p;
   uint32_t head = uint32_t((16 - (a & 15)) & 15);
   if (head > upto - p) head = upto - p;
-  if (lane < head) s.out[p + lane] = s.ring[(s.tmod + p + lane) & kRingMask];
+  if (lane < head) s.out[p + lane] = s.ring[(s.tmod + p + lane) & RingGeo<RB>::kMask];
   p += head;
   const uint32_t nvec = (upto - p) >> 4;
   for (uint32_t v = lane; v < nvec; v += kWave) {
     const uint32_t q = p + 16 * v;
-    const uint4 x = *reinterpret_cast<const uint4*>(s.ring + ((s.tmod + q) & kRingMask));
+    const uint4 x = *reinterpret_cast<const uint4*>(s.ring + ((s.tmod + q) & RingGeo<RB>::kMask));
     *reinterpret_cast<uint4*>(s.out + q) = x;
   }
   p += 16 * nvec;
   if (final) {
-    if (lane < upto - p) s.out[p + lane] = s.ring[(s.tmod + p + lane) & kRingMask];
+    if (lane < upto - p) s.out[p + lane] = s.ring[(s.tmod + p + lane) & RingGeo<RB>::kMask];
     p = upto;
   }
   s.fp = p;
 }
 
-template <bool kProf>
+template <bool kProf, uint32_t RB>
 __device__ __forceinline__ void sink_advance(Sink& s, uint32_t cnt, uint32_t lane) {
   s.op += cnt;
   if (s.op - s.fp >= kFlushAt) {
     const uint64_t t0 = kProf ? clk() : 0;
-    sink_flush(s, s.op, false, lane);
+    sink_flush<RB>(s, s.op, false, lane);
     if (kProf) {
       s.t_flush += clk() - t0;
       s.nflush++;
@@ -312,19 +317,19 @@ __device__ __forceinline__ void sink_advance(Sink& s, uint32_t cnt, uint32_t lan
 }
 
 // Copy `len` literal bytes starting at stream position a.
-template <bool kProf>
+template <bool kProf, uint32_t RB>
 __device__ __forceinline__ void copy_literals(Sink& s, Win& w, uint32_t a, uint32_t len, uint32_t lane) {
   for (uint32_t b = 0; b < len; b += kWave) {
     const uint32_t cnt = len - b < kWave ? len - b : kWave;
     win_seek(w, a + b, lane);
     const uint32_t v = win_lane_u8(w, a + b, lane);
     // unconditional: lanes past the literal write ring slots ahead of op (see lz4_fast)
-    s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(v);
-    sink_advance<kProf>(s, cnt, lane);
+    s.ring[(s.tmod + s.op + lane) & RingGeo<RB>::kMask] = uint8_t(v);
+    sink_advance<kProf, RB>(s, cnt, lane);
   }
 }
 
-template <bool kProf>
+template <bool kProf, uint32_t RB>
 __device__ __forceinline__ void copy_match(Sink& s, uint32_t off, uint32_t ml, uint32_t lane) {
   // lane i of each 64-byte block copies from distance back = off * (1 + i / off): the periodic form
   // of an overlapping copy, so every source byte is already final.
@@ -333,21 +338,21 @@ __device__ __forceinline__ void copy_match(Sink& s, uint32_t off, uint32_t ml, u
     const uint32_t magic = (65536u + off - 1) / off;  // exact floor(lane / off) for lane, off < 64
     back = off * (1 + ((lane * magic) >> 16));
   }
-  if (off <= kRingReach) {
+  if (off <= RingGeo<RB>::kReach) {
     for (uint32_t b = 0; b < ml; b += kWave) {
       const uint32_t cnt = ml - b < kWave ? ml - b : kWave;
       const uint32_t o = s.op + lane;
       __builtin_amdgcn_wave_barrier();
-      if (lane < cnt) s.ring[(s.tmod + o) & kRingMask] = s.ring[(s.tmod + o - back) & kRingMask];
-      sink_advance<kProf>(s, cnt, lane);
+      if (lane < cnt) s.ring[(s.tmod + o) & RingGeo<RB>::kMask] = s.ring[(s.tmod + o - back) & RingGeo<RB>::kMask];
+      sink_advance<kProf, RB>(s, cnt, lane);
     }
   } else {
     for (uint32_t b = 0; b < ml; b += kWave) {
       const uint32_t cnt = ml - b < kWave ? ml - b : kWave;
       const uint32_t o = s.op + lane;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < cnt) s.ring[(s.tmod + o) & kRingMask] = uint8_t(load_u8_coherent(s.out + out_pos(s, o - back)));
-      sink_advance<kProf>(s, cnt, lane);
+      if (lane < cnt) s.ring[(s.tmod + o) & RingGeo<RB>::kMask] = uint8_t(load_u8_coherent(s.out + out_pos(s, o - back)));
+      sink_advance<kProf, RB>(s, cnt, lane);
     }
   }
 }
@@ -360,8 +365,8 @@ __device__ __forceinline__ void copy_match(Sink& s, uint32_t off, uint32_t ml, u
 // next flush) and one offset range test, bytes come from one window gather (lane l = stream byte
 // ip + l) plus read-lanes, and ring writes are unconditional: lanes past the sequence write into
 // ring slots ahead of `op`, which are rewritten before they are flushed and lie more than
-// kRingReach behind every later match source.  Returns at the first sequence it cannot take.
-template <bool kProf>
+// RingGeo<RB>::kReach behind every later match source.  Returns at the first sequence it cannot take.
+template <bool kProf, uint32_t RB>
 __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t end, uint32_t lane) {
   const uint32_t ip_end = end >= 18 ? end - 18 : 0;
   const uint32_t op_room = s.n >= 32 ? s.n - 32 : 0;
@@ -373,7 +378,7 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
     do {
       if (s.op >= op_lim) {
         if (s.op >= op_room) return;
-        sink_flush(s, s.op, false, lane);
+        sink_flush<RB>(s, s.op, false, lane);
         op_lim = op_room < s.fp + kFlushAt ? op_room : s.fp + kFlushAt;
       }
       const uint32_t v = win_lane_u8(w, ip, lane);  // lane l: stream byte ip + l
@@ -384,23 +389,23 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
       // general path then decodes the sequence, or reports it)
       if (uint32_t(lit == 15) | uint32_t(mlc == 15) | uint32_t(off - 1 >= s.op + lit)) return;
       const uint32_t litv = __shfl_down(v, 1, kWave);  // lane l: stream byte ip + 1 + l
-      s.ring[(s.tmod + s.op + lane) & kRingMask] = uint8_t(litv);
+      s.ring[(s.tmod + s.op + lane) & RingGeo<RB>::kMask] = uint8_t(litv);
       const uint32_t mo = s.op + lit;
       uint8_t m;
-      if (off <= kRingReach) {
+      if (off <= RingGeo<RB>::kReach) {
         uint32_t back = off;
         if (off < kWave) back = off * (1 + ((lane * ((65536u + off - 1) / off)) >> 16));
         __builtin_amdgcn_wave_barrier();
-        m = s.ring[(s.tmod + mo + lane - back) & kRingMask];
+        m = s.ring[(s.tmod + mo + lane - back) & RingGeo<RB>::kMask];
       } else {
-        // Far match (off > kRingReach >= 64, so no overlap): the source was flushed >= kRingReach -
+        // Far match (off > RingGeo<RB>::kReach >= 64, so no overlap): the source was flushed >= RingGeo<RB>::kReach -
         // kFlushAt bytes ago; wait for this wave's stores, then read it back through L2.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         m = uint8_t(load_u8_coherent(s.out + out_pos(s, mo + lane - off)));
         if (kProf) s.nfar++;
       }
       __builtin_amdgcn_wave_barrier();
-      s.ring[(s.tmod + mo + lane) & kRingMask] = m;
+      s.ring[(s.tmod + mo + lane) & RingGeo<RB>::kMask] = m;
       __builtin_amdgcn_wave_barrier();
       if (kProf) {
         s.nseq++;
@@ -415,13 +420,13 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
 }
 
 // One LZ4 block at stream positions [blk, blk + blen). Returns false on malformed input.
-template <bool kProf>
+template <bool kProf, uint32_t RB>
 __device__ bool lz4_block(Sink& s, Win& w, uint32_t blk, uint32_t blen, uint32_t lane) {
   const uint32_t end = blk + blen;
   uint32_t ip = blk;
   while (true) {
     if (ip >= end) return false;
-    lz4_fast<kProf>(s, w, ip, end, lane);
+    lz4_fast<kProf, RB>(s, w, ip, end, lane);
     win_seek(w, ip, lane);
     const uint32_t token = win_u8(w, ip);
     ++ip;
@@ -440,7 +445,7 @@ __device__ bool lz4_block(Sink& s, Win& w, uint32_t blk, uint32_t blen, uint32_t
     if (kProf) s.nseq++;
     if (lit) {
       const uint64_t t0 = kProf ? clk() : 0;
-      copy_literals<kProf>(s, w, ip, lit, lane);
+      copy_literals<kProf, RB>(s, w, ip, lit, lane);
       if (kProf) {
         s.t_lit += clk() - t0;
         s.lit_bytes += lit;
@@ -467,18 +472,18 @@ __device__ bool lz4_block(Sink& s, Win& w, uint32_t blk, uint32_t blen, uint32_t
     ml += 4;
     if (ml > s.n - s.op) return false;
     const uint64_t t0 = kProf ? clk() : 0;
-    copy_match<kProf>(s, off, ml, lane);
+    copy_match<kProf, RB>(s, off, ml, lane);
     if (kProf) {
       s.t_match += clk() - t0;
       s.match_bytes += ml;
-      s.nfar += off > kRingReach;
+      s.nfar += off > RingGeo<RB>::kReach;
       s.nshort += off < kWave;
     }
   }
 }
 
 // Decode an LZ4 frame of clen bytes; returns false on malformed input.
-template <bool kProf>
+template <bool kProf, uint32_t RB>
 __device__ bool lz4_frame(Sink& s, const uint8_t* payload, uint32_t clen, uint32_t lane) {
   Win w;
   win_init(w, payload, lane);
@@ -501,20 +506,20 @@ __device__ bool lz4_frame(Sink& s, const uint8_t* payload, uint32_t clen, uint32
     if (len > clen - ip) return false;
     if (bs & 0x80000000u) {
       if (len > s.n - s.op) return false;
-      copy_literals<kProf>(s, w, k + ip, len, lane);
-    } else if (!lz4_block<kProf>(s, w, k + ip, len, lane)) {
+      copy_literals<kProf, RB>(s, w, k + ip, len, lane);
+    } else if (!lz4_block<kProf, RB>(s, w, k + ip, len, lane)) {
       return false;
     }
     ip += len + (block_ck ? 4 : 0);
   }
 }
 
-template <bool kProf>
-__global__ void __launch_bounds__(256) k_decode_lz4(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+template <bool kProf, uint32_t RB>
+__global__ void __launch_bounds__(256, RB <= 4096 ? 8 : 5) k_decode_lz4(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const ZgChunk* __restrict__ chunks, int n_chunks,
                                                     uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
                                                     uint64_t src_n, uint64_t dst_n) {
-  __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][kRing];
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][RB];
   const uint32_t lane = lane_id();
   const int wave = wave_uniform(int(threadIdx.x >> 6));
   const int stride = int(gridDim.x) * kWavesPerBlock;
@@ -540,13 +545,13 @@ __global__ void __launch_bounds__(256) k_decode_lz4(const uint8_t* __restrict__ 
     s.ring = rings[wave];
     s.out = clipped ? g_clip_scratch[ch.dst < clip_lo ? 0 : 1] : dst + ch.dst;
     s.bg4 = ch.scheme == 2;
-    s.tmod = s.bg4 ? 0u : uint32_t(reinterpret_cast<uintptr_t>(s.out) & kRingMask);
+    s.tmod = s.bg4 ? 0u : uint32_t(reinterpret_cast<uintptr_t>(s.out) & RingGeo<RB>::kMask);
     s.n = ch.ulen;
     const uint32_t q = ch.ulen >> 2, r = ch.ulen & 3;
     s.g1 = q + (r > 0 ? 1u : 0u);
     s.g2 = s.g1 + q + (r > 1 ? 1u : 0u);
     s.g3 = s.g2 + q + (r > 2 ? 1u : 0u);
-    const bool ok = lz4_frame<kProf>(s, src + ch.src, ch.clen, lane);
+    const bool ok = lz4_frame<kProf, RB>(s, src + ch.src, ch.clen, lane);
     if (!ok) {
       if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
       continue;
@@ -555,7 +560,7 @@ __global__ void __launch_bounds__(256) k_decode_lz4(const uint8_t* __restrict__ 
       if (lane == 0) report(err, ZG_ERR_SIZE, uint32_t(c));
       continue;
     }
-    sink_flush(s, s.op, true, lane);
+    sink_flush<RB>(s, s.op, true, lane);
     if (kProf) {
       const uint64_t v[10] = {s.t_lit, s.t_match, s.t_flush, clk() - t_start, s.nseq,
                               s.lit_bytes, s.match_bytes, s.nfar, s.nflush, s.nshort};
@@ -705,29 +710,45 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                      dst, chunks, n_chunks, clip_lo, clip_hi, src_n, dst_n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // Persistent grid: up to 5 blocks (20 waves) per CU on 256 CUs.
-  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   // ZG_LZ4_GRID caps the persistent grid (occupancy experiments: 256 = one wave per SIMD).
   static const int grid_cap = [] {
     const char* v = getenv("ZG_LZ4_GRID");
     const int g = v ? atoi(v) : 0;
     return g > 0 && g < 1280 ? g : 1280;
   }();
-  const int grid = blocks < grid_cap ? blocks : grid_cap;
   static const bool prof = [] {
     const char* v = getenv("ZG_LZ4_PROF");
     return v && *v && *v != '0';
   }();
+  // ZG_LZ4_RING = ring KiB per wave (4, 8, 16 or 32); resident blocks per CU follow from the LDS.
+  // Measured on BG4 bf16 (1 GiB, 16.7k chunks): 4 KiB 46.3 GB/s (8 waves/SIMD, more matches read
+  // back from L2), 8 KiB 38.2, 16 KiB 29.9, 32 KiB 18.5 -- occupancy beats ring reach.
+  static const int ring_kib = [] {
+    const char* v = getenv("ZG_LZ4_RING");
+    const int k = v ? atoi(v) : 4;
+    return k == 8 || k == 16 || k == 32 ? k : 4;
+  }();
+  const int per_cu = ring_kib == 4 ? 8 : ring_kib == 8 ? 5 : ring_kib == 16 ? 2 : 1;
+  const int cap = grid_cap < 256 * per_cu ? grid_cap : 256 * per_cu;
+  const int grid = blocks < cap ? blocks : cap;
   if (prof) {
     unsigned long long zero[10] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lz4_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, stream);
   }
-  if (prof)
-    hipLaunchKernelGGL(k_decode_lz4<true>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
-                       clip_hi, err, src_n, dst_n);
-  else
-    hipLaunchKernelGGL(k_decode_lz4<false>, dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo,
-                       clip_hi, err, src_n, dst_n);
+#define ZG_LZ4_LAUNCH(P, R)                                                                                       \
+  hipLaunchKernelGGL((k_decode_lz4<P, R>), dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo, \
+                     clip_hi, err, src_n, dst_n)
+  if (ring_kib == 4) {
+    if (prof) ZG_LZ4_LAUNCH(true, 4096); else ZG_LZ4_LAUNCH(false, 4096);
+  } else if (ring_kib == 16) {
+    if (prof) ZG_LZ4_LAUNCH(true, 16384); else ZG_LZ4_LAUNCH(false, 16384);
+  } else if (ring_kib == 32) {
+    if (prof) ZG_LZ4_LAUNCH(true, 32768); else ZG_LZ4_LAUNCH(false, 32768);
+  } else {
+    if (prof) ZG_LZ4_LAUNCH(true, 8192); else ZG_LZ4_LAUNCH(false, 8192);
+  }
+#undef ZG_LZ4_LAUNCH
   if (prof) {
     unsigned long long v[10];
     hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lz4_prof), sizeof v, 0, hipMemcpyDeviceToHost, stream);
