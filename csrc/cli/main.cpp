@@ -146,8 +146,41 @@ std::vector<xet::Hash> cached_xorb_hashes(const Config& cfg) {
   return out;
 }
 
-// `zest pull <repo> --gpus N`: run N GPU workers (python -m torch.distributed.run ... -m
-// zest_amd.multigpu) as child processes of this CLI and return their exit status.
+int cmd_pull(const std::string& exe, const std::vector<std::string>& a);
+
+// One attempt of `zest pull --gpus N`: `python -m torch.distributed.run --nproc-per-node N -m
+// zest_amd.multigpu <args>` as a child process of this CLI (one worker per GPU).  Rank 0 writes
+// `status_path` once the whole job ran to the end (every rank alive through the final all-reduce).
+int spawn_gpu_workers(const std::vector<std::string>& pass, int gpus, int attempt, const std::string& status_path) {
+  const char* py = std::getenv("ZEST_PYTHON");
+  const char* mod = std::getenv("ZEST_GPU_WORKER_MODULE");  // tests substitute a stub worker
+  std::vector<std::string> args = {py ? py : "python3", "-m", "torch.distributed.run", "--nnodes", "1",
+                                   "--nproc-per-node", std::to_string(gpus), "--master-addr", "127.0.0.1",
+                                   "--master-port", std::to_string(29400 + (::getpid() * 7 + attempt * 131) % 2000),
+                                   "-m", mod && *mod ? mod : "zest_amd.multigpu"};
+  args.insert(args.end(), pass.begin(), pass.end());
+  ::setenv("ZEST_GPU_STATUS", status_path.c_str(), 1);
+  std::vector<char*> argv;
+  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
+  argv.push_back(nullptr);
+  pid_t pid = 0;
+  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
+    std::cerr << "Error: cannot start " << argv[0] << " for --gpus\n";
+    return 127;
+  }
+  int status = 0;
+  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  }
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+}
+
+// `zest pull <repo> --gpus N`: N GPU decode/verify workers, elastic over worker loss.  An attempt
+// that dies before the end (a worker crashed, a device or the RCCL communicator failed; torchrun then
+// stops the other ranks) is retried on one GPU fewer.  Files verified by earlier attempts stay on disk
+// and are skipped, so each retry pulls only what is missing; after the single-GPU attempt the host
+// pipeline finishes the job (ZEST_GPU_HOST_FALLBACK=0 turns that off).  An attempt that ran to the end
+// but failed files (rank 0 wrote its status) is final: fewer GPUs would not fix the data.  SURVEY
+// §5.3 ("elastic world size 8 -> 7"); the reference has no GPU path and no retry (main.zig:233-256).
 int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int gpus) {
   // exe = <pkg>/_bin/zest -> PYTHONPATH = parent of the package directory
   std::string pkg_parent = exe;
@@ -155,33 +188,36 @@ int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int 
     const size_t s = pkg_parent.rfind('/');
     pkg_parent = s == std::string::npos ? "." : pkg_parent.substr(0, s);
   }
-  const char* py = std::getenv("ZEST_PYTHON");
-  std::vector<std::string> args = {py ? py : "python3", "-m", "torch.distributed.run", "--nnodes", "1",
-                                   "--nproc-per-node", std::to_string(gpus), "--master-addr", "127.0.0.1",
-                                   "--master-port", std::to_string(29400 + (::getpid() % 2000)), "-m",
-                                   "zest_amd.multigpu"};
+  std::string pp = pkg_parent;
+  if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
+  ::setenv("PYTHONPATH", pp.c_str(), 1);
+  std::vector<std::string> pass;
   for (size_t i = 0; i < a.size(); ++i) {
     if (a[i] == "--gpus") {
       ++i;
       continue;
     }
-    args.push_back(a[i]);
+    pass.push_back(a[i]);
   }
-  std::string pp = pkg_parent;
-  if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
-  ::setenv("PYTHONPATH", pp.c_str(), 1);
-  std::vector<char*> argv;
-  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
-  argv.push_back(nullptr);
-  pid_t pid = 0;
-  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
-    std::cerr << "Error: cannot start " << argv[0] << " for --gpus\n";
-    return 1;
+  const char* tmp = std::getenv("TMPDIR");
+  const std::string status = std::string(tmp && *tmp ? tmp : "/tmp") + "/zest-gpu-pull-" + std::to_string(::getpid()) +
+                             ".json";
+  int rc = 1;
+  for (int n = gpus, attempt = 0; n >= 1; --n, ++attempt) {
+    ::unlink(status.c_str());
+    rc = spawn_gpu_workers(pass, n, attempt, status);
+    const bool finished = ::access(status.c_str(), F_OK) == 0;
+    ::unlink(status.c_str());
+    if (rc == 0) return 0;
+    if (finished) return rc;
+    std::cerr << "zest: GPU pull on " << n << " GPU(s) stopped before the end (exit " << rc << ")";
+    if (n > 1) std::cerr << "; retrying on " << n - 1 << " GPU(s), keeping verified files";
+    std::cerr << "\n";
   }
-  int status = 0;
-  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
-  }
-  return WIFEXITED(status) ? WEXITSTATUS(status) : 1;
+  const char* fb = std::getenv("ZEST_GPU_HOST_FALLBACK");
+  if (fb && std::string(fb) == "0") return rc;
+  std::cerr << "zest: finishing the pull on the host\n";
+  return cmd_pull(exe, pass);
 }
 
 int cmd_pull(const std::string& exe, const std::vector<std::string>& a) {

@@ -49,17 +49,36 @@ void BtServer::start() {
   acceptor_ = std::thread([this] { accept_loop(); });
 }
 
+// Safe to call from several threads at once (the REST API's /v1/stop handler and the owner's
+// shutdown path both do): the TSan build caught the owner destroying the worker list while the
+// API's stop() was still joining it.
 void BtServer::stop() {
-  if (stop_.exchange(true)) return;
+  std::lock_guard<std::mutex> sg(stop_mu_);
+  if (stopped_) return;
+  stop_ = true;
   listener_.shutdown();
   if (acceptor_.joinable()) acceptor_.join();
+  std::list<Worker> ws;
   {
     std::lock_guard<std::mutex> g(mu_);
     for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
+    ws.swap(workers_);
   }
-  for (auto& t : workers_)
-    if (t.joinable()) t.join();
+  for (auto& w : ws)
+    if (w.thread.joinable()) w.thread.join();
   listener_.close();  // closed exactly once (server.zig double-closes)
+  stopped_ = true;
+}
+
+void BtServer::reap_locked() {
+  for (auto it = workers_.begin(); it != workers_.end();) {
+    if (it->done->load()) {
+      it->thread.join();
+      it = workers_.erase(it);
+    } else {
+      ++it;
+    }
+  }
 }
 
 ServerStats BtServer::stats() const {
@@ -83,18 +102,24 @@ void BtServer::accept_loop() {
       if (stop_) return;
       continue;
     }
-    if (!s.valid()) continue;
     std::lock_guard<std::mutex> g(mu_);
+    reap_locked();  // a long-running seeder must not accumulate one finished thread per connection
+    if (!s.valid()) continue;
     conns_.insert(s.fd());
-    workers_.emplace_back([this, sock = std::move(s), peer]() mutable {
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    std::thread t([this, sock = std::move(s), peer, done]() mutable {
       const int fd = sock.fd();
       try {
         handle(std::move(sock), peer);
       } catch (...) {
       }
-      std::lock_guard<std::mutex> g2(mu_);
-      conns_.erase(fd);
+      {
+        std::lock_guard<std::mutex> g2(mu_);
+        conns_.erase(fd);
+      }
+      done->store(true);
     });
+    workers_.push_back(Worker{std::move(t), std::move(done)});
   }
 }
 

@@ -12,6 +12,8 @@
 #include <array>
 #include <atomic>
 #include <functional>
+#include <list>
+#include <memory>
 #include <mutex>
 #include <optional>
 #include <set>
@@ -64,11 +66,19 @@ class BtServer {
   PieceProvider provider_;
   net::Socket listener_;
   uint16_t port_ = 0;
+  struct Worker {
+    std::thread thread;
+    std::shared_ptr<std::atomic<bool>> done;
+  };
+  void reap_locked();  // join finished connection threads (mu_ held)
+
   std::atomic<bool> stop_{false};
+  std::mutex stop_mu_;  // serializes stop(): a second caller returns only after the first finished
+  bool stopped_ = false;
   std::thread acceptor_;
   std::mutex mu_;
   std::set<int> conns_;
-  std::vector<std::thread> workers_;
+  std::list<Worker> workers_;
   std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0};
   FaultSpec fault_;
 };

@@ -1,0 +1,31 @@
+"""Stand-in for zest_amd.multigpu in the elastic `zest pull --gpus N` tests (no GPU needed).
+
+ZEST_STUB_MODE=lose-last: in a multi-rank attempt the highest rank dies like a lost GPU (rank 0
+waits, so torchrun stops it before it can report completion); a single-rank attempt succeeds.
+ZEST_STUB_MODE=always-crash: every attempt dies, so the CLI falls back to the host pull.
+Each attempt appends its world size to ZEST_STUB_LOG.
+"""
+import json
+import os
+import time
+
+
+def main() -> int:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if rank == 0:
+        with open(os.environ["ZEST_STUB_LOG"], "a") as fh:
+            fh.write(f"{world}\n")
+    mode = os.environ.get("ZEST_STUB_MODE", "lose-last")
+    if mode == "always-crash" or (world > 1 and rank == world - 1):
+        os._exit(17)
+    if world > 1:
+        time.sleep(60)  # never reached in the tests: torchrun tears the group down first
+    if rank == 0:
+        with open(os.environ["ZEST_GPU_STATUS"], "w") as fh:
+            json.dump({"complete": True, "world": world, "failed_files": 0}, fh)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

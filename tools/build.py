@@ -8,7 +8,7 @@ Everything is built IN-TREE so the artefacts travel with the repo snapshot to th
   zest_amd/_bin/zest        native CLI (pull/seed/serve/start/stop/bench/version/help)  [g++]
 
 Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
-Usage: python tools/build.py [--jobs N] [--clean] [--only core|hip|cli] [--debug] [--asan]
+Usage: python tools/build.py [--jobs N] [--clean] [--only core|hip|cli] [--debug] [--asan | --tsan]
 """
 from __future__ import annotations
 
@@ -56,13 +56,13 @@ def _run(cmd: list[str]) -> None:
 
 
 class Builder:
-    def __init__(self, jobs: int, debug: bool, asan: bool):
+    def __init__(self, jobs: int, debug: bool, san: str = ""):
         self.jobs = jobs
         self.debug = debug
-        self.asan = asan
         self.hdr_time = _newest_header()
-        opt = ["-O0", "-g"] if debug else ["-O3", "-g1"]
-        san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"] if asan else []
+        opt = ["-O0", "-g"] if debug else ["-O1", "-g"] if san == "tsan" else ["-O3", "-g1"]
+        san = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+               "tsan": ["-fsanitize=thread", "-fno-omit-frame-pointer"]}.get(san, [])
         self.cxxflags = ["-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread",
                          "-march=x86-64-v2", "-mtune=generic", f"-I{CSRC}", f"-I{CSRC / 'core'}",
                          f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__=1"] + opt + san
@@ -114,19 +114,21 @@ def core_sources() -> list[Path]:
     return sorted((CSRC / "core").glob("*.cpp"))
 
 
-def build(only: str | None = None, jobs: int | None = None, debug: bool = False, asan: bool = False) -> dict:
+def build(only: str | None = None, jobs: int | None = None, debug: bool = False, asan: bool = False,
+          tsan: bool = False) -> dict:
     jobs = jobs or min(16, os.cpu_count() or 4)
-    b = Builder(jobs, debug, asan)
+    san = "asan" if asan else "tsan" if tsan else ""
+    b = Builder(jobs, debug, san)
     built = {}
-    if asan:
-        # Host-only sanitizer build (ASan + UBSan) of the core, CLI and native unit tests, kept out
-        # of the package (build/asan/): python tools/build.py --asan && build/asan/core_tests
-        core_objs = b.compile(core_sources(), "asan/core")
-        t_objs = b.compile(sorted((ROOT / "tests" / "cpp").glob("*.cpp")), "asan/tests")
-        b.link(t_objs + core_objs, BUILD / "asan" / "core_tests", shared=False, libs=["-lssl", "-lcrypto"])
-        cli_objs = b.compile(sorted((CSRC / "cli").glob("*.cpp")), "asan/cli")
-        b.link(cli_objs + core_objs, BUILD / "asan" / "zest", shared=False, libs=["-lssl", "-lcrypto", "-ldl"])
-        return {"asan_tests": BUILD / "asan" / "core_tests", "asan_cli": BUILD / "asan" / "zest"}
+    if san:
+        # Host-only sanitizer build (ASan + UBSan, or TSan) of the core, CLI and native unit tests,
+        # kept out of the package: python tools/build.py --asan && build/asan/core_tests
+        core_objs = b.compile(core_sources(), f"{san}/core")
+        t_objs = b.compile(sorted((ROOT / "tests" / "cpp").glob("*.cpp")), f"{san}/tests")
+        b.link(t_objs + core_objs, BUILD / san / "core_tests", shared=False, libs=["-lssl", "-lcrypto"])
+        cli_objs = b.compile(sorted((CSRC / "cli").glob("*.cpp")), f"{san}/cli")
+        b.link(cli_objs + core_objs, BUILD / san / "zest", shared=False, libs=["-lssl", "-lcrypto", "-ldl"])
+        return {f"{san}_tests": BUILD / san / "core_tests", f"{san}_cli": BUILD / san / "zest"}
     core_objs = b.compile(core_sources(), "core")
     ssl_libs = ["-lssl", "-lcrypto"]
     if only in (None, "core"):
@@ -168,10 +170,11 @@ def main() -> None:
     ap.add_argument("--only", choices=["core", "hip", "cli", "tests"], default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host-only ASan/UBSan build of core + cli")
+    ap.add_argument("--tsan", action="store_true", help="host-only ThreadSanitizer build of core + cli")
     a = ap.parse_args()
     if a.clean and BUILD.exists():
         shutil.rmtree(BUILD)
-    out = build(a.only, a.jobs, a.debug, a.asan)
+    out = build(a.only, a.jobs, a.debug, a.asan, a.tsan)
     for k, v in out.items():
         print(f"built {k}: {v.relative_to(ROOT)}")
 

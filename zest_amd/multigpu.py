@@ -100,6 +100,10 @@ def main(argv=None) -> int:
     if world > 1:
         dist.all_reduce(tot)
     dt = time.time() - t0
+    status = os.environ.get("ZEST_GPU_STATUS")
+    if rank == 0 and status:  # every rank reached the end: tells the CLI not to retry on fewer GPUs
+        with open(status, "w") as fh:
+            json.dump({"complete": True, "world": world, "failed_files": int(tot[1].item())}, fh)
     if rank == 0:
         b, f_, peer, cdn, cache = tot.tolist()
         src = peer + cdn + cache
