@@ -628,6 +628,9 @@ void bind_extra(py::module_& m) {
   mtr.def("enabled", &trace::enabled);
   mtr.def("mode", &trace::mode);
   mtr.def("now_us", &trace::now_us);
+  mtr.def("roctx_enabled", &trace::roctx_enabled);
+  mtr.def("roctx_push", &trace::roctx_push);
+  mtr.def("roctx_pop", &trace::roctx_pop);
   mtr.def("log", [](const std::string& cat, const std::string& msg) { trace::log(cat.c_str(), msg); });
   mtr.def("complete", [](const std::string& cat, const std::string& name, uint64_t ts, uint64_t dur,
                          const std::string& args) {

@@ -26,6 +26,7 @@
 #include "config.h"
 #include "storage.h"
 #include "swarm.h"
+#include "trace.h"
 #include "xet_hash.h"
 #include "xorb.h"
 
@@ -192,9 +193,12 @@ class DeviceXetPull {
         }
         Slot& s = slots_[slot];
         if (s.busy) {
+          trace::Span sp("device", "wait staging slot");
           hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
           s.busy = false;
         }
+        trace::Span batch_span("device", "fetch batch");
+        batch_span.arg("\"terms\":" + std::to_string(end - next));
         std::vector<uint64_t> len(end - next, 0), src_at(end - next, 0);
         std::atomic<size_t> k{next};
         std::mutex em;
@@ -254,6 +258,8 @@ class DeviceXetPull {
         const int nchunks = int(c1 - c0);
         s.terms_dev.ensure(size_t(nterms));
         s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
+        batch_span.arg("\"bytes\":" + std::to_string(top));
+        trace::Span submit_span("device", "H2D + index/place/hash submit");
         hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
         hip_check(hipMemcpyAsync(s.terms_dev.p, s.terms.data(), sizeof(ZgTerm) * size_t(nterms),
                                  hipMemcpyHostToDevice, stream_),
@@ -278,6 +284,7 @@ class DeviceXetPull {
     hip_check(hipMemcpy(&e, err_.p, sizeof e, hipMemcpyDeviceToHost), "err D2H");
     if (e) throw Error("IngestError", "code " + std::to_string(e >> 32) + " at " + std::to_string(e & 0xFFFFFFFFu));
     // Merkle verify of every file in one launch
+    trace::Span merkle_span("device", "merkle verify");
     std::vector<ZgMerkleJob> jobs(nf);
     uint64_t max_leaves = 1;
     for (size_t f = 0; f < nf; ++f) {

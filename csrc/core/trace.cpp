@@ -1,5 +1,7 @@
 #include "trace.h"
 
+#include <dlfcn.h>
+
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -52,6 +54,42 @@ void init_locked(State& s, const char* v) {
 }
 
 }  // namespace
+
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  bool on = false;
+};
+
+const Roctx& roctx() {
+  static const Roctx r = [] {
+    Roctx x;
+    const char* e = std::getenv("ZEST_ROCTX");
+    if (!e || !*e || *e == '0') return x;
+    for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
+      if (void* h = ::dlopen(lib, RTLD_NOW | RTLD_GLOBAL)) {
+        x.push = reinterpret_cast<int (*)(const char*)>(::dlsym(h, "roctxRangePushA"));
+        x.pop = reinterpret_cast<int (*)()>(::dlsym(h, "roctxRangePop"));
+        if (x.push && x.pop) break;
+      }
+    }
+    x.on = x.push && x.pop;
+    return x;
+  }();
+  return r;
+}
+}  // namespace
+
+bool roctx_enabled() { return roctx().on; }
+
+void roctx_push(const std::string& name) {
+  if (roctx().on) roctx().push(name.c_str());
+}
+
+void roctx_pop() {
+  if (roctx().on) roctx().pop();
+}
 
 int mode() {
   State& s = st();

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import json
+import os
 import subprocess
 import sys
 
@@ -67,3 +68,22 @@ def test_cli_pull_trace_file(tmp_path):
         n.close()
     finally:
         hub.stop()
+
+
+def test_roctx_ranges_optional():
+    """ZEST_ROCTX=1 turns spans into roctx ranges (dlopen'ed ROCm library); push/pop must balance
+    and never fail, with or without the library."""
+    import subprocess
+    import sys
+    code = ("from zest_amd import _core\n"
+            "from zest_amd.utils.trace import Span\n"
+            "on = _core.trace.roctx_enabled()\n"
+            "with Span('engine', 'round 0'):\n"
+            "    with Span('engine', 'inner'): pass\n"
+            "print('roctx', on)\n")
+    for val, want in (("1", None), ("0", "False")):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, ZEST_ROCTX=val))
+        assert r.returncode == 0, r.stderr
+        if want:
+            assert r.stdout.strip() == f"roctx {want}"

@@ -6,8 +6,9 @@ in rounds through a pinned-host -> HBM staging ring:
 
     copy stream : hipMemcpyAsync(origin span k -> staging[k % S])           (CDN/PCIe ingest)
     compute     : index_terms -> place (copy | LZ4/BG4 decode) -> chunk hashes  (zest_amd.ops)
-    RCCL        : round-k regions exchanged peer-to-peer over xGMI (batch_isend_irecv), overlapped
-                  with round k+1 ingest (every GPU acts as a BitTorrent peer)
+    RCCL        : round-k regions replicated over xGMI (batched p2p, coalesced broadcasts or slab
+                  all-gather, whichever autotune_exchange measured fastest), overlapped with round
+                  k+1 ingest (every GPU acts as a BitTorrent peer)
     end         : chunk-hash all-reduce (have-map, C2) -> Merkle file hashes on every rank (K2) ->
                   compare with the repository's file hashes -> error all-reduce (C3)
 
@@ -26,7 +27,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import ops
+from . import _core, ops
 from .synthetic import SyntheticWorld
 
 EXCHANGE_MODES = ("p2p", "bcast", "allgather")
@@ -127,6 +128,7 @@ class DevicePuller:
         self.exchange = exchange
         self.exchange_times: dict = {}
         self._gather_bufs = None
+        self._rx = _core.trace.roctx_enabled()  # ZEST_ROCTX=1: one roctx range per round (host-side issue)
         self.is_cuda = self.device.type == "cuda"
         T = world.terms
         self.rank_terms = plan_rank_terms(world, n_ranks, seeders)
@@ -400,6 +402,8 @@ class DevicePuller:
             st = comp.cuda_stream
             for k, rw in enumerate(self.rounds):
                 s = k % self.slots
+                if self._rx:
+                    _core.trace.roctx_push(f"engine: round {k}")
                 with torch.cuda.stream(self.copy_stream):
                     self.copy_stream.wait_event(self.slot_free[s])
                     if rw.span_len:
@@ -420,6 +424,8 @@ class DevicePuller:
                 self.slot_free[s].record(comp)
                 if self.n_ranks > 1:
                     works += self._exchange(k)
+                if self._rx:
+                    _core.trace.roctx_pop()
         else:
             for k, rw in enumerate(self.rounds):
                 if rw.term_b > rw.term_a:

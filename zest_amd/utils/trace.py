@@ -3,6 +3,8 @@
 ZEST_TRACE=1 prints span lines on stderr; ZEST_TRACE=/path/trace.json writes a Chrome trace-event
 file at exit containing host spans from C++ (pull, CDN fetches, peer requests) and Python, plus
 device spans measured with HIP events (`device_span`) placed on the host timeline.
+ZEST_ROCTX=1 additionally turns every span (C++ and Python) into a roctx range, so
+`rocprofv3 --marker-trace` shows the pull phases alongside the kernels.
 """
 from __future__ import annotations
 
@@ -24,13 +26,18 @@ class Span:
     def __init__(self, cat: str, name: str, **args):
         self.cat, self.name, self.args = cat, name, args
         self.on = _tr.enabled()
+        self.rx = _tr.roctx_enabled()
 
     def __enter__(self):
+        if self.rx:
+            _tr.roctx_push(f"{self.cat}: {self.name}")
         if self.on:
             self.t0 = _tr.now_us()
         return self
 
     def __exit__(self, *exc):
+        if self.rx:
+            _tr.roctx_pop()
         if self.on:
             _tr.complete(self.cat, self.name, self.t0, _tr.now_us() - self.t0,
                          json.dumps(self.args)[1:-1] if self.args else "")
