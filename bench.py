@@ -52,7 +52,7 @@ def main() -> None:
     ap.add_argument("--seeders", type=int, default=0,
                     help="ranks that pull from the origin (default all); the rest leech everything from "
                          "them over xGMI (BASELINE config 2: --gpus 2 --seeders 1)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "bcast", "allgather"],
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "bcast", "allgather", "ipc"],
                     help="intra-node replication strategy; auto = time each on this machine during setup")
     a = ap.parse_args()
 
@@ -104,6 +104,10 @@ def main() -> None:
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
     if world_size > 1:
+        ipc = a.exchange in ("auto", "ipc") and puller.enable_ipc()
+        log(rank, f"peer arenas mapped over HIP IPC: {ipc}")
+        if a.exchange == "ipc" and not ipc:
+            raise SystemExit("--exchange ipc: mapping the peers' arenas failed")
         if a.exchange == "auto":
             t_x = puller.autotune_exchange()
             log(rank, "exchange autotune (s over the first rounds): "
@@ -115,13 +119,28 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
-    # Warm-up steps on a poisoned arena: proves every byte is really placed by the pull.
-    for _ in range(a.warmup):
-        arena.fill_(0xA5)
-        puller.err.zero_()
-        puller.step()
-        torch.cuda.synchronize()
-        puller.check()
+    # Warm-up steps on a poisoned arena: proves every byte is really placed by the pull, and re-hashes
+    # every chunk received from a peer so the chosen exchange strategy is checked on this machine.
+    verify_timed = puller.verify_received
+    puller.verify_received = True
+
+    def warmup():
+        for _ in range(a.warmup):
+            arena.fill_(0xA5)
+            puller.err.zero_()
+            puller.step()
+            torch.cuda.synchronize()
+            puller.check()
+
+    try:
+        warmup()
+    except ops.IngestError as e:  # the error word is all-reduced: every rank takes this branch
+        if world_size == 1 or puller.exchange == "p2p":
+            raise
+        log(rank, f"exchange {puller.exchange} failed verification ({e}); falling back to p2p")
+        puller.exchange = "p2p"
+        warmup()
+    puller.verify_received = verify_timed
     puller.err.zero_()
     barrier()
     torch.cuda.synchronize()

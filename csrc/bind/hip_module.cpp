@@ -53,6 +53,19 @@ PYBIND11_MODULE(_hip, m) {
     py::gil_scoped_release nogil;
     check(hipHostFree(reinterpret_cast<void*>(p)), "hipHostFree");
   });
+  // Let the current device's copy engines read `peer`'s memory directly over xGMI (IPC exchange).
+  m.def("enable_peer_access", [](int peer) {
+    int dev = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    if (peer == dev) return true;
+    int can = 0;
+    check(hipDeviceCanAccessPeer(&can, dev, peer), "hipDeviceCanAccessPeer");
+    if (!can) return false;
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    else check(e, "hipDeviceEnablePeerAccess");
+    return true;
+  });
   m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
     check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault, S(st)),
           "hipMemcpyAsync");

@@ -30,7 +30,7 @@ import torch
 from . import _core, ops
 from .synthetic import SyntheticWorld
 
-EXCHANGE_MODES = ("p2p", "bcast", "allgather")
+EXCHANGE_MODES = ("p2p", "bcast", "allgather", "ipc")
 
 
 class _StreamJoin:
@@ -128,6 +128,7 @@ class DevicePuller:
         self.exchange = exchange
         self.exchange_times: dict = {}
         self._gather_bufs = None
+        self._peer_arenas = None  # ipc mode: every peer's arena mapped into this process
         self._rx = _core.trace.roctx_enabled()  # ZEST_ROCTX=1: one roctx range per round (host-side issue)
         self.is_cuda = self.device.type == "cuda"
         T = world.terms
@@ -258,8 +259,13 @@ class DevicePuller:
                         broadcasts, zero copy).
         * ``allgather`` equal-size slabs through all_gather_into_tensor into a double-buffered
                         gather buffer, then D2D unpack on a side stream (RCCL's ring/mesh allgather).
+        * ``ipc``       no collective: every rank maps its peers' arenas (HIP IPC, `enable_ipc`) and
+                        pulls their regions with DMA copies, one stream per peer group, so the
+                        copies of all 7 peers run over their own xGMI links at once.
         """
         mode = mode or self.exchange
+        if mode == "ipc":
+            return self._exchange_ipc(k)
         if mode == "bcast":
             return self._exchange_bcast(k)
         if mode == "allgather":
@@ -354,6 +360,64 @@ class DevicePuller:
         self._gather_used[b] = True
         return [_StreamJoin(self._unpack_stream)]
 
+    def enable_ipc(self) -> bool:
+        """Map every peer's arena into this process (HIP IPC over dmabuf) for the ``ipc`` exchange.
+        Collective; returns True only if every rank mapped every peer (MIN-reduced)."""
+        import torch.distributed as dist
+        from torch.multiprocessing.reductions import reduce_tensor
+        if not self.is_cuda or self.n_ranks == 1:
+            return False
+        try:
+            mine = reduce_tensor(self.arena)
+        except Exception:
+            mine = None
+        objs = [None] * self.n_ranks
+        dist.all_gather_object(objs, mine, group=self.group)
+        peers = [None] * self.n_ranks
+        ok = 1
+        try:
+            H = ops.hip()
+            for p, o in enumerate(objs):
+                if p != self.rank:
+                    fn, args = o
+                    peers[p] = fn(*args)
+                    if peers[p].device != self.device and not H.enable_peer_access(peers[p].device.index):
+                        ok = 0
+        except Exception:
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if not int(flag.item()):
+            return False
+        self._peer_arenas = peers
+        # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
+        self._host_group = dist.new_group(backend="gloo")
+        self._ipc_streams = [torch.cuda.Stream(self.device) for _ in range(min(self.n_ranks - 1, 4))]
+        self._ipc_done = {}
+        return True
+
+    def _exchange_ipc(self, k: int):
+        """Pull every peer's round-k region from its mapped arena.  The owners' regions must be
+        complete: this rank waits for its own round-k kernels (event recorded by step()), then a
+        host barrier says every owner did the same."""
+        import torch.distributed as dist
+        ev = self._ipc_done.get(k)
+        if ev is None:  # called outside step() (autotune): everything queued so far
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        ev.synchronize()
+        dist.barrier(group=self._host_group)
+        H = ops.hip()
+        used = []
+        for p, (lo, hi) in enumerate(self.regions[k]):
+            if p == self.rank or hi <= lo:
+                continue
+            st = self._ipc_streams[len(used) % len(self._ipc_streams)]
+            if st not in used:
+                used.append(st)
+            H.memcpy_async(self.arena.data_ptr() + lo, self._peer_arenas[p].data_ptr() + lo, hi - lo, st.cuda_stream)
+        return [_StreamJoin(st) for st in used]
+
     def autotune_exchange(self, modes=EXCHANGE_MODES, max_rounds: int = 4) -> dict:
         """Time each exchange strategy on this machine and keep the fastest (setup, untimed).
 
@@ -362,7 +426,7 @@ class DevicePuller:
         import torch.distributed as dist
         if self.n_ranks == 1:
             return {}
-        modes = tuple(modes)
+        modes = tuple(m for m in modes if m != "ipc" or self._peer_arenas is not None)
         rounds = range(min(self.n_rounds, max_rounds))
         times = {}
         for mode in modes:
@@ -423,9 +487,20 @@ class DevicePuller:
                                   self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
                 self.slot_free[s].record(comp)
                 if self.n_ranks > 1:
-                    works += self._exchange(k)
+                    if self.exchange == "ipc":
+                        # peers read round k once its kernels are done; wait for that only after
+                        # round k+1's copy and kernels are queued, so the GPU never idles on it
+                        self._ipc_done[k] = torch.cuda.Event()
+                        self._ipc_done[k].record(comp)
+                        if k > 0:
+                            works += self._exchange(k - 1)
+                    else:
+                        works += self._exchange(k)
                 if self._rx:
                     _core.trace.roctx_pop()
+            if self.n_ranks > 1 and self.exchange == "ipc":
+                works += self._exchange(self.n_rounds - 1)
+                self._ipc_done.clear()
         else:
             for k, rw in enumerate(self.rounds):
                 if rw.term_b > rw.term_a:
