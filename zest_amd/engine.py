@@ -434,14 +434,17 @@ class DevicePuller:
                 self._sync()
                 dist.barrier(group=self.group)
                 t0 = time.perf_counter()
-                works = []
-                for k in rounds:
-                    works += self._exchange(k, mode)
-                for w in works:
-                    w.wait()
-                self._sync()
-                dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                                  device=self.device if self.is_cuda else "cpu")
+                try:
+                    works = []
+                    for k in rounds:
+                        works += self._exchange(k, mode)
+                    for w in works:
+                        w.wait()
+                    self._sync()
+                    elapsed = time.perf_counter() - t0
+                except (RuntimeError, ValueError):  # argument checks fail the same way on every rank
+                    elapsed = float("inf")
+                dt = torch.tensor([elapsed], dtype=torch.float64, device=self.device if self.is_cuda else "cpu")
                 dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
                 times[mode] = float(dt.item())
         self.exchange = min(modes, key=lambda m: times[m])
