@@ -7,7 +7,8 @@ in its HBM arena:
 
   origin (pinned host, = the CDN bytes of this rank's 1/N of the reconstruction terms)
     --hipMemcpyAsync--> HBM staging ring --HIP index/place/BLAKE3--> arena
-    --RCCL over xGMI--> every other GPU; chunk-hash all-reduce; GPU Merkle file-hash check.
+    --RCCL / IPC over xGMI--> every other GPU, which BLAKE3-hashes what it received as each round
+    lands; GPU Merkle file hashes on every rank against the published ones.
 
 The replication strategy (batched p2p sends, coalesced broadcasts, or equal-slab all-gather) is
 picked during setup by timing each one on the machine (--exchange auto, DevicePuller.autotune_exchange).
@@ -47,7 +48,6 @@ def main() -> None:
     ap.add_argument("--mode", default="random", choices=["random", "bf16"])
     ap.add_argument("--round-mb", type=int, default=1024, help="per-rank bytes per pipeline round")
     ap.add_argument("--slots", type=int, default=3)
-    ap.add_argument("--verify-received", action="store_true", help="re-hash bytes received from peers")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--seeders", type=int, default=0,
                     help="ranks that pull from the origin (default all); the rest leech everything from "
@@ -98,7 +98,7 @@ def main() -> None:
         assert int(lo.item()) == int(hi.item()), "ranks disagree on the synthetic repository"
     seeders = a.seeders if a.seeders > 0 else world_size
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
-                          verify_received=a.verify_received, seeders=seeders)
+                          seeders=seeders)
     puller.build_origin()
     torch.cuda.synchronize()
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
@@ -119,11 +119,8 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
-    # Warm-up steps on a poisoned arena: proves every byte is really placed by the pull, and re-hashes
-    # every chunk received from a peer so the chosen exchange strategy is checked on this machine.
-    verify_timed = puller.verify_received
-    puller.verify_received = True
-
+    # Warm-up steps on a poisoned arena: prove every byte is really placed (every step re-hashes every
+    # chunk of every replica, so a faulty exchange strategy shows up here as a hash mismatch).
     def warmup():
         for _ in range(a.warmup):
             arena.fill_(0xA5)
@@ -140,7 +137,6 @@ def main() -> None:
         log(rank, f"exchange {puller.exchange} failed verification ({e}); falling back to p2p")
         puller.exchange = "p2p"
         warmup()
-    puller.verify_received = verify_timed
     puller.err.zero_()
     barrier()
     torch.cuda.synchronize()
@@ -185,7 +181,7 @@ def main() -> None:
                    "chunks": world.n_chunks, "xorbs": world.n_xorbs, "terms": int(len(world.terms)),
                    "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": puller.exchange if world_size > 1 else "none",
                    "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
-                   "verify": "merkle_file_hash" + ("+received" if a.verify_received else "")},
+                   "verify": "blake3 of every chunk on every rank + merkle file hashes"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

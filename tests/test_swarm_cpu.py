@@ -98,3 +98,53 @@ def test_cpu_swarm_exchange_modes(exchange):
     assert len(chosen) == 1, chosen  # all ranks agree
     if exchange != "auto":
         assert chosen == {exchange}
+
+
+def _corrupt_worker(rank, port, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from zest_amd import ops
+        from zest_amd.engine import DevicePuller
+        from zest_amd.synthetic import SyntheticWorld
+
+        class Flaky(DevicePuller):
+            """Flips one received byte on rank 0 before it is hashed (a bad link / faulty peer)."""
+
+            def _hash_received(self, k, works):
+                for w in works:
+                    w.wait()
+                if self.rank == 0 and k == 0 and self.recv_runs[0]:
+                    c0, _ = self.recv_runs[0][0]
+                    self.arena[int(self.world.chunk_off[c0]) + 7] ^= 1
+                return super()._hash_received(k, [])
+
+        w = SyntheticWorld("llama-tiny", seed=3, mode="random", max_xorb_bytes=256 << 10)
+        contents = w.build_on_host()
+        arena = torch.zeros(w.arena_bytes + 4096, dtype=torch.uint8)[: w.arena_bytes]
+        p = Flaky(w, arena, rank, 2, round_bytes=512 << 10)
+        p.build_origin_host(contents)
+        p.step()
+        try:
+            p.check()
+            result_q.put((rank, "passed"))
+        except ops.IngestError as e:
+            result_q.put((rank, f"detected {e.code}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cpu_swarm_detects_corrupt_transfer():
+    """Every rank hashes what it received itself: one flipped byte on rank 0 fails the Merkle check,
+    and the error word is all-reduced so both ranks stop."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29760 + os.getpid() % 100
+    procs = [ctx.Process(target=_corrupt_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[1].split()[0] for r in res] == ["detected", "detected"], res

@@ -9,8 +9,10 @@ in rounds through a pinned-host -> HBM staging ring:
     RCCL        : round-k regions replicated over xGMI (batched p2p, coalesced broadcasts or slab
                   all-gather, whichever autotune_exchange measured fastest), overlapped with round
                   k+1 ingest (every GPU acts as a BitTorrent peer)
-    end         : chunk-hash all-reduce (have-map, C2) -> Merkle file hashes on every rank (K2) ->
-                  compare with the repository's file hashes -> error all-reduce (C3)
+    verify      : chunks received from peers are BLAKE3-hashed on a side stream as each round lands,
+                  so every rank hashes its whole replica itself (no peer's hashes are trusted)
+    end         : Merkle file hashes on every rank (K2) -> compare with the repository's published
+                  file hashes -> error all-reduce (C3)
 
 The reference's equivalent is parallel_download.zig:91-204 (16 concurrent term fetches, batch
 barrier, ordered writes) plus swarm.zig's peer fallback; here the "peers" of one node are GPUs and
@@ -117,14 +119,13 @@ def split_rounds(world: SyntheticWorld, a: int, b: int, n_rounds: int) -> list[t
 
 class DevicePuller:
     def __init__(self, world: SyntheticWorld, arena: torch.Tensor, rank: int = 0, n_ranks: int = 1,
-                 round_bytes: int = 1 << 30, slots: int = 3, group=None, verify_received: bool = False,
-                 exchange: str = "p2p", seeders: int | None = None):
+                 round_bytes: int = 1 << 30, slots: int = 3, group=None, exchange: str = "p2p",
+                 seeders: int | None = None):
         self.world = world
         self.arena = arena
         self.device = arena.device
         self.rank, self.n_ranks = rank, n_ranks
         self.group = group
-        self.verify_received = verify_received
         self.exchange = exchange
         self.exchange_times: dict = {}
         self._gather_bufs = None
@@ -189,6 +190,20 @@ class DevicePuller:
             self.copy_stream = torch.cuda.Stream(self.device)
             self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
             self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
+        # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
+        # every rank BLAKE3-hashes them as soon as they land, so each GPU verifies its whole replica
+        # against the published Merkle file hashes without trusting any peer's hashes.
+        self.recv_runs = [[] for _ in range(self.n_rounds)]
+        for k in range(self.n_rounds):
+            for p in range(n_ranks):
+                a, b = self.rounds_all[k][p]
+                if p != rank and b > a:
+                    c0 = int(T["c0"][a])
+                    self.recv_runs[k].append((c0, int(T["c1"][b - 1]) - c0))
+        if self.is_cuda and n_ranks > 1:
+            self.chunk_off_dev = torch.from_numpy(world.chunk_off.astype(np.int64)).to(self.device)
+            self.chunk_len_dev = torch.from_numpy(world.chunk_len.astype(np.int32)).to(self.device)
+            self.verify_stream = torch.cuda.Stream(self.device)
         self.bytes_received = sum(hi - lo for k in range(self.n_rounds) for r, (lo, hi) in
                                   enumerate(self.regions[k]) if r != rank)
         self.bytes_ingested = int(self.term_origin_off[-1])
@@ -496,14 +511,16 @@ class DevicePuller:
                         self._ipc_done[k] = torch.cuda.Event()
                         self._ipc_done[k].record(comp)
                         if k > 0:
-                            works += self._exchange(k - 1)
+                            works += self._hash_received(k - 1, self._exchange(k - 1))
                     else:
-                        works += self._exchange(k)
+                        works += self._hash_received(k, self._exchange(k))
                 if self._rx:
                     _core.trace.roctx_pop()
             if self.n_ranks > 1 and self.exchange == "ipc":
-                works += self._exchange(self.n_rounds - 1)
+                works += self._hash_received(self.n_rounds - 1, self._exchange(self.n_rounds - 1))
                 self._ipc_done.clear()
+            if self.n_ranks > 1:
+                works.append(_StreamJoin(self.verify_stream))
         else:
             for k, rw in enumerate(self.rounds):
                 if rw.term_b > rw.term_a:
@@ -511,13 +528,9 @@ class DevicePuller:
                     rec = np.frombuffer(rw.terms_dev.numpy().tobytes(), dtype=ops.TERM_DTYPE)
                     ops.ingest_terms(span, self.arena, rec, self.hashes, hash_base=rw.c0)
                 if self.n_ranks > 1:
-                    works += self._exchange(k)
+                    works += self._hash_received(k, self._exchange(k))
         for w in works:
             w.wait()
-        if self.n_ranks > 1:
-            dist.all_reduce(self.hashes.view(torch.int32), op=dist.ReduceOp.SUM, group=self.group)
-        if self.verify_received and self.n_ranks > 1:
-            self._verify_received()
         if self.is_cuda:
             H.merkle(self.hashes.data_ptr(), self.sizes.data_ptr(), self.jobs_dev.data_ptr(), len(self.jobs),
                      self.roots.data_ptr(), self.merkle_scratch.data_ptr(), self.merkle_sb, st)
@@ -533,25 +546,30 @@ class DevicePuller:
     def check(self) -> None:
         ops.raise_on_error(self.err)
 
-    def _verify_received(self):
-        """Re-hash every chunk that arrived from a peer and compare with the owner's hash."""
-        w = self.world
-        T = w.terms
-        a_r, b_r = self.rank_terms[self.rank]
-        mask = np.ones(w.n_chunks, dtype=bool)
-        if b_r > a_r:
-            mask[int(T["c0"][a_r]):int(T["c1"][b_r - 1])] = False
-        idx = np.flatnonzero(mask)
-        if len(idx) == 0:
-            return
-        got = ops.hash_ranges(self.arena, w.chunk_off[idx], w.chunk_len[idx])
-        want = self.hashes[torch.from_numpy(idx).to(self.device)]
-        bad = (got != want).any(1)
-        if self.is_cuda:
-            first = torch.where(bad.any(), torch.argmax(bad.to(torch.int32)), torch.tensor(-1, device=self.device))
-            self.err.copy_(torch.where(first >= 0, (6 << 32) + first, self.err))
-        elif bool(bad.any()):
-            self.err.fill_((6 << 32) | int(bad.nonzero()[0].item()))
+    def _hash_received(self, k: int, works: list) -> list:
+        """Hash round k's chunks received from peers into this rank's own table as soon as the
+        transfers land (side stream on the GPU, overlapped with later rounds).  Returns the works the
+        caller still has to wait for: none once they were waited here (a gloo work must not be waited
+        twice; on the GPU the caller's final join on the verify stream covers them)."""
+        runs = self.recv_runs[k]
+        if not runs:
+            return works
+        if not self.is_cuda:
+            for w in works:
+                w.wait()
+            wd = self.world
+            for c0, n in runs:
+                self.hashes[c0:c0 + n] = ops.hash_ranges(self.arena, wd.chunk_off[c0:c0 + n], wd.chunk_len[c0:c0 + n])
+            return []
+        H = ops.hip()
+        with torch.cuda.stream(self.verify_stream):
+            for w in works:
+                w.wait()  # the verify stream waits for round k's transfers
+            for c0, n in runs:
+                H.hash_ranges(self.arena.data_ptr(), self.chunk_off_dev.data_ptr() + 8 * c0,
+                              self.chunk_len_dev.data_ptr() + 4 * c0, n, self.hashes.data_ptr() + 32 * c0,
+                              ops.KEY_DATA, self.verify_stream.cuda_stream)
+        return []
 
     def close(self):
         self.origin.close()
