@@ -375,21 +375,23 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
     const uint32_t ip_lim = ip_end < w.wofs + 256 ? ip_end : w.wofs + 256;
     if (ip >= ip_lim) return;
     uint32_t op_lim = op_room < s.fp + kFlushAt ? op_room : s.fp + kFlushAt;
+    // One gather per sequence, aligned to its literals: lane l holds stream byte ip + 1 + l, so the
+    // offset (lanes lit, lit + 1) and the NEXT token (lane lit + 2) are read-lanes of the same vector.
+    uint32_t token = win_u8(w, ip);
     do {
       if (s.op >= op_lim) {
         if (s.op >= op_room) return;
         sink_flush<RB>(s, s.op, false, lane);
         op_lim = op_room < s.fp + kFlushAt ? op_room : s.fp + kFlushAt;
       }
-      const uint32_t v = win_lane_u8(w, ip, lane);  // lane l: stream byte ip + l
-      const uint32_t token = __builtin_amdgcn_readfirstlane(v);
       const uint32_t lit = token >> 4, mlc = token & 15;
-      const uint32_t off = __builtin_amdgcn_readlane(v, int(lit + 1)) | (__builtin_amdgcn_readlane(v, int(lit + 2)) << 8);
+      const uint32_t v = win_lane_u8(w, ip + 1, lane);
+      const uint32_t off = __builtin_amdgcn_readlane(v, int(lit)) | (__builtin_amdgcn_readlane(v, int(lit + 1)) << 8);
+      const uint32_t next = __builtin_amdgcn_readlane(v, int(lit + 2));
       // one exit test: a length-extension nibble, or an offset of 0 / before the chunk start (the
       // general path then decodes the sequence, or reports it)
       if (uint32_t(lit == 15) | uint32_t(mlc == 15) | uint32_t(off - 1 >= s.op + lit)) return;
-      const uint32_t litv = __shfl_down(v, 1, kWave);  // lane l: stream byte ip + 1 + l
-      s.ring[(s.tmod + s.op + lane) & RingGeo<RB>::kMask] = uint8_t(litv);
+      s.ring[(s.tmod + s.op + lane) & RingGeo<RB>::kMask] = uint8_t(v);
       const uint32_t mo = s.op + lit;
       uint8_t m;
       if (off <= RingGeo<RB>::kReach) {
@@ -398,8 +400,8 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
         __builtin_amdgcn_wave_barrier();
         m = s.ring[(s.tmod + mo + lane - back) & RingGeo<RB>::kMask];
       } else {
-        // Far match (off > RingGeo<RB>::kReach >= 64, so no overlap): the source was flushed >= RingGeo<RB>::kReach -
-        // kFlushAt bytes ago; wait for this wave's stores, then read it back through L2.
+        // Far match (off > ring reach >= 64, so no overlap): the source was flushed at least
+        // reach - kFlushAt bytes ago; wait for this wave's stores, then read it back through L2.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         m = uint8_t(load_u8_coherent(s.out + out_pos(s, mo + lane - off)));
         if (kProf) s.nfar++;
@@ -415,6 +417,7 @@ __device__ __forceinline__ void lz4_fast(Sink& s, Win& w, uint32_t& ip, uint32_t
       }
       s.op = mo + mlc + 4;
       ip += lit + 3;
+      token = next;
     } while (ip < ip_lim);
   }
 }
