@@ -93,6 +93,20 @@ PYBIND11_MODULE(_hip, m) {
                          P<uint8_t>(out), key_mode, S(st)),
           "zg_hash_ranges");
   });
+  m.def("compress_chunks", [](uintptr_t data, uintptr_t offs, uintptr_t lens, int n, int bg4, uintptr_t scratch,
+                              uint64_t in_slot, uintptr_t out, uint64_t out_slot, uintptr_t out_len, uint32_t hc64,
+                              uint32_t hc256, uintptr_t st) {
+    check(zg_compress_chunks(P<const uint8_t>(data), P<const uint64_t>(offs), P<const uint32_t>(lens), n, bg4,
+                             P<uint8_t>(scratch), in_slot, P<uint8_t>(out), out_slot, P<uint32_t>(out_len), hc64, hc256,
+                             S(st)),
+          "zg_compress_chunks");
+  });
+  m.def("pack_frames", [](uintptr_t src, uintptr_t clen, uintptr_t ulen, uintptr_t scheme, uintptr_t out_off, int n,
+                          uintptr_t out, uintptr_t st) {
+    check(zg_pack_frames(P<const uint64_t>(src), P<const uint32_t>(clen), P<const uint32_t>(ulen),
+                         P<const uint8_t>(scheme), P<const uint64_t>(out_off), n, P<uint8_t>(out), S(st)),
+          "zg_pack_frames");
+  });
   m.def("merkle_scratch_bytes", &zg_merkle_scratch_bytes);
   m.def("merkle", [](uintptr_t hashes, uintptr_t sizes, uintptr_t jobs, int n_jobs, uintptr_t roots,
                      uintptr_t scratch, uint64_t scratch_bytes, uintptr_t st) {

@@ -79,6 +79,16 @@ hipError_t zg_cdc_candidates(const uint8_t* data, uint64_t n, uint64_t mask, uin
 // Synthetic content.  mode 0: uniform random bytes; mode 1: bf16 ~ N(0, 0.02).
 hipError_t zg_fill_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t stream_offset, int mode,
                              hipStream_t stream);
+// K7b: compress chunks (optional BG4 grouping into `scratch`, slot `in_slot` bytes per chunk) into
+// LZ4 frames at out + c * out_slot; out_len[c] = frame bytes, or 0 when the chunk does not compress.
+// hc64 / hc256: frame header checksum bytes for the 64 KiB / 256 KiB block-size descriptors.
+hipError_t zg_compress_chunks(const uint8_t* data, const uint64_t* offs, const uint32_t* lens, int n, int bg4,
+                              uint8_t* scratch, uint64_t in_slot, uint8_t* out, uint64_t out_slot, uint32_t* out_len,
+                              uint32_t hc64, uint32_t hc256, hipStream_t stream);
+// Serialize chunks (header + payload copied from per-chunk device addresses) into xorb bodies.
+hipError_t zg_pack_frames(const uint64_t* src, const uint32_t* clen, const uint32_t* ulen, const uint8_t* scheme,
+                          const uint64_t* out_off, int n, uint8_t* out, hipStream_t stream);
+
 // Pack uncompressed chunks into serialized xorb bodies: header (version 0, scheme 0) + payload.
 hipError_t zg_pack_chunks(const uint8_t* data, const uint64_t* data_off, const uint32_t* lens,
                           const uint64_t* out_off, int n, uint8_t* out, hipStream_t stream);

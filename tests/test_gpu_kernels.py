@@ -262,3 +262,35 @@ def test_sha1_info_hash_kernel():
     for i in range(0, 1000, 37):
         assert got[i].tobytes() == hashlib.sha1(b"zest-xet-v1:" + hs[i].numpy().tobytes()).digest()
     assert ops.sha1_info_hash(hs[:0].cuda()).shape == (0, 20)
+
+
+def test_gpu_lz4_compress_roundtrip_host_decoder():
+    """K7b: GPU BG4/LZ4 frames decode with the host decoder (same frame format as hf_xet) to the
+    original bytes; incompressible chunks are reported as raw; ratios close to the host encoder."""
+    from zest_amd import _core, ops
+    rng = np.random.default_rng(5)
+    w = (rng.standard_normal(300_000).astype(np.float32) * 0.02)
+    bf16 = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+    parts = [bf16[:65536], bf16[65536:65536 + 131072], rng.integers(0, 8, 70_000, dtype=np.uint8).tobytes(),
+             rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes(), bytes(40_000), b"abc" * 9, b"x" * 12,
+             bf16[200_000:200_000 + 8191]]
+    blob = b"".join(parts)
+    offs = np.cumsum([0] + [len(p) for p in parts[:-1]]).astype(np.uint64)
+    lens = np.array([len(p) for p in parts], dtype=np.uint32)
+    dev = torch.device("cuda:0")
+    buf = ops.padded_empty(len(blob), dev)
+    buf.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+    for bg4, scheme in ((True, 2), (False, 1)):
+        frames, flen = ops.compress_chunks(buf, offs, lens, bg4=bg4)
+        host = frames.cpu().numpy()
+        gpu_total = host_total = 0
+        for i, p in enumerate(parts):
+            if flen[i] == 0:
+                assert len(p) < 64 or len(_core.compress_chunk(p, "bg4" if bg4 else "lz4")[1]) >= len(p) * 0.95, i
+                gpu_total += len(p)
+            else:
+                fr = host[i * ops.LZ4_SLOT:i * ops.LZ4_SLOT + int(flen[i])].tobytes()
+                assert _core.decompress_chunk(scheme, fr, len(p)) == p, (bg4, i)
+                gpu_total += int(flen[i])
+            host_total += min(len(p), len(_core.compress_chunk(p, "bg4" if bg4 else "lz4")[1]))
+        assert gpu_total <= host_total * 1.15, (bg4, gpu_total, host_total)

@@ -366,3 +366,64 @@ def pack_chunks(data: torch.Tensor, data_off: np.ndarray, lens: np.ndarray, out_
     o_off = torch.from_numpy(out_off.view(np.int64).copy()).to(dev)
     H.pack_chunks(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), o_off.data_ptr(), n, out.data_ptr(),
                   _stream(dev))
+
+
+# ----------------------------------------------------------------------------------------------
+# K7b: chunk compression (BG4 grouping + LZ4 frame) and serialization of compressed chunks
+# ----------------------------------------------------------------------------------------------
+LZ4_SLOT = 132 << 10  # device bytes per chunk for one frame (>= LZ4 bound of 128 KiB + frame overhead)
+
+
+@functools.lru_cache(maxsize=1)
+def _lz4_header_checksums() -> tuple[int, int]:
+    """Frame-descriptor checksum bytes the host encoder writes for 64 KiB / 256 KiB blocks."""
+    return _core.lz4_compress_frame(b"\0" * 16)[6], _core.lz4_compress_frame(b"\0" * 65537)[6]
+
+
+def compress_chunks(buf: torch.Tensor, offsets, lens, bg4: bool = True):
+    """Compress each chunk buf[off:off+len] on the GPU into an LZ4 frame (BG4-grouped first when
+    `bg4`), the layout the host encoder and hf_xet use.  Returns (frames, frame_len): frames is a
+    device buffer holding chunk i's frame at i * LZ4_SLOT; frame_len[i] == 0 means the chunk does
+    not compress and is stored raw (scheme 0), as Xet does."""
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint32)
+    n = len(offsets)
+    if buf.device.type != "cuda":
+        raise ValueError("compress_chunks runs on the GPU")
+    if n and (np.any(lens > 128 * 1024) or np.any(offsets + lens > buf.numel() * buf.element_size())):
+        raise ValueError("compress_chunks: chunk larger than 128 KiB or past the buffer")
+    dev = buf.device
+    frames = padded_empty(max(1, n) * LZ4_SLOT, dev)
+    flen = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    if n:
+        H = hip()
+        buf = _as_padded_u8(buf)
+        scratch = padded_empty(n * LZ4_SLOT if bg4 else 1, dev)
+        offs_d = torch.from_numpy(offsets.view(np.int64).copy()).to(dev)
+        lens_d = torch.from_numpy(lens.view(np.int32).copy()).to(dev)
+        hc64, hc256 = _lz4_header_checksums()
+        H.compress_chunks(buf.data_ptr(), offs_d.data_ptr(), lens_d.data_ptr(), n, int(bg4), scratch.data_ptr(),
+                          LZ4_SLOT, frames.data_ptr(), LZ4_SLOT, flen.data_ptr(), hc64, hc256,
+                          torch.cuda.current_stream(dev).cuda_stream)
+    return frames, flen[:n].cpu().numpy().astype(np.int64)
+
+
+def pack_frames(src_addr: np.ndarray, clen: np.ndarray, ulen: np.ndarray, scheme: np.ndarray, out_off: np.ndarray,
+                out: torch.Tensor) -> None:
+    """Serialize chunks whose payload (compressed frame or raw bytes) sits at device address
+    src_addr[i]: 8-byte header [0][clen u24][scheme][ulen u24] + payload, into `out` at out_off[i]."""
+    n = len(clen)
+    if n == 0:
+        return
+    clen = np.asarray(clen, dtype=np.uint32)
+    out_off = np.asarray(out_off, dtype=np.uint64)
+    if np.any(out_off + clen + 8 > out.numel()):
+        raise ValueError("pack_frames range out of bounds")
+    dev = out.device
+    H = hip()
+    t = [torch.from_numpy(np.ascontiguousarray(a).copy()).to(dev) for a in
+         (np.asarray(src_addr, dtype=np.uint64).view(np.int64), clen.view(np.int32),
+          np.asarray(ulen, dtype=np.uint32).view(np.int32), np.asarray(scheme, dtype=np.uint8),
+          out_off.view(np.int64))]
+    H.pack_frames(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), t[4].data_ptr(), n,
+                  out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
