@@ -75,7 +75,9 @@ def main() -> None:
     t_setup = time.time()
     ops.hip()
     spec = models.get(a.model)
-    world = SyntheticWorld(spec, seed=a.seed, mode=a.mode)
+    # bf16 mode stores chunks the way Xet stores real checkpoints: BG4-LZ4 frames (compressed on the
+    # GPU) when smaller than the chunk, so the pull decodes them on the GPU.
+    world = SyntheticWorld(spec, seed=a.seed, mode=a.mode, compression="bg4" if a.mode == "bf16" else "none")
     log(rank, f"model {spec.repo_id}: {world.model_bytes / 1e9:.2f} GB in {len(world.xet_files)} files; "
               f"arena {world.arena_bytes / 1e9:.2f} GB; ranks {world_size}")
     arena = ops.padded_empty(world.arena_bytes, device)
@@ -171,8 +173,10 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": f"synthetic ({a.mode}-byte weights of the real tensor shapes; real Xet CDC/xorbs/hashes; "
-                "origin = pinned host memory standing in for the CDN)",
+        "data": f"synthetic ({a.mode}-byte weights of the real tensor shapes; real Xet CDC/xorbs/hashes"
+                + ("; BG4-LZ4 compressed chunks, stored/raw ratio "
+                   f"{float(world.chunk_clen.sum()) / float(world.chunk_len.sum()):.3f}" if a.mode == "bf16" else "")
+                + "; origin = pinned host memory standing in for the CDN)",
         "p2p_ratio": round(p2p_ratio, 4),
         "ingest_GBps": round(float(ing.item()) / step_s / 1e9, 3),
         "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,

@@ -238,10 +238,9 @@ class DevicePuller:
             if u == t:
                 raise RuntimeError("term larger than pack batch")
             c0, c1 = int(T["c0"][t]), int(T["c1"][u - 1])
-            lens = w.chunk_len[c0:c1]
-            ser = lens.astype(np.uint64) + np.uint64(8)
+            ser = w.chunk_clen[c0:c1].astype(np.uint64) + np.uint64(8)
             out_off = (np.cumsum(ser) - ser).astype(np.uint64)
-            ops.pack_chunks(self.arena, w.chunk_off[c0:c1], lens, out_off, tmp)
+            w.pack_serialized(self.arena, c0, c1, tmp, out_off)
             n = int(self.term_origin_off[u - a_r] - base)
             H.memcpy_async(self.origin.ptr + base, tmp.data_ptr(), n, st)
             torch.cuda.synchronize(self.device)

@@ -22,13 +22,13 @@ class HbmXorbArena:
             raise ValueError("world must be built (build_on_device / build_on_host) first")
         self.world = world
         dev = torch.device(device) if device is not None else content.device
-        ser = world.chunk_len.astype(np.uint64) + np.uint64(8)
+        ser = world.chunk_clen.astype(np.uint64) + np.uint64(8)  # stored size (BG4-LZ4 frames in bf16 worlds)
         out_off = (np.cumsum(ser) - ser).astype(np.uint64)
         self.nbytes = int(ser.sum())
         self.buf = ops.padded_empty(self.nbytes, dev)
         for a in range(0, world.n_chunks, batch_chunks):
             b = min(world.n_chunks, a + batch_chunks)
-            ops.pack_chunks(content, world.chunk_off[a:b], world.chunk_len[a:b], out_off[a:b], self.buf)
+            world.pack_serialized(content, a, b, self.buf, out_off[a:b])
         x0 = world.xorb_chunk0
         x1 = np.concatenate([x0[1:], [world.n_chunks]])
         self.xorb_off = out_off[x0]

@@ -47,8 +47,14 @@ class SyntheticWorld:
     """Layout + Xet metadata of one synthetic repository."""
 
     def __init__(self, spec: models.ModelSpec | str, seed: int = 0, mode: str = "random",
-                 revision_sha: str | None = None, max_xorb_bytes: int = MAX_XORB_BYTES):
+                 revision_sha: str | None = None, max_xorb_bytes: int = MAX_XORB_BYTES, compression: str = "none"):
+        """compression: "none" stores every chunk raw (what Xet does for random bytes); "bg4" compresses
+        each chunk with BG4 + LZ4 on the GPU (build_on_device) and keeps the frame when it is smaller,
+        as Xet does for bf16 checkpoints."""
         self.spec = models.get(spec) if isinstance(spec, str) else spec
+        if compression not in ("none", "bg4"):
+            raise ValueError("compression must be 'none' or 'bg4'")
+        self.compression = compression
         self.max_xorb_bytes = max_xorb_bytes
         self.seed = seed
         self.mode = mode
@@ -76,6 +82,8 @@ class SyntheticWorld:
         self.xorb_of = None       # int64 per chunk
         self.ser_off = None       # uint64 offset of the chunk header inside its xorb
         self.terms = None         # structured array, see _plan_terms
+        self.chunk_clen = None    # uint32 stored payload length (== chunk_len when raw)
+        self.chunk_scheme = None  # uint8 0 = none, 2 = BG4-LZ4
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -126,12 +134,50 @@ class SyntheticWorld:
         fh = ops.merkle_roots(hashes, sizes, self.merkle_jobs(), file_hash=True)
         self.chunk_hashes = hashes.cpu().numpy()
         self.file_hashes = fh.cpu().numpy()
+        if self.compression == "bg4":
+            self._compress_sizes(arena)
         self._plan_xorbs()
+
+    def _compress_sizes(self, arena: torch.Tensor, batch: int = 8192) -> None:
+        """Stored size and scheme of every chunk under BG4-LZ4 (GPU compression, frames discarded:
+        the origin build compresses its own share again)."""
+        clen = self.chunk_len.astype(np.uint32).copy()
+        scheme = np.zeros(self.n_chunks, dtype=np.uint8)
+        for a in range(0, self.n_chunks, batch):
+            b = min(self.n_chunks, a + batch)
+            _, flen = ops.compress_chunks(arena, self.chunk_off[a:b], self.chunk_len[a:b], bg4=True)
+            keep = flen > 0
+            clen[a:b][keep] = flen[keep]
+            scheme[a:b][keep] = 2
+        self.chunk_clen, self.chunk_scheme = clen, scheme
+
+    def pack_serialized(self, arena: torch.Tensor, a: int, b: int, out: torch.Tensor, out_off: np.ndarray) -> None:
+        """Serialize chunks [a, b) ([8-byte header | stored payload], what the CAS serves) into `out`
+        at out_off (GPU).  Compressed worlds compress the chunks again — the kernel is
+        deterministic, so the frames are the ones the plan was sized with."""
+        lens = self.chunk_len[a:b]
+        if not self.chunk_scheme[a:b].any():
+            ops.pack_chunks(arena, self.chunk_off[a:b], lens, out_off, out)
+            return
+        for s0 in range(a, b, 4096):  # bounded compression scratch (2 x LZ4_SLOT per chunk)
+            s1 = min(b, s0 + 4096)
+            frames, flen = ops.compress_chunks(arena, self.chunk_off[s0:s1], self.chunk_len[s0:s1], bg4=True)
+            if not np.array_equal(np.where(flen > 0, flen, self.chunk_len[s0:s1]), self.chunk_clen[s0:s1]):
+                raise RuntimeError("GPU compression is not reproducible")
+            idx = np.arange(s1 - s0, dtype=np.uint64)
+            addr = np.where(flen > 0, np.uint64(frames.data_ptr()) + idx * np.uint64(ops.LZ4_SLOT),
+                            np.uint64(arena.data_ptr()) + self.chunk_off[s0:s1].astype(np.uint64))
+            ops.pack_frames(addr, self.chunk_clen[s0:s1], self.chunk_len[s0:s1], self.chunk_scheme[s0:s1],
+                            out_off[s0 - a:s1 - a], out)
+            torch.cuda.synchronize(out.device)
+            del frames
 
     # ------------------------------------------------------------------------------------------
     # Host build (tests / small models)
     # ------------------------------------------------------------------------------------------
     def build_on_host(self) -> dict[str, bytes]:
+        if self.compression != "none":
+            raise ValueError("compressed synthetic worlds are built on the GPU (build_on_device)")
         contents = {}
         offs, lens, fidx, hs = [], [], [], []
         for i, f in enumerate(self.xet_files):
@@ -171,7 +217,10 @@ class SyntheticWorld:
         return _core.xet_hex(self.file_hashes[i].tobytes())
 
     def _plan_xorbs(self) -> None:
-        ser = self.chunk_len.astype(np.uint64) + np.uint64(8)  # scheme 0 (random) serialized size
+        if self.chunk_clen is None:
+            self.chunk_clen = self.chunk_len.astype(np.uint32)
+            self.chunk_scheme = np.zeros(self.n_chunks, dtype=np.uint8)
+        ser = self.chunk_clen.astype(np.uint64) + np.uint64(8)  # 8-byte chunk header + stored payload
         self.xorb_of = np.asarray(_core.plan_xorbs(ser, self.max_xorb_bytes, MAX_XORB_CHUNKS), dtype=np.int64)
         # offset of each chunk header inside its xorb
         cum = np.cumsum(ser) - ser

@@ -163,6 +163,8 @@ class FakeHub:
                                  xet_suffixes=(".safetensors",), commit=world.commit)
         if world.terms is None:
             world.build_on_host()
+        if world.chunk_scheme is not None and world.chunk_scheme.any():
+            raise ValueError("exact publishing of a compressed world needs payload=False (bytes from an HBM seeder)")
         contents = {f.path: files[f.path] for f in world.xet_files}
         base = len(self.xorbs)
         with self.lock:
