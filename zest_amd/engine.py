@@ -171,7 +171,11 @@ class DevicePuller:
         self.regions = [[self._region(k, r) for r in range(n_ranks)] for k in range(self.n_rounds)]
         self.slots = max(1, min(slots, self.n_rounds))
         self.staging = [ops.padded_empty(max_span, self.device) for _ in range(self.slots)]
-        self.ws = ops.IngestWorkspace(self.device, max_terms, max_chunks)
+        # two compute lanes (main stream + side stream) take alternate rounds, so round k+1's kernels
+        # fill the GPU while round k's last chunks decode (a 1 GiB round is ~2 chunks per resident
+        # wave: a single stream leaves most CUs idle in each decode kernel's tail)
+        self.ws_lanes = [ops.IngestWorkspace(self.device, max_terms, max_chunks) for _ in range(2)]
+        self.ws = self.ws_lanes[0]
         self.hashes = torch.zeros((world.n_chunks, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.from_numpy(world.chunk_len.astype(np.int64)).to(self.device)
         self.expected = torch.from_numpy(world.file_hashes.copy()).to(self.device)
@@ -188,6 +192,7 @@ class DevicePuller:
             self.merkle_scratch = torch.empty(self.merkle_sb, dtype=torch.uint8, device=self.device)
             self.roots = torch.empty((len(self.jobs), 32), dtype=torch.uint8, device=self.device)
             self.copy_stream = torch.cuda.Stream(self.device)
+            self.side_stream = torch.cuda.Stream(self.device)
             self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
             self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
         # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
@@ -479,10 +484,13 @@ class DevicePuller:
         works = []
         if self.is_cuda:
             H = ops.hip()
-            comp = torch.cuda.current_stream(dev)
-            st = comp.cuda_stream
+            main = torch.cuda.current_stream(dev)
+            lanes = (main, self.side_stream)
+            self.side_stream.wait_stream(main)  # hashes.zero_() above
             for k, rw in enumerate(self.rounds):
                 s = k % self.slots
+                comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
+                st = comp.cuda_stream
                 if self._rx:
                     _core.trace.roctx_push(f"engine: round {k}")
                 with torch.cuda.stream(self.copy_stream):
@@ -491,30 +499,33 @@ class DevicePuller:
                         H.memcpy_async(self.staging[s].data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
                                        self.copy_stream.cuda_stream)
                     self.h2d_done[s].record(self.copy_stream)
-                comp.wait_event(self.h2d_done[s])
-                if rw.term_b > rw.term_a:
-                    nt = rw.term_b - rw.term_a
-                    src = self.staging[s]
-                    self.ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
-                    H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), nt, self.ws.chunks.data_ptr(),
-                                  self.err.data_ptr(), st)
-                    H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(),
-                                   self.ws.chunks.data_ptr(), rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
-                    H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), self.ws.chunks.data_ptr(), rw.n_chunks,
-                                  self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
-                self.slot_free[s].record(comp)
-                if self.n_ranks > 1:
-                    if self.exchange == "ipc":
-                        # peers read round k once its kernels are done; wait for that only after
-                        # round k+1's copy and kernels are queued, so the GPU never idles on it
-                        self._ipc_done[k] = torch.cuda.Event()
-                        self._ipc_done[k].record(comp)
-                        if k > 0:
-                            works += self._hash_received(k - 1, self._exchange(k - 1))
-                    else:
-                        works += self._hash_received(k, self._exchange(k))
+                with torch.cuda.stream(comp):
+                    comp.wait_event(self.h2d_done[s])
+                    if rw.term_b > rw.term_a:
+                        nt = rw.term_b - rw.term_a
+                        src = self.staging[s]
+                        ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
+                        H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), nt, ws.chunks.data_ptr(),
+                                      self.err.data_ptr(), st)
+                        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(),
+                                       ws.chunks.data_ptr(), rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
+                        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
+                                      self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
+                    self.slot_free[s].record(comp)
+                    if self.n_ranks > 1:
+                        if self.exchange == "ipc":
+                            # peers read round k once its kernels are done; wait for that only after
+                            # round k+1's copy and kernels are queued, so the GPU never idles on it
+                            self._ipc_done[k] = torch.cuda.Event()
+                            self._ipc_done[k].record(comp)
+                            if k > 0:
+                                works += self._hash_received(k - 1, self._exchange(k - 1))
+                        else:  # collectives wait for the issuing (this round's) stream
+                            works += self._hash_received(k, self._exchange(k))
                 if self._rx:
                     _core.trace.roctx_pop()
+            main.wait_stream(self.side_stream)
+            st = main.cuda_stream
             if self.n_ranks > 1 and self.exchange == "ipc":
                 works += self._hash_received(self.n_rounds - 1, self._exchange(self.n_rounds - 1))
                 self._ipc_done.clear()
