@@ -175,7 +175,6 @@ class DevicePuller:
         # fill the GPU while round k's last chunks decode (a 1 GiB round is ~2 chunks per resident
         # wave: a single stream leaves most CUs idle in each decode kernel's tail)
         self.ws_lanes = [ops.IngestWorkspace(self.device, max_terms, max_chunks) for _ in range(2)]
-        self.ws = self.ws_lanes[0]
         self.hashes = torch.zeros((world.n_chunks, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.from_numpy(world.chunk_len.astype(np.int64)).to(self.device)
         self.expected = torch.from_numpy(world.file_hashes.copy()).to(self.device)
