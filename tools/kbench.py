@@ -78,6 +78,20 @@ def main():
         host = arena[:4 * csize].cpu().numpy().tobytes()
         assert all(h[i].tobytes() == C.chunk_hash(host[i * csize:(i + 1) * csize]) for i in range(4))
 
+    if want("hash"):
+        # CDC chunks land at arbitrary byte offsets in the arena: the misaligned load path
+        uoffs = offs + (np.arange(nck, dtype=np.uint64) * 13) % 61
+        ulens = np.full(nck, csize - 64, dtype=np.uint32)
+        uoffs_d = torch.from_numpy(uoffs.view(np.int64)).to(dev)
+        ulens_d = torch.from_numpy(ulens.view(np.int32)).to(dev)
+        ms = timed(lambda: H.hash_ranges(arena.data_ptr(), uoffs_d.data_ptr(), ulens_d.data_ptr(), nck,
+                                         out.data_ptr(), 0, st), a.iters)
+        ub = int(ulens.sum())
+        emit(kernel="blake3_xet_chunks_64k_unaligned", bytes=ub, ms=ms, gbps=ub / ms / 1e6, chunks=nck)
+        h = out[:4].cpu().numpy()
+        host = arena[:5 * csize].cpu().numpy().tobytes()
+        assert all(h[i].tobytes() == C.chunk_hash(host[int(uoffs[i]):int(uoffs[i]) + int(ulens[i])]) for i in range(4))
+
     if want("cdc"):
         cap = n // 4096
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
