@@ -68,6 +68,8 @@ def main() -> None:
             raise SystemExit("for --gpus > 1 launch with torchrun --nproc-per-node N (one rank per GPU)")
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    from zest_amd.parallel import bind_local_numa
+    numa_cpus = bind_local_numa(device)
     dist = None
     if world_size > 1:
         import torch.distributed as dist
@@ -78,6 +80,8 @@ def main() -> None:
     # bf16 mode stores chunks the way Xet stores real checkpoints: BG4-LZ4 frames (compressed on the
     # GPU) when smaller than the chunk, so the pull decodes them on the GPU.
     world = SyntheticWorld(spec, seed=a.seed, mode=a.mode, compression="bg4" if a.mode == "bf16" else "none")
+    if numa_cpus:
+        log(rank, f"bound to {len(numa_cpus)} CPUs on the GPU's NUMA node")
     log(rank, f"model {spec.repo_id}: {world.model_bytes / 1e9:.2f} GB in {len(world.xet_files)} files; "
               f"arena {world.arena_bytes / 1e9:.2f} GB; ranks {world_size}")
     arena = ops.padded_empty(world.arena_bytes, device)
@@ -185,7 +189,8 @@ def main() -> None:
                    "chunks": world.n_chunks, "xorbs": world.n_xorbs, "terms": int(len(world.terms)),
                    "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": puller.exchange if world_size > 1 else "none",
                    "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
-                   "verify": "blake3 of every chunk on every rank + merkle file hashes"},
+                   "verify": "blake3 of every chunk on every rank + merkle file hashes",
+                   "numa_bound_cpus": len(numa_cpus)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
