@@ -148,3 +148,22 @@ def test_cpu_swarm_detects_corrupt_transfer():
     for p in procs:
         p.join(timeout=60)
     assert [r[1].split()[0] for r in res] == ["detected", "detected"], res
+
+
+def test_cpu_swarm_eight_ranks_autotuned():
+    """The round-end scaling bench's shape (8 ranks, one per GPU, exchange autotuned) rehearsed on
+    gloo: every rank verifies the full model, all agree on the exchange mode, ingest totals 1x."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + os.getpid() % 100
+    procs = [ctx.Process(target=_worker, args=(r, 8, port, "llama-tiny", q, None, "auto")) for r in range(8)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=400) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, *_ in res)
+    assert len({r[5] for r in res}) == 1
+    model = res[0][4]
+    assert sum(r[3] for r in res) < model * 1.01 + 8 * 4096
