@@ -10,8 +10,10 @@ in its HBM arena:
     --RCCL / IPC over xGMI--> every other GPU, which BLAKE3-hashes what it received as each round
     lands; GPU Merkle file hashes on every rank against the published ones.
 
-The replication strategy (batched p2p sends, coalesced broadcasts, or equal-slab all-gather) is
-picked during setup by timing each one on the machine (--exchange auto, DevicePuller.autotune_exchange).
+The replication strategy (batched RCCL p2p sends, coalesced broadcasts, equal-slab all-gather, DMA
+copies from the peers' IPC-mapped arenas, or the K8 gather kernel reading every peer at once over
+xGMI) is picked during setup by timing each one on the machine (--exchange auto,
+DevicePuller.autotune_exchange).
 
 value      = N * model_bytes / step_time   (bytes made resident + verified across all GPUs, GB/s)
 p2p_ratio  = fraction of each GPU's model bytes that arrived from peers rather than the origin
@@ -52,7 +54,7 @@ def main() -> None:
     ap.add_argument("--seeders", type=int, default=0,
                     help="ranks that pull from the origin (default all); the rest leech everything from "
                          "them over xGMI (BASELINE config 2: --gpus 2 --seeders 1)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "bcast", "allgather", "ipc"],
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "bcast", "allgather", "ipc", "xgmi"],
                     help="intra-node replication strategy; auto = time each on this machine during setup")
     a = ap.parse_args()
 
@@ -110,10 +112,10 @@ def main() -> None:
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
     if world_size > 1:
-        ipc = a.exchange in ("auto", "ipc") and puller.enable_ipc()
+        ipc = a.exchange in ("auto", "ipc", "xgmi") and puller.enable_ipc()
         log(rank, f"peer arenas mapped over HIP IPC: {ipc}")
-        if a.exchange == "ipc" and not ipc:
-            raise SystemExit("--exchange ipc: mapping the peers' arenas failed")
+        if a.exchange in ("ipc", "xgmi") and not ipc:
+            raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
         if a.exchange == "auto":
             t_x = puller.autotune_exchange()
             log(rank, "exchange autotune (s over the first rounds): "

@@ -3,10 +3,12 @@
 // shape/bounds validation happens in zest_amd/ops before launch.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstddef>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../gpu/zgpu.h"
 
@@ -69,6 +71,21 @@ PYBIND11_MODULE(_hip, m) {
   m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
     check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault, S(st)),
           "hipMemcpyAsync");
+  });
+  // K8 (xgmi exchange): one launch pulls every (peer src, local dst, bytes) segment.
+  m.def("peer_gather", [](const std::vector<uint64_t>& src, const std::vector<uint64_t>& dst,
+                          const std::vector<uint64_t>& n, uintptr_t st) {
+    if (src.size() != dst.size() || src.size() != n.size() || src.size() > size_t(kZgMaxPeerSegs))
+      throw std::invalid_argument("peer_gather: need equal-length src/dst/n lists of at most 16 segments");
+    ZgPeerSegs s{};
+    s.nseg = int(src.size());
+    for (size_t i = 0; i < src.size(); ++i) {
+      if ((src[i] & 15) != (dst[i] & 15)) throw std::invalid_argument("peer_gather: src/dst not congruent mod 16");
+      s.src[i] = src[i];
+      s.dst[i] = dst[i];
+      s.n[i] = n[i];
+    }
+    check(zg_peer_gather(&s, S(st)), "zg_peer_gather");
   });
   m.def("index_terms", [](uintptr_t src, uintptr_t terms, int n, uintptr_t chunks, uintptr_t err, uintptr_t st) {
     check(zg_index_terms(P<const uint8_t>(src), P<const ZgTerm>(terms), n, P<ZgChunk>(chunks),

@@ -93,6 +93,17 @@ hipError_t zg_pack_frames(const uint64_t* src, const uint32_t* clen, const uint3
 hipError_t zg_pack_chunks(const uint8_t* data, const uint64_t* data_off, const uint32_t* lens,
                           const uint64_t* out_off, int n, uint8_t* out, hipStream_t stream);
 
+// K8: pull each segment's bytes from a peer's IPC-mapped arena (xGMI) into this GPU's arena;
+// every segment is read concurrently.  src[i] and dst[i] must be congruent mod 16.
+enum { kZgMaxPeerSegs = 16 };
+typedef struct ZgPeerSegs {
+  uint64_t src[kZgMaxPeerSegs];
+  uint64_t dst[kZgMaxPeerSegs];
+  uint64_t n[kZgMaxPeerSegs];
+  int nseg;
+} ZgPeerSegs;
+hipError_t zg_peer_gather(const ZgPeerSegs* segs, hipStream_t stream);
+
 int zg_device_count(void);
 // K6: out[i] (20 B) = SHA1("zest-xet-v1:" || hashes[i] (32 B)); out must be 4-byte aligned.
 hipError_t zg_sha1_info_hash(const uint8_t* hashes, int n, uint8_t* out, hipStream_t stream);

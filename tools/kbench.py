@@ -92,6 +92,24 @@ def main():
         host = arena[:5 * csize].cpu().numpy().tobytes()
         assert all(h[i].tobytes() == C.chunk_hash(host[int(uoffs[i]):int(uoffs[i]) + int(ulens[i])]) for i in range(4))
 
+    if want("gather"):
+        # K8 peer gather on local memory (copy engine vs kernel; on the 8-GPU node the same launch
+        # reads the peers' arenas over xGMI): 7 segments, as for 8 ranks
+        seg = n // 8
+        dst_g = ops.padded_empty(n, dev)
+        srcs = [arena.data_ptr() + i * seg + 3 for i in range(7)]
+        dsts = [dst_g.data_ptr() + i * seg + 3 for i in range(7)]
+        ms = timed(lambda: H.peer_gather(srcs, dsts, [seg - 64] * 7, st), a.iters)
+        emit(kernel="peer_gather_k8_local(7 segs)", bytes=7 * seg, ms=ms, gbps=7 * seg / ms / 1e6)
+        assert torch.equal(dst_g[3:seg - 61], arena[3:seg - 61])
+
+        def dma():
+            for i in range(7):
+                H.memcpy_async(dsts[i], srcs[i], seg - 64, st)
+        ms = timed(dma, a.iters)
+        emit(kernel="hipMemcpyAsync_local(7 segs)", bytes=7 * seg, ms=ms, gbps=7 * seg / ms / 1e6)
+        del dst_g
+
     if want("cdc"):
         cap = n // 4096
         cand = torch.empty(cap, dtype=torch.int64, device=dev)

@@ -32,7 +32,8 @@ import torch
 from . import _core, ops
 from .synthetic import SyntheticWorld
 
-EXCHANGE_MODES = ("p2p", "bcast", "allgather", "ipc")
+EXCHANGE_MODES = ("p2p", "bcast", "allgather", "ipc", "xgmi")
+PEER_MAPPED_MODES = ("ipc", "xgmi")  # need enable_ipc()
 
 
 class _StreamJoin:
@@ -280,10 +281,13 @@ class DevicePuller:
         * ``ipc``       no collective: every rank maps its peers' arenas (HIP IPC, `enable_ipc`) and
                         pulls their regions with DMA copies, one stream per peer group, so the
                         copies of all 7 peers run over their own xGMI links at once.
+        * ``xgmi``      same mapping, but one K8 kernel (csrc/gpu/xgmi.hip) pulls every peer's region
+                        with 16-byte loads from all CUs, so every link is read concurrently from a
+                        single launch.
         """
         mode = mode or self.exchange
-        if mode == "ipc":
-            return self._exchange_ipc(k)
+        if mode in PEER_MAPPED_MODES:
+            return self._exchange_ipc(k, kernel=(mode == "xgmi"))
         if mode == "bcast":
             return self._exchange_bcast(k)
         if mode == "allgather":
@@ -414,10 +418,11 @@ class DevicePuller:
         self._ipc_done = {}
         return True
 
-    def _exchange_ipc(self, k: int):
-        """Pull every peer's round-k region from its mapped arena.  The owners' regions must be
-        complete: this rank waits for its own round-k kernels (event recorded by step()), then a
-        host barrier says every owner did the same."""
+    def _exchange_ipc(self, k: int, kernel: bool = False):
+        """Pull every peer's round-k region from its mapped arena: DMA copies (``ipc``) or one K8
+        gather kernel (``xgmi``).  The owners' regions must be complete: this rank waits for its
+        own round-k kernels (event recorded by step()), then a host barrier says every owner did
+        the same."""
         import torch.distributed as dist
         ev = self._ipc_done.get(k)
         if ev is None:  # called outside step() (autotune): everything queued so far
@@ -426,6 +431,15 @@ class DevicePuller:
         ev.synchronize()
         dist.barrier(group=self._host_group)
         H = ops.hip()
+        if kernel:
+            segs = [(self._peer_arenas[p].data_ptr() + lo, self.arena.data_ptr() + lo, hi - lo)
+                    for p, (lo, hi) in enumerate(self.regions[k]) if p != self.rank and hi > lo]
+            st = self._ipc_streams[0]
+            for i in range(0, len(segs), 16):
+                part = segs[i:i + 16]
+                H.peer_gather([a for a, _, _ in part], [b for _, b, _ in part], [n for _, _, n in part],
+                              st.cuda_stream)
+            return [_StreamJoin(st)] if segs else []
         used = []
         for p, (lo, hi) in enumerate(self.regions[k]):
             if p == self.rank or hi <= lo:
@@ -444,7 +458,7 @@ class DevicePuller:
         import torch.distributed as dist
         if self.n_ranks == 1:
             return {}
-        modes = tuple(m for m in modes if m != "ipc" or self._peer_arenas is not None)
+        modes = tuple(m for m in modes if m not in PEER_MAPPED_MODES or self._peer_arenas is not None)
         rounds = range(min(self.n_rounds, max_rounds))
         times = {}
         for mode in modes:
@@ -512,7 +526,7 @@ class DevicePuller:
                                       self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
                     self.slot_free[s].record(comp)
                     if self.n_ranks > 1:
-                        if self.exchange == "ipc":
+                        if self.exchange in PEER_MAPPED_MODES:
                             # peers read round k once its kernels are done; wait for that only after
                             # round k+1's copy and kernels are queued, so the GPU never idles on it
                             self._ipc_done[k] = torch.cuda.Event()
@@ -525,7 +539,7 @@ class DevicePuller:
                     _core.trace.roctx_pop()
             main.wait_stream(self.side_stream)
             st = main.cuda_stream
-            if self.n_ranks > 1 and self.exchange == "ipc":
+            if self.n_ranks > 1 and self.exchange in PEER_MAPPED_MODES:
                 works += self._hash_received(self.n_rounds - 1, self._exchange(self.n_rounds - 1))
                 self._ipc_done.clear()
             if self.n_ranks > 1:
