@@ -14,6 +14,7 @@
 
 #include <cerrno>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -78,7 +79,9 @@ void print_usage(std::ostream& w) {
        "  --concurrency, -j <n>    Parallel term downloads (default: 16)\n"
        "  --no-verify              Skip the Xet file-hash check\n"
        "  --no-serve               Do not auto-start the background seeder\n"
-       "  --gpus <n>               Decode + verify on n GPUs (one worker per GPU, RCCL)\n"
+       "  --gpus <n|list>          Decode + verify on n GPUs, or on the listed devices (\"0,2,5\");\n"
+       "                           one worker per GPU, RCCL. Default: $ZEST_GPUS\n"
+       "  --pipeline-depth <MB>    Pinned staging per GPU worker (default: 1024)\n"
        "\n"
        "Seed options:\n"
        "  --tracker, -t <url>      BT tracker URL\n"
@@ -181,7 +184,7 @@ int spawn_gpu_workers(const std::vector<std::string>& pass, int gpus, int attemp
 // pipeline finishes the job (ZEST_GPU_HOST_FALLBACK=0 turns that off).  An attempt that ran to the end
 // but failed files (rank 0 wrote its status) is final: fewer GPUs would not fix the data.  SURVEY
 // §5.3 ("elastic world size 8 -> 7"); the reference has no GPU path and no retry (main.zig:233-256).
-int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int gpus) {
+int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int gpus, const std::vector<int>& devices) {
   // exe = <pkg>/_bin/zest -> PYTHONPATH = parent of the package directory
   std::string pkg_parent = exe;
   for (int i = 0; i < 3; ++i) {
@@ -204,6 +207,11 @@ int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int 
                              ".json";
   int rc = 1;
   for (int n = gpus, attempt = 0; n >= 1; --n, ++attempt) {
+    if (!devices.empty()) {  // an explicit device list: the first n of it (retries drop the last)
+      std::string vis;
+      for (int i = 0; i < n; ++i) vis += (i ? "," : "") + std::to_string(devices[size_t(i)]);
+      ::setenv("HIP_VISIBLE_DEVICES", vis.c_str(), 1);
+    }
     ::unlink(status.c_str());
     rc = spawn_gpu_workers(pass, n, attempt, status);
     const bool finished = ::access(status.c_str(), F_OK) == 0;
@@ -217,12 +225,40 @@ int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int 
   const char* fb = std::getenv("ZEST_GPU_HOST_FALLBACK");
   if (fb && std::string(fb) == "0") return rc;
   std::cerr << "zest: finishing the pull on the host\n";
+  ::unsetenv("ZEST_GPUS");  // the host pass must not start GPU workers again
   return cmd_pull(exe, pass);
 }
 
+// `--gpus` value: a count ("4") or a device list ("0,2,5", also "3," for the single device 3).
+// Returns the number of GPUs (0 = host path) and fills `devices` for a list.
+int parse_gpus(const std::string& v, std::vector<int>& devices) {
+  devices.clear();
+  if (v.find(',') == std::string::npos) return std::max(0, std::atoi(v.c_str()));
+  size_t s = 0;
+  while (s < v.size()) {
+    size_t e = v.find(',', s);
+    if (e == std::string::npos) e = v.size();
+    const std::string tok = v.substr(s, e - s);
+    if (!tok.empty()) {
+      if (tok.find_first_not_of("0123456789") != std::string::npos) return 0;
+      devices.push_back(std::atoi(tok.c_str()));
+    }
+    s = e + 1;
+  }
+  return int(devices.size());
+}
+
 int cmd_pull(const std::string& exe, const std::vector<std::string>& a) {
+  std::string gpus_arg;
   for (size_t i = 0; i + 1 < a.size(); ++i)
-    if (a[i] == "--gpus" && std::atoi(a[i + 1].c_str()) > 0) return pull_on_gpus(exe, a, std::atoi(a[i + 1].c_str()));
+    if (a[i] == "--gpus") gpus_arg = a[i + 1];
+  if (gpus_arg.empty())
+    if (const char* g = std::getenv("ZEST_GPUS")) gpus_arg = g;
+  if (!gpus_arg.empty()) {
+    std::vector<int> devices;
+    const int n = parse_gpus(gpus_arg, devices);
+    if (n > 0) return pull_on_gpus(exe, a, n, devices);
+  }
   if (a.empty() || a[0].rfind("-", 0) == 0) {
     std::cerr << "Error: missing repository ID\n"
               << "Usage: zest pull <repo_id> [--revision <ref>] [--tracker <url>] [--no-p2p]\n";

@@ -3,7 +3,7 @@
 ZEST_STUB_MODE=lose-last: in a multi-rank attempt the highest rank dies like a lost GPU (rank 0
 waits, so torchrun stops it before it can report completion); a single-rank attempt succeeds.
 ZEST_STUB_MODE=always-crash: every attempt dies, so the CLI falls back to the host pull.
-Each attempt appends its world size to ZEST_STUB_LOG.
+Each attempt appends its world size (and HIP_VISIBLE_DEVICES, when the CLI set one) to ZEST_STUB_LOG.
 """
 import json
 import os
@@ -15,7 +15,8 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if rank == 0:
         with open(os.environ["ZEST_STUB_LOG"], "a") as fh:
-            fh.write(f"{world}\n")
+            vis = os.environ.get("HIP_VISIBLE_DEVICES")
+            fh.write(f"{world}" + (f"@{vis}" if vis else "") + "\n")
     mode = os.environ.get("ZEST_STUB_MODE", "lose-last")
     if mode == "always-crash" or (world > 1 and rank == world - 1):
         os._exit(17)

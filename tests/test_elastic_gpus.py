@@ -46,3 +46,20 @@ def test_gpu_pull_falls_back_to_host(tmp_path):
         assert r.returncode != 0 and "finishing the pull on the host" not in r.stderr
     finally:
         hub.stop()
+
+
+def test_gpu_pull_device_list_and_env_default(tmp_path):
+    """`--gpus 4,6,7` pins the workers to those devices (HIP_VISIBLE_DEVICES), retries drop the
+    last listed device; ZEST_GPUS supplies --gpus when the flag is absent."""
+    hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        n = Node(hub, tmp_path, "a")
+        n.run("pull", "org/elastic", "--gpus", "4,6,7", env=_env(tmp_path, "lose-last"), timeout=300)
+        log = tmp_path / "attempts.log"
+        assert log.read_text().split() == ["3@4,6,7", "2@4,6", "1@4"]
+        log.unlink()
+        n.run("pull", "org/elastic", env=dict(_env(tmp_path, "lose-last"), ZEST_GPUS="2"), timeout=300)
+        assert log.read_text().split() == ["2", "1"]
+    finally:
+        hub.stop()

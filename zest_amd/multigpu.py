@@ -31,11 +31,18 @@ def main(argv=None) -> int:
     ap.add_argument("--no-dht", action="store_true")
     ap.add_argument("--dht-bootstrap", action="append", default=[])
     ap.add_argument("--repo-type", default="model")
-    a = ap.parse_args(argv)
+    ap.add_argument("--include", action="append", default=[], help="only files ending in this suffix")
+    ap.add_argument("--concurrency", "-j", type=int, default=16, help="fetch threads per GPU worker")
+    ap.add_argument("--pipeline-depth", type=int, default=1024,
+                    help="pinned staging ring per GPU worker, MB (network -> staging -> HBM)")
+    # the reference ignores unknown flags (main.zig:98-119); so do the GPU workers
+    a, _unknown = ap.parse_known_args(argv)
     rank, world, local, dev = init_from_env()
     t0 = time.time()
     commit, files = _core.list_repo_files(a.repo, a.revision, a.repo_type)
     commit = commit or a.revision
+    if a.include:
+        files = [f for f in files if any(f["path"].endswith(s) for s in a.include)]
     cfg = json.loads(_core.config_json())
     snap = os.path.join(cfg["hf_cache_dir"], _core.repo_folder_name(a.repo, a.repo_type), "snapshots", commit)
     xet = [f for f in files if f["xet_hash"]]
@@ -50,7 +57,7 @@ def main(argv=None) -> int:
     failed = 0
     if mine:
         dp = ops.hip().DeviceXetPull(a.repo, a.revision, a.repo_type, p2p, a.peer, a.tracker, not a.no_dht,
-                                     a.dht_bootstrap, dev.index or 0, 1 << 30, 16)
+                                     a.dht_bootstrap, dev.index or 0, max(16, a.pipeline_depth) << 20, max(1, a.concurrency))
         todo = []
         for f in mine:
             dst = os.path.join(snap, f["path"])
