@@ -90,6 +90,8 @@ void print_usage(std::ostream& w) {
        "  --listen, -l <addr>      Listen address (default: 0.0.0.0:6881)\n"
        "  --reannounce <sec>       Re-announce interval (default: 900)\n"
        "  --announce-only          Announce and exit (reference behaviour)\n"
+       "  --hbm-cache-gb <G>       Upload up to G GB of the xorb cache to GPU memory and seed from it\n"
+       "  --device <n>             GPU for --hbm-cache-gb (default: 0)\n"
        "\n"
        "Serve options:\n"
        "  --http-port <port>       HTTP API port (default: 9847)\n"
@@ -301,8 +303,40 @@ int cmd_pull(const std::string& exe, const std::vector<std::string>& a) {
   }
 }
 
-int cmd_seed(const std::vector<std::string>& a) {
+// `zest seed --hbm-cache-gb G [--device N]`: seed from GPU memory — the disk xorb cache is uploaded
+// to HBM and served by the HBM seeder (`python -m zest_amd.seed`, csrc/bind/hip_seed.cpp), run as a
+// child process of this CLI.
+int seed_from_hbm(const std::string& exe, const Config& cfg, const std::string& gb, const std::string& device) {
+  std::string pkg_parent = exe;
+  for (int i = 0; i < 3; ++i) {
+    const size_t s = pkg_parent.rfind('/');
+    pkg_parent = s == std::string::npos ? "." : pkg_parent.substr(0, s);
+  }
+  std::string pp = pkg_parent;
+  if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
+  ::setenv("PYTHONPATH", pp.c_str(), 1);
+  const char* py = std::getenv("ZEST_PYTHON");
+  const char* mod = std::getenv("ZEST_SEED_MODULE");  // tests substitute a stub
+  std::vector<std::string> args = {py ? py : "python3", "-m", mod && *mod ? mod : "zest_amd.seed",
+                                   "--port", std::to_string(cfg.listen_port), "--device", "cuda:" + device,
+                                   "--max-gb", gb};
+  std::vector<char*> argv;
+  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
+  argv.push_back(nullptr);
+  pid_t pid = 0;
+  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
+    std::cerr << "Error: cannot start " << argv[0] << " for --hbm-cache-gb\n";
+    return 127;
+  }
+  int status = 0;
+  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  }
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+}
+
+int cmd_seed(const std::string& exe, const std::vector<std::string>& a) {
   Config cfg = Config::from_env();
+  std::string hbm_gb, hbm_dev = "0";
   std::optional<std::string> tracker;
   std::vector<net::Addr> boot;
   int reannounce = 900;
@@ -320,7 +354,10 @@ int cmd_seed(const std::vector<std::string>& a) {
       }
     } else if (f == "--reannounce") reannounce = std::max(5, std::atoi(next().c_str()));
     else if (f == "--announce-only") announce_only = true;
+    else if (f == "--hbm-cache-gb") hbm_gb = next();
+    else if (f == "--device") hbm_dev = next();
   }
+  if (!hbm_gb.empty()) return seed_from_hbm(exe, cfg, hbm_gb, hbm_dev);
   std::cout << "Scanning local xorb cache...\n";
   auto hashes = cached_xorb_hashes(cfg);
   std::cout << "Found " << hashes.size() << " cached xorbs\n";
@@ -531,7 +568,7 @@ int main(int argc, char** argv) {
   std::vector<std::string> rest(argv + 2, argv + argc);
   try {
     if (cmd == "pull") return cmd_pull(exe, rest);
-    if (cmd == "seed") return cmd_seed(rest);
+    if (cmd == "seed") return cmd_seed(exe, rest);
     if (cmd == "bench") return cmd_bench(rest);
     if (cmd == "serve") return cmd_serve(rest);
     if (cmd == "start") return cmd_start(exe);

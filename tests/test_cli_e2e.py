@@ -357,3 +357,16 @@ def test_cached_file_is_verified(hub, nodes):
     out = a.run("pull", REPO_ID, "--no-p2p").stdout
     assert f"{big} (cached)" in out
     assert any(marker_root.rglob("*"))
+
+
+def test_seed_hbm_cache_option(nodes, tmp_path):
+    """`zest seed --hbm-cache-gb G --device N` hands seeding to the HBM seeder process
+    (`python -m zest_amd.seed`, stubbed here; the real one is covered by tests/test_gpu_seed.py)."""
+    import sys
+    n = nodes("a")
+    log = tmp_path / "seed_argv.json"
+    n.run("seed", "--hbm-cache-gb", "12.5", "--device", "3", "--listen", "7001",
+          env={"ZEST_SEED_MODULE": "tests.seed_stub_module", "ZEST_PYTHON": sys.executable, "ZEST_STUB_LOG": str(log),
+               "PYTHONPATH": str(ROOT)})
+    assert json.loads(log.read_text()) == ["--port", "7001", "--device", "cuda:3", "--max-gb", "12.5"]
+    assert "--hbm-cache-gb" in n.run("help").stdout

@@ -150,7 +150,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="seed the local xorb cache from GPU memory")
     ap.add_argument("--port", type=int, default=6881)
     ap.add_argument("--device", default="cuda:0")
-    ap.add_argument("--max-gb", type=float, default=None)
+    ap.add_argument("--max-gb", "--hbm-cache-gb", dest="max_gb", type=float, default=None)
     a = ap.parse_args(argv)
     arena = HbmCacheArena(a.device, None if a.max_gb is None else int(a.max_gb * 1e9))
     srv = HbmCacheSeedServer(arena, a.port)
