@@ -13,42 +13,74 @@ namespace {
 
 __constant__ uint64_t kGearDev[256] = ZEST_GEAR_TABLE_INIT;
 
-constexpr uint32_t kSeg = 256;
+// CDC: one lane per 1 KiB segment (warm-up overhead 64/1024), read with 16-byte loads from a
+// 16-byte-aligned view of the buffer (the old lane-per-256-B dword reader made every load touch 64
+// cache lines for 4 useful bytes each and thrashed L1, 274 GB/s).  The candidate test is folded
+// into a per-16-byte "any hit" flag; a hit (rare: 1 in 2^16 positions for the Xet mask) re-scans
+// those 16 bytes on a slow path that emits the offsets.
+constexpr uint32_t kSeg = 1024;
 
-struct ByteReader {
-  const uint8_t* base;
-  uint64_t cached_addr = ~0ull;
-  uint32_t w = 0;
-  __device__ __forceinline__ uint32_t get(uint64_t i) {
-    const uint64_t a = reinterpret_cast<uintptr_t>(base) + i;
-    const uint64_t aw = a & ~3ull;
-    if (aw != cached_addr) {
-      w = *reinterpret_cast<const uint32_t*>(aw);
-      cached_addr = aw;
-    }
-    return (w >> (8 * (a & 3))) & 0xFF;
-  }
-};
+template <bool kHiOnly>
+__device__ __forceinline__ bool gear_zero(uint64_t h, uint64_t mask) {
+  if (kHiOnly) return (uint32_t(h >> 32) & uint32_t(mask >> 32)) == 0;
+  return (h & mask) == 0;
+}
 
+template <bool kHiOnly>
 __global__ void __launch_bounds__(256) k_cdc_candidates(const uint8_t* __restrict__ data, uint64_t n, uint64_t mask,
                                                         uint64_t* __restrict__ out, unsigned long long* count,
                                                         uint64_t cap) {
   __shared__ uint64_t gear[256];
   gear[threadIdx.x] = kGearDev[threadIdx.x];
   __syncthreads();
-  const uint64_t seg = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t start = seg * kSeg;
-  if (start >= n) return;
-  const uint64_t end = start + kSeg < n ? start + kSeg : n;
-  ByteReader rd{data};
+  const uint64_t a0 = reinterpret_cast<uintptr_t>(data);
+  const uint32_t shift = uint32_t(a0 & 15);
+  const uint4* base = reinterpret_cast<const uint4*>(a0 - shift);  // virtual position v = index + shift
+  const uint64_t vend = n + shift;
+  const uint64_t vs = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) * kSeg;
+  if (vs >= vend) return;
+  const uint64_t ve = vs + kSeg < vend ? vs + kSeg : vend;
   uint64_t h = 0;
-  const uint64_t warm = start >= 63 ? start - 63 : 0;
-  for (uint64_t i = warm; i < start; ++i) h = (h << 1) + gear[rd.get(i)];
-  for (uint64_t i = start; i < end; ++i) {
-    h = (h << 1) + gear[rd.get(i)];
-    if ((h & mask) == 0) {
-      const unsigned long long k = atomicAdd(count, 1ull);
-      if (k < cap) out[k] = i + 1;
+  // 64 bytes per step: four 16-byte loads issued together cover half a 128-byte line, so the line
+  // is used while it is still in L1 (lanes are 1 KiB apart).  The first step is the warm-up over
+  // the 64 bytes before the segment (h depends on the last 64 bytes only).
+  for (uint64_t q = vs >= 64 ? vs - 64 : vs; q < ve; q += 64) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 x = q + 16 * k < vend ? base[(q >> 4) + k] : make_uint4(0, 0, 0, 0);
+      w[4 * k] = x.x;
+      w[4 * k + 1] = x.y;
+      w[4 * k + 2] = x.z;
+      w[4 * k + 3] = x.w;
+    }
+    const bool warm = q < vs;
+    const uint64_t h0 = h;
+    bool any = false;
+    if (q >= shift && q + 64 <= vend) {
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        h = (h << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        any |= gear_zero<kHiOnly>(h, mask);
+      }
+    } else {
+      for (int j = 0; j < 64; ++j) {
+        if (q + j < shift || q + j >= vend) continue;
+        h = (h << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        any |= gear_zero<kHiOnly>(h, mask);
+      }
+    }
+    if (any && !warm) {  // rare: replay the 64 bytes and emit END offsets (index + 1)
+      uint64_t g = h0;
+      for (int j = 0; j < 64; ++j) {
+        const uint64_t v = q + j;
+        if (v < shift || v >= vend) continue;
+        g = (g << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        if (gear_zero<kHiOnly>(g, mask)) {
+          const unsigned long long k = atomicAdd(count, 1ull);
+          if (k < cap) out[k] = v - shift + 1;
+        }
+      }
     }
   }
 }
@@ -164,9 +196,13 @@ extern "C" {
 hipError_t zg_cdc_candidates(const uint8_t* data, uint64_t n, uint64_t mask, uint64_t* out,
                              unsigned long long* count, uint64_t capacity, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const uint64_t segs = (n + kSeg - 1) / kSeg;
-  hipLaunchKernelGGL(k_cdc_candidates, dim3(uint32_t((segs + 255) / 256)), dim3(256), 0, stream, data, n, mask, out,
-                     count, capacity);
+  const uint64_t segs = (n + 15 + kSeg - 1) / kSeg;
+  if ((mask & 0xFFFFFFFFull) == 0)
+    hipLaunchKernelGGL(k_cdc_candidates<true>, dim3(uint32_t((segs + 255) / 256)), dim3(256), 0, stream, data, n, mask,
+                       out, count, capacity);
+  else
+    hipLaunchKernelGGL(k_cdc_candidates<false>, dim3(uint32_t((segs + 255) / 256)), dim3(256), 0, stream, data, n,
+                       mask, out, count, capacity);
   return hipGetLastError();
 }
 

@@ -217,6 +217,20 @@ def test_cdc_candidates_match_cpu_chunker():
     assert list(map(int, ends)) == C.chunk_ends(data)
 
 
+def test_cdc_candidates_misaligned_and_low_mask():
+    """Candidate offsets at every buffer alignment and across segment edges, for the Xet mask (high
+    word only) and a mask with low-word bits (the generic path), against the CPU oracle."""
+    rng = random.Random(12)
+    data = rng.randbytes(300_000)
+    for off in (1, 3, 8, 15):
+        t = ops.padded_empty(len(data) + off, DEV)
+        t[off:].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        for mask in (ops.XET_MASK, 0xF0000000000000F0):
+            got = ops.cdc_candidates(t[off:], mask=mask)
+            want = ops.cdc_candidates(t[off:].cpu(), mask=mask)
+            assert got.tolist() == want.tolist(), (off, hex(mask))
+
+
 def test_pack_chunks_matches_builder():
     rng = random.Random(4)
     data = rng.randbytes(900_000)
