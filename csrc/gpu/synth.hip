@@ -13,12 +13,13 @@ namespace {
 
 __constant__ uint64_t kGearDev[256] = ZEST_GEAR_TABLE_INIT;
 
-// CDC: one lane per 1 KiB segment (warm-up overhead 64/1024), read with 16-byte loads from a
+// CDC: one lane per 2 KiB segment (warm-up overhead 128/2048), read with 16-byte loads from a
 // 16-byte-aligned view of the buffer (the old lane-per-256-B dword reader made every load touch 64
 // cache lines for 4 useful bytes each and thrashed L1, 274 GB/s).  The candidate test is folded
-// into a per-16-byte "any hit" flag; a hit (rare: 1 in 2^16 positions for the Xet mask) re-scans
-// those 16 bytes on a slow path that emits the offsets.
-constexpr uint32_t kSeg = 1024;
+// into a per-step "any hit" flag; a hit (rare: 1 in 2^16 positions for the Xet mask) re-scans
+// the step's bytes on a slow path that emits the offsets.
+constexpr uint32_t kSeg = 2048;
+constexpr uint32_t kStep = 128;  // bytes per lane per step: one full 128-byte line
 
 template <bool kHiOnly>
 __device__ __forceinline__ bool gear_zero(uint64_t h, uint64_t mask) {
@@ -41,13 +42,13 @@ __global__ void __launch_bounds__(256) k_cdc_candidates(const uint8_t* __restric
   if (vs >= vend) return;
   const uint64_t ve = vs + kSeg < vend ? vs + kSeg : vend;
   uint64_t h = 0;
-  // 64 bytes per step: four 16-byte loads issued together cover half a 128-byte line, so the line
-  // is used while it is still in L1 (lanes are 1 KiB apart).  The first step is the warm-up over
-  // the 64 bytes before the segment (h depends on the last 64 bytes only).
-  for (uint64_t q = vs >= 64 ? vs - 64 : vs; q < ve; q += 64) {
-    uint32_t w[16];
+  // 128 bytes per step: eight 16-byte loads issued together cover one whole line, so each line is
+  // fetched once even though lanes are 2 KiB apart (L1 cannot hold a line per lane across steps).
+  // The first step is the warm-up over the bytes before the segment (h depends on the last 64).
+  for (uint64_t q = vs >= kStep ? vs - kStep : vs; q < ve; q += kStep) {
+    uint32_t w[kStep / 4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < int(kStep / 16); ++k) {
       const uint4 x = q + 16 * k < vend ? base[(q >> 4) + k] : make_uint4(0, 0, 0, 0);
       w[4 * k] = x.x;
       w[4 * k + 1] = x.y;
@@ -57,22 +58,22 @@ __global__ void __launch_bounds__(256) k_cdc_candidates(const uint8_t* __restric
     const bool warm = q < vs;
     const uint64_t h0 = h;
     bool any = false;
-    if (q >= shift && q + 64 <= vend) {
+    if (q >= shift && q + kStep <= vend) {
 #pragma unroll
-      for (int j = 0; j < 64; ++j) {
+      for (int j = 0; j < int(kStep); ++j) {
         h = (h << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
         any |= gear_zero<kHiOnly>(h, mask);
       }
     } else {
-      for (int j = 0; j < 64; ++j) {
+      for (int j = 0; j < int(kStep); ++j) {
         if (q + j < shift || q + j >= vend) continue;
         h = (h << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
         any |= gear_zero<kHiOnly>(h, mask);
       }
     }
-    if (any && !warm) {  // rare: replay the 64 bytes and emit END offsets (index + 1)
+    if (any && !warm) {  // rare: replay the step's bytes and emit END offsets (index + 1)
       uint64_t g = h0;
-      for (int j = 0; j < 64; ++j) {
+      for (int j = 0; j < int(kStep); ++j) {
         const uint64_t v = q + j;
         if (v < shift || v >= vend) continue;
         g = (g << 1) + gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
