@@ -37,8 +37,8 @@ BASELINE_METRIC = "aggregate pull GB/s + P2P ratio, Llama-3.1-70B at 1/2/4/8 MI3
 
 
 def log(rank, *a):
-    if rank == 0:
-        print("[bench]", *a, file=sys.stderr, flush=True)
+    if rank == 0 or os.environ.get("ZEST_BENCH_LOG_ALL") == "1":
+        print(f"[bench{'' if rank == 0 else f' r{rank}'}]", *a, file=sys.stderr, flush=True)
 
 
 def main() -> None:
@@ -68,14 +68,24 @@ def main() -> None:
     if world_size != a.gpus:
         if world_size == 1 and a.gpus > 1:
             raise SystemExit("for --gpus > 1 launch with torchrun --nproc-per-node N (one rank per GPU)")
-    device = torch.device("cuda", local_rank)
+    # ZEST_BENCH_BACKEND=gloo is a rehearsal mode for one-GPU boxes: several ranks share the device,
+    # control traffic goes over gloo, and only the peer-mapped exchanges (ipc / xgmi) can move the
+    # data.  Its numbers are not xGMI measurements; the JSON line says so in config.backend.
+    backend = os.environ.get("ZEST_BENCH_BACKEND", "nccl")
+    if os.environ.get("ZEST_BENCH_WATCHDOG"):  # diagnostics: dump every thread's stack and exit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["ZEST_BENCH_WATCHDOG"]), exit=True)
+    device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank)
     torch.cuda.set_device(device)
     from zest_amd.parallel import bind_local_numa
     numa_cpus = bind_local_numa(device)
     dist = None
     if world_size > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     t_setup = time.time()
     ops.hip()
     spec = models.get(a.model)
@@ -112,7 +122,11 @@ def main() -> None:
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
     if world_size > 1:
-        ipc = a.exchange in ("auto", "ipc", "xgmi") and puller.enable_ipc()
+        # The peer-mapped exchanges are opt-in under auto (ZEST_EXCHANGE_IPC=1): importing a peer's
+        # 16 GB arena handle hung inside hipIpcOpenMemHandle in a 2-rank rehearsal on one GPU
+        # (tools/gpu_bench_rehearsal.sh), and a hang here would cost the whole scaling run.
+        want_ipc = a.exchange in ("ipc", "xgmi") or (a.exchange == "auto" and os.environ.get("ZEST_EXCHANGE_IPC") == "1")
+        ipc = want_ipc and puller.enable_ipc()
         log(rank, f"peer arenas mapped over HIP IPC: {ipc}")
         if a.exchange in ("ipc", "xgmi") and not ipc:
             raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
@@ -192,7 +206,8 @@ def main() -> None:
                    "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": puller.exchange if world_size > 1 else "none",
                    "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
                    "verify": "blake3 of every chunk on every rank + merkle file hashes",
-                   "numa_bound_cpus": len(numa_cpus)},
+                   "numa_bound_cpus": len(numa_cpus),
+                   "backend": backend if world_size > 1 else "none"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

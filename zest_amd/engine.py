@@ -395,25 +395,31 @@ class DevicePuller:
             mine = None
         objs = [None] * self.n_ranks
         dist.all_gather_object(objs, mine, group=self.group)
+        # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
+        self._host_group = dist.new_group(backend="gloo")
         peers = [None] * self.n_ranks
         ok = 1
-        try:
-            H = ops.hip()
-            for p, o in enumerate(objs):
-                if p != self.rank:
-                    fn, args = o
-                    peers[p] = fn(*args)
-                    if peers[p].device != self.device and not H.enable_peer_access(peers[p].device.index):
-                        ok = 0
-        except Exception:
-            ok = 0
+        # One rank imports at a time: two processes opening each other's large dmabuf handles at
+        # the same moment deadlock inside hipIpcOpenMemHandle (seen with 16 GB arenas, 2 ranks on
+        # one MI355X: both stuck in the open); an exporter that is idle in a barrier answers at once.
+        for turn in range(self.n_ranks):
+            if turn == self.rank:
+                try:
+                    H = ops.hip()
+                    for p, o in enumerate(objs):
+                        if p != self.rank:
+                            fn, args = o
+                            peers[p] = fn(*args)
+                            if peers[p].device != self.device and not H.enable_peer_access(peers[p].device.index):
+                                ok = 0
+                except Exception:
+                    ok = 0
+            dist.barrier(group=self._host_group)
         flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         if not int(flag.item()):
             return False
         self._peer_arenas = peers
-        # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
-        self._host_group = dist.new_group(backend="gloo")
         self._ipc_streams = [torch.cuda.Stream(self.device) for _ in range(min(self.n_ranks - 1, 4))]
         self._ipc_done = {}
         return True
