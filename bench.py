@@ -117,19 +117,22 @@ def main() -> None:
     seeders = a.seeders if a.seeders > 0 else world_size
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
                           seeders=seeders)
-    puller.build_origin()
-    torch.cuda.synchronize()
-    log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
-              f"setup {time.time() - t_setup:.1f}s")
     if world_size > 1:
-        # The peer-mapped exchanges are opt-in under auto (ZEST_EXCHANGE_IPC=1): importing a peer's
-        # 16 GB arena handle hung inside hipIpcOpenMemHandle in a 2-rank rehearsal on one GPU
-        # (tools/gpu_bench_rehearsal.sh), and a hang here would cost the whole scaling run.
+        # The peer-mapped exchanges are opt-in under auto (ZEST_EXCHANGE_IPC=1): in a 2-rank bench
+        # rehearsal on one GPU (tools/gpu_bench_rehearsal.sh) importing a peer's 16 GB arena handle
+        # hung inside hipIpcOpenMemHandle, before or after the origin build, while a standalone
+        # probe with the same sizes, pinned memory and NUMA binding imports in 1 ms
+        # (tools/gpu_ipc_probe2.sh); cause not found yet, and a hang would cost the scaling run.
         want_ipc = a.exchange in ("ipc", "xgmi") or (a.exchange == "auto" and os.environ.get("ZEST_EXCHANGE_IPC") == "1")
         ipc = want_ipc and puller.enable_ipc()
         log(rank, f"peer arenas mapped over HIP IPC: {ipc}")
         if a.exchange in ("ipc", "xgmi") and not ipc:
             raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
+    puller.build_origin()
+    torch.cuda.synchronize()
+    log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
+              f"setup {time.time() - t_setup:.1f}s")
+    if world_size > 1:
         if a.exchange == "auto":
             t_x = puller.autotune_exchange()
             log(rank, "exchange autotune (s over the first rounds): "
