@@ -61,5 +61,8 @@ def test_gpu_pull_device_list_and_env_default(tmp_path):
         log.unlink()
         n.run("pull", "org/elastic", env=dict(_env(tmp_path, "lose-last"), ZEST_GPUS="2"), timeout=300)
         assert log.read_text().split() == ["2", "1"]
+        log.unlink()
+        n.run("pull", "org/elastic", "--gpus", "5,", env=_env(tmp_path, "lose-last"), timeout=300)
+        assert log.read_text().split() == ["1@5"]  # a one-device list
     finally:
         hub.stop()
