@@ -598,6 +598,12 @@ void bind_extra(py::module_& m) {
     storage::write_verified_marker(cfg, repo, commit, path, xet_hex, file);
   }, py::arg("repo"), py::arg("commit"), py::arg("path"), py::arg("xet_hash"), py::arg("file"),
      "Record that `file` (snapshot path) was verified against its Xet hash");
+  m.def("check_verified_marker", [](std::string repo, std::string commit, std::string path, std::string xet_hex,
+                                    std::string file) {
+    Config cfg = Config::from_env();
+    return storage::check_verified_marker(cfg, repo, commit, path, xet_hex, file);
+  }, py::arg("repo"), py::arg("commit"), py::arg("path"), py::arg("xet_hash"), py::arg("file"),
+     "True when `file` carries a verified marker matching its Xet hash, size and mtime");
   m.def("xet_hash_of_file", [](std::string file, int threads) {
     py::gil_scoped_release nogil;
     return storage::xet_hash_of_file(file, threads);

@@ -93,11 +93,13 @@ PYBIND11_MODULE(_hip, m) {
           "zg_index_terms");
   });
   m.def("place_chunks", [](uintptr_t src, uint64_t src_n, uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n,
-                           uint64_t lo, uint64_t hi, uintptr_t err, uintptr_t st) {
+                           uint64_t lo, uint64_t hi, uintptr_t err, uintptr_t st, uintptr_t clip_scratch) {
     check(zg_place_chunks(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, lo, hi,
-                          P<unsigned long long>(err), S(st)),
+                          P<uint8_t>(clip_scratch), P<unsigned long long>(err), S(st)),
           "zg_place_chunks");
-  });
+  }, py::arg("src"), py::arg("src_n"), py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"),
+     py::arg("lo"), py::arg("hi"), py::arg("err"), py::arg("stream"), py::arg("clip_scratch") = 0);
+  m.attr("CLIP_SCRATCH_BYTES") = ZG_CLIP_SCRATCH_BYTES;
   m.def("hash_chunks", [](uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n, uintptr_t hashes, uintptr_t sizes,
                           uint32_t base, uintptr_t st) {
     check(zg_hash_chunks(P<const uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, P<uint8_t>(hashes),

@@ -12,6 +12,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -107,6 +108,11 @@ class DeviceXetPull {
   // cross file boundaries, so there is no per-file drain; every file's Merkle hash is checked in a
   // single kernel launch at the end.  Term destinations are device addresses relative to the
   // lowest destination pointer.
+  //
+  // Peer runs are quarantined in the disk cache until their file verified; a file that fails
+  // (Merkle mismatch, or any device decode error) has its peer runs dropped and its cache runs
+  // evicted, then is pulled once more straight from the CDN with the refetched runs replacing the
+  // cached ones — so one corrupt copy costs one refetch, not a permanently failing pull.
   py::list pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
     const auto t0 = std::chrono::steady_clock::now();
     const size_t nf = files.size();
@@ -130,6 +136,95 @@ class DeviceXetPull {
       for (size_t f = 0; f < nf; ++f)
         if (!errs[f].empty()) throw Error("DownloadFailed", std::get<0>(files[f]) + ": " + errs[f]);
     }
+    std::vector<size_t> todo(nf);
+    for (size_t f = 0; f < nf; ++f) todo[f] = f;
+    std::vector<std::string> got(nf);
+    uint64_t fetched = 0;
+    for (int attempt = 0; attempt < 2 && !todo.empty(); ++attempt) {
+      FetchOptions opt;
+      opt.repair = attempt > 0;
+      Attempt at = run_once(files, recs, todo, opt);
+      fetched += at.fetched;
+      if (!at.fetch_err.empty()) {
+        settle_all(at, recs, todo, [](size_t) { return false; });
+        throw Error("DownloadFailed", at.fetch_err);
+      }
+      std::vector<size_t> bad;
+      for (size_t j = 0; j < todo.size(); ++j) {
+        got[todo[j]] = at.roots[j];
+        if (at.ingest_err || at.roots[j] != std::get<0>(files[todo[j]])) bad.push_back(j);
+      }
+      settle_all(at, recs, todo, [&](size_t j) { return std::find(bad.begin(), bad.end(), j) == bad.end(); });
+      if (bad.empty()) {
+        todo.clear();
+        break;
+      }
+      if (attempt == 0) bridge_->stats().verify_failures += bad.size();
+      else if (at.ingest_err)
+        throw Error("IngestError", "code " + std::to_string(at.ingest_err >> 32) + " at " +
+                                       std::to_string(at.ingest_err & 0xFFFFFFFFu));
+      std::vector<size_t> again;
+      for (size_t j : bad) again.push_back(todo[j]);
+      if (attempt == 0) bridge_->stats().refetches += again.size();
+      todo = std::move(again);
+    }
+    for (size_t f : todo)
+      throw Error("HashMismatch", "device bytes hash " + got[f] + " != " + std::get<0>(files[f]));
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    py::list out;
+    for (size_t f = 0; f < nf; ++f) {
+      uint64_t nck = 0;
+      for (auto& t : recs[f].terms) nck += t.range.end - t.range.start;
+      py::dict d;
+      d["bytes"] = std::get<2>(files[f]);
+      d["terms"] = recs[f].terms.size();
+      d["chunks"] = nck;
+      d["seconds"] = secs;
+      d["fetched_bytes"] = fetched;  // for the whole call
+      out.append(d);
+    }
+    return out;
+  }
+
+  std::string stats_json() const { return bridge_->stats_json(); }
+
+  size_t staging_bytes() const { return cap_; }
+
+ private:
+  struct TermSource {
+    Source src = Source::Cdn;
+    uint32_t run_offset = 0;
+    bool pending = false;
+  };
+  struct Attempt {
+    std::vector<std::string> roots;  // per file of the attempt: Merkle root (Xet hex)
+    std::vector<std::vector<TermSource>> sources;  // per file, per term
+    unsigned long long ingest_err = 0;
+    std::string fetch_err;
+    uint64_t fetched = 0;
+  };
+
+  // Publish (ok) or drop/evict (!ok) the cache runs behind every term of the attempt's files.
+  template <typename OkFn>
+  void settle_all(const Attempt& at, const std::vector<cas::Reconstruction>& recs, const std::vector<size_t>& todo,
+                  OkFn ok) {
+    for (size_t j = 0; j < todo.size(); ++j) {
+      const auto& rec = recs[todo[j]];
+      const bool good = ok(j);
+      for (size_t i = 0; i < at.sources[j].size() && i < rec.terms.size(); ++i) {
+        const TermSource& ts = at.sources[j][i];
+        bridge_->settle(rec.terms[i].hash_hex, ts.src, ts.run_offset, ts.pending, good);
+      }
+    }
+  }
+
+  // One pass over files[todo]: fetch -> staging -> H2D -> index/place/hash -> Merkle roots.
+  Attempt run_once(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& all_files,
+                   const std::vector<cas::Reconstruction>& all_recs, const std::vector<size_t>& todo,
+                   const FetchOptions& opt) {
+    const size_t nf = todo.size();
+    Attempt at;
+    at.sources.resize(nf);
     // Global term list in file order; chunk indices are global (one hash array for all files).
     struct GTerm {
       size_t file, term;
@@ -142,22 +237,24 @@ class DeviceXetPull {
     std::vector<uint64_t> file_chunk0(nf + 1, 0);
     uintptr_t base = UINTPTR_MAX, top_addr = 0;
     for (size_t f = 0; f < nf; ++f) {
-      base = std::min(base, std::get<1>(files[f]));
-      top_addr = std::max<uintptr_t>(top_addr, std::get<1>(files[f]) + std::get<2>(files[f]));
+      const auto& fl = all_files[todo[f]];
+      base = std::min(base, std::get<1>(fl));
+      top_addr = std::max<uintptr_t>(top_addr, std::get<1>(fl) + std::get<2>(fl));
     }
     for (size_t f = 0; f < nf; ++f) {
-      const auto& rec = recs[f];
+      const auto& fl = all_files[todo[f]];
+      const auto& rec = all_recs[todo[f]];
       if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
+      at.sources[f].resize(rec.terms.size());
       uint64_t off = 0, c = file_chunk0[f];
       for (size_t i = 0; i < rec.terms.size(); ++i) {
         const auto& t = rec.terms[i];
         const uint32_t n = uint32_t(t.range.end - t.range.start);
-        gt.push_back({f, i, std::get<1>(files[f]) - base + off, c, n, t.unpacked_length});
+        gt.push_back({f, i, std::get<1>(fl) - base + off, c, n, t.unpacked_length});
         off += t.unpacked_length;
         c += n;
       }
-      if (off != std::get<2>(files[f]))
-        throw Error("SizeMismatch", std::get<0>(files[f]) + " is " + std::to_string(off) + " bytes");
+      if (off != std::get<2>(fl)) throw Error("SizeMismatch", std::get<0>(fl) + " is " + std::to_string(off) + " bytes");
       file_chunk0[f + 1] = c;
     }
     const uint64_t nck = file_chunk0[nf];
@@ -167,8 +264,7 @@ class DeviceXetPull {
     uint8_t* dst = reinterpret_cast<uint8_t*>(base);
     const uint64_t dst_size = nf ? uint64_t(top_addr - base) : 0;
     hip_check(hipMemsetAsync(err_.p, 0, sizeof(unsigned long long), stream_), "hipMemset");
-    uint64_t fetched = 0;
-    std::string fetch_err;
+    std::string& fetch_err = at.fetch_err;
     {
       py::gil_scoped_release nogil;
       size_t next = 0;
@@ -207,13 +303,14 @@ class DeviceXetPull {
             const size_t i = k.fetch_add(1);
             if (i >= end) return;
             try {
-              const auto& rec = recs[gt[i].file];
+              const auto& rec = all_recs[todo[gt[i].file]];
               // The run is received straight into this term's region of the pinned buffer when it
               // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
               uint8_t* region = s.host + off[i - next];
               const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
               auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-              XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, true, true, sink);
+              XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
+              at.sources[gt[i].file][gt[i].term] = TermSource{r.source, r.run_offset, r.pending};
               auto idx = xet::index_chunks(r.bytes(), r.size());
               if (r.local_end > idx.size() || r.local_start >= r.local_end)
                 throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
@@ -249,7 +346,7 @@ class DeviceXetPull {
           t.n_chunks = gt[i].nchunks;
           t.ulen = gt[i].ulen;
           s.terms.push_back(t);
-          fetched += t.src_len;
+          at.fetched += t.src_len;
           top = std::max<uint64_t>(top, t.src + t.src_len);
         }
         const int nterms = int(end - next);
@@ -266,7 +363,8 @@ class DeviceXetPull {
                   "H2D terms");
         hip_check(hipMemsetAsync(s.chunks_dev.p, 0, sizeof(ZgChunk) * size_t(nchunks), stream_), "memset");
         hip_check(zg_index_terms(s.dev.p, s.terms_dev.p, nterms, s.chunks_dev.p, err_.p, stream_), "index");
-        hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, err_.p, stream_),
+        hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
+                                  stream_),
                   "place");
         hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
                                  stream_),
@@ -279,11 +377,9 @@ class DeviceXetPull {
       hip_check(hipStreamSynchronize(stream_), "sync");
       for (auto& s : slots_) s.busy = false;
     }
-    if (!fetch_err.empty()) throw Error("DownloadFailed", fetch_err);
-    unsigned long long e = 0;
-    hip_check(hipMemcpy(&e, err_.p, sizeof e, hipMemcpyDeviceToHost), "err D2H");
-    if (e) throw Error("IngestError", "code " + std::to_string(e >> 32) + " at " + std::to_string(e & 0xFFFFFFFFu));
-    // Merkle verify of every file in one launch
+    if (!fetch_err.empty()) return at;
+    hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
+    // Merkle roots of every file in one launch
     trace::Span merkle_span("device", "merkle verify");
     std::vector<ZgMerkleJob> jobs(nf);
     uint64_t max_leaves = 1;
@@ -304,30 +400,14 @@ class DeviceXetPull {
       hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
       hip_check(hipStreamSynchronize(stream_), "sync");
     }
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    py::list out;
     for (size_t f = 0; f < nf; ++f) {
       xet::Hash h;
       std::memcpy(h.data(), roots.data() + 32 * f, 32);
-      const std::string got = xet::to_hex(h);
-      if (got != std::get<0>(files[f]))
-        throw Error("HashMismatch", "device bytes hash " + got + " != " + std::get<0>(files[f]));
-      py::dict d;
-      d["bytes"] = std::get<2>(files[f]);
-      d["terms"] = recs[f].terms.size();
-      d["chunks"] = file_chunk0[f + 1] - file_chunk0[f];
-      d["seconds"] = secs;
-      d["fetched_bytes"] = fetched;  // for the whole call
-      out.append(d);
+      at.roots.push_back(xet::to_hex(h));
     }
-    return out;
+    return at;
   }
 
-  std::string stats_json() const { return bridge_->stats_json(); }
-
-  size_t staging_bytes() const { return cap_; }
-
- private:
   // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does
   // not help, so the payload is <= its unpacked size plus LZ4 frame overhead; + 8-byte headers.
   static uint64_t term_bound(uint64_t unpacked, uint64_t nchunks) {

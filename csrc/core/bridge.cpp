@@ -36,8 +36,8 @@ bool covers(const uint8_t* data, size_t n, uint32_t chunk_offset, uint64_t start
 }
 }  // namespace
 
-XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p,
-                                      bool allow_cache, const bt::PayloadSink& sink) {
+XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstruction& recon,
+                                      const FetchOptions& opt, const bt::PayloadSink& sink) {
   // Copy a run into sink memory when the caller provided room for it; else keep it in `data`.
   auto land = [&](XorbFetchResult& out, const uint8_t* p, size_t n, Bytes* owned) {
     if (uint8_t* d = sink ? sink(n) : nullptr) {
@@ -57,7 +57,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   if (!fi) throw Error("NoMatchingFetchInfo", hex);
   XorbFetchResult out;
   // 1. local xorb cache: any cached run covering the term's chunks
-  if (allow_cache && cache_) {
+  if (opt.allow_cache && !opt.repair && cache_) {
     trace::Span sp("cache", "find");
     if (auto hit = cache_->find(hex, uint32_t(term.range.start), uint32_t(term.range.end))) {
       stats_.xorbs_from_cache++;
@@ -67,19 +67,24 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
       out.local_start = uint32_t(term.range.start - hit->chunk_offset);
       out.local_end = uint32_t(term.range.end - hit->chunk_offset);
       out.source = Source::Cache;
+      out.run_offset = hit->run_offset;
       return out;
     }
   }
   // 2. P2P swarm with the FetchInfo's chunk range
-  if (allow_p2p && swarm_ && swarm_->p2p_enabled()) {
+  if (opt.allow_p2p && !opt.repair && swarm_ && swarm_->p2p_enabled()) {
     if (auto r = swarm_->try_peers(term.hash, uint32_t(fi->range.start), uint32_t(fi->range.end), sink)) {
       if (covers(r->bytes(), r->size(), r->chunk_offset, term.range.start, term.range.end)) {
         stats_.xorbs_from_peer++;
         stats_.bytes_from_peer += r->size();
+        // Nothing has checked these bytes yet: quarantine the run until the caller verified the
+        // file (settle), so a corrupt peer copy is never seeded on or read back as a cache hit.
         if (cache_ && cfg_.cache_writes) {
           try {
-            trace::Span sp("cache", "put_run");
-            cache_->put_run(hex, r->chunk_offset, r->bytes(), r->size());
+            trace::Span sp("cache", "put_pending");
+            cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
+            out.pending = true;
+            out.run_offset = r->chunk_offset;
           } catch (const Error&) {
           }
         }
@@ -114,7 +119,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   }
   if (cache_ && cfg_.cache_writes) {
     try {
-      cache_->put_run(hex, uint32_t(fi->range.start), body.data(), body.size());
+      cache_->put_run(hex, uint32_t(fi->range.start), body.data(), body.size(), opt.repair);
     } catch (const Error&) {
     }
   }
@@ -123,6 +128,23 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   out.local_end = uint32_t(term.range.end - fi->range.start);
   out.source = Source::Cdn;
   return out;
+}
+
+void XetBridge::settle(const std::string& xorb_hex, Source src, uint32_t run_offset, bool pending, bool ok) {
+  if (!cache_) return;
+  try {
+    if (src == Source::Peer && pending) {
+      if (ok) cache_->promote(xorb_hex, run_offset);
+      else cache_->discard_pending(xorb_hex, run_offset);
+    } else if (src == Source::Cache && !ok) {
+      cache_->evict(xorb_hex, run_offset);
+    }
+  } catch (const Error&) {
+  }
+}
+
+void XetBridge::settle(const std::string& xorb_hex, const XorbFetchResult& r, bool ok) {
+  settle(xorb_hex, r.source, r.run_offset, r.pending, ok);
 }
 
 void XetBridge::print_stats(std::ostream& w) const {

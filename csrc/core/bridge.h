@@ -27,13 +27,27 @@ struct FetchStats {
   std::atomic<uint64_t> verify_failures{0}, refetches{0};
 };
 
-enum class Source { Cache, Peer, Cdn };
+// Resumed: restored from a .zest-resume sidecar (bytes written by an earlier, interrupted run).
+enum class Source { Cache, Peer, Cdn, Resumed };
+
+struct FetchOptions {
+  bool allow_p2p = true;
+  bool allow_cache = true;
+  // CDN refetch repairing a copy that failed verification: the CDN run replaces whatever the
+  // cache holds under its name (put_run normally keeps an existing longer run).
+  bool repair = false;
+};
 
 struct XorbFetchResult {
   Bytes data;
   uint32_t local_start = 0, local_end = 0;  // chunk indices inside the fetched run
   Source source = Source::Cdn;
   std::string peer;
+  // Cache bookkeeping for verification: Cache -> the run the hit came from (evicted when the file
+  // fails verification); Peer -> the run quarantined with put_pending (`pending` true), published by
+  // XetBridge::settle once the file hash checked out.
+  uint32_t run_offset = 0;
+  bool pending = false;
   // With a sink: the run was written to sink memory instead of `data`.
   uint8_t* ext = nullptr;
   size_t ext_len = 0;
@@ -51,8 +65,13 @@ class XetBridge {
   cas::Reconstruction get_reconstruction(const std::string& file_hash_hex) const;
   // `sink` (optional) supplies destination memory for the fetched run (e.g. a pinned staging
   // region); when it returns nullptr the run lands in XorbFetchResult::data as usual.
-  XorbFetchResult fetch_term(const cas::Term& term, const cas::Reconstruction& recon, bool allow_p2p = true,
-                             bool allow_cache = true, const bt::PayloadSink& sink = {});
+  XorbFetchResult fetch_term(const cas::Term& term, const cas::Reconstruction& recon, const FetchOptions& opt = {},
+                             const bt::PayloadSink& sink = {});
+  // After the file a term belongs to was verified (ok) or failed (!ok): publish or drop a peer
+  // run quarantined by fetch_term; on failure also evict the cached run a cache hit came from, so
+  // the repair refetch cannot read the same bad bytes again.
+  void settle(const std::string& xorb_hex, const XorbFetchResult& r, bool ok);
+  void settle(const std::string& xorb_hex, Source src, uint32_t run_offset, bool pending, bool ok);
   FetchStats& stats() { return stats_; }
   void print_stats(std::ostream& w) const;
   std::string stats_json() const;

@@ -91,6 +91,11 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
 
   std::vector<std::vector<xet::HashSize>> hashes(n);
   std::vector<uint8_t> done(n, 0);
+  // Where each term's bytes came from, and the cache run behind them (for settle()).
+  std::vector<Source> src(n, Source::Cdn);
+  std::vector<std::string> peer(n);
+  std::vector<uint32_t> run_off(n, 0);
+  std::vector<uint8_t> pending(n, 0);
   size_t resumed = 0;
   // ---- resume from sidecar
   if (storage::exists(tmp) && storage::exists(side)) {
@@ -108,6 +113,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
         }
         hashes[t] = std::move(hs);
         if (!done[t]) ++resumed;
+        src[t] = Source::Resumed;
         done[t] = 1;
         p += 8 + size_t(k) * 40;
       }
@@ -131,18 +137,25 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     if (::write(sc.fd, h.data(), h.size()) != 72) throw Error("IoError", "resume header");
   }
 
-  std::vector<Source> src(n, Source::Cdn);
-  std::vector<std::string> peer(n);
   std::atomic<size_t> next{0};
   std::atomic<bool> failed{false};
   std::string first_err;
   std::mutex err_mu;
 
-  auto do_term = [&](size_t i, bool allow_p2p, bool allow_cache) {
+  // A term's earlier copy failed (decode error or file hash): drop/evict the cached run behind
+  // it and blame the peer that served it.
+  auto reject = [&](size_t i) {
+    if (src[i] == Source::Peer && !peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
+    bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i] != 0, false);
+    pending[i] = 0;
+  };
+  auto do_term = [&](size_t i, const FetchOptions& opt) {
     const cas::Term& t = rec.terms[i];
-    XorbFetchResult f = bridge_.fetch_term(t, rec, allow_p2p, allow_cache);
+    XorbFetchResult f = bridge_.fetch_term(t, rec, opt);
     src[i] = f.source;  // recorded before decoding so a bad peer copy can be attributed
     peer[i] = f.peer;
+    run_off[i] = f.run_offset;
+    pending[i] = f.pending;
     // Uncompressed chunks are hashed and written straight from the fetched run (no decode
     // buffer); compressed ones are decoded into one buffer for the term.
     std::vector<xet::HashSize> hs;
@@ -202,14 +215,14 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       if (i >= n) return;
       if (done[i]) continue;
       try {
-        do_term(i, true, true);
+        do_term(i, FetchOptions{});
         if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
       } catch (const std::exception& e) {
         // A peer/cache copy that does not decode: retry straight from the CDN once.
         ZTRACE("download", "term " << i << " via " << int(src[i]) << " failed (" << e.what() << "), CDN retry");
         try {
-          if (src[i] != Source::Cdn && !peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
-          do_term(i, false, false);
+          if (src[i] != Source::Cdn) reject(i);
+          do_term(i, FetchOptions{false, false, /*repair=*/src[i] != Source::Cdn});
           if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
         } catch (const std::exception& e2) {
           std::lock_guard<std::mutex> g(err_mu);
@@ -225,6 +238,8 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   for (auto& t : ts) t.join();
   if (failed) {
     ::close(fd);
+    for (size_t i = 0; i < n; ++i)
+      if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
     throw Error("DownloadFailed", first_err);
   }
   bool ok = true;
@@ -236,12 +251,21 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     };
     ok = file_hash_now() == hex;
     if (!ok) {
+      // Repair: every term not fetched from the CDN in this run — peer runs, cache hits and terms
+      // restored from the resume sidecar — is refetched from the CDN, replacing its cached copy.
       bridge_.stats().verify_failures++;
-      for (size_t i = 0; i < n; ++i) {
-        if (src[i] == Source::Cdn) continue;
-        if (!peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
-        do_term(i, false, false);
-        bridge_.stats().refetches++;
+      try {
+        for (size_t i = 0; i < n; ++i) {
+          if (src[i] == Source::Cdn) continue;
+          reject(i);
+          do_term(i, FetchOptions{false, false, /*repair=*/true});
+          bridge_.stats().refetches++;
+        }
+      } catch (...) {  // the CDN failed too: keep the sidecar (resumed terms are re-checked next run)
+        ::close(fd);
+        for (size_t i = 0; i < n; ++i)
+          if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
+        throw;
       }
       ok = file_hash_now() == hex;
     }
@@ -251,6 +275,9 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       throw Error("HashMismatch", "file " + hex);
     }
   }
+  // The file checked out (or the caller skipped verification): publish the quarantined peer runs.
+  for (size_t i = 0; i < n; ++i)
+    if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, true);
   ::fdatasync(fd);
   ::close(fd);
   if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);

@@ -142,7 +142,10 @@ std::vector<std::string> list_cached_xorbs(const Config& cfg) {
     while (dirent* f = ::readdir(sd)) {
       std::string n = f->d_name;
       if (n.size() < 64 || n.compare(0, 2, pfx) != 0) continue;
-      if (n.size() == 64 || (n[64] == '.' && n.find(".tmp") == std::string::npos)) out.insert(n.substr(0, 64));
+      // full `{hex}` or partial `{hex}.{digits}`; temp files and quarantined `.unverified` runs
+      // are not cached xorbs
+      if (n.size() == 64 || (n[64] == '.' && n.size() > 65 && std::all_of(n.begin() + 65, n.end(), ::isdigit)))
+        out.insert(n.substr(0, 64));
     }
     ::closedir(sd);
   }
@@ -269,6 +272,7 @@ std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, 
     const uint64_t hi = idx[b - 1].header_off + xet::kChunkHeaderLen + idx[b - 1].clen;
     CacheHit h;
     h.chunk_offset = start;
+    h.run_offset = *it;
     h.ext = base + lo;
     h.ext_len = hi - lo;
     h.keep = m;
@@ -284,13 +288,43 @@ std::optional<CacheHit> XorbCache::get_with_range(const std::string& hex, uint32
   return std::nullopt;
 }
 
-void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
-  const std::string key = chunk_offset == 0 ? hex : hex + "." + std::to_string(chunk_offset);
-  const std::string path = cfg_.xorb_cache_path(key);
-  if (exists(path) && file_size(path) >= n) return;  // keep the longer run
+std::string XorbCache::run_path(const std::string& hex, uint32_t chunk_offset) const {
+  return cfg_.xorb_cache_path(chunk_offset == 0 ? hex : hex + "." + std::to_string(chunk_offset));
+}
+
+void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace) {
+  const std::string path = run_path(hex, chunk_offset);
+  if (!replace && exists(path) && file_size(path) >= n) return;  // keep the longer run
   write_file_atomic(path, data, n, /*durable=*/false);
   if (registry_) registry_->add(hex);
 }
+
+void XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+  write_file_atomic(run_path(hex, chunk_offset) + kPendingSuffix, data, n, /*durable=*/false);
+}
+
+bool XorbCache::promote(const std::string& hex, uint32_t chunk_offset) {
+  const std::string path = run_path(hex, chunk_offset);
+  const std::string pending = path + kPendingSuffix;
+  const uint64_t n = file_size(pending);
+  if (!exists(pending)) return false;
+  if (exists(path) && file_size(path) >= n) {  // a published run at least as long already exists
+    remove_file(pending);
+    return true;
+  }
+  if (::rename(pending.c_str(), path.c_str()) != 0) {
+    remove_file(pending);
+    return false;
+  }
+  if (registry_) registry_->add(hex);
+  return true;
+}
+
+void XorbCache::discard_pending(const std::string& hex, uint32_t chunk_offset) {
+  remove_file(run_path(hex, chunk_offset) + kPendingSuffix);
+}
+
+void XorbCache::evict(const std::string& hex, uint32_t chunk_offset) { remove_file(run_path(hex, chunk_offset)); }
 
 uint64_t XorbCache::bytes_on_disk() const {
   uint64_t t = 0;

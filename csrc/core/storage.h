@@ -45,6 +45,7 @@ std::vector<std::string> list_cached_xorbs(const Config& cfg);
 struct CacheHit {
   Bytes data;
   uint32_t chunk_offset = 0;  // chunk index of data's first chunk inside the xorb
+  uint32_t run_offset = 0;    // first chunk of the cached run the hit was sliced from (its file name)
   // Zero-copy alternative to `data` (e.g. a pinned staging buffer filled from HBM), valid while
   // `keep` is held.
   const uint8_t* ext = nullptr;
@@ -104,8 +105,20 @@ class XorbCache {
   // Legacy lookup kept for callers that want the raw run at an exact offset.
   std::optional<CacheHit> get_with_range(const std::string& hex, uint32_t range_start) const;
   // Store a run of serialized chunks starting at chunk `chunk_offset`: offset 0 goes to `{hex}`,
-  // others to `{hex}.{offset}`; an existing longer run under the same name is kept.
-  void put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  // others to `{hex}.{offset}`; an existing longer run under the same name is kept unless
+  // `replace` (a CDN refetch repairing a cached copy that failed verification).
+  void put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace = false);
+  // Runs that nothing has verified yet (received from a peer) are quarantined under
+  // `{run name}.unverified`, which no lookup, listing or seeding path sees.  After the file hash
+  // checked out, promote() publishes the run (keeping an existing longer one); otherwise
+  // discard_pending() drops it.  The reference caches peer runs unverified (swarm.zig:416-420) and
+  // then serves them on; it caches only CDN bytes in the bridge (xet_bridge.zig:203-208).
+  void put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  bool promote(const std::string& hex, uint32_t chunk_offset);
+  void discard_pending(const std::string& hex, uint32_t chunk_offset);
+  // Drop a published run (a cached copy whose bytes failed verification).
+  void evict(const std::string& hex, uint32_t chunk_offset);
+  static constexpr const char* kPendingSuffix = ".unverified";
   void put(const std::string& hex, const uint8_t* data, size_t n) { put_run(hex, 0, data, n); }
   void put_partial(const std::string& hex, uint32_t range_start, const uint8_t* data, size_t n) {
     put_run(hex, range_start, data, n);
@@ -114,6 +127,7 @@ class XorbCache {
   uint64_t bytes_on_disk() const;
 
  private:
+  std::string run_path(const std::string& hex, uint32_t chunk_offset) const;
   const Config& cfg_;
   XorbRegistry* registry_;
 };

@@ -174,8 +174,10 @@ __global__ void __launch_bounds__(256) k_place_raw(const uint8_t* __restrict__ s
 //    those bytes were flushed by this wave at least ring - 320 - 2 KiB earlier.
 //  * BG4: the grouped stream is scattered to its interleaved position (4*j + g) on flush, and
 //    long-distance match reads use the same mapping, so no regroup pass or scratch is needed.
-//  * chunks clipped by [clip_lo, clip_hi) decode into a 128 KiB global scratch slot (one for the
-//    chunk straddling clip_lo, one for clip_hi), then the clipped range is copied out.
+//  * chunks clipped by [clip_lo, clip_hi) decode into a 128 KiB slot of the caller's per-launch
+//    scratch (one for the chunk straddling clip_lo, one for clip_hi), then the clipped range is
+//    copied out.  The scratch belongs to the launch, so clipped decodes on several streams never
+//    share it.
 // --------------------------------------------------------------------------------------------
 // Ring geometry (bytes per wave) is a template parameter RB: a larger ring keeps more match
 // sources in LDS (fewer L2 read-backs) at the price of fewer resident waves per CU.
@@ -185,7 +187,8 @@ template <uint32_t RB> struct RingGeo {
 };
 constexpr uint32_t kFlushAt = 2048;
 
-__device__ uint8_t g_clip_scratch[2][kMaxChunk + 256];
+constexpr uint32_t kClipSlot = kMaxChunk + 256;
+static_assert(2 * kClipSlot == ZG_CLIP_SCRATCH_BYTES, "clip scratch layout");
 
 // Compressed-stream window: three dwords per lane = bytes [wofs, wofs + 768) of the payload,
 // addressed relative to the 4-byte-aligned payload base.  Reads stay inside [wofs, wofs + 320);
@@ -520,8 +523,8 @@ __device__ bool lz4_frame(Sink& s, const uint8_t* payload, uint32_t clen, uint32
 template <bool kProf, uint32_t RB>
 __global__ void __launch_bounds__(256, RB <= 4096 ? 8 : 5) k_decode_lz4(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const ZgChunk* __restrict__ chunks, int n_chunks,
-                                                    uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
-                                                    uint64_t src_n, uint64_t dst_n) {
+                                                    uint64_t clip_lo, uint64_t clip_hi, uint8_t* __restrict__ clip_scratch,
+                                                    unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][RB];
   const uint32_t lane = lane_id();
   const int wave = wave_uniform(int(threadIdx.x >> 6));
@@ -546,7 +549,7 @@ __global__ void __launch_bounds__(256, RB <= 4096 ? 8 : 5) k_decode_lz4(const ui
     const uint64_t t_start = kProf ? clk() : 0;
     Sink s{};
     s.ring = rings[wave];
-    s.out = clipped ? g_clip_scratch[ch.dst < clip_lo ? 0 : 1] : dst + ch.dst;
+    s.out = clipped ? clip_scratch + (ch.dst < clip_lo ? 0u : kClipSlot) : dst + ch.dst;
     s.bg4 = ch.scheme == 2;
     s.tmod = s.bg4 ? 0u : uint32_t(reinterpret_cast<uintptr_t>(s.out) & RingGeo<RB>::kMask);
     s.n = ch.ulen;
@@ -706,9 +709,10 @@ hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, 
 }
 
 hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
-                           int n_chunks, uint64_t clip_lo, uint64_t clip_hi, unsigned long long* err,
-                           hipStream_t stream) {
+                           int n_chunks, uint64_t clip_lo, uint64_t clip_hi, uint8_t* clip_scratch,
+                           unsigned long long* err, hipStream_t stream) {
   if (n_chunks <= 0) return hipSuccess;
+  if ((clip_lo > 0 || clip_hi < dst_n) && clip_scratch == nullptr) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_place_raw, dim3((n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, stream, src,
                      dst, chunks, n_chunks, clip_lo, clip_hi, src_n, dst_n);
   hipError_t e = hipGetLastError();
@@ -741,7 +745,7 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
   }
 #define ZG_LZ4_LAUNCH(P, R)                                                                                       \
   hipLaunchKernelGGL((k_decode_lz4<P, R>), dim3(grid), dim3(256), 0, stream, src, dst, chunks, n_chunks, clip_lo, \
-                     clip_hi, err, src_n, dst_n)
+                     clip_hi, clip_scratch, err, src_n, dst_n)
   if (ring_kib == 4) {
     if (prof) ZG_LZ4_LAUNCH(true, 4096); else ZG_LZ4_LAUNCH(false, 4096);
   } else if (ring_kib == 16) {

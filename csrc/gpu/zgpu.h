@@ -58,10 +58,14 @@ enum {
 // All launchers return hipError_t of the launch and never synchronize.
 hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
                           unsigned long long* err, hipStream_t stream);
-// Descriptors are bounds-checked in-kernel against src_n / dst_n (bytes).
+// Descriptors are bounds-checked in-kernel against src_n / dst_n (bytes).  A clip window narrower
+// than [0, dst_n) needs `clip_scratch` (ZG_CLIP_SCRATCH_BYTES of device memory owned by the caller,
+// one per concurrently running launch): compressed chunks that straddle the window decode there
+// before their clipped part is copied out.  Without it such a launch returns hipErrorInvalidValue.
+#define ZG_CLIP_SCRATCH_BYTES (2u * (128u * 1024u + 256u))
 hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                            const ZgChunk* chunks, int n_chunks, uint64_t clip_lo, uint64_t clip_hi,
-                           unsigned long long* err, hipStream_t stream);
+                           uint8_t* clip_scratch, unsigned long long* err, hipStream_t stream);
 hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
                           uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, hipStream_t stream);
 // Hash raw (offset, len) messages with the Xet data key: out[i] = keyed(DATA_KEY, buf[off:off+len]).

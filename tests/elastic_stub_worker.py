@@ -13,12 +13,19 @@ import time
 def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # all ranks of one attempt are children of the same torchrun agent
+    ready = f"{os.environ['ZEST_STUB_LOG']}.ready.{os.getppid()}"
     if rank == 0:
         with open(os.environ["ZEST_STUB_LOG"], "a") as fh:
             vis = os.environ.get("HIP_VISIBLE_DEVICES")
             fh.write(f"{world}" + (f"@{vis}" if vis else "") + "\n")
+        open(ready, "w").close()
     mode = os.environ.get("ZEST_STUB_MODE", "lose-last")
     if mode == "always-crash" or (world > 1 and rank == world - 1):
+        # die only after rank 0 logged the attempt (torchrun stops rank 0 as soon as a peer dies)
+        t0 = time.time()
+        while rank != 0 and not os.path.exists(ready) and time.time() - t0 < 60:
+            time.sleep(0.01)
         os._exit(17)
     if world > 1:
         time.sleep(60)  # never reached in the tests: torchrun tears the group down first

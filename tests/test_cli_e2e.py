@@ -177,6 +177,49 @@ def test_p2p_corrupt_peer_falls_back_to_cdn(hub, nodes):
     assert_snapshot(b, REPO_ID, commit, files)
     assert p2p_ratio(r.stdout) < 100.0
     assert hub.counters.get("xorb_get", 0) > 0
+    # Nothing the corrupt peer sent was published to the leecher's xorb cache (peer runs stay
+    # quarantined until their file verifies): no quarantined run is left behind, and a re-pull served
+    # by that cache alone (CDN dead, no peers) is exact.
+    assert not [p for p in b.xorb_files() if p.name.endswith(".unverified")]
+    snap = b.snapshot(REPO_ID, commit)
+    for name in files:
+        (snap / name).unlink()
+    hub.fail_xorbs.update(x.hash_hex for x in hub.xorbs)
+    b.run("pull", REPO_ID, "--no-p2p")
+    assert_snapshot(b, REPO_ID, commit, files)
+
+
+def test_resumed_bad_peer_terms_are_repaired(nodes, tmp_path):
+    # An interrupted run stored (in its .zest-resume sidecar) terms that a corrupt peer served: raw
+    # chunks, so they decode and only the file hash exposes them.  The next run resumes them and
+    # must refetch them from the CDN when the file hash does not match.
+    h = FakeHub(policy="none", max_xorb_bytes=1 << 20)
+    h.start()
+    try:
+        files = {"model.safetensors": sample_files(big=4_000_000)["model.safetensors"]}
+        commit = h.add_repo(REPO_ID, files, xet_min_size=1)
+        a = Node(h, tmp_path, "seeder")
+        b = Node(h, tmp_path, "leecher")
+        try:
+            a.run("pull", REPO_ID, "--no-p2p")
+            a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port),
+                    "--fault", "corrupt:1.0")
+            a.wait_healthy()
+            h.fail_xorbs.add(h.xorbs[-1].hash_hex)  # the CDN repair of run 1 fails on this xorb
+            r = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{a.listen_port}", "--no-dht", check=False)
+            snap = b.snapshot(REPO_ID, commit)
+            assert r.returncode != 0 or not (snap / "model.safetensors").exists(), r.stdout
+            assert (snap / "model.safetensors.zest-resume").exists()
+            assert not [p for p in b.xorb_files() if p.name.endswith(".unverified")]
+            h.fail_xorbs.clear()
+            out = b.run("pull", REPO_ID, "--no-p2p").stdout
+            assert "resumed" in out
+            assert_snapshot(b, REPO_ID, commit, files)
+        finally:
+            a.close()
+            b.close()
+    finally:
+        h.stop()
 
 
 def test_p2p_dead_peer_falls_back_to_cdn(hub, nodes):

@@ -98,6 +98,44 @@ def test_direct_pull_to_device(tmp_path, monkeypatch, policy):
         hub.stop()
 
 
+@pytest.mark.parametrize("policy", ["none", "bg4"])
+def test_direct_pull_repairs_corrupt_peer(tmp_path, monkeypatch, policy):
+    """A corrupt seeder: the device-direct pull catches the bad bytes in the GPU Merkle check (or the
+    GPU decoder), drops the quarantined peer runs and pulls the file again from the CDN; the leecher's
+    xorb cache ends up holding only verified runs (a cache-only re-pull is exact)."""
+    import zest_amd
+    from e2e_util import Node
+
+    world = SyntheticWorld(models.get("llama-tiny"), seed=13, mode="bf16")
+    hub = FakeHub(policy=policy, max_xorb_bytes=1 << 20)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path / "a")).items():
+            monkeypatch.setenv(k, v)
+        host = zdev.load_snapshot(zest_amd.pull(world.spec.repo_id, p2p=False), "cpu")
+        seeder = Node(hub, tmp_path, "seed-a")
+        seeder.env.update(hub.env(str(tmp_path / "a")))
+        seeder.spawn("serve", "--listen-port", str(seeder.listen_port), "--http-port", str(seeder.http_port),
+                     "--fault", "corrupt:1.0")
+        seeder.wait_healthy()
+        for k, v in hub.env(str(tmp_path / "b")).items():
+            monkeypatch.setenv(k, v)
+        got = zest_amd.pull(world.spec.repo_id, device="cuda:0", direct=True,
+                            peers=[f"127.0.0.1:{seeder.listen_port}"], dht=False)
+        for k, t in got.items():
+            assert torch.equal(t.cpu().view(torch.uint8), host[k].view(torch.uint8)), k
+        seeder.close()
+        xorbs = tmp_path / "b" / "zest" / "xorbs"
+        assert not [p for p in xorbs.rglob("*.unverified")]
+        hub.fail_xorbs.update(x.hash_hex for x in hub.xorbs)  # CDN dead: only the cache can serve
+        again = zest_amd.pull(world.spec.repo_id, device="cuda:0", direct=True, p2p=False)
+        for k, t in again.items():
+            assert torch.equal(t.cpu().view(torch.uint8), host[k].view(torch.uint8)), k
+    finally:
+        hub.stop()
+
+
 def test_cli_pull_gpus(tmp_path):
     """`zest pull <repo> --gpus 1`: CLI spawns a torchrun GPU worker that decodes + verifies every Xet
     file on the GPU and writes the HF snapshot (single-command multi-GPU UX)."""

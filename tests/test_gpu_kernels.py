@@ -130,6 +130,41 @@ def test_ingest_clip_window():
     assert inside and all(got[i].tobytes() == want[i] for i in inside)
 
 
+def test_clipped_ingests_on_two_streams():
+    # Each workspace owns its clip scratch, so clipped decodes running concurrently on two streams
+    # cannot overwrite each other's straddling chunks (they shared one global buffer before).
+    data, ends, b = _make_runs("lz4", seed=11)
+    body = b.serialize(False)
+    nck = len(ends)
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(bytearray(body), dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, nck, len(data))
+    windows = [(70_001, 650_003), (650_003, len(data) - 99_991)]
+    dsts = [ops.padded_empty(len(data), DEV) for _ in windows]
+    hashes = [torch.zeros((nck, 32), dtype=torch.uint8, device=DEV) for _ in windows]
+    wss = [ops.IngestWorkspace(DEV, 1, nck) for _ in windows]
+    streams = [torch.cuda.Stream(DEV) for _ in windows]
+    for d in dsts:
+        d.zero_()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for d, h, ws, st, w in zip(dsts, hashes, wss, streams, windows):
+            with torch.cuda.stream(st):
+                ops.ingest_terms(src, d, terms, h, clip=w, ws=ws, check=False)
+    torch.cuda.synchronize()
+    for d, ws, (lo, hi) in zip(dsts, wss, windows):
+        ops.raise_on_error(ws.err)
+        out = d.cpu().numpy().tobytes()
+        assert out[lo:hi] == data[lo:hi]
+        assert out[:lo] == bytes(lo) and out[hi:] == bytes(len(data) - hi)
+    # a clipped launch without scratch is refused instead of racing on shared memory
+    H = ops.hip()
+    with pytest.raises(RuntimeError):
+        H.place_chunks(src.data_ptr(), len(body), dsts[0].data_ptr(), len(data), wss[0].chunks.data_ptr(), nck,
+                       1, len(data), wss[0].err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+
+
 def test_ingest_detects_corruption():
     data, ends, b = _make_runs("auto", seed=5)
     body = bytearray(b.serialize(False))

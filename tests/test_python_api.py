@@ -15,6 +15,7 @@ import torch
 
 from e2e_util import free_port
 import zest_amd
+import zest_amd.client  # noqa: F401  (submodule used as zest_amd.client below)
 from zest_amd import device as zdev
 from zest_amd import hf_backend, models
 from zest_amd.synthetic import SyntheticWorld

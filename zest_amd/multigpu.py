@@ -21,6 +21,20 @@ from . import _core, ops
 from .parallel import assign_owners, init_from_env
 
 
+def cached_file_ok(repo: str, commit: str, f: dict, dst: str) -> bool:
+    """A snapshot file counts as cached only when it is verified: a matching verified marker, or a
+    re-hash that matches its Xet hash (then the marker is written).  Same rule as the host pull
+    (csrc/core/pull.cpp); the reference trusts existence alone (main.zig:222-225)."""
+    if not (os.path.exists(dst) and os.path.getsize(dst) == f["size"]):
+        return False
+    if _core.check_verified_marker(repo, commit, f["path"], f["xet_hash"], dst):
+        return True
+    if _core.xet_hash_of_file(dst) == f["xet_hash"]:
+        _core.write_verified_marker(repo, commit, f["path"], f["xet_hash"], dst)
+        return True
+    return False
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="zest pull --gpus N")
     ap.add_argument("repo")
@@ -61,7 +75,7 @@ def main(argv=None) -> int:
         todo = []
         for f in mine:
             dst = os.path.join(snap, f["path"])
-            if os.path.exists(dst) and os.path.getsize(dst) == f["size"]:
+            if cached_file_ok(a.repo, commit, f, dst):
                 print(f"[rank {rank}] {f['path']} (cached)", flush=True)
                 continue
             todo.append(f)

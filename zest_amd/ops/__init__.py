@@ -149,6 +149,13 @@ class IngestWorkspace:
         self.err = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.terms_host = torch.empty(max_terms * TERM_DTYPE.itemsize, dtype=torch.uint8).pin_memory() \
             if self.device.type == "cuda" else None
+        self._clip_scratch = None
+
+    def clip_scratch(self) -> int:
+        """Device scratch for clipped decodes, private to this workspace (so to its stream)."""
+        if self._clip_scratch is None:
+            self._clip_scratch = torch.empty(hip().CLIP_SCRATCH_BYTES, dtype=torch.uint8, device=self.device)
+        return self._clip_scratch.data_ptr()
 
 
 def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes: torch.Tensor,
@@ -200,7 +207,7 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     ws.chunks[: n_chunks * CHUNK_DTYPE.itemsize].zero_()  # gaps between terms become no-op descriptors
     H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(), ws.err.data_ptr(), st)
     H.place_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, lo, hi,
-                   ws.err.data_ptr(), st)
+                   ws.err.data_ptr(), st, ws.clip_scratch() if (lo > 0 or hi < dst_n) else 0)
     hptr = hashes.data_ptr() + 32 * hash_base
     H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st)
     if check:
