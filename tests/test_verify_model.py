@@ -108,3 +108,48 @@ def test_enable_from_pretrained_repo_id(hub_with_gpt2, gpt2_checkpoint, tmp_path
     assert (snap / "model.safetensors").is_file()
     assert "falling back to huggingface_hub" not in r.stderr, r.stderr[-4000:]  # zest served every file
     assert hub.counters.get("xorb_get", 0) > 0
+
+
+def _zest_from_pretrained(hub, tmp_path, monkeypatch, device, direct):
+    import zest_amd
+
+    for k, v in hub.env(str(tmp_path)).items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+    return zest_amd.from_pretrained(REPO, device=device, direct=direct, p2p=False, dht=False)
+
+
+def test_zest_from_pretrained_cpu(hub_with_gpt2, gpt2_checkpoint, tmp_path, monkeypatch):
+    """zest_amd.from_pretrained: the model is built around the pulled, hash-verified tensors (no
+    second copy); logits and greedy generation match the uploaded model."""
+    hub, commit = hub_with_gpt2
+    _, ids, logits, gen = gpt2_checkpoint
+    model = _zest_from_pretrained(hub, tmp_path, monkeypatch, "cpu", False)
+    assert type(model).__name__ == "GPT2LMHeadModel"
+    assert all(p.device.type == "cpu" for p in model.parameters())
+    with torch.no_grad():
+        assert torch.equal(model(ids).logits, logits)
+        assert torch.equal(model.generate(ids[:1], max_new_tokens=8, do_sample=False, pad_token_id=0), gen)
+    # config/tokenizer files are in the snapshot; the weights never went through from_pretrained's reader
+    assert (Path(model.zest_snapshot_dir) / "config.json").is_file()
+
+
+@pytest.mark.gpu
+def test_zest_from_pretrained_direct_to_hbm(hub_with_gpt2, gpt2_checkpoint, tmp_path, monkeypatch):
+    """Network -> HBM (GPU decode + Merkle verify, no disk for the weights) -> transformers model whose
+    parameters are those HBM buffers; outputs match the uploaded model."""
+    hub, commit = hub_with_gpt2
+    files, ids, logits, gen = gpt2_checkpoint
+    model = _zest_from_pretrained(hub, tmp_path, monkeypatch, "cuda:0", True)
+    assert all(p.device.type == "cuda" for p in model.parameters())
+    snap = Path(model.zest_snapshot_dir)
+    assert not (snap / "model.safetensors").exists()  # weights bypassed the disk
+    import safetensors.torch as st
+
+    want = st.load(files["model.safetensors"])
+    got = model.state_dict()
+    for k, v in want.items():
+        assert torch.equal(got[k].cpu(), v), k
+    with torch.no_grad():
+        out = model(ids.cuda()).logits.cpu()
+    assert torch.allclose(out, logits, atol=1e-4, rtol=1e-4)

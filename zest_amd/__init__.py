@@ -6,6 +6,7 @@ Usage (same API as the reference's `zest` package, python/zest/__init__.py:1-73)
     zest.enable()                    # background seeder + huggingface_hub patch
     path = zest.pull("meta-llama/Llama-3.1-8B")
     weights = zest.pull("meta-llama/Llama-3.1-8B", device="cuda:0")   # HBM tensors, GPU-verified
+    model = zest.from_pretrained("meta-llama/Llama-3.1-8B")            # transformers model on those tensors
     print(zest.status()); zest.stop()
 
 Layers (see docs/ARCHITECTURE.md):
@@ -91,6 +92,13 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
 
     res = _client.pull_detailed(repo, revision, **kw)
     return load_snapshot(res.snapshot_dir, device or "cuda:0", res.xet_hashes() if verify else None)
+
+
+def from_pretrained(repo: str, revision: str = "main", **kw):
+    """transformers model built around weights pulled into `device` memory (zest_amd.hf_model)."""
+    from .hf_model import from_pretrained as _fp
+
+    return _fp(repo, revision, **kw)
 
 
 def status() -> dict:
