@@ -85,7 +85,8 @@ def main() -> None:
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=device)
+            from zest_amd.parallel import nccl_options
+            dist.init_process_group("nccl", device_id=device, pg_options=nccl_options())
     t_setup = time.time()
     ops.hip()
     spec = models.get(a.model)

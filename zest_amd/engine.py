@@ -191,8 +191,16 @@ class DevicePuller:
             self.merkle_sb = H.merkle_scratch_bytes(max(j[1] for j in self.jobs), len(self.jobs))
             self.merkle_scratch = torch.empty(self.merkle_sb, dtype=torch.uint8, device=self.device)
             self.roots = torch.empty((len(self.jobs), 32), dtype=torch.uint8, device=self.device)
-            self.copy_stream = torch.cuda.Stream(self.device)
-            self.side_stream = torch.cuda.Stream(self.device)
+            # Ingest (H2D copies, index/place/hash of this rank's rounds) is on the critical path:
+            # its streams run at high priority; the receive-side verification (verify_stream) stays
+            # at normal priority and fills whatever the ingest and the exchange leave idle.
+            try:
+                hi = int(torch.cuda.Stream.priority_range()[1])  # (least, greatest); lower = more urgent
+            except Exception:
+                hi = -1
+            self.copy_stream = torch.cuda.Stream(self.device, priority=hi)
+            self.lane_stream = torch.cuda.Stream(self.device, priority=hi)
+            self.side_stream = torch.cuda.Stream(self.device, priority=hi)
             self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
             self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
         # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
@@ -504,8 +512,9 @@ class DevicePuller:
         if self.is_cuda:
             H = ops.hip()
             main = torch.cuda.current_stream(dev)
-            lanes = (main, self.side_stream)
-            self.side_stream.wait_stream(main)  # hashes.zero_() above
+            lanes = (self.lane_stream, self.side_stream)
+            for ln in lanes:
+                ln.wait_stream(main)  # hashes.zero_() above, and the caller's earlier work
             for k, rw in enumerate(self.rounds):
                 s = k % self.slots
                 comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
@@ -543,6 +552,7 @@ class DevicePuller:
                             works += self._hash_received(k, self._exchange(k))
                 if self._rx:
                     _core.trace.roctx_pop()
+            main.wait_stream(self.lane_stream)
             main.wait_stream(self.side_stream)
             st = main.cuda_stream
             if self.n_ranks > 1 and self.exchange in PEER_MAPPED_MODES:

@@ -39,9 +39,19 @@ def init_from_env(backend: str | None = None, timeout_s: int = 600):
         dev = torch.device("cpu")
     if not dist.is_initialized():
         import datetime
-        kw = {"device_id": dev} if backend == "nccl" else {}
+        kw = {"device_id": dev, "pg_options": nccl_options()} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world, local, dev
+
+
+def nccl_options():
+    """ProcessGroupNCCL options for the swarm: RCCL's internal stream at high priority, so the piece
+    exchange's kernels are dispatched ahead of the receive-side BLAKE3 verification that runs
+    concurrently on a normal-priority stream (both want every CU; the exchange is on the critical
+    path, the verification is not)."""
+    from torch.distributed import ProcessGroupNCCL
+
+    return ProcessGroupNCCL.Options(is_high_priority_stream=True)
 
 
 def parse_cpulist(text: str) -> set[int]:
@@ -89,5 +99,5 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ["DevicePuller", "assign_owners", "bind_local_numa", "gpu_local_cpus", "init_from_env", "parse_cpulist",
-           "swarm_load"]
+__all__ = ["DevicePuller", "assign_owners", "bind_local_numa", "gpu_local_cpus", "init_from_env", "nccl_options",
+           "parse_cpulist", "swarm_load"]
