@@ -61,6 +61,9 @@ def from_pretrained(repo: str, revision: str = "main", *, device="cuda:0", direc
     weights = pull(repo, revision, device=dev, direct=direct and dev.type == "cuda", verify=verify, p2p=p2p,
                    peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, repo_type=repo_type)
     cls = model_class(config, auto_class)
+    # place the model where the weights already are (without a device_map transformers would
+    # materialise it on the CPU and copy the tensors there)
+    model_kwargs.setdefault("device_map", {"": str(dev)})
     model = cls.from_pretrained(None, config=config, state_dict=weights, **model_kwargs)
     model.eval()
     model.zest_snapshot_dir = snap  # where the tokenizer / generation config live
