@@ -10,6 +10,7 @@
 #include <cstdlib>
 
 #include "blake3_dev.h"
+#include "lz4win.h"
 #include "zgpu.h"
 
 namespace {
@@ -190,65 +191,12 @@ constexpr uint32_t kFlushAt = 2048;
 constexpr uint32_t kClipSlot = kMaxChunk + 256;
 static_assert(2 * kClipSlot == ZG_CLIP_SCRATCH_BYTES, "clip scratch layout");
 
-// Compressed-stream window: three dwords per lane = bytes [wofs, wofs + 768) of the payload,
-// addressed relative to the 4-byte-aligned payload base.  Reads stay inside [wofs, wofs + 320);
-// the window slides by 256 bytes as the stream advances, so w2 is a 256-byte-ahead prefetch whose
-// load latency overlaps parsing.  Offsets are 32-bit (a chunk payload is < 16 MiB).
-struct Win {
-  const uint32_t* pb;
-  uint32_t wofs;
-  uint32_t w0, w1, w2;
-};
-
-__device__ __forceinline__ void win_init(Win& w, const uint8_t* payload, uint32_t lane) {
-  w.pb = reinterpret_cast<const uint32_t*>(payload - (reinterpret_cast<uintptr_t>(payload) & 3));
-  w.wofs = 0;
-  w.w0 = w.pb[lane];
-  w.w1 = w.pb[kWave + lane];
-  w.w2 = w.pb[2 * kWave + lane];
-}
-
-// Slide so that position a (relative to pb) is in the first 256 bytes of the window.  Callers
-// advance by < 256 bytes between seeks, so at most one slide happens (an `if`, not a loop: a loop
-// makes the compiler copy the freshly loaded prefetch register and wait for it immediately).
-__device__ __forceinline__ void win_seek(Win& w, uint32_t a, uint32_t lane) {
-  if (a >= w.wofs + 512) {  // long jump (raw block / checksum skip): reload
-    w.wofs = a & ~255u;
-    w.w0 = w.pb[(w.wofs >> 2) + lane];
-    w.w1 = w.pb[(w.wofs >> 2) + kWave + lane];
-    w.w2 = w.pb[(w.wofs >> 2) + 2 * kWave + lane];
-  } else if (a >= w.wofs + 256) {
-    w.wofs += 256;
-    w.w0 = w.w1;
-    w.w1 = w.w2;
-    w.w2 = w.pb[(w.wofs >> 2) + 2 * kWave + lane];
-  }
-}
-
-// Uniform byte at a (a in [wofs, wofs + 512)).
-__device__ __forceinline__ uint32_t win_u8(const Win& w, uint32_t a) {
-  const uint32_t rel = a - w.wofs;
-  uint32_t d;
-  if (rel < 256) d = __builtin_amdgcn_readlane(w.w0, int(rel >> 2));
-  else d = __builtin_amdgcn_readlane(w.w1, int((rel >> 2) - 64));
-  return (d >> (8 * (rel & 3))) & 0xFF;
-}
-
-// Lane i gets the byte at a + i (a in [wofs, wofs + 256)): two gathers and a select, no branch.
-__device__ __forceinline__ uint32_t win_lane_u8(const Win& w, uint32_t a, uint32_t lane) {
-  const uint32_t rel = a - w.wofs + lane;  // < 320: inside w0 | w1
-  const uint32_t idx = (rel >> 2) & 63;
-  const uint32_t d0 = __shfl(w.w0, int(idx), kWave), d1 = __shfl(w.w1, int(idx), kWave);
-  return ((rel < 256 ? d0 : d1) >> (8 * (rel & 3))) & 0xFF;
-}
-
-// L2-coherent byte load (bypasses this CU's L1, which never sees its own earlier stores).
-__device__ __forceinline__ uint32_t load_u8_coherent(const uint8_t* p) {
-  const uint32_t k = uint32_t(reinterpret_cast<uintptr_t>(p) & 3);
-  uint32_t* w = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(p - k));
-  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (v >> (8 * k)) & 0xFF;
-}
+using zgw::Win;
+using zgw::load_u8_coherent;
+using zgw::win_init;
+using zgw::win_lane_u8;
+using zgw::win_seek;
+using zgw::win_u8;
 
 // Optional decode profile (ZG_LZ4_PROF=1 selects the kProf instantiation).
 __device__ unsigned long long g_lz4_prof[10];
@@ -712,12 +660,19 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                            int n_chunks, uint64_t clip_lo, uint64_t clip_hi, uint8_t* clip_scratch,
                            unsigned long long* err, hipStream_t stream) {
   if (n_chunks <= 0) return hipSuccess;
-  if ((clip_lo > 0 || clip_hi < dst_n) && clip_scratch == nullptr) return hipErrorInvalidValue;
+  const bool clipped = clip_lo > 0 || clip_hi < dst_n;
+  if (clipped && clip_scratch == nullptr) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_place_raw, dim3((n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, stream, src,
                      dst, chunks, n_chunks, clip_lo, clip_hi, src_n, dst_n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-    const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  // ZG_LZ4_SEQ=0 forces the LDS-ring decoder (A/B runs); clip windows always use it.
+  static const bool batched = [] {
+    const char* v = getenv("ZG_LZ4_SEQ");
+    return !(v && *v == '0');
+  }();
+  if (batched && !clipped) return zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
+  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   // ZG_LZ4_GRID caps the persistent grid (occupancy experiments: 256 = one wave per SIMD).
   static const int grid_cap = [] {
     const char* v = getenv("ZG_LZ4_GRID");

@@ -1,0 +1,400 @@
+// K3c: batched LZ4 / BG4-LZ4 decode for gfx950 (CDNA4, wave64).
+//
+// Xet weight chunks decode into ~6.8k LZ4 sequences per 64 KiB (BG4 bf16: the exponent planes
+// are almost all 4-5 byte matches).  The LDS-ring decoder (k_decode_lz4, ingest.hip) executes
+// those sequences one at a time with the whole wave, so ~5 of 64 lanes do useful work and every
+// sequence pays a chain of read-lanes, LDS round trips and barriers (PMC: ~450 SIMD cycles per
+// sequence).  This decoder keeps one wave per chunk (full occupancy) but splits LZ4's sequential
+// and parallel halves:
+//
+//   parse    the token stream is walked with uniform (scalar) control flow, reading bytes from a
+//            wave-wide register window; each sequence becomes one record {gap, literal length,
+//            match length, offset} written into lane n of two VGPRs (a lane select) -- no memory.
+//   execute  every 64 records: DPP prefix sums give each record's literal source and output
+//            position; literal bytes, then match bytes, are produced one per lane per pass (the
+//            lane -> record map is a scatter of record heads into LDS + a DPP max-scan).  A match
+//            byte reads its periodic source (start - off + k mod off, always before the match);
+//            when that byte is written by another lane of the same pass, the lane follows that
+//            lane's source (pointer chase, almost never taken: it is skipped unless some source
+//            lies at or after the pass's first destination).  Output goes straight to HBM, read
+//            back through L2 after s_waitcnt vmcnt(0); BG4 chunks are scattered to their
+//            interleaved byte (4 j + group) on store.
+//
+// Lengths/offsets are validated in the execute step (lane-parallel) before any byte moves.
+// Clipped launches keep using the LDS-ring decoder.  Host oracle: csrc/core/lz4.cpp, compared
+// bit-exactly in tests/test_gpu_kernels.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "lz4win.h"
+#include "zgpu.h"
+
+namespace {
+
+using zgw::Win;
+using zgw::load_u8_coherent;
+using zgw::win_init;
+using zgw::win_lane_u8;
+using zgw::win_seek;
+using zgw::win_u8;
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr uint32_t kMaxChunk = 128u * 1024u;
+constexpr uint32_t kMaxRecsPerSeq = 6;  // 1 + 2 literal splits + 2 match splits, + 1 spare
+constexpr uint32_t kFlushAbove = kWave - kMaxRecsPerSeq;
+
+__device__ __forceinline__ void report(unsigned long long* err, uint32_t code, uint32_t idx) {
+  if (err) atomicCAS(err, 0ull, (static_cast<unsigned long long>(code) << 32) | idx);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return uint64_t(uni(uint32_t(v))) | (uint64_t(uni(uint32_t(v >> 32))) << 32);
+}
+
+__device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t lane) {
+  return uint32_t(__builtin_amdgcn_ds_bpermute(int(lane << 2), int(v)));
+}
+
+// DPP wave64 inclusive scans (row_shr within 16-lane rows, then row_bcast:15 / row_bcast:31
+// across rows -- gfx9 DPP): six VALU ops instead of six LDS permutes.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), kCtrl, kRowMask, 0xF, false));
+}
+__device__ __forceinline__ uint32_t scan_add(uint32_t v) {
+  v += dpp<0x111, 0xF>(v);
+  v += dpp<0x112, 0xF>(v);
+  v += dpp<0x114, 0xF>(v);
+  v += dpp<0x118, 0xF>(v);
+  v += dpp<0x142, 0xA>(v);
+  v += dpp<0x143, 0xC>(v);
+  return v;
+}
+__device__ __forceinline__ uint32_t scan_max(uint32_t v) {
+  v = max(v, dpp<0x111, 0xF>(v));
+  v = max(v, dpp<0x112, 0xF>(v));
+  v = max(v, dpp<0x114, 0xF>(v));
+  v = max(v, dpp<0x118, 0xF>(v));
+  v = max(v, dpp<0x142, 0xA>(v));
+  v = max(v, dpp<0x143, 0xC>(v));
+  return v;
+}
+
+// Smallest lane s with a[s] >= t (a non-decreasing over lanes); 64 if none.
+__device__ __forceinline__ uint32_t find_ge(uint32_t a, uint32_t t) {
+  uint32_t j = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) {
+    const uint32_t v = shfl(a, j + step - 1);
+    j += v < t ? step : 0u;
+  }
+  return j;
+}
+
+// k mod o for k < 2^16, 1 <= o < 2^16 (float reciprocal estimate + one correction).
+__device__ __forceinline__ uint32_t umod16(uint32_t k, uint32_t o) {
+  const int q = int(float(k) * __builtin_amdgcn_rcpf(float(o)));
+  int r = int(k) - q * int(o);
+  r += r < 0 ? int(o) : 0;
+  r -= r >= int(o) ? int(o) : 0;
+  return uint32_t(r);
+}
+
+struct Ctx {
+  const uint8_t* pay;  // chunk payload (LZ4 frame)
+  uint8_t* out;        // chunk output
+  uint32_t clen, ulen;
+  bool bg4;
+  uint32_t g1, g2, g3;  // BG4 group starts in the grouped stream
+  uint32_t sbase;       // payload offset where the next batch's first gap starts
+  uint32_t obase;       // output (grouped) offset of the next batch
+  uint32_t* heads;      // this wave's 64-entry LDS scratch
+};
+
+// Grouped-stream position -> byte offset in the chunk (identity unless BG4).
+__device__ __forceinline__ uint32_t bmap(const Ctx& X, uint32_t p) {
+  if (!X.bg4) return p;
+  const uint32_t a1 = p >= X.g1, a2 = p >= X.g2, a3 = p >= X.g3;
+  uint32_t base = a1 ? X.g1 : 0u;
+  base = a2 ? X.g2 : base;
+  base = a3 ? X.g3 : base;
+  return 4 * (p - base) + a1 + a2 + a3;
+}
+
+// Records of the current batch: lane i holds record i (rl = gap | lit << 16, rh = ml | off << 16).
+struct Batch {
+  uint32_t rl, rh;  // per lane
+  uint32_t n;       // uniform: records held
+  uint32_t gs;      // uniform: stream position where the next record's gap starts
+};
+
+// Lane -> index of the record whose [excl, incl) byte range covers byte t0 + lane: records that
+// intersect the pass write their index at their first byte in the pass (unique), then a max-scan.
+__device__ __forceinline__ uint32_t owner(const Ctx& X, uint32_t excl, uint32_t incl, uint32_t t0, uint32_t lane) {
+  X.heads[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (incl > excl && excl < t0 + kWave && incl > t0) X.heads[excl > t0 ? excl - t0 : 0] = lane;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const uint32_t h = X.heads[lane];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return scan_max(h);
+}
+
+// Execute the batch's records.  Returns false (nothing written for the bad records) when any
+// record is out of range.
+__device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
+  const uint32_t gap = B.rl & 0xFFFF, lit = B.rl >> 16, ml = B.rh & 0xFFFF, off = B.rh >> 16;
+  const uint32_t a1 = scan_add(gap + lit), a2 = scan_add(lit + ml);
+  const uint32_t li = scan_add(lit), mi = scan_add(ml);
+  const uint32_t lpos = X.sbase + a1 - lit;   // payload offset of this record's literals
+  const uint32_t opos = X.obase + a2 - lit - ml;  // output offset of the record
+  const uint32_t mstart = opos + lit;          // output offset of its match
+  const bool bad = lpos + lit > X.clen || mstart + ml > X.ulen || (ml && (off == 0 || off > mstart));
+  B.n = 0;
+  B.rl = B.rh = 0;
+  if (__builtin_amdgcn_ballot_w64(bad)) return false;
+  const uint32_t ltot = __builtin_amdgcn_readlane(li, 63), mtot = __builtin_amdgcn_readlane(mi, 63);
+  X.sbase += __builtin_amdgcn_readlane(a1, 63);
+  X.obase += __builtin_amdgcn_readlane(a2, 63);
+  for (uint32_t t0 = 0; t0 < ltot; t0 += kWave) {  // literal bytes, one per lane
+    const uint32_t t = t0 + lane;
+    const uint32_t s = owner(X, li - lit, li, t0, lane);
+    const uint32_t k = t - shfl(li - lit, s);
+    const uint32_t from = shfl(lpos, s) + k, to = shfl(opos, s) + k;
+    if (t < ltot) X.out[bmap(X, to)] = X.pay[from];
+  }
+  for (uint32_t t0 = 0; t0 < mtot; t0 += kWave) {  // match bytes, one per lane
+    const uint32_t t = t0 + lane;
+    const bool on = t < mtot;
+    const uint32_t s = owner(X, mi - ml, mi, t0, lane);
+    const uint32_t k = t - shfl(mi - ml, s);
+    const uint32_t st = shfl(mstart, s);
+    uint32_t o = shfl(off, s);
+    o = o ? o : 1u;
+    const uint32_t d = on ? st + k : 0xFFFFFFFFu;
+    uint32_t q = on ? st - o + umod16(k, o) : 0u;  // periodic source, before the match start
+    const uint32_t dfirst = uni(d);                 // lane 0 is always on
+    if (__builtin_amdgcn_ballot_w64(on && q >= dfirst)) {
+      while (true) {  // sources written by this pass: take the writer's source instead
+        uint32_t j = find_ge(d, q);
+        j = j > 63 ? 63 : j;
+        const bool pend = on && shfl(d, j) == q;
+        if (!__builtin_amdgcn_ballot_w64(pend)) break;
+        const uint32_t qj = shfl(q, j);
+        q = pend ? qj : q;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // earlier passes / literals have reached L2
+    if (on) X.out[bmap(X, d)] = uint8_t(load_u8_coherent(X.out + bmap(X, q)));
+  }
+  return true;
+}
+
+// Append one LZ4 sequence (literal run at stream position lp) as records; lengths are split at
+// 0xFFFF (continuations have gap 0; a split match keeps its offset, exact for LZ4's byte-
+// sequential copy).  A chunk is <= 128 KiB, so one call adds at most kMaxRecsPerSeq records; the
+// caller executes the batch before it could overflow.
+__device__ __forceinline__ bool emit(Batch& B, Ctx& X, uint32_t lane, uint32_t lp, uint32_t lit, uint32_t ml,
+                                     uint32_t off) {
+  uint32_t gap = lp - B.gs;
+  if (gap > 0xFFFFu) return false;
+  B.gs = lp + lit;
+  do {
+    const uint32_t l = lit > 0xFFFFu ? 0xFFFFu : lit;
+    const uint32_t m = lit > 0xFFFFu ? 0u : (ml > 0xFFFFu ? 0xFFFFu : ml);
+    const bool me = lane == B.n;  // the lane that holds this record
+    B.rl = me ? gap | (l << 16) : B.rl;
+    B.rh = me ? m | ((m ? off : 0u) << 16) : B.rh;
+    ++B.n;
+    gap = 0;
+    lit -= l;
+    ml -= m;
+  } while (lit | ml);
+  return true;
+}
+
+// Decode one LZ4 frame chunk; returns 0 or an error code.
+__device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
+  Win w;
+  win_init(w, X.pay, lane);
+  const uint32_t k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);  // stream pos = k0 + byte index
+  const uint32_t end = k0 + X.clen;
+  if (X.clen < 7) return ZG_ERR_LZ4;
+  const uint32_t magic = win_u8(w, k0) | (win_u8(w, k0 + 1) << 8) | (win_u8(w, k0 + 2) << 16) |
+                         (win_u8(w, k0 + 3) << 24);
+  if (magic != 0x184D2204u) return ZG_ERR_LZ4;
+  const uint32_t flg = win_u8(w, k0 + 4);
+  if ((flg >> 6) != 1) return ZG_ERR_LZ4;
+  uint32_t ip = k0 + 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+  const uint32_t bck = (flg & 0x10) ? 4 : 0;
+  Batch B{0, 0, 0, k0};
+  while (true) {
+    if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+    if (ip > end || end - ip < 4) return ZG_ERR_LZ4;
+    win_seek(w, ip, lane);
+    const uint32_t bs = win_u8(w, ip) | (win_u8(w, ip + 1) << 8) | (win_u8(w, ip + 2) << 16) |
+                        (win_u8(w, ip + 3) << 24);
+    ip += 4;
+    if (bs == 0) break;
+    const uint32_t len = bs & 0x7FFFFFFFu;
+    if (len > end - ip) return ZG_ERR_LZ4;
+    if (bs >> 31) {  // stored block
+      if (!emit(B, X, lane, ip, len, 0, 0)) return ZG_ERR_LZ4;
+      ip += len;
+    } else {
+      const uint32_t bend = uni(ip + len);
+      while (true) {
+        // loop-carried parse state is wave-uniform; the compiler's uniformity analysis loses track
+        // of it through the batch execution inlined into this loop, so restate it (one
+        // v_readfirstlane each) and keep every compare and branch of the parse on the scalar unit
+        ip = uni(ip);
+        w.wofs = uni(w.wofs);
+        B.n = uni(B.n);
+        B.gs = uni(B.gs);
+        if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+        if (ip >= bend) return ZG_ERR_LZ4;
+        win_seek(w, ip, lane);
+        // Fast loop over the common short sequence (literals < 15, match < 19: no length bytes):
+        // one window gather per sequence aligned to its literals (lane l = stream byte ip + 1 + l)
+        // gives the offset and the NEXT token by read-lanes; records go straight into lane n.
+        // Stays inside the 256-byte window half and the batch; everything else falls through to
+        // the general path below.
+        {
+          const uint32_t lim_blk = bend > 18 ? bend - 18 : 0u;  // >= 18 bytes left: never the last sequence
+          const uint32_t lim_win = w.wofs + 256;                 // gathered bytes stay inside w0 | w1
+          const uint32_t lim_ip = min(lim_blk, lim_win);
+          uint32_t n = B.n, gs = B.gs, rl = B.rl, rh = B.rh;
+          uint32_t token = win_u8(w, ip);
+          while (ip < lim_ip && n < kWave) {
+            const uint32_t lit = token >> 4, mlc = token & 15;
+            if (lit == 15 || mlc == 15) break;
+            const uint32_t v = win_lane_u8(w, ip + 1, lane);
+            const uint32_t off = __builtin_amdgcn_readlane(v, int(lit)) |
+                                 (__builtin_amdgcn_readlane(v, int(lit + 1)) << 8);
+            const uint32_t next = __builtin_amdgcn_readlane(v, int(lit + 2));
+            const bool me = lane == n;
+            rl = me ? (ip + 1 - gs) | (lit << 16) : rl;
+            rh = me ? (mlc + 4) | (off << 16) : rh;
+            gs = ip + 1 + lit;
+            ip += 3 + lit;
+            ++n;
+            token = next;
+          }
+          B.n = n;
+          B.gs = gs;
+          B.rl = rl;
+          B.rh = rh;
+          // batch full (execute) or window exhausted (slide): back to the top; a long-length or
+          // near-block-end sequence takes the general path (with room for its split records)
+          if (n > kFlushAbove || (ip >= lim_win && ip < lim_blk)) continue;
+        }
+        const uint32_t token = win_u8(w, ip);
+        ++ip;
+        uint32_t lit = token >> 4, ml = token & 15;
+        if (lit == 15) {
+          uint32_t b;
+          do {
+            if (ip >= bend || lit > kMaxChunk) return ZG_ERR_LZ4;
+            win_seek(w, ip, lane);
+            b = win_u8(w, ip);
+            ++ip;
+            lit += b;
+          } while (b == 255);
+        }
+        if (lit > bend - ip) return ZG_ERR_LZ4;
+        const uint32_t lp = ip;
+        ip += lit;
+        if (ip == bend) {  // last sequence of the block: literals only
+          if (!emit(B, X, lane, lp, lit, 0, 0)) return ZG_ERR_LZ4;
+          break;
+        }
+        if (bend - ip < 2) return ZG_ERR_LZ4;
+        win_seek(w, ip, lane);
+        const uint32_t off = win_u8(w, ip) | (win_u8(w, ip + 1) << 8);
+        ip += 2;
+        if (ml == 15) {
+          uint32_t b;
+          do {
+            if (ip >= bend || ml > kMaxChunk) return ZG_ERR_LZ4;
+            win_seek(w, ip, lane);
+            b = win_u8(w, ip);
+            ++ip;
+            ml += b;
+          } while (b == 255);
+        }
+        if (!emit(B, X, lane, lp, lit, ml + 4, off)) return ZG_ERR_LZ4;
+      }
+    }
+    ip += bck;
+  }
+  if (B.n && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+  return X.obase == X.ulen ? 0u : uint32_t(ZG_ERR_SIZE);
+}
+
+__global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                     const ZgChunk* __restrict__ chunks, int n_chunks,
+                                                     unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
+  __shared__ uint32_t heads[kWavesPerBlock][kWave];
+  const uint32_t lane = lane_id();
+  const int wave = int(uni(threadIdx.x >> 6));
+  const int stride = int(gridDim.x) * kWavesPerBlock;
+  for (int c = int(uni(blockIdx.x * kWavesPerBlock + uint32_t(wave))); c < n_chunks; c += stride) {
+    ZgChunk ch = chunks[c];
+    // the descriptor is wave-uniform: say so, so the whole parse runs on SGPRs / the scalar unit
+    // (a vector load would otherwise make every derived position a VGPR and every branch divergent)
+    ch.src = uni64(ch.src);
+    ch.dst = uni64(ch.dst);
+    ch.clen = uni(ch.clen);
+    ch.ulen = uni(ch.ulen);
+    ch.scheme = uni(ch.scheme);
+    if (ch.scheme == 0) continue;
+    if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
+      if (lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
+      continue;
+    }
+    if (ch.ulen > kMaxChunk) {
+      if (lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      continue;
+    }
+    Ctx X;
+    X.pay = src + ch.src;
+    X.out = dst + ch.dst;
+    X.clen = ch.clen;
+    X.ulen = ch.ulen;
+    X.bg4 = ch.scheme == 2;
+    const uint32_t q = ch.ulen >> 2, r = ch.ulen & 3;
+    X.g1 = q + (r > 0 ? 1u : 0u);
+    X.g2 = X.g1 + q + (r > 1 ? 1u : 0u);
+    X.g3 = X.g2 + q + (r > 2 ? 1u : 0u);
+    X.sbase = 0;
+    X.obase = 0;
+    X.heads = heads[wave];
+    const uint32_t code = decode_chunk(X, lane);
+    if (code && lane == 0) report(err, code, uint32_t(c));
+  }
+}
+
+}  // namespace
+
+extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                            const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                            hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  // ZG_LZ4_GRID caps the persistent grid (occupancy experiments).
+  static const int grid_cap = [] {
+    const char* v = getenv("ZG_LZ4_GRID");
+    const int g = v ? atoi(v) : 0;
+    return g > 0 && g < 8192 ? g : 2048;
+  }();
+  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(k_lz4_batched, dim3(blocks < grid_cap ? blocks : grid_cap), dim3(256), 0, stream, src, dst,
+                     chunks, n_chunks, err, src_n, dst_n);
+  return hipGetLastError();
+}

@@ -63,9 +63,13 @@ hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, 
 // one per concurrently running launch): compressed chunks that straddle the window decode there
 // before their clipped part is copied out.  Without it such a launch returns hipErrorInvalidValue.
 #define ZG_CLIP_SCRATCH_BYTES (2u * (128u * 1024u + 256u))
+// Unclipped launches decode LZ4 chunks with the batched decoder (lz4seq.hip: scalar parse into
+// lane registers + lane-parallel execute); clipped ones with the LDS-ring decoder (ingest.hip).
 hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                            const ZgChunk* chunks, int n_chunks, uint64_t clip_lo, uint64_t clip_hi,
                            uint8_t* clip_scratch, unsigned long long* err, hipStream_t stream);
+hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                 const ZgChunk* chunks, int n_chunks, unsigned long long* err, hipStream_t stream);
 hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
                           uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, hipStream_t stream);
 // Hash raw (offset, len) messages with the Xet data key: out[i] = keyed(DATA_KEY, buf[off:off+len]).

@@ -167,6 +167,7 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     terms: TERM_DTYPE records; chunk_base indexes `hashes` (uint8 [N, 32]) relative to hash_base.
     clip: optional (lo, hi) arena byte window this rank owns: bytes outside are not written, and
     the hashes of chunks not entirely inside the window are unspecified.
+    LZ4 chunks take the batched decoder (lz4seq.hip) unless clipped (LDS-ring decoder).
     """
     terms = np.ascontiguousarray(terms, dtype=TERM_DTYPE)
     nt = len(terms)
@@ -206,8 +207,9 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     ws.err.zero_()
     ws.chunks[: n_chunks * CHUNK_DTYPE.itemsize].zero_()  # gaps between terms become no-op descriptors
     H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(), ws.err.data_ptr(), st)
+    clipped = lo > 0 or hi < dst_n
     H.place_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, lo, hi,
-                   ws.err.data_ptr(), st, ws.clip_scratch() if (lo > 0 or hi < dst_n) else 0)
+                   ws.err.data_ptr(), st, ws.clip_scratch() if clipped else 0)
     hptr = hashes.data_ptr() + 32 * hash_base
     H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st)
     if check:
