@@ -44,6 +44,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kMaxChunk = 128u * 1024u;
 constexpr uint32_t kMaxRecsPerSeq = 6;  // 1 + 2 literal splits + 2 match splits, + 1 spare
 constexpr uint32_t kFlushAbove = kWave - kMaxRecsPerSeq;
+constexpr uint32_t kRing = 4096;  // LDS history per wave (power of two): 8 waves / SIMD stay resident
 
 __device__ __forceinline__ void report(unsigned long long* err, uint32_t code, uint32_t idx) {
   if (err) atomicCAS(err, 0ull, (static_cast<unsigned long long>(code) << 32) | idx);
@@ -113,6 +114,7 @@ struct Ctx {
   uint32_t sbase;       // payload offset where the next batch's first gap starts
   uint32_t obase;       // output (grouped) offset of the next batch
   uint32_t* heads;      // this wave's 64-entry LDS scratch
+  uint8_t* ring;        // this wave's kRing-byte LDS history of recent output
 };
 
 // Grouped-stream position -> byte offset in the chunk (identity unless BG4).
@@ -147,8 +149,54 @@ __device__ __forceinline__ uint32_t owner(const Ctx& X, uint32_t excl, uint32_t 
   return scan_max(h);
 }
 
+// One match pass: lane -> (destination d, resolved source q) for match bytes t0 .. t0 + 63.
+struct MatchLane {
+  uint32_t d, q;
+  bool on;
+};
+
+__device__ __forceinline__ MatchLane match_pass(const Ctx& X, uint32_t mi, uint32_t ml, uint32_t mstart, uint32_t off,
+                                                uint32_t mtot, uint32_t t0, uint32_t lane) {
+  MatchLane m;
+  const uint32_t t = t0 + lane;
+  m.on = t < mtot;
+  const uint32_t s = owner(X, mi - ml, mi, t0, lane);
+  const uint32_t k = t - shfl(mi - ml, s);
+  const uint32_t st = shfl(mstart, s);
+  uint32_t o = shfl(off, s);
+  o = o ? o : 1u;
+  m.d = m.on ? st + k : 0xFFFFFFFFu;
+  m.q = m.on ? st - o + umod16(k, o) : 0u;  // periodic source, before the match start
+  const uint32_t dfirst = uni(m.d);           // lane 0 is always on
+  if (__builtin_amdgcn_ballot_w64(m.on && m.q >= dfirst)) {
+    while (true) {  // sources written by this same pass: take the writer's source instead
+      uint32_t j = find_ge(m.d, m.q);
+      j = j > 63 ? 63 : j;
+      const bool pend = m.on && shfl(m.d, j) == m.q;
+      if (!__builtin_amdgcn_ballot_w64(pend)) break;
+      const uint32_t qj = shfl(m.q, j);
+      m.q = pend ? qj : m.q;
+    }
+  }
+  return m;
+}
+
+// Output byte -> LDS history ring (recent output, for near match sources) and HBM.
+__device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
+  X.ring[p & (kRing - 1)] = uint8_t(v);
+  X.out[bmap(X, p)] = uint8_t(v);
+}
+
 // Execute the batch's records.  Returns false (nothing written for the bad records) when any
 // record is out of range.
+//
+// Sources: a byte less than kRing behind the batch's last output byte is still in this wave's LDS
+// ring (nothing newer has wrapped onto its slot, and a short batch writes no two bytes kRing
+// apart); older ("far") bytes come from HBM through L2.
+// All far bytes of a short batch precede the batch, and the s_waitcnt at batch start has made
+// every earlier store visible, so up to four passes' far loads are issued together and no pass
+// waits on a store.  A long batch (a long literal run) can have far sources inside itself: its
+// passes run one at a time, each after s_waitcnt vmcnt(0).
 __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   const uint32_t gap = B.rl & 0xFFFF, lit = B.rl >> 16, ml = B.rh & 0xFFFF, off = B.rh >> 16;
   const uint32_t a1 = scan_add(gap + lit), a2 = scan_add(lit + ml);
@@ -161,38 +209,69 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   B.rl = B.rh = 0;
   if (__builtin_amdgcn_ballot_w64(bad)) return false;
   const uint32_t ltot = __builtin_amdgcn_readlane(li, 63), mtot = __builtin_amdgcn_readlane(mi, 63);
+  const uint32_t span = __builtin_amdgcn_readlane(a2, 63);
   X.sbase += __builtin_amdgcn_readlane(a1, 63);
-  X.obase += __builtin_amdgcn_readlane(a2, 63);
-  for (uint32_t t0 = 0; t0 < ltot; t0 += kWave) {  // literal bytes, one per lane
-    const uint32_t t = t0 + lane;
-    const uint32_t s = owner(X, li - lit, li, t0, lane);
-    const uint32_t k = t - shfl(li - lit, s);
-    const uint32_t from = shfl(lpos, s) + k, to = shfl(opos, s) + k;
-    if (t < ltot) X.out[bmap(X, to)] = X.pay[from];
-  }
-  for (uint32_t t0 = 0; t0 < mtot; t0 += kWave) {  // match bytes, one per lane
-    const uint32_t t = t0 + lane;
-    const bool on = t < mtot;
-    const uint32_t s = owner(X, mi - ml, mi, t0, lane);
-    const uint32_t k = t - shfl(mi - ml, s);
-    const uint32_t st = shfl(mstart, s);
-    uint32_t o = shfl(off, s);
-    o = o ? o : 1u;
-    const uint32_t d = on ? st + k : 0xFFFFFFFFu;
-    uint32_t q = on ? st - o + umod16(k, o) : 0u;  // periodic source, before the match start
-    const uint32_t dfirst = uni(d);                 // lane 0 is always on
-    if (__builtin_amdgcn_ballot_w64(on && q >= dfirst)) {
-      while (true) {  // sources written by this pass: take the writer's source instead
-        uint32_t j = find_ge(d, q);
-        j = j > 63 ? 63 : j;
-        const bool pend = on && shfl(d, j) == q;
-        if (!__builtin_amdgcn_ballot_w64(pend)) break;
-        const uint32_t qj = shfl(q, j);
-        q = pend ? qj : q;
+  X.obase += span;
+  const uint32_t oend = X.obase;  // one past the batch's last output byte
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // earlier batches' stores are in L2
+  // literal bytes, one per lane; four passes' loads in flight at once
+  for (uint32_t g0 = 0; g0 < ltot; g0 += 4 * kWave) {
+    uint32_t to[4], v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t t0 = g0 + uint32_t(j) * kWave;
+      to[j] = 0xFFFFFFFFu;
+      v[j] = 0;
+      if (t0 < ltot) {
+        const uint32_t t = t0 + lane;
+        const uint32_t s = owner(X, li - lit, li, t0, lane);
+        const uint32_t k = t - shfl(li - lit, s);
+        const uint32_t from = shfl(lpos, s) + k, dst = shfl(opos, s) + k;  // all lanes shuffle
+        if (t < ltot) {
+          to[j] = dst;
+          v[j] = X.pay[from];
+        }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // earlier passes / literals have reached L2
-    if (on) X.out[bmap(X, d)] = uint8_t(load_u8_coherent(X.out + bmap(X, q)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (to[j] != 0xFFFFFFFFu) put_byte(X, to[j], v[j]);
+  }
+  if (span + 4 * kWave < kRing) {
+    // short batch: far sources all precede it (already visible); group four passes
+    for (uint32_t g0 = 0; g0 < mtot; g0 += 4 * kWave) {
+      MatchLane m[4];
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t t0 = g0 + uint32_t(j) * kWave;
+        m[j].on = false;
+        v[j] = 0;
+        if (t0 < mtot) {
+          m[j] = match_pass(X, mi, ml, mstart, off, mtot, t0, lane);
+          if (m[j].on && oend - m[j].q >= kRing) v[j] = load_u8_coherent(X.out + bmap(X, m[j].q));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!m[j].on) continue;
+        const uint32_t x = oend - m[j].q >= kRing ? v[j] : uint32_t(X.ring[m[j].q & (kRing - 1)]);
+        put_byte(X, m[j].d, x);
+      }
+    }
+  } else {
+    // Long batch: its literal phase wrote bytes kRing or more apart out of position order (a
+    // literal can be overwritten in the ring by an earlier match byte kRing before it), so the
+    // ring is not trusted here: every source is read back from HBM, one pass at a time, and the
+    // ring is rebuilt from HBM afterwards.
+    for (uint32_t t0 = 0; t0 < mtot; t0 += kWave) {
+      const MatchLane m = match_pass(X, mi, ml, mstart, off, mtot, t0, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this batch's earlier stores are in L2
+      if (m.on) X.out[bmap(X, m.d)] = uint8_t(load_u8_coherent(X.out + bmap(X, m.q)));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t lo = oend > kRing ? oend - kRing : 0u;
+    for (uint32_t p = lo + lane; p < oend; p += kWave) X.ring[p & (kRing - 1)] = uint8_t(load_u8_coherent(X.out + bmap(X, p)));
   }
   return true;
 }
@@ -342,6 +421,7 @@ __global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__
                                                      const ZgChunk* __restrict__ chunks, int n_chunks,
                                                      unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
   __shared__ uint32_t heads[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][kRing];
   const uint32_t lane = lane_id();
   const int wave = int(uni(threadIdx.x >> 6));
   const int stride = int(gridDim.x) * kWavesPerBlock;
@@ -376,6 +456,7 @@ __global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__
     X.sbase = 0;
     X.obase = 0;
     X.heads = heads[wave];
+    X.ring = rings[wave];
     const uint32_t code = decode_chunk(X, lane);
     if (code && lane == 0) report(err, code, uint32_t(c));
   }
