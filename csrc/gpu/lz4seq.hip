@@ -299,17 +299,27 @@ __device__ __forceinline__ bool emit(Batch& B, Ctx& X, uint32_t lane, uint32_t l
   return true;
 }
 
+// Stream reader for the (wave-uniform) parse: 8 bytes at stream position p through a scalar
+// load (s_load_dwordx2 at the dword below p).  The compressed payload is read-only for the whole
+// kernel, so the scalar data cache may serve it, and the parse then never waits on the vector
+// memory counter -- which on gfx9 also counts this wave's output stores (the compiler cannot prove
+// the payload unclobbered by those stores, so it would otherwise emit vector loads).  Loads only;
+// nothing is ever written through the scalar cache.  Bytes p .. p+4 are valid in the result.
+__device__ __forceinline__ uint64_t sload8(const uint32_t* w4, uint32_t p) {
+  uint64_t v;
+  const uint32_t off = p & ~3u;
+  asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(w4), "s"(off));
+  return v >> (8 * (p & 3));
+}
+
 // Decode one LZ4 frame chunk; returns 0 or an error code.
 __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
-  Win w;
-  win_init(w, X.pay, lane);
   const uint32_t k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);  // stream pos = k0 + byte index
+  const uint32_t* w4 = reinterpret_cast<const uint32_t*>(X.pay - k0);
   const uint32_t end = k0 + X.clen;
   if (X.clen < 7) return ZG_ERR_LZ4;
-  const uint32_t magic = win_u8(w, k0) | (win_u8(w, k0 + 1) << 8) | (win_u8(w, k0 + 2) << 16) |
-                         (win_u8(w, k0 + 3) << 24);
-  if (magic != 0x184D2204u) return ZG_ERR_LZ4;
-  const uint32_t flg = win_u8(w, k0 + 4);
+  if (uint32_t(sload8(w4, k0)) != 0x184D2204u) return ZG_ERR_LZ4;
+  const uint32_t flg = uint32_t(sload8(w4, k0 + 4)) & 0xFF;
   if ((flg >> 6) != 1) return ZG_ERR_LZ4;
   uint32_t ip = k0 + 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
   const uint32_t bck = (flg & 0x10) ? 4 : 0;
@@ -317,9 +327,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
   while (true) {
     if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
     if (ip > end || end - ip < 4) return ZG_ERR_LZ4;
-    win_seek(w, ip, lane);
-    const uint32_t bs = win_u8(w, ip) | (win_u8(w, ip + 1) << 8) | (win_u8(w, ip + 2) << 16) |
-                        (win_u8(w, ip + 3) << 24);
+    const uint32_t bs = uint32_t(sload8(w4, ip));
     ip += 4;
     if (bs == 0) break;
     const uint32_t len = bs & 0x7FFFFFFFu;
@@ -334,55 +342,45 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
         // of it through the batch execution inlined into this loop, so restate it (one
         // v_readfirstlane each) and keep every compare and branch of the parse on the scalar unit
         ip = uni(ip);
-        w.wofs = uni(w.wofs);
         B.n = uni(B.n);
         B.gs = uni(B.gs);
         if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
         if (ip >= bend) return ZG_ERR_LZ4;
-        win_seek(w, ip, lane);
         // Fast loop over the common short sequence (literals < 15, match < 19: no length bytes):
-        // one window gather per sequence aligned to its literals (lane l = stream byte ip + 1 + l)
-        // gives the offset and the NEXT token by read-lanes; records go straight into lane n.
-        // Stays inside the 256-byte window half and the batch; everything else falls through to
-        // the general path below.
+        // one 8-byte read at the end of its literals gives the offset and the NEXT token, so the
+        // dependent chain is one scalar load per sequence; records go straight into lane n.
         {
           const uint32_t lim_blk = bend > 18 ? bend - 18 : 0u;  // >= 18 bytes left: never the last sequence
-          const uint32_t lim_win = w.wofs + 256;                 // gathered bytes stay inside w0 | w1
-          const uint32_t lim_ip = min(lim_blk, lim_win);
           uint32_t n = B.n, gs = B.gs, rl = B.rl, rh = B.rh;
-          uint32_t token = win_u8(w, ip);
-          while (ip < lim_ip && n < kWave) {
+          uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
+          while (ip < lim_blk && n < kWave) {
             const uint32_t lit = token >> 4, mlc = token & 15;
             if (lit == 15 || mlc == 15) break;
-            const uint32_t v = win_lane_u8(w, ip + 1, lane);
-            const uint32_t off = __builtin_amdgcn_readlane(v, int(lit)) |
-                                 (__builtin_amdgcn_readlane(v, int(lit + 1)) << 8);
-            const uint32_t next = __builtin_amdgcn_readlane(v, int(lit + 2));
+            const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
             const bool me = lane == n;
             rl = me ? (ip + 1 - gs) | (lit << 16) : rl;
-            rh = me ? (mlc + 4) | (off << 16) : rh;
+            rh = me ? (mlc + 4) | (y << 16) : rh;
             gs = ip + 1 + lit;
             ip += 3 + lit;
             ++n;
-            token = next;
+            token = (y >> 16) & 0xFF;
           }
           B.n = n;
           B.gs = gs;
           B.rl = rl;
           B.rh = rh;
-          // batch full (execute) or window exhausted (slide): back to the top; a long-length or
-          // near-block-end sequence takes the general path (with room for its split records)
-          if (n > kFlushAbove || (ip >= lim_win && ip < lim_blk)) continue;
+          // batch full: back to the top to execute it; a long-length or near-block-end sequence
+          // takes the general path (with room for its split records)
+          if (n > kFlushAbove) continue;
         }
-        const uint32_t token = win_u8(w, ip);
+        const uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
         ++ip;
         uint32_t lit = token >> 4, ml = token & 15;
         if (lit == 15) {
           uint32_t b;
           do {
             if (ip >= bend || lit > kMaxChunk) return ZG_ERR_LZ4;
-            win_seek(w, ip, lane);
-            b = win_u8(w, ip);
+            b = uint32_t(sload8(w4, ip)) & 0xFF;
             ++ip;
             lit += b;
           } while (b == 255);
@@ -395,15 +393,13 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
           break;
         }
         if (bend - ip < 2) return ZG_ERR_LZ4;
-        win_seek(w, ip, lane);
-        const uint32_t off = win_u8(w, ip) | (win_u8(w, ip + 1) << 8);
+        const uint32_t off = uint32_t(sload8(w4, ip)) & 0xFFFF;
         ip += 2;
         if (ml == 15) {
           uint32_t b;
           do {
             if (ip >= bend || ml > kMaxChunk) return ZG_ERR_LZ4;
-            win_seek(w, ip, lane);
-            b = win_u8(w, ip);
+            b = uint32_t(sload8(w4, ip)) & 0xFF;
             ++ip;
             ml += b;
           } while (b == 255);
