@@ -101,6 +101,7 @@ void print_usage(std::ostream& w) {
        "\n"
        "Bench options:\n"
        "  --synthetic              Run synthetic benchmarks\n"
+       "  --gpu                    Run the MI355X kernel benchmarks\n"
        "  --json                   Output results as JSON\n"
        "\n"
        "Examples:\n"
@@ -406,18 +407,53 @@ int cmd_seed(const std::string& exe, const std::vector<std::string>& a) {
   return 0;
 }
 
-int cmd_bench(const std::vector<std::string>& a) {
-  bool json = false, synthetic = false, core_only = false;
+// `python -m <module> <args>` as a child process of this CLI (the package directory next to the
+// binary on PYTHONPATH); returns its exit code.  The CLI never initialises the GPU itself.
+int run_python_module(const std::string& exe, const std::string& module, const std::vector<std::string>& extra) {
+  std::string pkg_parent = exe;  // <pkg_parent>/zest_amd/_bin/zest
+  for (int i = 0; i < 3; ++i) {
+    const size_t s = pkg_parent.rfind('/');
+    pkg_parent = s == std::string::npos ? "." : pkg_parent.substr(0, s);
+  }
+  std::string pp = pkg_parent;
+  if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
+  ::setenv("PYTHONPATH", pp.c_str(), 1);
+  const char* py = std::getenv("ZEST_PYTHON");
+  std::vector<std::string> args = {py ? py : "python3", "-m", module};
+  args.insert(args.end(), extra.begin(), extra.end());
+  std::vector<char*> argv;
+  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
+  argv.push_back(nullptr);
+  pid_t pid = 0;
+  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
+    std::cerr << "Error: cannot start " << argv[0] << " -m " << module << "\n";
+    return 127;
+  }
+  int status = 0;
+  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  }
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+}
+
+int cmd_bench(const std::string& exe, const std::vector<std::string>& a) {
+  bool json = false, synthetic = false, core_only = false, gpu = false;
   for (auto& f : a) {
     if (f == "--json") json = true;
     else if (f == "--synthetic") synthetic = true;
     else if (f == "--core") core_only = true;
+    else if (f == "--gpu") gpu = true;
+  }
+  if (gpu) {  // device rows (K1-K6 kernels, H2D), same JSON schema: zest_amd/gpubench.py
+    std::vector<std::string> extra;
+    if (json) extra.push_back("--json");
+    return run_python_module(exe, "zest_amd.gpubench", extra);
   }
   if (!synthetic) {
     std::cerr << "Usage: zest bench --synthetic [--json]\n"
               << "  --synthetic  Run bencode/hash/wire benchmarks\n"
               << "  --json       Output results as JSON\n"
-              << "  --core       Only the five reference rows\n";
+              << "  --core       Only the five reference rows\n"
+              << "  --gpu        MI355X kernel rows (BLAKE3, SHA-1, CDC, xorb verify, LZ4/BG4, Merkle, H2D)\n";
     return 0;
   }
   auto r = bench::run_synthetic(!core_only);
@@ -569,7 +605,7 @@ int main(int argc, char** argv) {
   try {
     if (cmd == "pull") return cmd_pull(exe, rest);
     if (cmd == "seed") return cmd_seed(exe, rest);
-    if (cmd == "bench") return cmd_bench(rest);
+    if (cmd == "bench") return cmd_bench(exe, rest);
     if (cmd == "serve") return cmd_serve(rest);
     if (cmd == "start") return cmd_start(exe);
     if (cmd == "stop") return cmd_stop();

@@ -71,6 +71,15 @@ def test_bench_synthetic_json(nodes):
     assert "Usage: zest bench --synthetic [--json]" in r.stderr
 
 
+def test_bench_gpu_rows_without_gpu(nodes):
+    # `zest bench --gpu` runs the device rows in a child python (zest_amd.gpubench); here there is no
+    # GPU, so it must say so and fail cleanly instead of crashing
+    if __import__("torch").cuda.is_available():
+        pytest.skip("GPU present: covered by tests/test_gpu_device.py::test_cli_bench_gpu")
+    r = nodes("a").run("bench", "--gpu", "--json", check=False)
+    assert r.returncode == 2 and "no GPU visible" in r.stderr
+
+
 def test_pull_cdn_only(hub, nodes):
     files = sample_files()
     commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)

@@ -136,6 +136,25 @@ def test_direct_pull_repairs_corrupt_peer(tmp_path, monkeypatch, policy):
         hub.stop()
 
 
+def test_cli_bench_gpu(tmp_path):
+    """`zest bench --gpu --json`: device rows in the reference bench's JSON schema."""
+    import json
+    import subprocess
+
+    from e2e_util import ZEST
+
+    env = dict(os.environ, ZEST_GPUBENCH_MIB="64")
+    r = subprocess.run([str(ZEST), "bench", "--gpu", "--json"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    names = [row["name"] for row in out["results"]]
+    assert names == ["blake3_64kb_gpu", "sha1_info_hash_gpu", "cdc_gpu", "xorb_verify_gpu", "lz4_decode_gpu",
+                     "merkle_gpu", "h2d_pinned_gpu"]
+    for row in out["results"]:
+        assert set(row) == {"name", "runs", "median_ns", "throughput_mbps", "bytes_processed"}
+        assert row["median_ns"] > 0 and row["throughput_mbps"] > 0
+
+
 def test_cli_pull_gpus(tmp_path):
     """`zest pull <repo> --gpus 1`: CLI spawns a torchrun GPU worker that decodes + verifies every Xet
     file on the GPU and writes the HF snapshot (single-command multi-GPU UX)."""
