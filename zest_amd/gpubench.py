@@ -12,8 +12,11 @@ row per kernel, in that schema (median over `runs` launches; throughput = bytes 
   lz4_decode_gpu       the same for BG4-LZ4 bf16 weights (K3 batched decoder + K1)
   merkle_gpu           Xet Merkle file hashes over 8 x 80k leaves (K2)
   h2d_pinned_gpu       pinned host -> HBM copy (the ingest ceiling of a one-GPU pull)
+  rccl_allgather_xorb  (N ranks) RCCL all-gather of 64 MiB xorb slabs over xGMI, bytes received
+                       per GPU (the piece exchange of the intra-node swarm)
 
     python -m zest_amd.gpubench [--json] [--mib 1024] [--runs 5]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m zest_amd.gpubench --json   # + RCCL row
 """
 from __future__ import annotations
 
@@ -139,6 +142,19 @@ def run(mib: int = 1024, runs: int = 5, device="cuda:0") -> list[dict]:
     pin = torch.empty(min(n, 1 << 30), dtype=torch.uint8).pin_memory()
     d = torch.empty(pin.numel(), dtype=torch.uint8, device=dev)
     rows.append(_row("h2d_pinned_gpu", runs, _time(lambda: d.copy_(pin, non_blocking=True), runs), pin.numel()))
+    del pin, d
+
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        world = dist.get_world_size()
+        slab = 64 << 20
+        mine = torch.empty(slab, dtype=torch.uint8, device=dev)
+        every = torch.empty(world * slab, dtype=torch.uint8, device=dev)
+        dist.barrier()
+        ns = _time(lambda: dist.all_gather_into_tensor(every, mine), runs)
+        t = torch.tensor([ns], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rows.append(_row("rccl_allgather_xorb", runs, float(t.item()), (world - 1) * slab))
     return rows
 
 
@@ -159,7 +175,14 @@ def main(argv=None) -> int:
         print("zest bench --gpu: no GPU visible", file=sys.stderr)
         return 2
     t0 = time.time()
+    rank = 0
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun: one rank per GPU, RCCL row added
+        from .parallel import init_from_env
+        rank, _world, _local, dev = init_from_env()
+        a.device = str(dev)
     rows = run(a.mib, a.runs, a.device)
+    if rank != 0:
+        return 0
     if a.json:
         print(json.dumps({"results": rows, "device": torch.cuda.get_device_name(0)}))
     else:
