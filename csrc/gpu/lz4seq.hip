@@ -42,7 +42,7 @@ using zgw::win_u8;
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kMaxChunk = 128u * 1024u;
-constexpr uint32_t kMaxRecsPerSeq = 6;  // 1 + 2 literal splits + 2 match splits, + 1 spare
+constexpr uint32_t kMaxRecsPerSeq = 8;  // 1 + 2 literal splits + 4 match splits (<= 128 KiB), + 1 spare
 constexpr uint32_t kFlushAbove = kWave - kMaxRecsPerSeq;
 constexpr uint32_t kRing = 4096;  // LDS history per wave (power of two): 8 waves / SIMD stay resident
 
@@ -111,7 +111,7 @@ struct Ctx {
   uint32_t clen, ulen;
   bool bg4;
   uint32_t g1, g2, g3;  // BG4 group starts in the grouped stream
-  uint32_t sbase;       // payload offset where the next batch's first gap starts
+  uint32_t k0;          // payload address & 3: stream position = k0 + payload byte index
   uint32_t obase;       // output (grouped) offset of the next batch
   uint32_t* heads;      // this wave's 64-entry LDS scratch
   uint8_t* ring;        // this wave's kRing-byte LDS history of recent output
@@ -128,10 +128,15 @@ __device__ __forceinline__ uint32_t bmap(const Ctx& X, uint32_t p) {
 }
 
 // Records of the current batch: lane i holds record i (rl = gap | lit << 16, rh = ml | off << 16).
+// Record formats (per lane), chosen so the common sequence costs the parse almost nothing:
+//   short (fast path): rl = literal stream position | token << 24, rh = the 4 stream bytes after
+//                      the literals (offset in the low 16 bits), rx = 0
+//   general:           rl = literal stream position, rh = offset, rx = 1 << 31 | ml << 16 | lit
+//                      (lit <= 0xFFFF, ml <= 0x7FFF after splitting)
+// Stream positions are relative to the dword-aligned payload base (k0 + byte index).
 struct Batch {
-  uint32_t rl, rh;  // per lane
-  uint32_t n;       // uniform: records held
-  uint32_t gs;      // uniform: stream position where the next record's gap starts
+  uint32_t rl, rh, rx;  // per lane
+  uint32_t n;           // uniform: records held
 };
 
 // Lane -> index of the record whose [excl, incl) byte range covers byte t0 + lane: records that
@@ -198,19 +203,23 @@ __device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
 // waits on a store.  A long batch (a long literal run) can have far sources inside itself: its
 // passes run one at a time, each after s_waitcnt vmcnt(0).
 __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
-  const uint32_t gap = B.rl & 0xFFFF, lit = B.rl >> 16, ml = B.rh & 0xFFFF, off = B.rh >> 16;
-  const uint32_t a1 = scan_add(gap + lit), a2 = scan_add(lit + ml);
+  const bool valid = lane < B.n;
+  const bool gen = (B.rx >> 31) != 0;
+  const uint32_t tok = B.rl >> 24;
+  const uint32_t lit = !valid ? 0u : gen ? (B.rx & 0xFFFF) : tok >> 4;
+  const uint32_t ml = !valid ? 0u : gen ? ((B.rx >> 16) & 0x7FFF) : (tok & 15) + 4;
+  const uint32_t off = B.rh & 0xFFFF;
+  const uint32_t lpos = (B.rl & 0xFFFFFF) - X.k0;  // payload offset of this record's literals
+  const uint32_t a2 = scan_add(lit + ml);
   const uint32_t li = scan_add(lit), mi = scan_add(ml);
-  const uint32_t lpos = X.sbase + a1 - lit;   // payload offset of this record's literals
   const uint32_t opos = X.obase + a2 - lit - ml;  // output offset of the record
   const uint32_t mstart = opos + lit;          // output offset of its match
-  const bool bad = lpos + lit > X.clen || mstart + ml > X.ulen || (ml && (off == 0 || off > mstart));
+  const bool bad = valid && (lpos + lit > X.clen || mstart + ml > X.ulen || (ml && (off == 0 || off > mstart)));
   B.n = 0;
-  B.rl = B.rh = 0;
+  B.rl = B.rh = B.rx = 0;
   if (__builtin_amdgcn_ballot_w64(bad)) return false;
   const uint32_t ltot = __builtin_amdgcn_readlane(li, 63), mtot = __builtin_amdgcn_readlane(mi, 63);
   const uint32_t span = __builtin_amdgcn_readlane(a2, 63);
-  X.sbase += __builtin_amdgcn_readlane(a1, 63);
   X.obase += span;
   const uint32_t oend = X.obase;  // one past the batch's last output byte
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // earlier batches' stores are in L2
@@ -276,27 +285,23 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   return true;
 }
 
-// Append one LZ4 sequence (literal run at stream position lp) as records; lengths are split at
-// 0xFFFF (continuations have gap 0; a split match keeps its offset, exact for LZ4's byte-
-// sequential copy).  A chunk is <= 128 KiB, so one call adds at most kMaxRecsPerSeq records; the
+// Append one LZ4 sequence (literal run at stream position lp) as general records; literal runs
+// are split at 0xFFFF and matches at 0x7FFF (a split match keeps its offset, exact for LZ4's
+// byte-sequential copy).  A chunk is <= 128 KiB, so one call adds at most kMaxRecsPerSeq records; the
 // caller executes the batch before it could overflow.
-__device__ __forceinline__ bool emit(Batch& B, Ctx& X, uint32_t lane, uint32_t lp, uint32_t lit, uint32_t ml,
-                                     uint32_t off) {
-  uint32_t gap = lp - B.gs;
-  if (gap > 0xFFFFu) return false;
-  B.gs = lp + lit;
+__device__ __forceinline__ void emit(Batch& B, uint32_t lane, uint32_t lp, uint32_t lit, uint32_t ml, uint32_t off) {
   do {
     const uint32_t l = lit > 0xFFFFu ? 0xFFFFu : lit;
-    const uint32_t m = lit > 0xFFFFu ? 0u : (ml > 0xFFFFu ? 0xFFFFu : ml);
+    const uint32_t m = lit > 0xFFFFu ? 0u : (ml > 0x7FFFu ? 0x7FFFu : ml);
     const bool me = lane == B.n;  // the lane that holds this record
-    B.rl = me ? gap | (l << 16) : B.rl;
-    B.rh = me ? m | ((m ? off : 0u) << 16) : B.rh;
+    B.rl = me ? lp : B.rl;
+    B.rh = me ? off : B.rh;
+    B.rx = me ? 0x80000000u | (m << 16) | l : B.rx;
     ++B.n;
-    gap = 0;
+    lp += l;
     lit -= l;
     ml -= m;
   } while (lit | ml);
-  return true;
 }
 
 // Stream reader for the (wave-uniform) parse: 8 bytes at stream position p through a scalar
@@ -323,7 +328,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
   if ((flg >> 6) != 1) return ZG_ERR_LZ4;
   uint32_t ip = k0 + 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
   const uint32_t bck = (flg & 0x10) ? 4 : 0;
-  Batch B{0, 0, 0, k0};
+  Batch B{0, 0, 0, 0};
   while (true) {
     if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
     if (ip > end || end - ip < 4) return ZG_ERR_LZ4;
@@ -333,7 +338,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
     const uint32_t len = bs & 0x7FFFFFFFu;
     if (len > end - ip) return ZG_ERR_LZ4;
     if (bs >> 31) {  // stored block
-      if (!emit(B, X, lane, ip, len, 0, 0)) return ZG_ERR_LZ4;
+      emit(B, lane, ip, len, 0, 0);
       ip += len;
     } else {
       const uint32_t bend = uni(ip + len);
@@ -343,35 +348,38 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
         // v_readfirstlane each) and keep every compare and branch of the parse on the scalar unit
         ip = uni(ip);
         B.n = uni(B.n);
-        B.gs = uni(B.gs);
         if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
         if (ip >= bend) return ZG_ERR_LZ4;
         // Fast loop over the common short sequence (literals < 15, match < 19: no length bytes):
         // one 8-byte read at the end of its literals gives the offset and the NEXT token, so the
         // dependent chain is one scalar load per sequence; records go straight into lane n.
         {
-          const uint32_t lim_blk = bend > 18 ? bend - 18 : 0u;  // >= 18 bytes left: never the last sequence
-          uint32_t n = B.n, gs = B.gs, rl = B.rl, rh = B.rh;
+          // A fast sequence advances ip by at most 17 bytes, so `iters` of them are known to stay
+          // >= 18 bytes before the block end (never the last sequence) and inside the batch:
+          // one counter instead of two bounds tests per sequence.
+          const uint32_t lim_blk = uni(bend > 18 ? bend - 18 : 0u);
+          uint32_t n = B.n, rl = B.rl, rh = B.rh;
           uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
-          while (ip < lim_blk && n < kWave) {
-            const uint32_t lit = token >> 4, mlc = token & 15;
-            if (lit == 15 || mlc == 15) break;
+          uint32_t iters = uni(ip < lim_blk ? min(kWave - n, (lim_blk - ip + 16) / 17) : 0u);
+          // single-exit loop (a `break` makes the structurizer route the exit flag through VALU)
+          while (iters != 0 && (token & 0xF0) != 0xF0 && (token & 0x0F) != 0x0F) {
+            iters = uni(iters - 1);
+            const uint32_t lit = token >> 4;
             const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
             const bool me = lane == n;
-            rl = me ? (ip + 1 - gs) | (lit << 16) : rl;
-            rh = me ? (mlc + 4) | (y << 16) : rh;
-            gs = ip + 1 + lit;
+            rl = me ? (ip + 1) | (token << 24) : rl;  // short record (rx stays 0)
+            rh = me ? y : rh;
             ip += 3 + lit;
             ++n;
             token = (y >> 16) & 0xFF;
           }
           B.n = n;
-          B.gs = gs;
           B.rl = rl;
           B.rh = rh;
-          // batch full: back to the top to execute it; a long-length or near-block-end sequence
-          // takes the general path (with room for its split records)
-          if (n > kFlushAbove) continue;
+          // batch full (execute) or the counted run used up while still clear of the block end
+          // (count again): back to the top; a long-length or near-block-end sequence takes the
+          // general path (with room for its split records)
+          if (n > kFlushAbove || (iters == 0 && ip < lim_blk)) continue;
         }
         const uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
         ++ip;
@@ -389,7 +397,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
         const uint32_t lp = ip;
         ip += lit;
         if (ip == bend) {  // last sequence of the block: literals only
-          if (!emit(B, X, lane, lp, lit, 0, 0)) return ZG_ERR_LZ4;
+          emit(B, lane, lp, lit, 0, 0);
           break;
         }
         if (bend - ip < 2) return ZG_ERR_LZ4;
@@ -404,7 +412,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
             ml += b;
           } while (b == 255);
         }
-        if (!emit(B, X, lane, lp, lit, ml + 4, off)) return ZG_ERR_LZ4;
+        emit(B, lane, lp, lit, ml + 4, off);
       }
     }
     ip += bck;
@@ -449,7 +457,7 @@ __global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__
     X.g1 = q + (r > 0 ? 1u : 0u);
     X.g2 = X.g1 + q + (r > 1 ? 1u : 0u);
     X.g3 = X.g2 + q + (r > 2 ? 1u : 0u);
-    X.sbase = 0;
+    X.k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);
     X.obase = 0;
     X.heads = heads[wave];
     X.ring = rings[wave];

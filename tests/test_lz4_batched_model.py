@@ -23,8 +23,8 @@ RING = 4096
 
 
 def parse_frame(frame: bytes):
-    """LZ4 frame -> list of (literal_pos, literal_len, match_len, offset) records, lengths split at
-    0xFFFF exactly like the kernel's emit()."""
+    """LZ4 frame -> list of (literal_pos, literal_len, match_len, offset) records, literal runs split
+    at 0xFFFF and matches at 0x7FFF exactly like the kernel's emit()."""
     assert struct.unpack_from("<I", frame, 0)[0] == 0x184D2204
     flg = frame[4]
     ip = 7 + (8 if flg & 8 else 0) + (4 if flg & 1 else 0)
@@ -38,7 +38,7 @@ def parse_frame(frame: bytes):
             lit -= 0xFFFF
         first = True
         while first or ml:
-            m = min(ml, 0xFFFF)
+            m = min(ml, 0x7FFF)
             recs.append((lp, lit, m, off if m else 0))
             lp += lit
             lit = 0
