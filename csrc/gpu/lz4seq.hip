@@ -362,7 +362,8 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
           uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
           uint32_t iters = uni(ip < lim_blk ? min(kWave - n, (lim_blk - ip + 16) / 17) : 0u);
           // single-exit loop (a `break` makes the structurizer route the exit flag through VALU)
-          while (iters != 0 && (token & 0xF0) != 0xF0 && (token & 0x0F) != 0x0F) {
+          // continue while iters > 0 and neither nibble is 15: one integer test (min of the three)
+          while (min(min(iters, (token & 15) ^ 15), (token >> 4) ^ 15) != 0) {
             iters = uni(iters - 1);
             const uint32_t lit = token >> 4;
             const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
