@@ -22,7 +22,9 @@ everything zest does after bytes arrive from the network.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
+import os
 import time
 from dataclasses import dataclass
 
@@ -203,6 +205,13 @@ class DevicePuller:
             self.side_stream = torch.cuda.Stream(self.device, priority=hi)
             self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
             self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
+        # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
+        # and returns, so a caller looping over step() without syncing queues thousands of commands
+        # over many steps, and past ~10 steps queued the HIP runtime fed the device measurably slower
+        # (bench.py 20 steps: 51-52.6 GB/s vs 56.2 with 10; tools/step_times.py).  step() therefore
+        # waits until at most `steps_ahead` earlier steps are still in flight (0 = unbounded).
+        self.steps_ahead = int(os.environ.get("ZEST_STEPS_AHEAD", "1"))
+        self._inflight: collections.deque = collections.deque()
         # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
         # every rank BLAKE3-hashes them as soon as they land, so each GPU verifies its whole replica
         # against the published Merkle file hashes without trusting any peer's hashes.
@@ -507,6 +516,9 @@ class DevicePuller:
         """One full pull of the model onto every rank.  Returns per-step stats."""
         import torch.distributed as dist
         dev = self.device
+        if self.is_cuda and self.steps_ahead > 0:
+            while len(self._inflight) >= self.steps_ahead:
+                self._inflight.popleft().synchronize()
         self.hashes.zero_()  # err is NOT reset: the first error of any step persists until check()
         works = []
         if self.is_cuda:
@@ -574,6 +586,10 @@ class DevicePuller:
             H.merkle(self.hashes.data_ptr(), self.sizes.data_ptr(), self.jobs_dev.data_ptr(), len(self.jobs),
                      self.roots.data_ptr(), self.merkle_scratch.data_ptr(), self.merkle_sb, st)
             H.compare_hashes(self.roots.data_ptr(), self.expected.data_ptr(), len(self.jobs), self.err.data_ptr(), st)
+            if self.steps_ahead > 0:
+                done = torch.cuda.Event()
+                done.record(main)
+                self._inflight.append(done)
         else:
             roots = ops.merkle_roots(self.hashes, self.sizes, self.jobs)
             if not torch.equal(roots, self.expected):
