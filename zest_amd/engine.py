@@ -517,7 +517,7 @@ class DevicePuller:
         import torch.distributed as dist
         dev = self.device
         if self.is_cuda and self.steps_ahead > 0:
-            while len(self._inflight) >= self.steps_ahead:
+            while len(self._inflight) > self.steps_ahead:
                 self._inflight.popleft().synchronize()
         self.hashes.zero_()  # err is NOT reset: the first error of any step persists until check()
         works = []
