@@ -100,18 +100,21 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("src"), py::arg("src_n"), py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"),
      py::arg("lo"), py::arg("hi"), py::arg("err"), py::arg("stream"), py::arg("clip_scratch") = 0);
   m.attr("CLIP_SCRATCH_BYTES") = ZG_CLIP_SCRATCH_BYTES;
+  m.def("hash_scratch_bytes", [](int n, uint64_t total_bytes) { return zg_hash_scratch_bytes(n, total_bytes); });
   m.def("hash_chunks", [](uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n, uintptr_t hashes, uintptr_t sizes,
-                          uint32_t base, uintptr_t st) {
+                          uint32_t base, uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {
     check(zg_hash_chunks(P<const uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, P<uint8_t>(hashes),
-                         P<uint64_t>(sizes), base, S(st)),
+                         P<uint64_t>(sizes), base, P<uint8_t>(scratch), scratch_bytes, S(st)),
           "zg_hash_chunks");
-  });
+  }, py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"), py::arg("hashes"), py::arg("sizes"),
+     py::arg("base"), py::arg("stream"), py::arg("scratch") = 0, py::arg("scratch_bytes") = 0);
   m.def("hash_ranges", [](uintptr_t buf, uintptr_t offs, uintptr_t lens, int n, uintptr_t out, int key_mode,
-                          uintptr_t st) {
+                          uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {
     check(zg_hash_ranges(P<const uint8_t>(buf), P<const uint64_t>(offs), P<const uint32_t>(lens), n,
-                         P<uint8_t>(out), key_mode, S(st)),
+                         P<uint8_t>(out), key_mode, P<uint8_t>(scratch), scratch_bytes, S(st)),
           "zg_hash_ranges");
-  });
+  }, py::arg("buf"), py::arg("offs"), py::arg("lens"), py::arg("n"), py::arg("out"), py::arg("key_mode"),
+     py::arg("stream"), py::arg("scratch") = 0, py::arg("scratch_bytes") = 0);
   m.def("compress_chunks", [](uintptr_t data, uintptr_t offs, uintptr_t lens, int n, int bg4, uintptr_t scratch,
                               uint64_t in_slot, uintptr_t out, uint64_t out_slot, uintptr_t out_len, uint32_t hc64,
                               uint32_t hc256, uintptr_t st) {

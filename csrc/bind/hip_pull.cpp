@@ -366,8 +366,12 @@ class DeviceXetPull {
         hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
                                   stream_),
                   "place");
+        uint64_t ubytes = 0;
+        for (size_t i = next; i < end; ++i) ubytes += gt[i].ulen;
+        const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
+        hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
         hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
-                                 stream_),
+                                 hash_scratch_.p, hs_bytes, stream_),
                   "hash");
         hip_check(hipEventRecord(s.done, stream_), "event");
         s.busy = true;
@@ -443,6 +447,7 @@ class DeviceXetPull {
   DevBuf<uint64_t> sizes_;
   DevBuf<ZgMerkleJob> merkle_job_;
   DevBuf<uint8_t> merkle_scratch_;
+  DevBuf<uint8_t> hash_scratch_;
   DevBuf<uint8_t> root_;
 };
 

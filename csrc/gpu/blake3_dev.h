@@ -146,6 +146,70 @@ __device__ __forceinline__ void hash_chunk(const uint8_t* p, uint32_t len, uint6
   }
 }
 
+// 17 consecutive dwords from a 4-byte-aligned address (the 64-byte block plus the next dword that
+// the byte-alignment shift needs): four 16-byte loads + one dword.
+// (global address space, so they issue as global_load and not flat_load, which would also count
+// against lgkmcnt and serialize with the LDS/scalar waits)
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef const __attribute__((address_space(1))) u32x4_a4* gq4_t;
+typedef const __attribute__((address_space(1))) uint32_t* gw_t;
+__device__ __forceinline__ void fetch17(const uint32_t* w, uint32_t r[17]) {
+  gq4_t q = (gq4_t)w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u32x4_a4 v = q[i];
+    r[4 * i] = v.x;
+    r[4 * i + 1] = v.y;
+    r[4 * i + 2] = v.z;
+    r[4 * i + 3] = v.w;
+  }
+  r[16] = ((gw_t)w)[16];
+}
+
+// One <= 1 KiB BLAKE3 chunk like hash_chunk, with block b+1's loads in flight while block b
+// compresses (the lane's 1 KiB is read as 16 x 64 B; a shift of k bytes realigns every word with
+// v_alignbyte, which is the identity for k == 0, so there is no aligned/unaligned branch).
+__device__ __forceinline__ void hash_leaf(const uint8_t* p, uint32_t len, uint64_t counter, const Key8& key,
+                                          uint32_t mode_flags, bool is_root, uint32_t cv[8]) {
+  load_key(cv, key);
+  const uint32_t nblk = len == 0 ? 1 : (len + 63) >> 6;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t k = uint32_t(a & 3);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  uint32_t cur[17];
+  if (len) {
+    fetch17(w, cur);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 17; ++i) cur[i] = 0;
+  }
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint32_t nxt[17];
+    if (b + 1 < nblk) fetch17(w + 16 * (b + 1), nxt);
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(cur[i + 1], cur[i], k);
+    const uint32_t avail = len - 64 * b < 64 ? len - 64 * b : 64;
+    if (avail < 64) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int lo = 4 * i;
+        uint32_t keep;
+        if (int(avail) >= lo + 4) keep = 0xFFFFFFFFu;
+        else if (int(avail) <= lo) keep = 0u;
+        else keep = 0xFFFFFFFFu >> (8 * (lo + 4 - int(avail)));
+        m[i] &= keep;
+      }
+    }
+    uint32_t f = mode_flags;
+    if (b == 0) f |= CHUNK_START;
+    if (b + 1 == nblk) f |= CHUNK_END | (is_root ? ROOT : 0u);
+    compress(cv, m, is_root ? 0 : counter, avail, f);
+#pragma unroll
+    for (int i = 0; i < 17; ++i) cur[i] = nxt[i];
+  }
+}
+
 __device__ __forceinline__ void parent_cv(const uint32_t l[8], const uint32_t r[8], const Key8& key,
                                           uint32_t mode_flags, bool root, uint32_t out[8]) {
   uint32_t m[16];

@@ -531,9 +531,10 @@ __global__ void __launch_bounds__(256, RB <= 4096 ? 8 : 5) k_decode_lz4(const ui
 }
 
 // --------------------------------------------------------------------------------------------
-// K1: keyed BLAKE3 chunk hashes.  One wave per Xet chunk (4 per 256-thread block); lane l owns
-// BLAKE3 chunks l, l+64 (<= 128 for a 128 KiB Xet chunk); chaining values are merged pairwise
-// in LDS (pairwise-with-carry == BLAKE3's left-complete tree).
+// K1: keyed BLAKE3 chunk hashes, latency path (launches without scratch; the leaf-flat pipeline
+// in blake3_flat.hip is the throughput path).  One wave per Xet chunk (4 per 256-thread block);
+// lane l owns BLAKE3 chunks l, l+64 (<= 128 for a 128 KiB Xet chunk); chaining values are merged
+// pairwise in LDS (pairwise-with-carry == BLAKE3's left-complete tree).
 // --------------------------------------------------------------------------------------------
 __device__ void wave_hash(const uint8_t* base, uint32_t len, const zg::Key8& key, uint32_t mode, uint32_t* cvs,
                           uint32_t lane, uint32_t out[8]) {
@@ -726,16 +727,21 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
 }
 
 hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks, uint8_t* hashes,
-                          uint64_t* sizes, uint32_t hash_index_base, hipStream_t stream) {
+                          uint64_t* sizes, uint32_t hash_index_base, uint8_t* scratch, size_t scratch_bytes,
+                          hipStream_t stream) {
   if (n_chunks <= 0) return hipSuccess;
+  if (scratch)
+    return zg_hash_chunks_flat(dst, dst_n, chunks, n_chunks, hashes + 32 * uint64_t(hash_index_base),
+                               sizes ? sizes + hash_index_base : nullptr, scratch, scratch_bytes, stream);
   hipLaunchKernelGGL(k_hash_chunks, dim3((n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, stream, dst,
                      chunks, n_chunks, hashes, sizes, hash_index_base, dst_n);
   return hipGetLastError();
 }
 
 hipError_t zg_hash_ranges(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n, uint8_t* hashes,
-                          int key_mode, hipStream_t stream) {
+                          int key_mode, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
+  if (scratch) return zg_hash_ranges_flat(buf, offsets, lens, n, hashes, key_mode, scratch, scratch_bytes, stream);
   hipLaunchKernelGGL(k_hash_ranges, dim3((n + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, stream, buf, offsets,
                      lens, n, hashes, key_mode);
   return hipGetLastError();

@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "lz4win.h"
+#include "wave64.h"
 #include "zgpu.h"
 
 namespace {
@@ -38,6 +39,8 @@ using zgw::win_init;
 using zgw::win_lane_u8;
 using zgw::win_seek;
 using zgw::win_u8;
+using zwv::scan_add;
+using zwv::scan_max;
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
@@ -60,30 +63,6 @@ __device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t lane) {
   return uint32_t(__builtin_amdgcn_ds_bpermute(int(lane << 2), int(v)));
 }
 
-// DPP wave64 inclusive scans (row_shr within 16-lane rows, then row_bcast:15 / row_bcast:31
-// across rows -- gfx9 DPP): six VALU ops instead of six LDS permutes.
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), kCtrl, kRowMask, 0xF, false));
-}
-__device__ __forceinline__ uint32_t scan_add(uint32_t v) {
-  v += dpp<0x111, 0xF>(v);
-  v += dpp<0x112, 0xF>(v);
-  v += dpp<0x114, 0xF>(v);
-  v += dpp<0x118, 0xF>(v);
-  v += dpp<0x142, 0xA>(v);
-  v += dpp<0x143, 0xC>(v);
-  return v;
-}
-__device__ __forceinline__ uint32_t scan_max(uint32_t v) {
-  v = max(v, dpp<0x111, 0xF>(v));
-  v = max(v, dpp<0x112, 0xF>(v));
-  v = max(v, dpp<0x114, 0xF>(v));
-  v = max(v, dpp<0x118, 0xF>(v));
-  v = max(v, dpp<0x142, 0xA>(v));
-  v = max(v, dpp<0x143, 0xC>(v));
-  return v;
-}
 
 // Smallest lane s with a[s] >= t (a non-decreasing over lanes); 64 if none.
 __device__ __forceinline__ uint32_t find_ge(uint32_t a, uint32_t t) {

@@ -3,7 +3,7 @@
 // Pipeline for one batch of fetched xorb ranges ("terms"):
 //   zg_index_terms   one thread per term walks the 8-byte chunk headers -> ChunkDesc[]   (K4)
 //   zg_place_chunks  one wave per chunk: scheme 0 -> aligned copy, LZ4/BG4 -> LDS decode (K3)
-//   zg_hash_chunks   one wave per chunk: keyed BLAKE3 of the placed bytes -> chunk hashes (K1)
+//   zg_hash_chunks   keyed BLAKE3 of the placed bytes -> chunk hashes (K1; lane per 1 KiB leaf)
 //   zg_merkle_files  one workgroup per file: Xet Merkle tree -> root -> file hash compare (K2)
 // plus zg_cdc_candidates (K5), zg_pack_xorbs (K7) and synthetic data generators.
 #pragma once
@@ -70,11 +70,23 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                            uint8_t* clip_scratch, unsigned long long* err, hipStream_t stream);
 hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                  const ZgChunk* chunks, int n_chunks, unsigned long long* err, hipStream_t stream);
+// K1 keyed BLAKE3 of placed chunks (hashes[hash_index_base + c], sizes likewise when non-null) or of
+// raw (offset, len) messages (key_mode 0 Xet data key, 1 node key, 2 plain, 3 zero key; a message
+// over 128 KiB gets an all-ones hash).  With `scratch` (>= zg_hash_scratch_bytes(n, total message
+// bytes) of device memory owned by the caller, one per concurrently running launch) the leaf-flat
+// pipeline of blake3_flat.hip runs; without it, one wave per message (ingest.hip).
+size_t zg_hash_scratch_bytes(int n, uint64_t total_bytes);
 hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
-                          uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, hipStream_t stream);
-// Hash raw (offset, len) messages with the Xet data key: out[i] = keyed(DATA_KEY, buf[off:off+len]).
+                          uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, uint8_t* scratch,
+                          size_t scratch_bytes, hipStream_t stream);
 hipError_t zg_hash_ranges(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,
-                          uint8_t* hashes, int key_mode, hipStream_t stream);
+                          uint8_t* hashes, int key_mode, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream);
+hipError_t zg_hash_chunks_flat(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
+                               uint8_t* hashes, uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes,
+                               hipStream_t stream);
+hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,
+                               uint8_t* hashes, int key_mode, uint8_t* scratch, size_t scratch_bytes,
+                               hipStream_t stream);
 hipError_t zg_merkle(const uint8_t* leaf_hashes, const uint64_t* leaf_sizes, const ZgMerkleJob* jobs,
                      int n_jobs, uint8_t* roots, uint8_t* scratch, uint64_t scratch_bytes,
                      hipStream_t stream);

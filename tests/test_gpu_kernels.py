@@ -56,6 +56,94 @@ def test_hash_ranges_matches_cpu_all_sizes_and_alignments():
         assert got_node[i].tobytes() == C.internal_node_hash(data[o:o + l])
 
 
+def _raw_hash_ranges(buf, offs, lens, key_mode=ops.KEY_DATA, scratch_bytes=None):
+    """K1 straight through the binding: leaf-flat pipeline when scratch_bytes != 0, else the
+    wave-per-message kernel."""
+    H = ops.hip()
+    n = len(offs)
+    offs_d = torch.tensor(np.asarray(offs, dtype=np.int64), device=DEV)
+    lens_d = torch.tensor(np.asarray(lens, dtype=np.uint32).view(np.int32), device=DEV)
+    out = torch.full((n, 32), 0x5A, dtype=torch.uint8, device=DEV)
+    sb = H.hash_scratch_bytes(n, int(np.asarray(lens, dtype=np.uint64).sum())) if scratch_bytes is None else scratch_bytes
+    scratch = torch.full((max(sb, 1),), 0xA5, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    H.hash_ranges(buf.data_ptr(), offs_d.data_ptr(), lens_d.data_ptr(), n, out.data_ptr(), key_mode, st,
+                  scratch.data_ptr() if sb else 0, sb)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def test_hash_leaf_flat_vs_wave_kernel_cdc_sizes():
+    """Both K1 paths bit-exact vs the host oracle on CDC-like sizes: 8-128 KiB with every tree depth,
+    one-leaf and empty messages, odd alignments, n not a multiple of the 8-chunk tree group, runs
+    of tiny messages that put up to 64 owners in one leaf task."""
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 24 << 20, dtype=np.uint8).tobytes()
+    buf = ops.padded_empty(len(data), DEV)
+    buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    lens = list(rng.integers(8 << 10, (128 << 10) + 1, 300)) + [131_072] * 9 + [1, 0, 1024, 1025, 2048, 3] \
+        + [int(x) for x in rng.integers(0, 1025, 150)] + list(rng.integers(8 << 10, 64 << 10, 7))
+    offs, pos = [], 3
+    for ln in lens:
+        offs.append(pos)
+        pos += int(ln) + int(rng.integers(0, 5))
+    assert pos < len(data)
+    want = [C.chunk_hash(data[o:o + int(ln)]) for o, ln in zip(offs, lens)]
+    flat = _raw_hash_ranges(buf, offs, lens)
+    wave = _raw_hash_ranges(buf, offs, lens, scratch_bytes=0)
+    for i in range(len(lens)):
+        assert flat[i].tobytes() == want[i], ("flat", i, lens[i])
+        assert wave[i].tobytes() == want[i], ("wave", i, lens[i])
+    # plain / node keys through the flat path
+    sub = slice(0, 24)
+    plain = _raw_hash_ranges(buf, offs[sub], lens[sub], ops.KEY_PLAIN)
+    node = _raw_hash_ranges(buf, offs[sub], lens[sub], ops.KEY_NODE)
+    for i, (o, ln) in enumerate(zip(offs[sub], lens[sub])):
+        assert plain[i].tobytes() == C.blake3(data[o:o + int(ln)])
+        assert node[i].tobytes() == C.internal_node_hash(data[o:o + int(ln)])
+
+
+def test_hash_leaf_flat_oversize_and_undersized_scratch():
+    data = bytes(range(256)) * 4096
+    buf = ops.padded_empty(len(data), DEV)
+    buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    offs, lens = [0, 10, 20], [5000, 131_073, 70_000]
+    got = _raw_hash_ranges(buf, offs, lens)
+    assert got[0].tobytes() == C.chunk_hash(data[:5000])
+    assert got[1].tobytes() == b"\xff" * 32  # over 128 KiB: rejected like the wave kernel does
+    assert got[2].tobytes() == C.chunk_hash(data[20:70_020])
+    # scratch sized for far fewer leaves than the launch has: every hash is all-ones (cannot verify)
+    small = ops.hip().hash_scratch_bytes(3, 2048)
+    bad = _raw_hash_ranges(buf, [0, 100, 200], [65_536, 65_536, 65_536], scratch_bytes=small)
+    assert all(bad[i].tobytes() == b"\xff" * 32 for i in range(3))
+
+
+def test_hash_chunks_flat_matches_wave_kernel_on_ingest():
+    data, ends, b = _make_runs("none", 3)
+    run = b.serialize(False)
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(run), 0, 0, len(ends), len(data))
+    src = ops.padded_empty(len(run), DEV)
+    src.copy_(torch.frombuffer(bytearray(run), dtype=torch.uint8))
+    dst = ops.padded_empty(len(data), DEV)
+    hashes = torch.zeros((len(ends), 32), dtype=torch.uint8, device=DEV)
+    ws = ops.IngestWorkspace(DEV, 1, len(ends))
+    ops.ingest_terms(src, dst, terms, hashes, ws=ws)  # flat path (workspace scratch)
+    H = ops.hip()
+    wave = torch.zeros_like(hashes)
+    sizes = torch.zeros(len(ends), dtype=torch.int64, device=DEV)
+    H.hash_chunks(dst.data_ptr(), dst.numel(), ws.chunks.data_ptr(), len(ends), wave.data_ptr(), sizes.data_ptr(), 0,
+                  torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(hashes, wave)
+    prev = 0
+    want = []
+    for e in ends:
+        want.append(C.chunk_hash(data[prev:e]))
+        prev = e
+    assert [hashes[i].cpu().numpy().tobytes() for i in range(len(ends))] == want
+    assert sizes.cpu().tolist() == list(np.diff([0] + list(ends)))
+
+
 def _make_runs(policy, seed=0):
     rng = random.Random(seed)
     parts = [rng.randbytes(700_000), _bf16(400_000, seed), b"zest xorb ingest test line. " * 20_000,

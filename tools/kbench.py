@@ -69,28 +69,33 @@ def main():
     offs_d = torch.from_numpy(offs.view(np.int64)).to(dev)
     lens_d = torch.from_numpy(lens.view(np.int32)).to(dev)
     out = torch.empty((nck, 32), dtype=torch.uint8, device=dev)
-    if want("hash"):
-        ms = timed(lambda: H.hash_ranges(arena.data_ptr(), offs_d.data_ptr(), lens_d.data_ptr(), nck,
-                                         out.data_ptr(), 0, st), a.iters)
-        emit(kernel="blake3_xet_chunks_64k", bytes=n, ms=ms, gbps=n / ms / 1e6, chunks=nck)
-        # correctness spot check
-        h = out[:4].cpu().numpy()
-        host = arena[:4 * csize].cpu().numpy().tobytes()
-        assert all(h[i].tobytes() == C.chunk_hash(host[i * csize:(i + 1) * csize]) for i in range(4))
+    hs = ops.HashScratch(dev)
+
+    def hash_case(name, o, ln, check_n=4):
+        """K1 over (offset, len) messages: wave-per-message kernel vs the leaf-flat pipeline."""
+        o_d = torch.from_numpy(o.astype(np.int64)).to(dev)
+        l_d = torch.from_numpy(ln.astype(np.uint32).view(np.int32)).to(dev)
+        m = len(o)
+        res = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+        nb = int(ln.sum())
+        sp, sb = hs.get(m, nb)
+        for path, scr in (("wave", (0, 0)), ("flat", (sp, sb))):
+            ms = timed(lambda: H.hash_ranges(arena.data_ptr(), o_d.data_ptr(), l_d.data_ptr(), m, res.data_ptr(), 0,
+                                             st, *scr), a.iters)
+            emit(kernel=f"blake3_{name}[{path}]", bytes=nb, ms=ms, gbps=nb / ms / 1e6, chunks=m)
+            h = res[:check_n].cpu().numpy()
+            host = arena[: int(o[check_n - 1] + ln[check_n - 1])].cpu().numpy().tobytes()
+            assert all(h[i].tobytes() == C.chunk_hash(host[int(o[i]):int(o[i]) + int(ln[i])]) for i in range(check_n))
 
     if want("hash"):
+        hash_case("xet_chunks_64k", offs, lens)
         # CDC chunks land at arbitrary byte offsets in the arena: the misaligned load path
-        uoffs = offs + (np.arange(nck, dtype=np.uint64) * 13) % 61
-        ulens = np.full(nck, csize - 64, dtype=np.uint32)
-        uoffs_d = torch.from_numpy(uoffs.view(np.int64)).to(dev)
-        ulens_d = torch.from_numpy(ulens.view(np.int32)).to(dev)
-        ms = timed(lambda: H.hash_ranges(arena.data_ptr(), uoffs_d.data_ptr(), ulens_d.data_ptr(), nck,
-                                         out.data_ptr(), 0, st), a.iters)
-        ub = int(ulens.sum())
-        emit(kernel="blake3_xet_chunks_64k_unaligned", bytes=ub, ms=ms, gbps=ub / ms / 1e6, chunks=nck)
-        h = out[:4].cpu().numpy()
-        host = arena[:5 * csize].cpu().numpy().tobytes()
-        assert all(h[i].tobytes() == C.chunk_hash(host[int(uoffs[i]):int(uoffs[i]) + int(ulens[i])]) for i in range(4))
+        hash_case("xet_chunks_64k_unaligned", offs + (np.arange(nck, dtype=np.uint64) * 13) % 61,
+                  np.full(nck, csize - 64, dtype=np.uint32))
+        # the real size mix: Xet CDC chunks (8-128 KiB) of the arena's own bytes
+        ends = np.asarray(C.chunk_ends(arena[: min(n, 256 << 20)].cpu().numpy().tobytes()), dtype=np.uint64)
+        starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+        hash_case("xet_chunks_cdc", starts, (ends - starts).astype(np.uint32))
 
     if want("gather"):
         # K8 peer gather on local memory (copy engine vs kernel; on the 8-GPU node the same launch
@@ -150,7 +155,11 @@ def main():
         emit(kernel="place_raw(+lz4 scan)", bytes=n, ms=ms, gbps=n / ms / 1e6)
         ms = timed(lambda: H.hash_chunks(dst.data_ptr(), n, ws.chunks.data_ptr(), nck, hashes.data_ptr(), 0, 0, st),
                    a.iters)
-        emit(kernel="hash_chunks", bytes=n, ms=ms, gbps=n / ms / 1e6)
+        emit(kernel="hash_chunks[wave]", bytes=n, ms=ms, gbps=n / ms / 1e6)
+        sp, sb = hs.get(nck, n)
+        ms = timed(lambda: H.hash_chunks(dst.data_ptr(), n, ws.chunks.data_ptr(), nck, hashes.data_ptr(), 0, 0, st,
+                                         sp, sb), a.iters)
+        emit(kernel="hash_chunks[flat]", bytes=n, ms=ms, gbps=n / ms / 1e6)
         del body, dst
 
     def ingest_case(name, raw, policy, iters):

@@ -226,6 +226,8 @@ class DevicePuller:
             self.chunk_off_dev = torch.from_numpy(world.chunk_off.astype(np.int64)).to(self.device)
             self.chunk_len_dev = torch.from_numpy(world.chunk_len.astype(np.int32)).to(self.device)
             self.verify_stream = torch.cuda.Stream(self.device)
+            self._verify_scratch = ops.HashScratch(self.device)
+            self._chunk_len_csum = np.concatenate([[0], np.cumsum(world.chunk_len, dtype=np.int64)])
         self.bytes_received = sum(hi - lo for k in range(self.n_rounds) for r, (lo, hi) in
                                   enumerate(self.regions[k]) if r != rank)
         self.bytes_ingested = int(self.term_origin_off[-1])
@@ -549,8 +551,9 @@ class DevicePuller:
                                       self.err.data_ptr(), st)
                         H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(),
                                        ws.chunks.data_ptr(), rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
+                        sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
                         H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
-                                      self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st)
+                                      self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
                     self.slot_free[s].record(comp)
                     if self.n_ranks > 1:
                         if self.exchange in PEER_MAPPED_MODES:
@@ -621,10 +624,14 @@ class DevicePuller:
             for w in works:
                 w.wait()  # the verify stream waits for round k's transfers
             for c0, n in runs:
+                sp, sb = self._verify_scratch.get(n, self._run_bytes(c0, n))
                 H.hash_ranges(self.arena.data_ptr(), self.chunk_off_dev.data_ptr() + 8 * c0,
                               self.chunk_len_dev.data_ptr() + 4 * c0, n, self.hashes.data_ptr() + 32 * c0,
-                              ops.KEY_DATA, self.verify_stream.cuda_stream)
+                              ops.KEY_DATA, self.verify_stream.cuda_stream, sp, sb)
         return []
+
+    def _run_bytes(self, c0: int, n: int) -> int:
+        return int(self._chunk_len_csum[c0 + n] - self._chunk_len_csum[c0])
 
     def close(self):
         self.origin.close()

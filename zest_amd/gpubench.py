@@ -6,6 +6,7 @@ bench.zig:28-33).  These rows time the MI355X kernels of the same pipeline with 
 row per kernel, in that schema (median over `runs` launches; throughput = bytes / 2^20 / s):
 
   blake3_64kb_gpu      keyed BLAKE3 of many 64 KiB chunks (K1; the reference's blake3_64kb row)
+  blake3_cdc_gpu       the same over Xet CDC chunks (8-128 KiB), as a pull hashes them
   sha1_info_hash_gpu   SHA-1 info-hashes of 44-byte messages (K6; the reference's sha1_info_hash)
   cdc_gpu              GearHash CDC boundary candidates (K5)
   xorb_verify_gpu      header walk + placement + BLAKE3 of uncompressed xorb runs (K4 fused ingest)
@@ -96,9 +97,22 @@ def run(mib: int = 1024, runs: int = 5, device="cuda:0") -> list[dict]:
     offs = torch.from_numpy((np.arange(nb, dtype=np.uint64) * 65536).view(np.int64)).to(dev)
     lens = torch.full((nb,), 65536, dtype=torch.int32, device=dev)
     out = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
+    hs = ops.HashScratch(dev)
+    sp, sb = hs.get(nb, nb * 65536)
     ns = _time(lambda: H.hash_ranges(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), nb, out.data_ptr(),
-                                     ops.KEY_DATA, st), runs)
+                                     ops.KEY_DATA, st, sp, sb), runs)
     rows.append(_row("blake3_64kb_gpu", runs, ns, nb * 65536))
+    # the same bytes cut like a real pull: Xet CDC chunks (8-128 KiB)
+    ends = _core.chunk_ends(arena[: min(n, 256 << 20)].cpu().numpy().tobytes())
+    cst = np.concatenate([[0], np.asarray(ends[:-1], dtype=np.int64)])
+    clen = np.diff(np.concatenate([[0], np.asarray(ends, dtype=np.int64)]))
+    coffs = torch.from_numpy(cst).to(dev)
+    clens = torch.from_numpy(clen.astype(np.int32)).to(dev)
+    cout = torch.empty((len(ends), 32), dtype=torch.uint8, device=dev)
+    sp, sb = hs.get(len(ends), int(clen.sum()))
+    ns = _time(lambda: H.hash_ranges(arena.data_ptr(), coffs.data_ptr(), clens.data_ptr(), len(ends), cout.data_ptr(),
+                                     ops.KEY_DATA, st, sp, sb), runs)
+    rows.append(_row("blake3_cdc_gpu", runs, ns, int(clen.sum())))
 
     nh = 1 << 22
     hs = torch.randint(0, 256, (nh, 32), dtype=torch.uint8, device=dev)

@@ -113,9 +113,28 @@ def hash_ranges(buf: torch.Tensor, offsets, lens, key_mode: int = KEY_DATA) -> t
     offs_d = torch.from_numpy(offsets.view(np.int64).copy()).to(buf.device)
     lens_d = torch.from_numpy(lens.view(np.int32).copy()).to(buf.device)
     out = torch.empty((n, 32), dtype=torch.uint8, device=buf.device)
+    sb = H.hash_scratch_bytes(n, int(lens.sum(dtype=np.uint64)))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=buf.device)
     H.hash_ranges(buf.data_ptr(), offs_d.data_ptr(), lens_d.data_ptr(), n, out.data_ptr(), key_mode,
-                  _stream(buf.device))
+                  _stream(buf.device), scratch.data_ptr(), sb)
     return out
+
+
+class HashScratch:
+    """Device scratch of the leaf-flat K1 pipeline (blake3_flat.hip), grown on demand.  Use one per
+    stream, and call get() with that stream current: launches on one stream are ordered, so they
+    can share the buffer, and when it grows the caching allocator hands the old block only to later
+    allocations on that same stream, i.e. after the launches already queued on it."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = None
+
+    def get(self, n: int, total_bytes: int) -> tuple[int, int]:
+        need = hip().hash_scratch_bytes(int(n), int(total_bytes))
+        if self.buf is None or self.buf.numel() < need:
+            self.buf = torch.empty(need + (need >> 3), dtype=torch.uint8, device=self.device)
+        return self.buf.data_ptr(), self.buf.numel()
 
 
 # ----------------------------------------------------------------------------------------------
@@ -150,6 +169,7 @@ class IngestWorkspace:
         self.terms_host = torch.empty(max_terms * TERM_DTYPE.itemsize, dtype=torch.uint8).pin_memory() \
             if self.device.type == "cuda" else None
         self._clip_scratch = None
+        self.hash_scratch = HashScratch(self.device) if self.device.type == "cuda" else None
 
     def clip_scratch(self) -> int:
         """Device scratch for clipped decodes, private to this workspace (so to its stream)."""
@@ -211,7 +231,8 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     H.place_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, lo, hi,
                    ws.err.data_ptr(), st, ws.clip_scratch() if clipped else 0)
     hptr = hashes.data_ptr() + 32 * hash_base
-    H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st)
+    sp, sb = ws.hash_scratch.get(n_chunks, int(terms["ulen"].sum()))
+    H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st, sp, sb)
     if check:
         raise_on_error(ws.err)
 
