@@ -148,7 +148,7 @@ def test_cli_bench_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     names = [row["name"] for row in out["results"]]
-    assert names == ["blake3_64kb_gpu", "sha1_info_hash_gpu", "cdc_gpu", "xorb_verify_gpu", "lz4_decode_gpu",
+    assert names == ["blake3_64kb_gpu", "blake3_cdc_gpu", "sha1_info_hash_gpu", "cdc_gpu", "xorb_verify_gpu", "lz4_decode_gpu",
                      "merkle_gpu", "h2d_pinned_gpu"]
     for row in out["results"]:
         assert set(row) == {"name", "runs", "median_ns", "throughput_mbps", "bytes_processed"}

@@ -484,6 +484,10 @@ class DevicePuller:
         if self.n_ranks == 1:
             return {}
         modes = tuple(m for m in modes if m not in PEER_MAPPED_MODES or self._peer_arenas is not None)
+        if self.is_cuda and self._backend() == "gloo":
+            # gloo moves device tensors only through its collectives; a batched isend/irecv of
+            # device tensors never completed (2-rank rehearsal on one GPU, tools/gpu_check_r2.sh)
+            modes = tuple(m for m in modes if m != "p2p")
         rounds = range(min(self.n_rounds, max_rounds))
         times = {}
         for mode in modes:
