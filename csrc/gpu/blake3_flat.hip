@@ -48,7 +48,6 @@ struct Layout {
   uint32_t* WF;
   uint32_t* CV;
   uint32_t cap;
-  uint32_t wf_cap;
 };
 
 __host__ __device__ inline uint64_t cv_offset(int n, uint64_t cap) {
@@ -62,7 +61,6 @@ __host__ __device__ inline Layout layout(uint8_t* s, int n, uint32_t cap) {
   l.WF = l.P + n + 1;
   l.CV = reinterpret_cast<uint32_t*>(s + cv_offset(n, cap));
   l.cap = cap;
-  l.wf_cap = cap / 64 + 2;
   return l;
 }
 
@@ -130,7 +128,7 @@ __global__ void __launch_bounds__(kPlanThreads) k_hash_plan(Src s, int n, uint8_
 #pragma unroll
   for (int k = 0; k < kPlanRegs; ++k) nbv[k] = n_leaves(s, min(k * kPlanThreads + t, n - 1));
   uint32_t carry = 0;
-  // pass 1: total leaf count (decides overflow before anything is placed)
+  // exclusive scan over the tiles: P[c] = first leaf of chunk c; carry = leaves of the tiles so far
   for (int k = 0; k < tiles; ++k) {
     uint32_t v = 0;
     if (k < kPlanRegs) {
