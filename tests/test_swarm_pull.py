@@ -1,0 +1,111 @@
+"""Intra-node swarm pull (zest_amd.parallel.swarm_pull) over gloo process groups on CPU: every rank
+ends with every tensor, each Xet file fetched from the (fake) hub by exactly one owner rank, the rest
+received from peers and re-verified; a rank whose fetch fails makes every rank raise (no hang).
+The GPU variant (device-direct fetch + RCCL/gloo broadcast of device buffers) is in
+test_gpu_device.py."""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+import struct
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from e2e_util import free_port
+from zest_amd import models
+from zest_amd.synthetic import SyntheticWorld
+from zest_amd.testing import FakeHub
+
+
+def _sharded_world(seed: int) -> SyntheticWorld:
+    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
+    return SyntheticWorld(spec, seed=seed, mode="bf16")
+
+
+def _expected(world):
+    out = {}
+    for f in world.xet_files:
+        data = world.file_bytes_host(f)
+        (hlen,) = struct.unpack("<Q", data[:8])
+        for name, ent in json.loads(data[8:8 + hlen]).items():
+            if name != "__metadata__":
+                a, b = ent["data_offsets"]
+                out[name] = data[8 + hlen + a:8 + hlen + b]
+    return out
+
+
+def _worker(rank, world_size, port, repo, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from zest_amd.parallel import swarm_pull
+        st = {}
+        try:
+            t = swarm_pull(repo, p2p=False, dht=False, stats=st)
+            q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
+        except Exception as e:
+            q.put((rank, type(e).__name__, str(e), st))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world_size, repo):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, repo, q)) for r in range(world_size)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.fixture
+def hub_env(tmp_path, monkeypatch):
+    world = _sharded_world(21)
+    assert len(world.xet_files) >= 3  # several owners
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    hub.add_world(world)
+    for k, v in hub.env(str(tmp_path)).items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+    yield world, hub
+    hub.stop()
+
+
+@pytest.mark.parametrize("world_size", [1, 3])
+def test_swarm_pull_every_rank_gets_every_tensor(hub_env, world_size):
+    world, hub = hub_env
+    want = _expected(world)
+    res = _run(world_size, world.spec.repo_id)
+    assert [r[1] for r in res] == ["ok"] * world_size, res
+    for _, _, got, _ in res:
+        assert got.keys() == want.keys()
+        assert all(got[k] == want[k] for k in want)
+    # each file crossed the network once: owners' fetched bytes add up to the model, and each rank
+    # received exactly what it did not fetch
+    total = sum(f.size for f in world.xet_files)
+    assert sum(r[3]["fetched_bytes"] for r in res) == total
+    for r in res:
+        assert r[3]["fetched_bytes"] + r[3]["received_bytes"] == total
+    assert hub.counters.get("xorb_get", 0) > 0
+
+
+def test_swarm_pull_failed_owner_fails_every_rank(hub_env):
+    world, hub = hub_env
+    # the CDN refuses every xorb behind one file: its owner cannot fetch it
+    victim = world.xet_files[0]
+    xh = hub.xet_hash(world.spec.repo_id, victim.path)
+    hub.fail_xorbs = {t["hash"] for t in hub.reconstruction(xh)["terms"]}
+    res = _run(3, world.spec.repo_id)
+    assert all(r[1] == "SwarmPullError" for r in res), res
+    assert sum("rank" in r[2] for r in res) == 3

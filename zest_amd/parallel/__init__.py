@@ -3,6 +3,8 @@
 * `DevicePuller` (zest_amd.engine): owner-sharded term ingest + peer-to-peer round exchange of the
   HBM arena — the swarm pull used by bench.py.
 * `swarm_load`: replicate a pulled snapshot into every GPU's HBM, each file read by one owner rank.
+* `swarm_pull`: the same straight from the network: each Xet file pulled device-direct by one owner
+  rank, broadcast over xGMI to the others, re-verified on every GPU.
 * `init_from_env`: torchrun-style rendezvous (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
 * `bind_local_numa`: pin a rank to the CPUs of its GPU's NUMA node, so its pinned host staging and
   origin pages are first-touched next to the GPU's PCIe root (8 ranks x ~57 GB/s of H2D must not
@@ -16,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .swarm_load import assign_owners, swarm_load
+from .swarm_pull import SwarmPullError, swarm_pull
 
 
 def init_from_env(backend: str | None = None, timeout_s: int = 600):
@@ -100,4 +103,4 @@ def __getattr__(name):
 
 
 __all__ = ["DevicePuller", "assign_owners", "bind_local_numa", "gpu_local_cpus", "init_from_env", "nccl_options",
-           "parse_cpulist", "swarm_load"]
+           "parse_cpulist", "swarm_load", "swarm_pull", "SwarmPullError"]
