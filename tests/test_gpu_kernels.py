@@ -330,6 +330,23 @@ def test_merkle_matches_cpu(n):
     assert raw[0].tobytes() == C.merkle_root(leaves)
 
 
+def test_merkle_large_sizes_and_many_jobs():
+    """Sizes past 2^32 (the 64-bit decimal path), leaf and node sizes with 1..14 digits, and many
+    small trees next to large ones (level-1 work spread over 8 workgroups per tree)."""
+    rng = np.random.default_rng(99)
+    n = 30_000
+    hs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sz = (rng.integers(1, 10, size=n) * 10 ** rng.integers(0, 13, size=n)).astype(np.int64)
+    sz[:50] = (1 << 32) + rng.integers(0, 1000, size=50)
+    leaves = [(hs[i].tobytes(), int(sz[i])) for i in range(n)]
+    h_d = torch.from_numpy(hs).to(DEV)
+    s_d = torch.from_numpy(sz).to(DEV)
+    jobs = [(0, n), (5, 1), (10, 2), (100, 17), (1000, 9000), (20_000, 10_000)] + [(i * 7, 7) for i in range(40)]
+    roots = ops.merkle_roots(h_d, s_d, jobs, file_hash=True).cpu().numpy()
+    for j, (b, m) in enumerate(jobs):
+        assert roots[j].tobytes() == C.file_hash(leaves[b:b + m]), (b, m)
+
+
 def test_cdc_candidates_match_cpu_chunker():
     rng = random.Random(11)
     data = rng.randbytes(3_000_000) + _bf16(500_000, 1) + bytes(200_000)
