@@ -167,3 +167,33 @@ def test_cpu_swarm_eight_ranks_autotuned():
     assert len({r[5] for r in res}) == 1
     model = res[0][4]
     assert sum(r[3] for r in res) < model * 1.01 + 8 * 4096
+
+
+def test_round_plan_taper_covers_every_term_once():
+    """Tapered rounds (small head and tail rounds, full rounds <= round_bytes) partition each rank's
+    terms in order, identically shaped on every rank."""
+    from types import SimpleNamespace
+
+    from zest_amd.engine import plan_rank_terms, round_weights, split_rounds
+
+    # the planners read only the terms' byte sizes: 3000 terms of 8-128 KiB
+    T = np.zeros(3000, dtype=[("ulen", np.int64)])
+    T["ulen"] = np.random.default_rng(5).integers(8 << 10, 128 << 10, len(T))
+    w = SimpleNamespace(terms=T)
+    for n_ranks in (1, 3):
+        shares = plan_rank_terms(w, n_ranks)
+        biggest = max(int(T["ulen"][a:b].sum()) for a, b in shares)
+        rb = biggest // 12
+        weights = round_weights(biggest, rb)
+        assert weights[:2] == [0.25, 0.5] and weights[-3:] == [0.5, 0.25, 0.125]
+        assert sum(weights) * rb >= biggest
+        for a, b in shares:
+            rounds = split_rounds(w, a, b, weights)
+            assert len(rounds) == len(weights)
+            assert rounds[0][0] == a and rounds[-1][1] == b
+            assert all(r0[1] == r1[0] for r0, r1 in zip(rounds, rounds[1:]))
+            sizes = [int(T["ulen"][x:y].sum()) for x, y in rounds]
+            full = sum(sizes[2:-3]) / max(1, len(sizes) - 5)
+            assert sizes[0] < full and sizes[-1] < full
+    assert round_weights(3 << 20, 1 << 20) == [1.0] * 3          # short plans are not tapered
+    assert round_weights(40 << 20, 1 << 20, taper=False) == [1.0] * 40

@@ -106,15 +106,39 @@ def plan_rank_terms(world: SyntheticWorld, n_ranks: int, seeders: int | None = N
     return [(int(bounds[r]), int(bounds[r + 1])) for r in range(n_ranks)]
 
 
-def split_rounds(world: SyntheticWorld, a: int, b: int, n_rounds: int) -> list[tuple[int, int]]:
+HEAD_TAPER = (0.25, 0.5)        # first rounds, as fractions of a full round
+TAIL_TAPER = (0.5, 0.25, 0.125)  # last rounds
+
+
+def round_weights(share_bytes: int, round_bytes: int, taper: bool = True) -> list[float]:
+    """Relative sizes of one rank's rounds.  Full rounds are at most `round_bytes`; with `taper`
+    the first and last rounds shrink geometrically: nothing overlaps the first round's H2D and
+    nothing overlaps the last round's exchange + verification, so those two rounds are the
+    pipeline's head and tail (at 8 GPUs a 1 GiB tail is ~20 ms of xGMI traffic per ~0.35 s step,
+    a 128 MiB one ~2.5 ms)."""
+    n = max(1, -(-share_bytes // round_bytes))
+    if not taper or n < 4:
+        return [1.0] * n
+    mid = max(1, -(-int(share_bytes - (sum(HEAD_TAPER) + sum(TAIL_TAPER)) * round_bytes) // round_bytes))
+    return list(HEAD_TAPER) + [1.0] * mid + list(TAIL_TAPER)
+
+
+def split_rounds(world: SyntheticWorld, a: int, b: int, weights) -> list[tuple[int, int]]:
+    """Cut terms [a, b) into len(weights) rounds of (whole-term) byte sizes ~ proportional to
+    `weights` (an int n means n equal rounds)."""
     T = world.terms
+    if isinstance(weights, int):
+        weights = [1.0] * weights
+    n_rounds = len(weights)
     if b <= a:
         return [(a, a)] * n_rounds
     cu = np.cumsum(T["ulen"][a:b].astype(np.float64))
     total = cu[-1]
+    frac = np.cumsum(np.asarray(weights, dtype=np.float64))
+    frac /= frac[-1]
     cuts = [a]
     for k in range(1, n_rounds):
-        cuts.append(a + int(np.searchsorted(cu, total * k / n_rounds, side="left")) + 1)
+        cuts.append(a + int(np.searchsorted(cu, total * frac[k - 1], side="left")) + 1)
     cuts.append(b)
     cuts = np.maximum.accumulate(np.minimum(np.array(cuts), b))
     return [(int(cuts[k]), int(cuts[k + 1])) for k in range(n_rounds)]
@@ -138,9 +162,10 @@ class DevicePuller:
         T = world.terms
         self.rank_terms = plan_rank_terms(world, n_ranks, seeders)
         max_share = max((int(T["ulen"][a:b].sum()) for a, b in self.rank_terms), default=0)
-        self.n_rounds = max(1, -(-max_share // round_bytes))
+        self.round_weights = round_weights(max_share, round_bytes, os.environ.get("ZEST_ROUND_TAPER", "1") != "0")
+        self.n_rounds = len(self.round_weights)
         # rounds[k][r] = (a, b) term range for rank r in round k
-        per_rank = [split_rounds(world, a, b, self.n_rounds) for a, b in self.rank_terms]
+        per_rank = [split_rounds(world, a, b, self.round_weights) for a, b in self.rank_terms]
         self.rounds_all = [[per_rank[r][k] for r in range(n_ranks)] for k in range(self.n_rounds)]
         # this rank's origin layout: its terms' serialized bytes back to back, in order
         a_r, b_r = self.rank_terms[rank]
@@ -488,7 +513,8 @@ class DevicePuller:
             # gloo moves device tensors only through its collectives; a batched isend/irecv of
             # device tensors never completed (2-rank rehearsal on one GPU, tools/gpu_check_r2.sh)
             modes = tuple(m for m in modes if m != "p2p")
-        rounds = range(min(self.n_rounds, max_rounds))
+        full = [k for k, w in enumerate(self.round_weights) if w == 1.0]  # time full-size rounds
+        rounds = (full or list(range(self.n_rounds)))[:max_rounds]
         times = {}
         for mode in modes:
             for _ in range(2):
