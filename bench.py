@@ -131,6 +131,11 @@ def main() -> None:
             raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
     puller.build_origin()
     torch.cuda.synchronize()
+    # ZEST_GRAPH=1 (one GPU): a step is one HIP graph launch.  Opt-in: the graph's H2D copies ran at
+    # 51.2 GB/s against 56.2 for the eager copy-stream pipeline (profiles/hip_graph_r2.md).
+    graph = puller.capture_graph() if world_size == 1 and os.environ.get("ZEST_GRAPH") == "1" else False
+    if graph:
+        log(rank, "step captured in a HIP graph")
     log(rank, f"origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
     if world_size > 1:
@@ -210,7 +215,7 @@ def main() -> None:
                    "rounds": puller.n_rounds, "round_mb": a.round_mb, "exchange": puller.exchange if world_size > 1 else "none",
                    "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
                    "verify": "blake3 of every chunk on every rank + merkle file hashes",
-                   "numa_bound_cpus": len(numa_cpus),
+                   "numa_bound_cpus": len(numa_cpus), "hip_graph": bool(graph),
                    "backend": backend if world_size > 1 else "none"},
     }
     if rank == 0:

@@ -476,3 +476,38 @@ def test_gpu_pull_of_bg4_compressed_world():
         for f in w.xet_files:  # (the alignment gaps between files are not part of the repository)
             assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size]), f.path
     p.close()
+
+
+@pytest.mark.parametrize("compression", ["none", "bg4"])
+def test_device_puller_hip_graph_replay(compression):
+    """A whole one-GPU step captured into a HIP graph and replayed: byte-exact arena, the Merkle
+    check still runs every replay (a corrupted origin byte is caught on the next replay)."""
+    from zest_amd import ops
+    from zest_amd.engine import DevicePuller
+    from zest_amd.synthetic import SyntheticWorld
+    dev = torch.device("cuda:0")
+    w = SyntheticWorld("llama-tiny", seed=10, mode="bf16", max_xorb_bytes=256 << 10, compression=compression)
+    arena = ops.padded_empty(w.arena_bytes, dev)
+    w.generate_on_device(arena)
+    w.build_on_device(arena)
+    want = arena.clone()
+    p = DevicePuller(w, arena, 0, 1, round_bytes=256 << 10)  # > 4 rounds: tapered, slots reused
+    assert p.n_rounds > p.slots + 2
+    p.build_origin()
+    assert p.capture_graph()
+    for _ in range(3):
+        arena.fill_(0xA5)
+        p.err.zero_()
+        p.step()
+        torch.cuda.synchronize()
+        p.check()
+        for f in w.xet_files:
+            assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size]), f.path
+    # the replayed graph reads the live origin: flip one payload byte there and the check fails
+    p.origin.array[p.origin.n // 2] ^= 0x40
+    p.err.zero_()
+    p.step()
+    torch.cuda.synchronize()
+    with pytest.raises(ops.IngestError):
+        p.check()
+    p.close()

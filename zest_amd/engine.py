@@ -237,6 +237,8 @@ class DevicePuller:
         # waits until at most `steps_ahead` earlier steps are still in flight (0 = unbounded).
         self.steps_ahead = int(os.environ.get("ZEST_STEPS_AHEAD", "1"))
         self._inflight: collections.deque = collections.deque()
+        self._graph = None        # one-GPU steps replayed from a HIP graph (capture_graph)
+        self._capturing = False
         # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
         # every rank BLAKE3-hashes them as soon as they land, so each GPU verifies its whole replica
         # against the published Merkle file hashes without trusting any peer's hashes.
@@ -544,13 +546,77 @@ class DevicePuller:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
+    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int) -> None:
+        """Round rw's kernels on stream st: header walk, place/decode, BLAKE3 chunk hashes."""
+        if rw.term_b <= rw.term_a:
+            return
+        ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
+        H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, ws.chunks.data_ptr(),
+                      self.err.data_ptr(), st)
+        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(),
+                       rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
+        sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
+        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
+                      self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
+
+    def _issue_graph_rounds(self, H, lanes) -> None:
+        """The rounds of a captured step.  Round k runs entirely on lane k % 2 -- its H2D copy into
+        staging slot k % 4, then its kernels -- so a slot is only ever reused by the same lane, in
+        stream order, and the graph needs no cross-stream events: a stream waiting on an event
+        recorded by another side stream that itself depends on the first (copy stream -> lane ->
+        copy stream, as the eager pipeline does) crashed hipStreamEndCapture on ROCm 7
+        (tools/graph_probe3.py X).  The two lanes' copies still overlap each other's kernels."""
+        for k, rw in enumerate(self.rounds):
+            comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
+            src = self._graph_staging[k % len(self._graph_staging)]
+            with torch.cuda.stream(comp):
+                if rw.span_len:
+                    H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, comp.cuda_stream)
+                self._ingest_round(H, rw, src, ws, comp.cuda_stream)
+
+    def capture_graph(self) -> bool:
+        """One GPU: record a whole step (every round's H2D copy, event waits across the copy stream and
+        the two compute lanes, index/place/hash kernels, the Merkle check) into one HIP graph, so a
+        step is a single graph launch instead of ~1300 HIP calls from Python.  Collectives stay eager
+        (N > 1 is not captured).  Returns False, leaving eager steps, where capture is unavailable
+        (ZEST_GRAPH=0, CPU, N > 1, or the runtime refuses).
+
+        Host cost per step drops from ~1300 Python-issued HIP calls to one launch, but on a 70B pull
+        the graph ran at 51.2 GB/s against 56.2 for the eager pipeline (its copies ride the compute
+        lanes, see _issue_graph_rounds), so bench.py uses it only with ZEST_GRAPH=1."""
+        if not self.is_cuda or self.n_ranks > 1 or os.environ.get("ZEST_GRAPH", "1") == "0":
+            return False
+        # four staging slots (two per lane); the eager pipeline's three are reused
+        self._graph_staging = (self.staging + [ops.padded_empty(self.staging[0].numel(), self.device)
+                                               for _ in range(max(0, 4 - len(self.staging)))])[:4]
+        self.step()  # eager pass: every buffer (hash scratch) exists before capture
+        self._sync()
+        g = torch.cuda.CUDAGraph()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g):
+                self.step()
+        except Exception:  # noqa: BLE001 - fall back to eager steps
+            self._capturing = False
+            self._sync()
+            return False
+        self._capturing = False
+        self._graph = g
+        return True
+
     def step(self) -> dict:
         """One full pull of the model onto every rank.  Returns per-step stats."""
         import torch.distributed as dist
         dev = self.device
-        if self.is_cuda and self.steps_ahead > 0:
+        if self.is_cuda and self.steps_ahead > 0 and not self._capturing:
             while len(self._inflight) > self.steps_ahead:
                 self._inflight.popleft().synchronize()
+        if self._graph is not None:
+            self._graph.replay()
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(dev))
+            self._inflight.append(done)
+            return {"rounds": self.n_rounds, "graph": True}
         self.hashes.zero_()  # err is NOT reset: the first error of any step persists until check()
         works = []
         if self.is_cuda:
@@ -559,7 +625,9 @@ class DevicePuller:
             lanes = (self.lane_stream, self.side_stream)
             for ln in lanes:
                 ln.wait_stream(main)  # hashes.zero_() above, and the caller's earlier work
-            for k, rw in enumerate(self.rounds):
+            if self._capturing:
+                self._issue_graph_rounds(H, lanes)
+            for k, rw in enumerate(self.rounds if not self._capturing else ()):
                 s = k % self.slots
                 comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
                 st = comp.cuda_stream
@@ -573,17 +641,7 @@ class DevicePuller:
                     self.h2d_done[s].record(self.copy_stream)
                 with torch.cuda.stream(comp):
                     comp.wait_event(self.h2d_done[s])
-                    if rw.term_b > rw.term_a:
-                        nt = rw.term_b - rw.term_a
-                        src = self.staging[s]
-                        ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
-                        H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), nt, ws.chunks.data_ptr(),
-                                      self.err.data_ptr(), st)
-                        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(),
-                                       ws.chunks.data_ptr(), rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
-                        sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
-                        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
-                                      self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
+                    self._ingest_round(H, rw, self.staging[s], ws, st)
                     self.slot_free[s].record(comp)
                     if self.n_ranks > 1:
                         if self.exchange in PEER_MAPPED_MODES:
@@ -619,7 +677,7 @@ class DevicePuller:
             H.merkle(self.hashes.data_ptr(), self.sizes.data_ptr(), self.jobs_dev.data_ptr(), len(self.jobs),
                      self.roots.data_ptr(), self.merkle_scratch.data_ptr(), self.merkle_sb, st)
             H.compare_hashes(self.roots.data_ptr(), self.expected.data_ptr(), len(self.jobs), self.err.data_ptr(), st)
-            if self.steps_ahead > 0:
+            if self.steps_ahead > 0 and not self._capturing:
                 done = torch.cuda.Event()
                 done.record(main)
                 self._inflight.append(done)
