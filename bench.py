@@ -49,7 +49,7 @@ def main() -> None:
     ap.add_argument("--model", default="llama-3.1-70b")
     ap.add_argument("--mode", default="random", choices=["random", "bf16"])
     ap.add_argument("--round-mb", type=int, default=1024, help="per-rank bytes per pipeline round")
-    ap.add_argument("--slots", type=int, default=3)
+    ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--seeders", type=int, default=0,
                     help="ranks that pull from the origin (default all); the rest leech everything from "

@@ -1,7 +1,8 @@
 """Bisect the engine-step capture crash with the engine's own buffers and streams, re-issuing the
 step's stream/event structure by hand: python tools/graph_probe4.py <flags>
 flags: e = eager pass before capture (as capture_graph does), z = hashes.zero_() on the capture
-stream, c = ws.chunks zero_ per round, r = real engine streams (else fresh default-priority ones)."""
+stream, c = ws.chunks zero_ per round, r = the engine's lane streams (else fresh default-priority ones).
+(Reproduces the copy-stream pipeline the engine used before round 2's per-lane copies.)"""
 import faulthandler
 import sys
 from pathlib import Path
@@ -23,10 +24,8 @@ w.generate_on_device(arena)
 w.build_on_device(arena)
 p = DevicePuller(w, arena, 0, 1, round_bytes=256 << 10)
 p.build_origin()
-if "r" in flags:
-    copy_s, lanes = p.copy_stream, (p.lane_stream, p.side_stream)
-else:
-    copy_s, lanes = torch.cuda.Stream(dev), (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+copy_s = torch.cuda.Stream(dev)
+lanes = (p.lane_stream, p.side_stream) if "r" in flags else (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
 
 
 def body():

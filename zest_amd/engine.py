@@ -4,8 +4,8 @@ One process per GPU.  Each rank owns a contiguous, byte-balanced share of the mo
 reconstruction terms (SURVEY §2.E P1 "term-parallel fetch", sharded by owner rank) and streams it
 in rounds through a pinned-host -> HBM staging ring:
 
-    copy stream : hipMemcpyAsync(origin span k -> staging[k % S])           (CDN/PCIe ingest)
-    compute     : index_terms -> place (copy | LZ4/BG4 decode) -> chunk hashes  (zest_amd.ops)
+    lane k % 2  : hipMemcpyAsync(origin span k -> staging[k % 4])            (CDN/PCIe ingest)
+                  -> index_terms -> place (copy | LZ4/BG4 decode) -> chunk hashes  (zest_amd.ops)
     RCCL        : round-k regions replicated over xGMI (batched p2p, coalesced broadcasts or slab
                   all-gather, whichever autotune_exchange measured fastest), overlapped with round
                   k+1 ingest (every GPU acts as a BitTorrent peer)
@@ -197,11 +197,15 @@ class DevicePuller:
             max_terms = max(max_terms, b - a)
             max_chunks = max(max_chunks, nck)
         self.regions = [[self._region(k, r) for r in range(n_ranks)] for k in range(self.n_rounds)]
-        self.slots = max(1, min(slots, self.n_rounds))
-        self.staging = [ops.padded_empty(max_span, self.device) for _ in range(self.slots)]
-        # two compute lanes (main stream + side stream) take alternate rounds, so round k+1's kernels
-        # fill the GPU while round k's last chunks decode (a 1 GiB round is ~2 chunks per resident
-        # wave: a single stream leaves most CUs idle in each decode kernel's tail)
+        # Two compute lanes take alternate rounds.  Round k runs entirely on lane k % 2: its H2D copy
+        # into staging slot k % slots, then its kernels.  With an even slot count a slot is reused
+        # only by the same lane, in stream order, so the pipeline needs no events, and there is
+        # always a copy queued behind the other lane's kernels: the two lanes' copies keep PCIe busy
+        # (56.9 GB/s vs 56.2 for one copy stream gated by slot-free events, 70B pull,
+        # tools/step_times.py), while round k+1's kernels fill the CUs left idle in the tail of
+        # round k's decode (a 1 GiB round is ~2 chunks per resident wave).
+        self.slots = max(2, slots + (slots & 1))
+        self.staging = [ops.padded_empty(max_span, self.device) for _ in range(min(self.slots, self.n_rounds))]
         self.ws_lanes = [ops.IngestWorkspace(self.device, max_terms, max_chunks) for _ in range(2)]
         self.hashes = torch.zeros((world.n_chunks, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.from_numpy(world.chunk_len.astype(np.int64)).to(self.device)
@@ -225,11 +229,8 @@ class DevicePuller:
                 hi = int(torch.cuda.Stream.priority_range()[1])  # (least, greatest); lower = more urgent
             except Exception:
                 hi = -1
-            self.copy_stream = torch.cuda.Stream(self.device, priority=hi)
             self.lane_stream = torch.cuda.Stream(self.device, priority=hi)
             self.side_stream = torch.cuda.Stream(self.device, priority=hi)
-            self.h2d_done = [torch.cuda.Event() for _ in range(self.slots)]
-            self.slot_free = [torch.cuda.Event() for _ in range(self.slots)]
         # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
         # and returns, so a caller looping over step() without syncing queues thousands of commands
         # over many steps, and past ~10 steps queued the HIP runtime fed the device measurably slower
@@ -559,36 +560,21 @@ class DevicePuller:
         H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
                       self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
 
-    def _issue_graph_rounds(self, H, lanes) -> None:
-        """The rounds of a captured step.  Round k runs entirely on lane k % 2 -- its H2D copy into
-        staging slot k % 4, then its kernels -- so a slot is only ever reused by the same lane, in
-        stream order, and the graph needs no cross-stream events: a stream waiting on an event
-        recorded by another side stream that itself depends on the first (copy stream -> lane ->
-        copy stream, as the eager pipeline does) crashed hipStreamEndCapture on ROCm 7
-        (tools/graph_probe3.py X).  The two lanes' copies still overlap each other's kernels."""
-        for k, rw in enumerate(self.rounds):
-            comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
-            src = self._graph_staging[k % len(self._graph_staging)]
-            with torch.cuda.stream(comp):
-                if rw.span_len:
-                    H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, comp.cuda_stream)
-                self._ingest_round(H, rw, src, ws, comp.cuda_stream)
-
     def capture_graph(self) -> bool:
-        """One GPU: record a whole step (every round's H2D copy, event waits across the copy stream and
-        the two compute lanes, index/place/hash kernels, the Merkle check) into one HIP graph, so a
+        """One GPU: record a whole step (every round's H2D copy and index/place/hash kernels on the two
+        compute lanes, the Merkle check) into one HIP graph, so a
         step is a single graph launch instead of ~1300 HIP calls from Python.  Collectives stay eager
         (N > 1 is not captured).  Returns False, leaving eager steps, where capture is unavailable
         (ZEST_GRAPH=0, CPU, N > 1, or the runtime refuses).
 
-        Host cost per step drops from ~1300 Python-issued HIP calls to one launch, but on a 70B pull
-        the graph ran at 51.2 GB/s against 56.2 for the eager pipeline (its copies ride the compute
-        lanes, see _issue_graph_rounds), so bench.py uses it only with ZEST_GRAPH=1."""
+        The step's stream shape captures as is: every round lives on one lane, so the graph has no
+        cross-stream events (an earlier pipeline whose copy stream and lanes waited on each other
+        crashed hipStreamEndCapture, ROCm 7: tools/graph_probe3.py X).  Host cost per step drops from
+        ~1300 Python-issued HIP calls to one launch, but the graph's copy nodes ran slower (70B pull:
+        51.2 GB/s, the same shape issued eagerly 56.9; profiles/hip_graph_r2.md), so bench.py uses it
+        only with ZEST_GRAPH=1."""
         if not self.is_cuda or self.n_ranks > 1 or os.environ.get("ZEST_GRAPH", "1") == "0":
             return False
-        # four staging slots (two per lane); the eager pipeline's three are reused
-        self._graph_staging = (self.staging + [ops.padded_empty(self.staging[0].numel(), self.device)
-                                               for _ in range(max(0, 4 - len(self.staging)))])[:4]
         self.step()  # eager pass: every buffer (hash scratch) exists before capture
         self._sync()
         g = torch.cuda.CUDAGraph()
@@ -625,24 +611,16 @@ class DevicePuller:
             lanes = (self.lane_stream, self.side_stream)
             for ln in lanes:
                 ln.wait_stream(main)  # hashes.zero_() above, and the caller's earlier work
-            if self._capturing:
-                self._issue_graph_rounds(H, lanes)
-            for k, rw in enumerate(self.rounds if not self._capturing else ()):
-                s = k % self.slots
+            for k, rw in enumerate(self.rounds):
                 comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
+                src = self.staging[k % len(self.staging)]
                 st = comp.cuda_stream
                 if self._rx:
                     _core.trace.roctx_push(f"engine: round {k}")
-                with torch.cuda.stream(self.copy_stream):
-                    self.copy_stream.wait_event(self.slot_free[s])
-                    if rw.span_len:
-                        H.memcpy_async(self.staging[s].data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
-                                       self.copy_stream.cuda_stream)
-                    self.h2d_done[s].record(self.copy_stream)
                 with torch.cuda.stream(comp):
-                    comp.wait_event(self.h2d_done[s])
-                    self._ingest_round(H, rw, self.staging[s], ws, st)
-                    self.slot_free[s].record(comp)
+                    if rw.span_len:
+                        H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, st)
+                    self._ingest_round(H, rw, src, ws, st)
                     if self.n_ranks > 1:
                         if self.exchange in PEER_MAPPED_MODES:
                             # peers read round k once its kernels are done; wait for that only after
