@@ -159,9 +159,10 @@ struct LevelLds {
 // Group boundaries of one level (block-wide): cut flags u64(hash[24:32]) % 4 == 0, then the chain
 // p -> p + cut(p) (close after the first flagged child at index >= 2, at most 9 children) computed
 // in parallel: thread t owns positions [t*B, (t+1)*B); a group that starts before a block ends at
-// most 8 positions into it, so (A) each thread walks its block from all 9 possible entry offsets,
-// (B) one thread chains the 1024 exit offsets, (C) each thread re-walks from its true entry
-// counting starts, and after a block scan (D) writes them.  O(n/T) dependent steps per thread.
+// most 8 positions into it, so (A) each thread maps its block's 9 possible entry offsets to exit
+// offsets, (B) a scan of the map composition gives every block its true entry, (C) each thread
+// re-walks from its entry counting starts, and after a block scan (D) writes them.  O(n/T)
+// dependent steps per thread.
 // Returns the group count; s.starts[0..ng] holds the boundaries.
 __device__ uint32_t level_starts(const uint8_t* cur_h, uint64_t n, const JobScratch& s, LevelLds& L) {
   const uint32_t tid = threadIdx.x;
@@ -199,20 +200,47 @@ __device__ uint32_t level_starts(const uint8_t* cur_h, uint64_t n, const JobScra
     return end;
   };
   if (lo < hi) {
-    for (uint32_t e = 0; e < 9; ++e) {
-      uint64_t p = lo + e;
-      while (p < hi) p += cut_at(p);
-      L.exit[tid][e] = uint8_t(p >= hi ? p - hi : 0);
+    // entry 0 walks the whole block; every other entry walks only until its chain lands on a
+    // position of entry 0's chain (chains merge within a group or two), then shares its exit
+    uint64_t p0 = lo;
+    while (p0 < hi) p0 += cut_at(p0);
+    const uint8_t ex0 = uint8_t(p0 - hi);
+    L.exit[tid][0] = ex0;
+    for (uint32_t e = 1; e < 9; ++e) {
+      uint64_t p = lo + e, q = lo;
+      uint8_t ex = 0xFF;
+      while (p < hi) {
+        while (q < p) q += cut_at(q);
+        if (q == p) {
+          ex = ex0;
+          break;
+        }
+        p += cut_at(p);
+      }
+      L.exit[tid][e] = ex != 0xFF ? ex : uint8_t(p - hi);
     }
+  } else {
+#pragma unroll
+    for (uint32_t e = 0; e < 9; ++e) L.exit[tid][e] = uint8_t(e);  // past the end: identity map
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t entry = 0;
-    for (uint32_t t = 0; t < uint32_t(kThreads) && uint64_t(t) * B < n; ++t) {
-      L.entry[t] = uint8_t(entry);
-      entry = L.exit[t][entry];
+  // Block entries: entry_t = (X_{t-1} o ... o X_0)(0) with X_t the block's entry -> exit map.
+  // Inclusive scan of the map composition (Hillis-Steele, 10 steps) instead of one thread
+  // chaining all 1024 blocks.
+  for (uint32_t d = 1; d < uint32_t(kThreads); d <<= 1) {
+    uint8_t nxt[9];
+    if (tid >= d) {
+#pragma unroll
+      for (uint32_t e = 0; e < 9; ++e) nxt[e] = L.exit[tid][L.exit[tid - d][e]];
     }
+    __syncthreads();
+    if (tid >= d) {
+#pragma unroll
+      for (uint32_t e = 0; e < 9; ++e) L.exit[tid][e] = nxt[e];
+    }
+    __syncthreads();
   }
+  L.entry[tid] = tid == 0 ? 0 : L.exit[tid - 1][0];
   __syncthreads();
   uint32_t cnt = 0;
   if (lo < hi) {
