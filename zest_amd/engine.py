@@ -562,10 +562,10 @@ class DevicePuller:
 
     def capture_graph(self) -> bool:
         """One GPU: record a whole step (every round's H2D copy and index/place/hash kernels on the two
-        compute lanes, the Merkle check) into one HIP graph, so a
-        step is a single graph launch instead of ~1300 HIP calls from Python.  Collectives stay eager
-        (N > 1 is not captured).  Returns False, leaving eager steps, where capture is unavailable
-        (ZEST_GRAPH=0, CPU, N > 1, or the runtime refuses).
+        compute lanes, the Merkle check) into one HIP graph, so a step is a single graph launch
+        instead of ~1300 HIP calls from Python.  Collectives stay eager (N > 1 is not captured).
+        Returns False, leaving eager steps, where capture is unavailable (ZEST_GRAPH=0, CPU, N > 1,
+        or the runtime refuses).
 
         The step's stream shape captures as is: every round lives on one lane, so the graph has no
         cross-stream events (an earlier pipeline whose copy stream and lanes waited on each other
