@@ -2,6 +2,8 @@
 // raw device pointers (ints) and a hipStream_t (int, e.g. torch.cuda.current_stream().cuda_stream);
 // shape/bounds validation happens in zest_amd/ops before launch.
 #include <hip/hip_runtime.h>
+
+#include <cstring>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -67,6 +69,33 @@ PYBIND11_MODULE(_hip, m) {
     if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
     else check(e, "hipDeviceEnablePeerAccess");
     return true;
+  });
+  // Raw HIP IPC (dmabuf) of a device allocation, without torch's IPC wrapper (which also exports
+  // an event and a ref-counter file): export the allocation holding `ptr` as bytes, open a peer's.
+  // Returns (handle bytes, offset of ptr from the start of its allocation).
+  m.def("ipc_get_handle", [](uintptr_t ptr) {
+    hipIpcMemHandle_t h;
+    check(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)), "hipIpcGetMemHandle");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    check(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(ptr)), "hipMemGetAddressRange");
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof h),
+                          uint64_t(ptr - reinterpret_cast<uintptr_t>(base)));
+  });
+  m.def("ipc_open_handle", [](const py::bytes& b) {
+    const std::string s = b;
+    if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("ipc handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, s.data(), sizeof h);
+    void* p = nullptr;
+    {
+      py::gil_scoped_release nogil;
+      check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    }
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("ipc_close_handle", [](uintptr_t p) {
+    check(hipIpcCloseMemHandle(reinterpret_cast<void*>(p)), "hipIpcCloseMemHandle");
   });
   m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
     check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault, S(st)),
