@@ -475,6 +475,12 @@ def test_gpu_pull_of_bg4_compressed_world():
         p.check()
         for f in w.xet_files:  # (the alignment gaps between files are not part of the repository)
             assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size]), f.path
+    # back-to-back steps without a host sync: the host stays at most `steps_ahead` steps ahead
+    for _ in range(6):
+        p.step()
+        assert len(p._inflight) <= p.steps_ahead + 1
+    torch.cuda.synchronize()
+    p.check()
     p.close()
 
 
