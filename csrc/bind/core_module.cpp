@@ -254,6 +254,62 @@ PYBIND11_MODULE(_core, m) {
       out.append(py::make_tuple(e.header_off, e.clen, int(e.scheme), e.ulen, e.unpacked_off));
     return out;
   });
+  // Host header walk over a staging span of fetched runs: the same records and error words as the
+  // device kernel k_index_terms (csrc/gpu/ingest.hip), for callers whose bytes are in host memory
+  // anyway (the pull engine's origin): a pointer chase runs at host DRAM latency instead of HBM
+  // latency, and the GPU then only places and hashes.  terms: TERM_DTYPE records (40 B), out:
+  // CHUNK_DTYPE records (32 B) for n_out chunks (gaps between terms become zero no-op records).
+  // Returns 0, or code << 32 | term for the first bad term (codes as ZG_ERR_*).
+  m.def("index_runs", [](uintptr_t span, uint64_t span_len, uintptr_t terms, int n_terms, uintptr_t out,
+                         uint64_t n_out) -> uint64_t {
+    struct Term {
+      uint64_t src, src_len, dst;
+      uint32_t chunk_base, n_chunks;
+      uint64_t ulen;
+    };
+    struct Chunk {
+      uint64_t src, dst;
+      uint32_t clen, ulen, scheme, term;
+    };
+    static_assert(sizeof(Term) == 40 && sizeof(Chunk) == 32, "TERM_DTYPE / CHUNK_DTYPE layout");
+    py::gil_scoped_release nogil;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(span);
+    const Term* tv = reinterpret_cast<const Term*>(terms);
+    Chunk* cv = reinterpret_cast<Chunk*>(out);
+    std::memset(cv, 0, n_out * sizeof(Chunk));
+    uint64_t first_err = 0;
+    for (int t = 0; t < n_terms; ++t) {
+      const Term tm = tv[t];
+      uint64_t err = 0;
+      if (uint64_t(tm.chunk_base) + tm.n_chunks > n_out || tm.src + tm.src_len > span_len) err = 2;  // ZG_ERR_RANGE
+      uint64_t off = 0, uoff = 0;
+      for (uint32_t c = 0; c < tm.n_chunks && !err; ++c) {
+        if (off + 8 > tm.src_len) {
+          err = 3;  // ZG_ERR_COUNT
+          break;
+        }
+        const uint8_t* h = base + tm.src + off;
+        const uint32_t clen = uint32_t(h[1]) | uint32_t(h[2]) << 8 | uint32_t(h[3]) << 16;
+        const uint32_t scheme = h[4];
+        const uint32_t ulen = uint32_t(h[5]) | uint32_t(h[6]) << 8 | uint32_t(h[7]) << 16;
+        if (h[0] != 0 || scheme > 2 || (scheme == 0 && clen != ulen)) err = 1;  // ZG_ERR_HEADER
+        else if (off + 8 + clen > tm.src_len || (tm.ulen != 0 && uoff + ulen > tm.ulen)) err = 2;
+        else if (ulen > 128u * 1024u) err = 7;  // ZG_ERR_CAPACITY
+        if (err) break;
+        cv[tm.chunk_base + c] = Chunk{tm.src + off + 8, tm.dst + uoff, clen, ulen, scheme, uint32_t(t)};
+        off += 8 + clen;
+        uoff += ulen;
+      }
+      if (err) {  // the term's records stay zero (no-ops), as the device kernel leaves them
+        if (uint64_t(tm.chunk_base) + tm.n_chunks <= n_out)
+          std::memset(cv + tm.chunk_base, 0, size_t(tm.n_chunks) * sizeof(Chunk));
+      } else if (off != tm.src_len || (tm.ulen != 0 && uoff != tm.ulen)) {
+        err = 3;
+      }
+      if (err && !first_err) first_err = err << 32 | uint32_t(t);
+    }
+    return first_err;
+  }, py::arg("span"), py::arg("span_len"), py::arg("terms"), py::arg("n_terms"), py::arg("out"), py::arg("n_out"));
   m.def("parse_footer", [](py::buffer b) -> py::object {
     ByteSpan s = span_of(b);
     size_t st = 0;

@@ -517,3 +517,47 @@ def test_device_puller_hip_graph_replay(compression):
     with pytest.raises(ops.IngestError):
         p.check()
     p.close()
+
+
+def test_device_puller_host_header_walk_matches_device_walk():
+    """The engine's host header walk (default) and the device walk (ZEST_HOST_INDEX=0) give the
+    same byte-exact pull; a corrupted chunk header in the origin is reported by the host walk."""
+    import os
+
+    from zest_amd import ops
+    from zest_amd.engine import DevicePuller
+    from zest_amd.synthetic import SyntheticWorld
+    dev = torch.device("cuda:0")
+    w = SyntheticWorld("llama-tiny", seed=12, mode="bf16", max_xorb_bytes=256 << 10, compression="bg4")
+    arena = ops.padded_empty(w.arena_bytes, dev)
+    w.generate_on_device(arena)
+    w.build_on_device(arena)
+    want = arena.clone()
+    pullers = []
+    for host in ("1", "0"):
+        os.environ["ZEST_HOST_INDEX"] = host
+        try:
+            p = DevicePuller(w, arena, 0, 1, round_bytes=256 << 10)
+        finally:
+            os.environ.pop("ZEST_HOST_INDEX", None)
+        assert p.host_index == (host == "1")
+        p.build_origin()
+        for _ in range(3):  # both parities of the host record tables
+            arena.fill_(0x5A)
+            p.err.zero_()
+            p.step()
+            torch.cuda.synchronize()
+            p.check()
+            for f in w.xet_files:
+                assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size])
+        pullers.append(p)
+    p = pullers[0]
+    p.origin.array[0] = 7  # version byte of the first chunk header of the first term
+    p.err.zero_()
+    p.step()
+    torch.cuda.synchronize()
+    with pytest.raises(ops.IngestError) as ei:
+        p.check()
+    assert ei.value.code == 1
+    for q in pullers:
+        q.close()

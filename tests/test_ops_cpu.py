@@ -46,3 +46,49 @@ def test_select_boundaries_equals_chunker():
             cands.append(i + 1)
     ends = ops.select_chunks(np.array(cands, dtype=np.uint64), len(data))
     assert list(map(int, ends)) == C.chunk_ends(data)
+
+
+def test_host_index_runs_matches_chunk_index_and_reports_errors():
+    """_core.index_runs (the engine's host header walk) produces the device kernel's CHUNK_DTYPE
+    records for every term, zero records in gaps, and the kernel's error words."""
+    import random
+
+    rng = random.Random(4)
+    data = rng.randbytes(600_000) + bytes(200_000) + b"xorb index " * 30_000
+    ends = C.chunk_ends(data)
+    b = C.XorbBuilder("auto")
+    prev = 0
+    for e in ends:
+        b.add_chunk(data[prev:e])
+        prev = e
+    body = b.serialize(False)
+    idx = C.index_chunks(body)
+    n = len(idx)
+    bounds = b.chunk_boundaries()
+    cut = n // 2
+    span = np.frombuffer(body + bytes(64), dtype=np.uint8).copy()
+    terms = np.zeros(2, dtype=ops.TERM_DTYPE)
+    ulen0 = sum(e[3] for e in idx[:cut])
+    terms[0] = (0, bounds[cut - 1], 1000, 0, cut, ulen0)
+    terms[1] = (bounds[cut - 1], len(body) - bounds[cut - 1], 1000 + ulen0, cut + 3, n - cut,
+                len(data) - ulen0)  # 3-record gap before the second term
+    out = np.zeros(n + 3, dtype=ops.CHUNK_DTYPE)
+    err = C.index_runs(span.ctypes.data, len(body), terms.ctypes.data, 2, out.ctypes.data, len(out))
+    assert err == 0
+    for i, (hoff, clen, scheme, ulen, uoff) in enumerate(idx):
+        r = out[i if i < cut else i + 3]
+        assert (int(r["src"]), int(r["clen"]), int(r["scheme"]), int(r["ulen"])) == (hoff + 8, clen, scheme, ulen)
+        assert int(r["dst"]) == 1000 + uoff and int(r["term"]) == (0 if i < cut else 1)
+    assert not out[cut:cut + 3].view(np.uint8).any()
+    # a corrupted header version byte: error code 1 (bad header) for that term, its records zeroed
+    bad = span.copy()
+    bad[bounds[cut + 1]] = 9
+    err = C.index_runs(bad.ctypes.data, len(body), terms.ctypes.data, 2, out.ctypes.data, len(out))
+    assert err >> 32 == 1 and err & 0xFFFFFFFF == 1
+    assert not out[cut + 3:].view(np.uint8).any() and out[:cut]["clen"].all()
+    # a term claiming one chunk more than its bytes hold: count/size mismatch (3)
+    t2 = terms.copy()
+    t2[0]["n_chunks"] = cut + 1
+    t2[0]["ulen"] = 0
+    err = C.index_runs(span.ctypes.data, len(body), t2.ctypes.data, 1, out.ctypes.data, len(out))
+    assert err >> 32 in (2, 3) and err & 0xFFFFFFFF == 0

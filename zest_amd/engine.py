@@ -59,6 +59,8 @@ class RoundWork:
     span_len: int
     region: tuple        # arena [lo, hi) produced by this rank this round
     terms_dev: torch.Tensor | None = None  # TERM_DTYPE records (src relative to the staging slot)
+    terms_host: np.ndarray | None = None   # the same records on the host (host header walk)
+    table_off: int = 0                     # byte offset of the round's chunk records in a host table
 
 
 class OriginStore:
@@ -192,7 +194,8 @@ class DevicePuller:
                 terms_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
             else:
                 c0, nck, rec, region, terms_dev = 0, 0, None, (0, 0), None
-            self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev))
+            self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev, rec,
+                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize))
             max_span = max(max_span, span_len)
             max_terms = max(max_terms, b - a)
             max_chunks = max(max_chunks, nck)
@@ -238,6 +241,19 @@ class DevicePuller:
         # waits until at most `steps_ahead` earlier steps are still in flight (0 = unbounded).
         self.steps_ahead = int(os.environ.get("ZEST_STEPS_AHEAD", "1"))
         self._inflight: collections.deque = collections.deque()
+        # Header walk on the host (ZEST_HOST_INDEX, default on): the origin bytes are in host memory,
+        # where the walk's pointer chase (chunk i+1's header position depends on chunk i's length)
+        # runs at DRAM latency; each round's chunk records then reach the GPU with its copy, and the
+        # lane runs only place + hash (the device walk, k_index_terms, was a serial 0.84 ms HBM
+        # pointer chase per 1 GiB round and the largest kernel in the profile).  Pinned record
+        # tables alternate by step parity, which is race-free while at most one earlier step is in
+        # flight (steps_ahead == 1); otherwise, and inside a HIP graph, the device walk runs.
+        self.host_index = (self.is_cuda and self.steps_ahead == 1
+                           and os.environ.get("ZEST_HOST_INDEX", "1") != "0")
+        if self.host_index:
+            nbytes = max(1, sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize)
+            self._tables = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self._step_no = 0
         self._graph = None        # one-GPU steps replayed from a HIP graph (capture_graph)
         self._capturing = False
         # Chunks this rank receives in each round, as contiguous index runs (one per sending peer):
@@ -548,12 +564,22 @@ class DevicePuller:
             torch.cuda.synchronize(self.device)
 
     def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int) -> None:
-        """Round rw's kernels on stream st: header walk, place/decode, BLAKE3 chunk hashes."""
+        """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes."""
         if rw.term_b <= rw.term_a:
             return
-        ws.chunks[: rw.n_chunks * ops.CHUNK_DTYPE.itemsize].zero_()
-        H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, ws.chunks.data_ptr(),
-                      self.err.data_ptr(), st)
+        nbytes = rw.n_chunks * ops.CHUNK_DTYPE.itemsize
+        if self.host_index and not self._capturing:
+            tab = self._tables[self._step_no & 1]
+            rec_ptr = tab.data_ptr() + rw.table_off
+            e = _core.index_runs(self.origin.ptr + rw.span_off, rw.span_len, rw.terms_host.ctypes.data,
+                                 rw.term_b - rw.term_a, rec_ptr, rw.n_chunks)
+            if e:
+                self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
+            H.memcpy_async(ws.chunks.data_ptr(), rec_ptr, nbytes, st)
+        else:
+            ws.chunks[:nbytes].zero_()
+            H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, ws.chunks.data_ptr(),
+                          self.err.data_ptr(), st)
         H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(),
                        rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
         sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
@@ -604,6 +630,7 @@ class DevicePuller:
             self._inflight.append(done)
             return {"rounds": self.n_rounds, "graph": True}
         self.hashes.zero_()  # err is NOT reset: the first error of any step persists until check()
+        self._step_no += 1
         works = []
         if self.is_cuda:
             H = ops.hip()
