@@ -1,6 +1,8 @@
 // Device-direct pull: fetch a Xet file's reconstruction terms through the native cache -> P2P ->
-// CDN waterfall into pinned staging buffers and ingest them on the GPU (header walk, LZ4/BG4
-// decode, BLAKE3 chunk hashes) straight into a caller-provided HBM buffer, then verify the file's
+// CDN waterfall into pinned staging buffers and ingest them on the GPU (LZ4/BG4 decode, BLAKE3
+// chunk hashes; the chunk records come from the header index the fetch workers build anyway while
+// validating each run, so the GPU has no header walk to do) straight into a caller-provided HBM
+// buffer, then verify the file's
 // Xet hash with the Merkle kernel.  The host only moves compressed bytes; decompression and
 // verification never touch the CPU (the host pull path, csrc/core/downloader.cpp, does both on
 // the CPU).  North-star path for `zest_amd.pull(..., device=...)`.
@@ -59,9 +61,8 @@ struct DevBuf {
 struct Slot {
   uint8_t* host = nullptr;  // pinned
   DevBuf<uint8_t> dev;      // device staging (padded)
-  std::vector<ZgTerm> terms;
-  DevBuf<ZgTerm> terms_dev;
   DevBuf<ZgChunk> chunks_dev;
+  std::vector<ZgChunk> chunks_host;  // chunk records of the batch, built by the fetch workers
   hipEvent_t done = nullptr;
   bool busy = false;
 };
@@ -218,7 +219,7 @@ class DeviceXetPull {
     }
   }
 
-  // One pass over files[todo]: fetch -> staging -> H2D -> index/place/hash -> Merkle roots.
+  // One pass over files[todo]: fetch (+ chunk records) -> staging -> H2D -> place/hash -> Merkle roots.
   Attempt run_once(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& all_files,
                    const std::vector<cas::Reconstruction>& all_recs, const std::vector<size_t>& todo,
                    const FetchOptions& opt) {
@@ -296,6 +297,9 @@ class DeviceXetPull {
         trace::Span batch_span("device", "fetch batch");
         batch_span.arg("\"terms\":" + std::to_string(end - next));
         std::vector<uint64_t> len(end - next, 0), src_at(end - next, 0);
+        // Chunk records of the batch, filled by the workers from the index they build anyway
+        // (disjoint ranges per term), so the GPU needs no header walk of its own.
+        s.chunks_host.assign(size_t((end < n ? gt[end].chunk : file_chunk0[nf]) - gt[next].chunk), ZgChunk{});
         std::atomic<size_t> k{next};
         std::mutex em;
         auto worker = [&]() {
@@ -324,6 +328,24 @@ class DeviceXetPull {
                 src_at[i - next] = off[i - next];
               }
               len[i - next] = b - a;
+              // the device records of this term's chunks; a term that does not match its plan keeps
+              // zero (no-op) records, so its file fails the Merkle check and takes the repair path
+              ZgChunk* cr = s.chunks_host.data() + (gt[i].chunk - gt[next].chunk);
+              const uint64_t run0 = src_at[i - next];
+              uint64_t uoff = 0;
+              bool ok = r.local_end - r.local_start == gt[i].nchunks;
+              for (uint32_t j = r.local_start; ok && j < r.local_end; ++j) {
+                const xet::ChunkEntry& e = idx[j];
+                const uint32_t sc = uint32_t(e.scheme);
+                if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
+                  ok = false;
+                  break;
+                }
+                cr[j - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
+                                                 e.clen, e.ulen, sc, uint32_t(i - next)};
+                uoff += e.ulen;
+              }
+              if (!ok || uoff != gt[i].ulen) std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
             } catch (const std::exception& e) {
               std::lock_guard<std::mutex> g(em);
               if (fetch_err.empty()) fetch_err = e.what();
@@ -335,34 +357,22 @@ class DeviceXetPull {
         for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
         for (auto& t : ts) t.join();
         if (!fetch_err.empty()) break;
-        s.terms.clear();
         uint64_t top = 0;
         for (size_t i = next; i < end; ++i) {
-          ZgTerm t{};
-          t.src = src_at[i - next];
-          t.src_len = len[i - next];
-          t.dst = gt[i].dst;
-          t.chunk_base = uint32_t(gt[i].chunk - gt[next].chunk);
-          t.n_chunks = gt[i].nchunks;
-          t.ulen = gt[i].ulen;
-          s.terms.push_back(t);
-          at.fetched += t.src_len;
-          top = std::max<uint64_t>(top, t.src + t.src_len);
+          at.fetched += len[i - next];
+          top = std::max<uint64_t>(top, src_at[i - next] + len[i - next]);
         }
-        const int nterms = int(end - next);
         const uint64_t c0 = gt[next].chunk;
         const uint64_t c1 = end < n ? gt[end].chunk : nck;
         const int nchunks = int(c1 - c0);
-        s.terms_dev.ensure(size_t(nterms));
         s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
         batch_span.arg("\"bytes\":" + std::to_string(top));
-        trace::Span submit_span("device", "H2D + index/place/hash submit");
+        trace::Span submit_span("device", "H2D + place/hash submit");
         hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
-        hip_check(hipMemcpyAsync(s.terms_dev.p, s.terms.data(), sizeof(ZgTerm) * size_t(nterms),
-                                 hipMemcpyHostToDevice, stream_),
-                  "H2D terms");
-        hip_check(hipMemsetAsync(s.chunks_dev.p, 0, sizeof(ZgChunk) * size_t(nchunks), stream_), "memset");
-        hip_check(zg_index_terms(s.dev.p, s.terms_dev.p, nterms, s.chunks_dev.p, err_.p, stream_), "index");
+        if (nchunks)
+          hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
+                                   hipMemcpyHostToDevice, stream_),
+                    "H2D chunk records");
         hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
                                   stream_),
                   "place");
