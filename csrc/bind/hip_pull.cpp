@@ -7,9 +7,9 @@
 // verification never touch the CPU (the host pull path, csrc/core/downloader.cpp, does both on
 // the CPU).  North-star path for `zest_amd.pull(..., device=...)`.
 //
-// Pipeline per file: batches of terms fill one of two pinned buffers (fetch threads) while the
-// previous batch's H2D + kernels run on a private HIP stream; a buffer is reused only after its
-// stream event completed.
+// Pipeline: batches of terms fill one of two pinned buffers (fetch threads that run on across
+// batch boundaries) while the previous batch's H2D + kernels run on a private HIP stream; a buffer
+// is refilled only after its stream event completed.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -64,7 +65,6 @@ struct Slot {
   DevBuf<ZgChunk> chunks_dev;
   std::vector<ZgChunk> chunks_host;  // chunk records of the batch, built by the fetch workers
   hipEvent_t done = nullptr;
-  bool busy = false;
 };
 
 class DeviceXetPull {
@@ -268,128 +268,175 @@ class DeviceXetPull {
     std::string& fetch_err = at.fetch_err;
     {
       py::gil_scoped_release nogil;
-      size_t next = 0;
-      int slot = 0;
-      while (next < n && fetch_err.empty()) {
-        // Batch [next, end) by an upper bound of each term's fetched size, so every term fetched
-        // in the batch has a reserved region of the pinned buffer (no refetch, no second copy
-        // pass): workers receive / copy their run straight into place.
-        std::vector<uint64_t> off;
+      // Batches: consecutive terms whose fetched-size bounds fit one staging slot, so every term
+      // has a reserved region of the pinned buffer (no refetch, no second copy pass: workers
+      // receive / copy their run straight into place).  Batch b fills slot b % 2.
+      uint64_t max_bound = 0;
+      for (size_t i = 0; i < n; ++i) max_bound = std::max(max_bound, term_bound(gt[i].ulen, gt[i].nchunks));
+      if (max_bound > cap_) grow_staging(max_bound);  // one huge term: enlarge both slots
+      struct Batch {
+        size_t begin = 0, end = 0;
+        std::vector<uint64_t> off, len, src_at;  // per term: region, fetched bytes, run start
+      };
+      std::vector<Batch> batches;
+      std::vector<uint32_t> batch_of(n);
+      for (size_t next = 0; next < n;) {
+        Batch bt;
+        bt.begin = next;
         uint64_t pos = 0;
         size_t end = next;
         while (end < n) {
           const uint64_t bound = term_bound(gt[end].ulen, gt[end].nchunks);
-          if (bound > cap_) {
-            if (end > next) break;
-            grow_staging(bound);  // one huge term: enlarge both slots (waits for them)
-          }
           if (pos + bound > cap_ && end > next) break;
-          off.push_back(pos);
+          bt.off.push_back(pos);
           pos += bound;
-          ++end;
+          batch_of[end++] = uint32_t(batches.size());
         }
-        Slot& s = slots_[slot];
-        if (s.busy) {
-          trace::Span sp("device", "wait staging slot");
-          hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
-          s.busy = false;
-        }
-        trace::Span batch_span("device", "fetch batch");
-        batch_span.arg("\"terms\":" + std::to_string(end - next));
-        std::vector<uint64_t> len(end - next, 0), src_at(end - next, 0);
-        // Chunk records of the batch, filled by the workers from the index they build anyway
-        // (disjoint ranges per term), so the GPU needs no header walk of its own.
-        s.chunks_host.assign(size_t((end < n ? gt[end].chunk : file_chunk0[nf]) - gt[next].chunk), ZgChunk{});
-        std::atomic<size_t> k{next};
-        std::mutex em;
-        auto worker = [&]() {
-          while (true) {
-            const size_t i = k.fetch_add(1);
-            if (i >= end) return;
-            try {
-              const auto& rec = all_recs[todo[gt[i].file]];
-              // The run is received straight into this term's region of the pinned buffer when it
-              // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
-              uint8_t* region = s.host + off[i - next];
-              const uint64_t room = (i + 1 < end ? off[i + 1 - next] : cap_) - off[i - next];
-              auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-              XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
-              at.sources[gt[i].file][gt[i].term] = TermSource{r.source, r.run_offset, r.pending};
-              auto idx = xet::index_chunks(r.bytes(), r.size());
-              if (r.local_end > idx.size() || r.local_start >= r.local_end)
-                throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
-              const uint64_t a = idx[r.local_start].header_off;
-              const uint64_t b = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
-              if (r.ext) {
-                src_at[i - next] = off[i - next] + a;  // already in place
-              } else {
-                if (b - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
-                std::memcpy(region, r.data.data() + a, b - a);
-                src_at[i - next] = off[i - next];
-              }
-              len[i - next] = b - a;
-              // the device records of this term's chunks; a term that does not match its plan keeps
-              // zero (no-op) records, so its file fails the Merkle check and takes the repair path
-              ZgChunk* cr = s.chunks_host.data() + (gt[i].chunk - gt[next].chunk);
-              const uint64_t run0 = src_at[i - next];
-              uint64_t uoff = 0;
-              bool ok = r.local_end - r.local_start == gt[i].nchunks;
-              for (uint32_t j = r.local_start; ok && j < r.local_end; ++j) {
-                const xet::ChunkEntry& e = idx[j];
-                const uint32_t sc = uint32_t(e.scheme);
-                if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
-                  ok = false;
-                  break;
-                }
-                cr[j - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
-                                                 e.clen, e.ulen, sc, uint32_t(i - next)};
-                uoff += e.ulen;
-              }
-              if (!ok || uoff != gt[i].ulen) std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
-            } catch (const std::exception& e) {
-              std::lock_guard<std::mutex> g(em);
-              if (fetch_err.empty()) fetch_err = e.what();
-            }
-          }
-        };
-        std::vector<std::thread> ts;
-        const int nt = int(std::min<size_t>(size_t(threads_), end - next));
-        for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
-        for (auto& t : ts) t.join();
-        if (!fetch_err.empty()) break;
-        uint64_t top = 0;
-        for (size_t i = next; i < end; ++i) {
-          at.fetched += len[i - next];
-          top = std::max<uint64_t>(top, src_at[i - next] + len[i - next]);
-        }
-        const uint64_t c0 = gt[next].chunk;
-        const uint64_t c1 = end < n ? gt[end].chunk : nck;
-        const int nchunks = int(c1 - c0);
-        s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
-        batch_span.arg("\"bytes\":" + std::to_string(top));
-        trace::Span submit_span("device", "H2D + place/hash submit");
-        hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
-        if (nchunks)
-          hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
-                                   hipMemcpyHostToDevice, stream_),
-                    "H2D chunk records");
-        hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
-                                  stream_),
-                  "place");
-        uint64_t ubytes = 0;
-        for (size_t i = next; i < end; ++i) ubytes += gt[i].ulen;
-        const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
-        hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
-        hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
-                                 hash_scratch_.p, hs_bytes, stream_),
-                  "hash");
-        hip_check(hipEventRecord(s.done, stream_), "event");
-        s.busy = true;
+        bt.end = end;
+        bt.len.assign(end - next, 0);
+        bt.src_at.assign(end - next, 0);
+        batches.push_back(std::move(bt));
         next = end;
-        slot ^= 1;
       }
+      const size_t nb = batches.size();
+      auto chunk_lo = [&](size_t b) { return gt[batches[b].begin].chunk; };
+      auto chunk_hi = [&](size_t b) { return batches[b].end < n ? gt[batches[b].end].chunk : nck; };
+      // Continuous pipeline: the fetch workers take terms in order across batch boundaries, so the
+      // next batch's terms are already in flight while the current batch's slowest transfers finish
+      // (a per-batch join left the connections ~45 % idle: tools/direct_bench.py under ZEST_TRACE).
+      // A worker may fill slot b % 2 for batch b once ready[b % 2] >= b, i.e. once the GPU work of
+      // batch b - 2 on that slot has completed; the submitting thread (this one) waits for each
+      // batch's last term, queues its H2D + kernels, and frees the slot when they are done.
+      std::mutex mu;
+      std::condition_variable cv;
+      size_t ready[2] = {0, 1};
+      std::vector<size_t> remaining(nb);
+      for (size_t b = 0; b < nb; ++b) remaining[b] = batches[b].end - batches[b].begin;
+      bool abort = false;
+      for (size_t b = 0; b < std::min<size_t>(2, nb); ++b)
+        slots_[b].chunks_host.assign(size_t(chunk_hi(b) - chunk_lo(b)), ZgChunk{});
+      std::atomic<size_t> k{0};
+      auto fail = [&](const std::string& what) {
+        std::lock_guard<std::mutex> g(mu);
+        if (fetch_err.empty()) fetch_err = what;
+        abort = true;
+        cv.notify_all();
+      };
+      auto worker = [&]() {
+        while (true) {
+          const size_t i = k.fetch_add(1);
+          if (i >= n) return;
+          const size_t b = batch_of[i];
+          Batch& bt = batches[b];
+          Slot& s = slots_[b & 1];
+          {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return abort || ready[b & 1] >= b; });
+            if (abort) return;
+          }
+          const size_t j = i - bt.begin;
+          try {
+            const auto& rec = all_recs[todo[gt[i].file]];
+            // The run is received straight into this term's region of the pinned buffer when it
+            // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
+            uint8_t* region = s.host + bt.off[j];
+            const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
+            auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
+            XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
+            at.sources[gt[i].file][gt[i].term] = TermSource{r.source, r.run_offset, r.pending};
+            auto idx = xet::index_chunks(r.bytes(), r.size());
+            if (r.local_end > idx.size() || r.local_start >= r.local_end)
+              throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
+            const uint64_t a = idx[r.local_start].header_off;
+            const uint64_t e_end = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
+            if (r.ext) {
+              bt.src_at[j] = bt.off[j] + a;  // already in place
+            } else {
+              if (e_end - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
+              std::memcpy(region, r.data.data() + a, e_end - a);
+              bt.src_at[j] = bt.off[j];
+            }
+            bt.len[j] = e_end - a;
+            // the device records of this term's chunks; a term that does not match its plan keeps
+            // zero (no-op) records, so its file fails the Merkle check and takes the repair path
+            ZgChunk* cr = s.chunks_host.data() + (gt[i].chunk - chunk_lo(b));
+            const uint64_t run0 = bt.src_at[j];
+            uint64_t uoff = 0;
+            bool ok = r.local_end - r.local_start == gt[i].nchunks;
+            for (uint32_t c = r.local_start; ok && c < r.local_end; ++c) {
+              const xet::ChunkEntry& e = idx[c];
+              const uint32_t sc = uint32_t(e.scheme);
+              if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
+                ok = false;
+                break;
+              }
+              cr[c - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
+                                               e.clen, e.ulen, sc, uint32_t(j)};
+              uoff += e.ulen;
+            }
+            if (!ok || uoff != gt[i].ulen) std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
+          } catch (const std::exception& e) {
+            fail(e.what());
+            return;
+          }
+          std::lock_guard<std::mutex> g(mu);
+          if (--remaining[b] == 0) cv.notify_all();
+        }
+      };
+      std::vector<std::thread> ts;
+      const int nt = int(std::min<size_t>(size_t(threads_), n));
+      for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
+      try {
+        for (size_t b = 0; b < nb; ++b) {
+          {
+            trace::Span sp("device", "wait fetch batch");
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return abort || remaining[b] == 0; });
+            if (abort) break;
+          }
+          const Batch& bt = batches[b];
+          Slot& s = slots_[b & 1];
+          uint64_t top = 0;
+          for (size_t j = 0; j < bt.len.size(); ++j) {
+            at.fetched += bt.len[j];
+            top = std::max<uint64_t>(top, bt.src_at[j] + bt.len[j]);
+          }
+          const uint64_t c0 = chunk_lo(b);
+          const int nchunks = int(chunk_hi(b) - c0);
+          s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
+          trace::Span submit_span("device", "H2D + place/hash");
+          submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
+          hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
+          if (nchunks)
+            hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
+                                     hipMemcpyHostToDevice, stream_),
+                      "H2D chunk records");
+          hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
+                                    stream_),
+                    "place");
+          uint64_t ubytes = 0;
+          for (size_t i = bt.begin; i < bt.end; ++i) ubytes += gt[i].ulen;
+          const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
+          hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
+          hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
+                                   hash_scratch_.p, hs_bytes, stream_),
+                    "hash");
+          hip_check(hipEventRecord(s.done, stream_), "event");
+          // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
+          hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
+          if (b + 2 < nb) s.chunks_host.assign(size_t(chunk_hi(b + 2) - chunk_lo(b + 2)), ZgChunk{});
+          std::lock_guard<std::mutex> g(mu);
+          ready[b & 1] = b + 2;
+          cv.notify_all();
+        }
+      } catch (const std::exception& e) {
+        fail(e.what());
+        for (auto& t : ts) t.join();
+        (void)hipStreamSynchronize(stream_);
+        throw;
+      }
+      for (auto& t : ts) t.join();
       hip_check(hipStreamSynchronize(stream_), "sync");
-      for (auto& s : slots_) s.busy = false;
     }
     if (!fetch_err.empty()) return at;
     hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
@@ -429,11 +476,8 @@ class DeviceXetPull {
   }
 
   void grow_staging(uint64_t bytes) {
+    hip_check(hipStreamSynchronize(stream_), "sync");  // no copy still reads the old buffers
     for (auto& s : slots_) {
-      if (s.busy) {
-        hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
-        s.busy = false;
-      }
       if (s.host) (void)hipHostFree(s.host);
       s.host = nullptr;
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), bytes + 4096, hipHostMallocDefault), "hipHostMalloc");

@@ -161,12 +161,18 @@ std::vector<ChunkResult> PeerSession::request_many(const std::vector<XetRequest>
 }
 
 std::shared_ptr<PeerSession> PeerPool::lease(const std::shared_ptr<PeerSession>& s) {
+  // Constructed in place and non-copyable: the count is raised once and dropped once.  (A
+  // temporary `Lease{s}` copied into make_shared ran the destructor twice, so every finished
+  // request left its session one below zero, and "least used" then sent every later request to
+  // the one session used most -- all workers queued on a single connection.)
   struct Lease {
-    std::shared_ptr<PeerSession> s;
+    explicit Lease(std::shared_ptr<PeerSession> p) : s(std::move(p)) { s->users_.fetch_add(1, std::memory_order_relaxed); }
+    Lease(const Lease&) = delete;
+    Lease& operator=(const Lease&) = delete;
     ~Lease() { s->users_.fetch_sub(1, std::memory_order_relaxed); }
+    std::shared_ptr<PeerSession> s;
   };
-  s->users_.fetch_add(1, std::memory_order_relaxed);
-  auto l = std::make_shared<Lease>(Lease{s});
+  auto l = std::make_shared<Lease>(s);
   return std::shared_ptr<PeerSession>(l, s.get());  // aliasing: lives as long as the lease
 }
 

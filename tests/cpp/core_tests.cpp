@@ -13,6 +13,8 @@
 
 #include "bencode.h"
 #include "blake3.h"
+#include "bt_peer.h"
+#include "bt_server.h"
 #include "bt_wire.h"
 #include "cdc.h"
 #include "config.h"
@@ -310,6 +312,45 @@ TEST(xorb_cache_runs) {
   CHECK(h->data.size() == body.size() - idx[4].header_off);
   CHECK(!cache.find(hx, 2, 4).has_value());
   CHECK(storage::list_cached_xorbs(cfg).size() == 1);
+}
+
+TEST(peer_pool_leases) {
+  // Lease accounting of the connection pool against a loopback seeding server: a lease raises its
+  // session's user count by exactly one for its lifetime, busy sessions make the pool open more
+  // connections up to the per-peer limit, and idle sessions are handed out one per caller.
+  char tmpl[] = "/tmp/zest_cpp_pool_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  setenv("ZEST_CACHE_DIR", dir, 1);
+  Config cfg = Config::from_env();
+  storage::XorbCache cache(cfg);
+  bt::BtServer srv(cfg, &cache, {}, 0);
+  srv.start();
+  const net::Addr a = net::Addr::parse("127.0.0.1:" + std::to_string(srv.port()), 6881);
+  Sha1Digest ih{};
+  bt::PeerPool pool(cfg.peer_id, 0, 64, 5000, 4);
+  std::vector<std::shared_ptr<bt::PeerSession>> held;
+  for (int i = 0; i < 4; ++i) held.push_back(pool.get_or_connect(a, ih));
+  CHECK(pool.count(a) == 4);
+  std::vector<bt::PeerSession*> raw;
+  for (auto& h : held) {
+    CHECK(h->users() == 1);
+    raw.push_back(h.get());
+  }
+  for (int i = 0; i < 4; ++i)
+    for (int j = i + 1; j < 4; ++j) CHECK(raw[i] != raw[j]);
+  held.clear();
+  for (auto* r : raw) CHECK(r->users() == 0);
+  // many sequential lease/release cycles keep the count at zero, and concurrent holders still get
+  // distinct sessions (before the fix every cycle drove the session one lower)
+  for (int k = 0; k < 10; ++k) (void)pool.get_or_connect(a, ih);
+  for (auto* r : raw) CHECK(r->users() == 0);
+  for (int i = 0; i < 4; ++i) held.push_back(pool.get_or_connect(a, ih));
+  CHECK(pool.count(a) == 4);
+  for (int i = 0; i < 4; ++i)
+    for (int j = i + 1; j < 4; ++j) CHECK(held[i].get() != held[j].get());
+  held.clear();
+  srv.stop();
 }
 
 int main() {
