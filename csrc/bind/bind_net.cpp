@@ -470,6 +470,7 @@ void bind_extra(py::module_& m) {
         r["chunks_served"] = st.chunks_served;
         r["bytes_served"] = st.bytes_served;
         r["not_found"] = st.not_found;
+        r["rejected"] = st.rejected;
         return r;
       })
       .def("stop", [](PySeeder& s) {

@@ -163,6 +163,7 @@ void bind_hip_seed(py::module_& m) {
         d["chunk_units"] = st.chunk_units;
         d["bytes_served"] = st.bytes_served;
         d["not_found"] = st.not_found;
+        d["rejected"] = st.rejected;
         return d;
       });
 }

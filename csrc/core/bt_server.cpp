@@ -89,6 +89,7 @@ ServerStats BtServer::stats() const {
   s.bytes_served = bytes_.load();
   s.not_found = nf_.load();
   s.chunk_units = units_.load();
+  s.rejected = rejected_.load();
   return s;
 }
 
@@ -105,6 +106,13 @@ void BtServer::accept_loop() {
     std::lock_guard<std::mutex> g(mu_);
     reap_locked();  // a long-running seeder must not accumulate one finished thread per connection
     if (!s.valid()) continue;
+    // Every connection is served by its own thread: past max_inbound (ZEST_MAX_INBOUND) a new peer
+    // is closed at once, so a flood of connections cannot exhaust threads or file descriptors (the
+    // reference's server.zig accepts without bound).  The peer sees EOF and moves on.
+    if (cfg_.max_inbound && conns_.size() >= cfg_.max_inbound) {
+      rejected_++;
+      continue;  // `s` closes here
+    }
     conns_.insert(s.fd());
     auto done = std::make_shared<std::atomic<bool>>(false);
     std::thread t([this, sock = std::move(s), peer, done]() mutable {

@@ -38,6 +38,7 @@ struct ServerStats {
   uint64_t bytes_served = 0;
   uint64_t not_found = 0;
   uint64_t chunk_units = 0;  // Xet chunks delivered (sum of requested range lengths)
+  uint64_t rejected = 0;     // connections closed at accept: max_inbound already being served
 };
 
 struct FaultSpec {
@@ -79,7 +80,7 @@ class BtServer {
   std::mutex mu_;
   std::set<int> conns_;
   std::list<Worker> workers_;
-  std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0};
+  std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0}, rejected_{0};
   FaultSpec fault_;
 };
 

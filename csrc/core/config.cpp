@@ -67,6 +67,7 @@ Config Config::from_env() {
   c.listen_port = port_env("ZEST_LISTEN_PORT", kDefaultListenPort);
   c.dht_port = port_env("ZEST_DHT_PORT", kDefaultDhtPort);
   if (const char* v = env("ZEST_MAX_PEERS")) c.max_peers = uint32_t(std::strtoul(v, nullptr, 10));
+  if (const char* v = env("ZEST_MAX_INBOUND")) c.max_inbound = uint32_t(std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_PEER_CONNECTIONS")) c.peer_connections = uint32_t(std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_CONCURRENCY")) c.concurrency = std::max(1ul, std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_GPUS")) c.gpus = std::atoi(v);
@@ -101,7 +102,7 @@ std::string Config::to_json() const {
   w.key("version").str(kVersion).key("hub_url").str(hub_url).key("hf_cache_dir").str(hf_cache_dir);
   w.key("cache_dir").str(cache_dir).key("xorb_cache_dir").str(xorb_cache_dir).key("chunk_cache_dir").str(chunk_cache_dir);
   w.key("pid_file").str(pid_file).key("dht_port").num(int64_t(dht_port)).key("listen_port").num(int64_t(listen_port));
-  w.key("http_port").num(int64_t(http_port)).key("max_peers").num(int64_t(max_peers));
+  w.key("http_port").num(int64_t(http_port)).key("max_peers").num(int64_t(max_peers)).key("max_inbound").num(int64_t(max_inbound));
   w.key("peer_connections").num(int64_t(peer_connections)).key("cache_writes").boolean(cache_writes);
   w.key("concurrency").num(int64_t(concurrency)).key("has_token").boolean(hf_token.has_value());
   w.key("gpus").num(int64_t(gpus)).key("hbm_cache_gb").num(hbm_cache_gb, 1);

@@ -41,6 +41,7 @@ struct Config {
   uint16_t listen_port = kDefaultListenPort;
   uint16_t http_port = kDefaultHttpPort;
   uint32_t max_peers = kDefaultMaxPeers;
+  uint32_t max_inbound = 512;      // ZEST_MAX_INBOUND: concurrent peer connections the seeding server serves
   uint32_t peer_connections = 16;  // ZEST_PEER_CONNECTIONS: parallel connections per peer (= default concurrency)
   uint32_t chunk_target = kDefaultChunkTarget;
   uint32_t concurrency = kDefaultConcurrency;

@@ -47,6 +47,7 @@ std::string ApiServer::status_json() const {
   w.key("bytes_served").num_u(s.bytes_served);
   w.key("total_peers").num_u(s.total_peers);
   w.key("not_found").num_u(s.not_found);
+  w.key("rejected").num_u(s.rejected);
   w.key("uptime_s").num(std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count(), 1);
   w.key("peer_id").str(std::string(reinterpret_cast<const char*>(cfg_.peer_id.data()), 8));
   if (extra_) w.key("device").raw(extra_());

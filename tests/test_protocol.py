@@ -260,3 +260,48 @@ def test_reconstruction_json_roundtrip():
     back = json.loads(_core.parse_reconstruction(json.dumps(rec)))
     assert back["terms"][0]["unpacked_length"] == 100
     assert back["fetch_info"]["ab" * 32][0]["url_range"] == {"start": 0, "end": 99}
+
+
+def test_seeder_caps_inbound_connections(monkeypatch, tmp_path):
+    """ZEST_MAX_INBOUND bounds the seeding server's connection threads: a peer past the cap is
+    closed at accept (counted in stats()["rejected"]); once a served peer leaves, a new one is
+    served again."""
+    import socket
+    import time
+
+    monkeypatch.setenv("HOME", str(tmp_path))
+    monkeypatch.setenv("ZEST_CACHE_DIR", str(tmp_path / "zc"))
+    monkeypatch.setenv("ZEST_MAX_INBOUND", "2")
+    seeder = _core.Seeder(port=0)
+
+    def wait_for(pred, what):
+        for _ in range(200):
+            if pred():
+                return
+            time.sleep(0.025)
+        raise AssertionError(f"timed out waiting for {what}: {seeder.stats()}")
+
+    def closed_by_server(sock):
+        sock.settimeout(5)
+        try:
+            return sock.recv(1) == b""
+        except ConnectionResetError:
+            return True
+
+    try:
+        held = [socket.create_connection(("127.0.0.1", seeder.port)) for _ in range(2)]
+        wait_for(lambda: seeder.stats()["active_peers"] == 2, "two served peers")
+        extra = socket.create_connection(("127.0.0.1", seeder.port))
+        assert closed_by_server(extra)
+        extra.close()
+        wait_for(lambda: seeder.stats()["rejected"] == 1, "one rejected peer")
+        held.pop().close()
+        wait_for(lambda: seeder.stats()["active_peers"] == 1, "the closed peer's thread to end")
+        again = socket.create_connection(("127.0.0.1", seeder.port))
+        wait_for(lambda: seeder.stats()["active_peers"] == 2, "the new peer to be served")
+        assert seeder.stats()["rejected"] == 1
+        again.close()
+        for s in held:
+            s.close()
+    finally:
+        seeder.stop()
