@@ -100,10 +100,12 @@ def test_swarm_pull_every_rank_gets_every_tensor(hub_env, world_size):
     assert hub.counters.get("xorb_get", 0) > 0
 
 
-def test_swarm_pull_failed_owner_fails_every_rank(hub_env):
+@pytest.mark.parametrize("victim_index", [0, -1])
+def test_swarm_pull_failed_owner_fails_every_rank(hub_env, victim_index):
     world, hub = hub_env
-    # the CDN refuses every xorb behind one file: its owner cannot fetch it
-    victim = world.xet_files[0]
+    # the CDN refuses every xorb behind one file: its owner cannot fetch it (file 0: a first-round
+    # fetch; the last file: a later round, after earlier rounds' broadcasts were issued)
+    victim = world.xet_files[victim_index]
     xh = hub.xet_hash(world.spec.repo_id, victim.path)
     hub.fail_xorbs = {t["hash"] for t in hub.reconstruction(xh)["terms"]}
     res = _run(3, world.spec.repo_id)

@@ -5,7 +5,8 @@ while each Xet file crosses the network (peers / CDN / local xorb cache) exactly
     tensors = swarm_pull("meta-llama/Llama-3.1-70B")   # collective; every rank gets all tensors
 
 Each Xet-backed safetensors file has one owner rank (LPT split by size, as `zest pull --gpus N`
-assigns files).  The owner pulls it device-direct (`_hip.DeviceXetPull`: compressed runs -> pinned
+assigns files).  The pull runs in rounds of one owned file per rank; a round's broadcasts overlap
+the next round's network fetch.  The owner pulls it device-direct (`_hip.DeviceXetPull`: compressed runs -> pinned
 staging -> GPU decode + BLAKE3 + Merkle check, with the peer-quarantine / CDN-repair rules of the
 native bridge) and then seeds it to the other GPUs with an RCCL broadcast over xGMI -- the GPUs act
 as BitTorrent peers for each other, with broadcast as the piece exchange (BASELINE configs 2 and 3,
@@ -76,17 +77,33 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     mine = [i for i, o in enumerate(owner) if o == rank]
     bufs = [ops.padded_empty(f["size"], device)[: f["size"]] if device.type == "cuda"
             else torch.empty(f["size"], dtype=torch.uint8) for f in todo]
-    err = ""
-    try:
-        _fetch_owned(repo, revision, repo_type, [todo[i] for i in mine], [bufs[i] for i in mine], device,
-                     p2p, peers, tracker, dht, dht_bootstrap, staging_bytes, threads)
-    except Exception as e:  # reported after the all-reduce, so no rank is left waiting in a broadcast
-        err = f"rank {rank}: {type(e).__name__}: {e}"
-    if not _all_ok(not err, device, group):
-        raise SwarmPullError(err or f"rank {rank}: a peer rank failed to fetch its files")
+    # Rounds: round j is every rank's j-th owned Xet file (rank 0's non-Xet files, fetched through
+    # the host pull, form its last round).  A round's broadcasts are issued
+    # asynchronously, so they cross xGMI while the owners fetch the next round's files from the
+    # network: the pull takes ~max(network, xGMI) instead of their sum.
+    plan = [[[i] for i in range(len(xet)) if owner[i] == r] for r in range(world)]
+    if plain:
+        plan[0].append(list(range(len(xet), len(todo))))
+    n_rounds = max(len(p) for p in plan)
     granks = [dist.get_global_rank(group, r) for r in range(world)] if group is not None else list(range(world))
-    works = [dist.broadcast(bufs[i], granks[owner[i]], group=group, async_op=True)
-             for i in range(len(todo)) if todo[i]["size"] > 0]
+    fetcher = _Fetcher(repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
+                       threads)
+    works = []
+    for j in range(n_rounds):
+        err = ""
+        mine_j = plan[rank][j] if j < len(plan[rank]) else []
+        try:
+            fetcher.fetch([todo[i] for i in mine_j], [bufs[i] for i in mine_j])
+        except Exception as e:  # reported after the all-reduce, so no rank is left waiting in a broadcast
+            err = f"rank {rank}: {type(e).__name__}: {e}"
+        if not _all_ok(not err, device, group):
+            for w in works:  # leave no collective of an earlier round in flight
+                w.wait()
+            raise SwarmPullError(err or f"rank {rank}: a peer rank failed to fetch its files")
+        for r in range(world):
+            for i in (plan[r][j] if j < len(plan[r]) else []):
+                if todo[i]["size"] > 0:
+                    works.append(dist.broadcast(bufs[i], granks[r], group=group, async_op=True))
     for w in works:
         w.wait()
     bad = []
@@ -113,23 +130,37 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     return out
 
 
-def _fetch_owned(repo, revision, repo_type, files, bufs, device, p2p, peers, tracker, dht, dht_bootstrap,
-                 staging_bytes, threads):
-    if not files:
-        return
-    xet = [(f, b) for f, b in zip(files, bufs) if f["xet_hash"]]
-    host = [(f, b) for f, b in zip(files, bufs) if not f["xet_hash"]]
-    if device.type == "cuda" and xet:
-        dp = ops.hip().DeviceXetPull(repo, revision, repo_type, p2p, list(peers or []), tracker, dht,
-                                     list(dht_bootstrap or []), device.index or 0, staging_bytes, threads)
-        torch.cuda.synchronize(device)  # the buffers exist before the pull's private stream writes them
-        dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in xet])
-    else:
-        host = xet + host
-    if host:
-        r = _core.pull(repo, revision, p2p, list(peers or []), tracker, dht, list(dht_bootstrap or []),
-                       [f["path"] for f, _ in host], True, 0, repo_type)
-        if r["failed_files"]:
-            raise SwarmPullError(f"host pull failed for {r['failed_files']} file(s)")
-        for f, b in host:
-            b.copy_(zdev.load_file(os.path.join(r["snapshot_dir"], f["path"]), device).view(torch.uint8))
+class _Fetcher:
+    """Fetches this rank's owned files into their buffers, one round at a time.  On a GPU the Xet
+    files go device-direct through one DeviceXetPull (built on first use and kept, so the hub
+    session and the peer connections carry over between rounds); otherwise, and for non-Xet
+    files, through the host pull."""
+
+    def __init__(self, repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
+                 threads):
+        self.repo, self.revision, self.repo_type, self.device = repo, revision, repo_type, device
+        self.p2p, self.peers, self.tracker, self.dht = p2p, list(peers or []), tracker, dht
+        self.dht_bootstrap, self.staging_bytes, self.threads = list(dht_bootstrap or []), staging_bytes, threads
+        self._dp = None
+
+    def fetch(self, files, bufs):
+        if not files:
+            return
+        xet = [(f, b) for f, b in zip(files, bufs) if f["xet_hash"]]
+        host = [(f, b) for f, b in zip(files, bufs) if not f["xet_hash"]]
+        if self.device.type == "cuda" and xet:
+            if self._dp is None:
+                self._dp = ops.hip().DeviceXetPull(self.repo, self.revision, self.repo_type, self.p2p, self.peers,
+                                                   self.tracker, self.dht, self.dht_bootstrap,
+                                                   self.device.index or 0, self.staging_bytes, self.threads)
+            torch.cuda.synchronize(self.device)  # the buffers exist before the pull's private stream writes them
+            self._dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in xet])
+        else:
+            host = xet + host
+        if host:
+            r = _core.pull(self.repo, self.revision, self.p2p, self.peers, self.tracker, self.dht,
+                           self.dht_bootstrap, [f["path"] for f, _ in host], True, 0, self.repo_type)
+            if r["failed_files"]:
+                raise SwarmPullError(f"host pull failed for {r['failed_files']} file(s)")
+            for f, b in host:
+                b.copy_(zdev.load_file(os.path.join(r["snapshot_dir"], f["path"]), self.device).view(torch.uint8))
