@@ -158,14 +158,19 @@ def _swarm_worker(rank, world, port, snap, hashes, q):
     try:
         from zest_amd.parallel import swarm_load
 
-        t = swarm_load(snap, xet_hashes=hashes, verify_all=True)
+        try:
+            t = swarm_load(snap, xet_hashes=hashes, verify_all=True)
+        except Exception as e:  # noqa: BLE001 - reported to the test
+            q.put((rank, type(e).__name__))
+            return
         digest = {k: v.contiguous().view(torch.uint8).sum().item() for k, v in t.items()}
         q.put((rank, digest))
     finally:
         dist.destroy_process_group()
 
 
-def test_swarm_load_gloo(world_hub, tmp_path):
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_swarm_load_gloo(world_hub, tmp_path, corrupt):
     import torch.multiprocessing as mp
 
     world, hub, commit = world_hub
@@ -187,6 +192,8 @@ def test_swarm_load_gloo(world_hub, tmp_path):
         body = b"".join(ref[n].contiguous().view(torch.uint8).numpy().tobytes() for n in sel)
         (snap2 / part).write_bytes(head + body)
     hashes = {p: _core_hash(snap2 / p) for p in ("a.safetensors", "b.safetensors")}
+    if corrupt:  # one owner's file fails its hash check: every rank raises, none hangs in a broadcast
+        hashes["b.safetensors"] = "0" * 64
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -197,6 +204,9 @@ def test_swarm_load_gloo(world_hub, tmp_path):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if corrupt:
+        assert got == {0: "VerifyError", 1: "VerifyError"}
+        return
     exp = {k: v.contiguous().view(torch.uint8).sum().item() for k, v in ref.items()}
     assert got[0] == exp and got[1] == exp
     del spec, src

@@ -33,6 +33,13 @@ def assign_owners(sizes: list[int], world: int) -> list[int]:
     return owner
 
 
+def _agree(ok: bool, device, group) -> bool:
+    """True on every rank iff `ok` on every rank."""
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    return int(flag.item()) == 0
+
+
 def swarm_load(snapshot_dir: str, group=None, device=None, xet_hashes: dict[str, str] | None = None,
                files: list[str] | None = None, verify_all: bool = False) -> dict[str, torch.Tensor]:
     """Collective: call on every rank of `group`. Returns {tensor_name: tensor} on this rank's device."""
@@ -53,21 +60,36 @@ def swarm_load(snapshot_dir: str, group=None, device=None, xet_hashes: dict[str,
     if not torch.equal(sig, ref):
         raise RuntimeError(f"rank {rank}: snapshot differs from rank 0 ({sig.tolist()} vs {ref.tolist()})")
     owner = assign_owners(sizes, world)
-    bufs = []
-    for i, rel in enumerate(files):
-        if owner[i] == rank:
-            buf = zdev.load_file(os.path.join(snapshot_dir, rel), device)
-            if xet_hashes and rel in xet_hashes:
-                got = zdev.xet_file_hash(buf)
-                if got != xet_hashes[rel]:
-                    raise zdev.VerifyError(f"rank {rank}: {rel} hash {got} != {xet_hashes[rel]}")
-        else:
-            buf = ops.padded_empty(sizes[i], device)[:sizes[i]] if device.type == "cuda" \
-                else torch.empty(sizes[i], dtype=torch.uint8)
-        bufs.append(buf)
+    bufs = [None if owner[i] == rank else
+            (ops.padded_empty(sizes[i], device)[:sizes[i]] if device.type == "cuda"
+             else torch.empty(sizes[i], dtype=torch.uint8)) for i in range(len(files))]
     global_ranks = [dist.get_global_rank(group, r) for r in range(world)] if group is not None else list(range(world))
-    works = [dist.broadcast(bufs[i], global_ranks[owner[i]], group=group, async_op=True)
-             for i in range(len(files)) if sizes[i] > 0]
+    # Rounds of one owned file per rank: round j's broadcasts cross xGMI while the owners read and
+    # upload round j + 1's files.  A failed read or owner-side hash check is agreed on by every rank
+    # (all-reduce) before any broadcast of that round, so no rank waits in a broadcast that its
+    # owner will never send.
+    plan = [[i for i in range(len(files)) if owner[i] == r] for r in range(world)]
+    works = []
+    for j in range(max(len(p) for p in plan)):
+        err = ""
+        if j < len(plan[rank]):
+            i = plan[rank][j]
+            rel = files[i]
+            try:
+                bufs[i] = zdev.load_file(os.path.join(snapshot_dir, rel), device)
+                if xet_hashes and rel in xet_hashes:
+                    got = zdev.xet_file_hash(bufs[i])
+                    if got != xet_hashes[rel]:
+                        err = f"rank {rank}: {rel} hash {got} != {xet_hashes[rel]}"
+            except OSError as e:
+                err = f"rank {rank}: reading {rel}: {e}"
+        if not _agree(not err, device, group):
+            for w in works:
+                w.wait()
+            raise zdev.VerifyError(err or f"rank {rank}: a peer rank could not load or verify its file")
+        for r in range(world):
+            if j < len(plan[r]) and sizes[plan[r][j]] > 0:
+                works.append(dist.broadcast(bufs[plan[r][j]], global_ranks[r], group=group, async_op=True))
     for w in works:
         w.wait()
     out: dict[str, torch.Tensor] = {}
