@@ -297,3 +297,66 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend):
         assert sum(r[2]["fetched_bytes"] for r in res) == total
     finally:
         hub.stop()
+
+
+def _swarm_load_gpu_worker(rank, world_size, port, snap, hashes, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from zest_amd.parallel import swarm_load
+        t = swarm_load(snap, device="cuda:0", xet_hashes=hashes, verify_all=True)
+        assert all(v.device.type == "cuda" for v in t.values())
+        q.put((rank, {k: v.contiguous().view(torch.uint8).cpu().numpy().tobytes() for k, v in t.items()}))
+    except Exception as e:  # noqa: BLE001 - reported to the test
+        q.put((rank, type(e).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_swarm_load_device(tmp_path, monkeypatch, corrupt):
+    """swarm_load of a pulled snapshot into HBM by 2 ranks sharing the GPU (gloo): each file is read
+    and GPU-verified by its owner, broadcast in rounds, re-verified by the receiver; a file failing
+    its owner's hash check makes both ranks raise instead of hanging in a broadcast."""
+    import dataclasses
+
+    import torch.multiprocessing as mp
+    import zest_amd
+
+    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
+    world = SyntheticWorld(spec, seed=23, mode="bf16")
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+        res = zest_amd.client.ZestClient().pull_detailed(world.spec.repo_id, p2p=False)
+        hashes = res.xet_hashes()
+        assert len(hashes) >= 3
+        if corrupt:
+            hashes[sorted(hashes)[-1]] = "0" * 64
+        want = zdev.load_snapshot(res.snapshot_dir, "cpu")
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = free_port()
+        procs = [ctx.Process(target=_swarm_load_gpu_worker, args=(r, 2, port, res.snapshot_dir, hashes, q))
+                 for r in range(2)]
+        for p in procs:
+            p.start()
+        got = dict(q.get(timeout=180) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+        if corrupt:
+            assert got == {0: "VerifyError", 1: "VerifyError"}
+            return
+        for r in range(2):
+            assert isinstance(got[r], dict), got[r]
+            assert got[r].keys() == want.keys()
+            assert all(got[r][k] == want[k].contiguous().view(torch.uint8).numpy().tobytes() for k in want)
+    finally:
+        hub.stop()
