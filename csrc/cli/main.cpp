@@ -155,15 +155,27 @@ std::vector<xet::Hash> cached_xorb_hashes(const Config& cfg) {
 int cmd_pull(const std::string& exe, const std::vector<std::string>& a);
 
 // One attempt of `zest pull --gpus N`: `python -m torch.distributed.run --nproc-per-node N -m
-// zest_amd.multigpu <args>` as a child process of this CLI (one worker per GPU).  Rank 0 writes
+// zest_amd.multigpu <args>` as a child process of this CLI (one worker per GPU; N = 1 runs
+// `python -m zest_amd.multigpu` directly).  Rank 0 writes
 // `status_path` once the whole job ran to the end (every rank alive through the final all-reduce).
 int spawn_gpu_workers(const std::vector<std::string>& pass, int gpus, int attempt, const std::string& status_path) {
   const char* py = std::getenv("ZEST_PYTHON");
   const char* mod = std::getenv("ZEST_GPU_WORKER_MODULE");  // tests substitute a stub worker
-  std::vector<std::string> args = {py ? py : "python3", "-m", "torch.distributed.run", "--nnodes", "1",
-                                   "--nproc-per-node", std::to_string(gpus), "--master-addr", "127.0.0.1",
-                                   "--master-port", std::to_string(29400 + (::getpid() * 7 + attempt * 131) % 2000),
-                                   "-m", mod && *mod ? mod : "zest_amd.multigpu"};
+  const std::string module = mod && *mod ? mod : "zest_amd.multigpu";
+  std::vector<std::string> args = {py ? py : "python3", "-m"};
+  if (gpus == 1) {
+    // One GPU needs no rendezvous: run the worker itself (no torchrun agent process and no RCCL
+    // communicator to start; `zest pull --gpus 1` of Llama-3.1-8B spent ~9 s of 13 before its worker
+    // began, profiles/gpu_cli_pull_r2.md).
+    args.push_back(module);
+  } else {
+    for (const std::string& s : {std::string("torch.distributed.run"), std::string("--nnodes"), std::string("1"),
+                                 std::string("--nproc-per-node"), std::to_string(gpus), std::string("--master-addr"),
+                                 std::string("127.0.0.1"), std::string("--master-port"),
+                                 std::to_string(29400 + (::getpid() * 7 + attempt * 131) % 2000), std::string("-m"),
+                                 module})
+      args.push_back(s);
+  }
   args.insert(args.end(), pass.begin(), pass.end());
   ::setenv("ZEST_GPU_STATUS", status_path.c_str(), 1);
   std::vector<char*> argv;

@@ -360,3 +360,15 @@ def test_swarm_load_device(tmp_path, monkeypatch, corrupt):
             assert all(got[r][k] == want[k].contiguous().view(torch.uint8).numpy().tobytes() for k in want)
     finally:
         hub.stop()
+
+
+@pytest.mark.parametrize("n", [1, (1 << 20) - 3, 5 * (1 << 20) + 12345])
+def test_write_device_file_pipelined(tmp_path, n):
+    """zest pull --gpus N snapshot writer: chunked D2H into pinned slots overlapped with pwrite."""
+    from zest_amd.multigpu import write_device_file
+
+    data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+    buf = torch.from_numpy(data).to("cuda:0")
+    p = tmp_path / "f.bin"
+    write_device_file(buf, str(p), chunk=1 << 20, slots=2)
+    assert p.read_bytes() == data.tobytes()

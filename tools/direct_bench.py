@@ -36,6 +36,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama-3.1-8b")
     ap.add_argument("--skip-host", action="store_true")
+    ap.add_argument("--skip-gpu-cli", action="store_true")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -108,6 +109,21 @@ def main() -> int:
             print(f"[host] zest pull to disk {total / (t1 - t0) / 1e9:.2f} GB/s, then load + GPU verify "
                   f"{total / (t2 - t1) / 1e9:.2f} GB/s -> end to end {total / (t2 - t0) / 1e9:.2f} GB/s", flush=True)
             del tensors
+        if not a.skip_gpu_cli:
+            # `zest pull --gpus 1`: the CLI's GPU worker (zest_amd.multigpu) pulls device-direct,
+            # decodes + verifies on the GPU and writes the HF-cache snapshot
+            env = dict(os.environ, **hub.env(str(work / "gpucli")))
+            t0 = time.time()
+            r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
+                                "--no-dht", "--gpus", "1"], env=env, capture_output=True, text=True, timeout=3600)
+            dt = time.time() - t0
+            if r.returncode != 0:
+                raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
+            tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
+            res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
+                       gpu_cli_summary=tail[-1] if tail else "")
+            print(f"[gpu cli] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s; {tail[-1] if tail else ''})",
+                  flush=True)
         res["seeder"] = srv.stats()
         print(json.dumps(res), flush=True)
         if a.out:

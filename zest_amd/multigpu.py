@@ -1,10 +1,11 @@
 """`zest pull <repo> --gpus N`: pull a repository with N GPUs as decode/verify engines.
 
 Launched by the CLI as `python -m torch.distributed.run --nproc-per-node N -m zest_amd.multigpu ...`
-(one process per GPU, SURVEY §7.3 item 6: single-command UX over per-rank workers).  Xet files are
+(N = 1: `python -m zest_amd.multigpu ...`, no rendezvous; one process per GPU, SURVEY §7.3 item 6: single-command UX over per-rank workers).  Xet files are
 assigned to ranks by size (LPT); each rank fetches its files' compressed runs through the native
 cache -> P2P -> CDN waterfall, decodes and verifies them on its own GPU (`_hip.DeviceXetPull`) and
-writes them into the HF-cache snapshot; rank 0 fetches the regular files and writes the ref.
+writes them into the HF-cache snapshot (file i's write overlaps file i + 1's pull); rank 0 fetches
+the regular files and writes the ref.
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 from . import _core, ops
-from .parallel import assign_owners, init_from_env
+from .parallel import assign_owners, bind_local_numa, init_from_env
 
 
 def cached_file_ok(repo: str, commit: str, f: dict, dst: str) -> bool:
@@ -33,6 +34,49 @@ def cached_file_ok(repo: str, commit: str, f: dict, dst: str) -> bool:
         _core.write_verified_marker(repo, commit, f["path"], f["xet_hash"], dst)
         return True
     return False
+
+
+_PINNED: list = []
+
+
+def write_device_file(buf: torch.Tensor, path: str, chunk: int = 256 << 20, slots: int = 3) -> None:
+    """Write a device byte buffer to `path`: D2H of chunk k + 1 into pinned memory (side stream)
+    overlaps the pwrite of chunk k (writer threads, GIL released), instead of one pageable `.cpu()`
+    copy of the whole file followed by one single-threaded write."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    n = buf.numel()
+    if len(_PINNED) < slots or _PINNED[0].numel() < chunk:  # reused across files
+        _PINNED[:] = [torch.empty(chunk, dtype=torch.uint8).pin_memory() for _ in range(slots)]
+    stream = torch.cuda.Stream(buf.device)
+    stream.wait_stream(torch.cuda.current_stream(buf.device))
+
+    def put(ev, fd, host, m, off):
+        ev.synchronize()
+        view = memoryview(host.numpy())[:m]
+        done = 0
+        while done < m:
+            done += os.pwrite(fd, view[done:], off + done)
+
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        with ThreadPoolExecutor(slots) as ex:
+            futs = [None] * slots
+            for k, off in enumerate(range(0, n, chunk)):
+                s = k % slots
+                if futs[s] is not None:
+                    futs[s].result()  # slot free: its previous chunk is on disk (page cache)
+                m = min(chunk, n - off)
+                with torch.cuda.stream(stream):
+                    _PINNED[s][:m].copy_(buf[off:off + m], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                futs[s] = ex.submit(put, ev, fd, _PINNED[s], m, off)
+            for f in futs:
+                if f is not None:
+                    f.result()
+    finally:
+        os.close(fd)
 
 
 def main(argv=None) -> int:
@@ -52,7 +96,15 @@ def main(argv=None) -> int:
     # the reference ignores unknown flags (main.zig:98-119); so do the GPU workers
     a, _unknown = ap.parse_known_args(argv)
     rank, world, local, dev = init_from_env()
+    if world == 1 and "RANK" not in os.environ:  # started directly by the CLI for one GPU (no torchrun)
+        torch.cuda.set_device(dev)
+        bind_local_numa(dev)
     t0 = time.time()
+    try:
+        import psutil
+        startup = t0 - psutil.Process().create_time()
+    except Exception:  # noqa: BLE001 - diagnostics only
+        startup = float("nan")
     commit, files = _core.list_repo_files(a.repo, a.revision, a.repo_type)
     commit = commit or a.revision
     if a.include:
@@ -69,6 +121,7 @@ def main(argv=None) -> int:
     p2p = not a.no_p2p
     done_bytes = 0
     failed = 0
+    t_pull = t_write = 0.0
     if mine:
         dp = ops.hip().DeviceXetPull(a.repo, a.revision, a.repo_type, p2p, a.peer, a.tracker, not a.no_dht,
                                      a.dht_bootstrap, dev.index or 0, max(16, a.pipeline_depth) << 20, max(1, a.concurrency))
@@ -81,30 +134,45 @@ def main(argv=None) -> int:
             todo.append(f)
         bufs = [ops.padded_empty(f["size"], dev)[:f["size"]] for f in todo]
         torch.cuda.synchronize(dev)
-        try:  # one pipeline for all of this rank's files
-            st = dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(todo, bufs)]) if todo else []
-        except Exception as e:  # fall back to file by file so one bad file does not sink the rest
-            print(f"[rank {rank}] batch pull failed ({e}); retrying file by file", file=sys.stderr, flush=True)
-            st = []
-            for f, b in zip(todo, bufs):
-                try:
-                    st.append(dp.pull_file(f["xet_hash"], b.data_ptr(), f["size"]))
-                except Exception as e2:
-                    print(f"[rank {rank}] {f['path']}: error {e2}", file=sys.stderr, flush=True)
-                    failed += 1
-                    st.append(None)
-        for f, buf, s_ in zip(todo, bufs, st):
-            if s_ is None:
-                continue
+        tp = time.time()
+
+        def write_back(f, buf, s_):
             dst = os.path.join(snap, f["path"])
             os.makedirs(os.path.dirname(dst), exist_ok=True)
             tmp = dst + ".incomplete"
-            buf.cpu().numpy().tofile(tmp)
+            tw = time.time()
+            if os.environ.get("ZEST_GPU_WRITER") == "simple":
+                buf.cpu().numpy().tofile(tmp)
+            else:
+                write_device_file(buf, tmp)
             os.replace(tmp, dst)
             _core.write_verified_marker(a.repo, commit, f["path"], f["xet_hash"], dst)  # verified on the GPU
-            done_bytes += f["size"]
             print(f"[rank {rank}] {f['path']} [xet, gpu {dev.index}] {f['size'] / 1e6:.1f} MB "
-                  f"verified ({s_['seconds']:.2f}s for this rank's batch)", flush=True)
+                  f"verified ({s_['seconds']:.2f}s device pull)", flush=True)
+            return time.time() - tw
+
+        # File by file: the snapshot write of file i (writer thread: D2H + pwrite, GIL released)
+        # overlaps the device pull of file i + 1 (the native pull releases the GIL too), and one
+        # bad file does not sink the others.
+        from concurrent.futures import ThreadPoolExecutor
+        writes = []
+        with ThreadPoolExecutor(1) as writer:
+            for f, buf in zip(todo, bufs):
+                try:
+                    s_ = dp.pull_file(f["xet_hash"], buf.data_ptr(), f["size"])
+                except Exception as e:  # noqa: BLE001 - counted as a failed file
+                    print(f"[rank {rank}] {f['path']}: error {e}", file=sys.stderr, flush=True)
+                    failed += 1
+                    continue
+                writes.append((f, writer.submit(write_back, f, buf, s_)))
+            t_pull = time.time() - tp
+            for f, fut in writes:
+                try:
+                    t_write += fut.result()
+                    done_bytes += f["size"]
+                except OSError as e:
+                    print(f"[rank {rank}] {f['path']}: write failed: {e}", file=sys.stderr, flush=True)
+                    failed += 1
         del bufs
         stats = json.loads(dp.stats_json())
     else:
@@ -130,7 +198,10 @@ def main(argv=None) -> int:
         src = peer + cdn + cache
         print(f"\nXorb fetch stats:\n  From peers:   {peer / 1e6:.1f} MB\n  From CDN:     {cdn / 1e6:.1f} MB\n"
               f"  From cache:   {cache / 1e6:.1f} MB\n  P2P ratio:    {100 * peer / src if src else 0:.1f}%", flush=True)
-        print(f"\n{b / 1e9:.2f} GB verified on {world} GPU(s) in {dt:.1f}s ({b / dt / 1e9:.2f} GB/s)", flush=True)
+        print(f"\n{b / 1e9:.2f} GB verified on {world} GPU(s) in {dt:.1f}s ({b / dt / 1e9:.2f} GB/s; "
+              f"rank 0: worker start {startup:.1f}s, device pulls {t_pull:.1f}s, snapshot writes {t_write:.1f}s "
+              f"overlapped with them)",
+              flush=True)
         print(f"\nDone! Model available at:\n  {snap}", flush=True)
     if world > 1:
         dist.barrier()
