@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <optional>
 #include <thread>
 
 #include "lz4.h"
@@ -76,9 +77,25 @@ void pwritev_all(int fd, std::vector<iovec>& iov, uint64_t off) {
 
 }  // namespace
 
+void ParallelDownloader::acquire_slot() {
+  std::unique_lock<std::mutex> g(gate_mu_);
+  gate_cv_.wait(g, [&] { return free_ > 0; });
+  --free_;
+}
+
+void ParallelDownloader::release_slot() {
+  {
+    std::lock_guard<std::mutex> g(gate_mu_);
+    ++free_;
+  }
+  gate_cv_.notify_one();
+}
+
 FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const std::string& out_path, bool verify) {
   const auto t0 = std::chrono::steady_clock::now();
+  std::optional<trace::Span> rec_span(std::in_place, "download", "get_reconstruction");
   cas::Reconstruction rec = bridge_.get_reconstruction(hex);
+  rec_span.reset();
   const size_t n = rec.terms.size();
   std::vector<uint64_t> offs(n + 1, 0);
   for (size_t i = 0; i < n; ++i) offs[i + 1] = offs[i] + rec.terms[i].unpacked_length;
@@ -214,6 +231,11 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       const size_t i = next.fetch_add(1);
       if (i >= n) return;
       if (done[i]) continue;
+      acquire_slot();
+      struct Slot {
+        ParallelDownloader* d;
+        ~Slot() { d->release_slot(); }
+      } slot{this};
       try {
         do_term(i, FetchOptions{});
         if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
@@ -249,7 +271,10 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       for (auto& h : hashes) leaves.insert(leaves.end(), h.begin(), h.end());
       return xet::to_hex(xet::file_hash(leaves));
     };
-    ok = file_hash_now() == hex;
+    {
+      trace::Span vs("download", "file hash verify");
+      ok = file_hash_now() == hex;
+    }
     if (!ok) {
       // Repair: every term not fetched from the CDN in this run — peer runs, cache hits and terms
       // restored from the resume sidecar — is refetched from the CDN, replacing its cached copy.
@@ -267,7 +292,10 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
           if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
         throw;
       }
+      {
+      trace::Span vs("download", "file hash verify");
       ok = file_hash_now() == hex;
+    }
     }
     if (!ok) {
       ::close(fd);

@@ -13,7 +13,10 @@
 #pragma once
 
 #include <cstdint>
+#include <algorithm>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -31,15 +34,26 @@ struct FileResult {
 
 class ParallelDownloader {
  public:
-  ParallelDownloader(XetBridge& bridge, int concurrency) : bridge_(bridge), concurrency_(concurrency) {}
+  ParallelDownloader(XetBridge& bridge, int concurrency)
+      : bridge_(bridge), concurrency_(concurrency), free_(size_t(std::max(1, concurrency))) {}
   // Optional hook: called with every verified-in-order byte range (file offset, bytes) after the
   // file hash check, e.g. to stage the file into device memory.
   using RangeHook = std::function<void(uint64_t, const uint8_t*, size_t)>;
+  // Thread-safe: several files may be reconstructed at once (pull.cpp runs a few Xet files
+  // concurrently).  Their workers share one gate of `concurrency` term slots, so at most that many
+  // terms are in flight in total, and one file's tail (its last few terms) is filled with the next
+  // file's terms instead of idle workers.
   FileResult reconstruct_to_file(const std::string& file_hash_hex, const std::string& out_path, bool verify = true);
 
  private:
+  void acquire_slot();
+  void release_slot();
+
   XetBridge& bridge_;
   int concurrency_;
+  std::mutex gate_mu_;
+  std::condition_variable gate_cv_;
+  size_t free_;
 };
 
 }  // namespace zest

@@ -1,5 +1,10 @@
 #include "pull.h"
 
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+#include <thread>
+
 #include <fcntl.h>
 #include <spawn.h>
 #include <sys/wait.h>
@@ -7,11 +12,13 @@
 
 #include <chrono>
 #include <iomanip>
+#include <optional>
 
 #include "bridge.h"
 #include "downloader.h"
 #include "http.h"
 #include "json.h"
+#include "trace.h"
 #include "hub.h"
 #include "storage.h"
 #include "swarm.h"
@@ -59,6 +66,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
   if (opt.p2p) out << "P2P enabled (peer_id: " << peer_id::kClientPrefix << "...)\n";
   else out << "P2P disabled (CDN only)\n";
   out << "Fetching model info from HuggingFace Hub...\n" << std::flush;
+  std::optional<trace::Span> listing_span(std::in_place, "pull", "list files + resolve commit");
   std::vector<hub::RepoFile> files = hub::list_files(cfg, opt.repo_id, opt.revision, opt.repo_type);
   if (!opt.include.empty()) {
     std::vector<hub::RepoFile> keep;
@@ -72,6 +80,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
   }
   auto sha = hub::resolve_commit(cfg, opt.repo_id, opt.revision, opt.repo_type);
   S.commit = sha ? *sha : opt.revision;
+  listing_span.reset();
   if (sha) out << "Found " << files.size() << " files (revision: " << opt.revision << " \xE2\x86\x92 " << S.commit << ")\n";
   else out << "Found " << files.size() << " files (revision: " << opt.revision << ")\n";
   out << "Detecting Xet-backed files...\n";
@@ -88,6 +97,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
       err << "Warning: invalid DHT bootstrap node: " << b << "\n";
     }
   }
+  std::optional<trace::Span> setup_span(std::in_place, "pull", "cache scan + swarm + auth");
   storage::XorbRegistry registry;
   storage::XorbCache cache(cfg, &registry);
   SwarmDownloader swarm(cfg, opt.tracker, opt.p2p, opt.dht && opt.p2p, boot);
@@ -109,9 +119,15 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
     }
   }
   ParallelDownloader dl(bridge, opt.concurrency > 0 ? opt.concurrency : int(cfg.concurrency));
+  setup_span.reset();
   S.snapshot_dir = cfg.snapshot_dir(opt.repo_id, S.commit);
   size_t k = 0;
   std::vector<uint8_t> ok(files.size(), 1);
+  struct XetJob {
+    size_t file;
+    std::string dst;
+  };
+  std::vector<XetJob> xet_jobs;
   for (auto& f : files) {
     ++k;
     uint8_t& file_ok = ok[k - 1];
@@ -145,16 +161,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
         file_ok = 0;
         continue;
       }
-      try {
-        FileResult r = dl.reconstruct_to_file(*f.xet_hash, dst, opt.verify);
-        S.bytes += r.bytes;
-        if (r.verified) storage::write_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, dst);
-        if (r.resumed_terms) out << "  resumed " << r.resumed_terms << "/" << r.terms << " terms\n";
-      } catch (const Error& e) {
-        err << "  Parallel download error (" << e.what() << ")\n";
-        file_ok = 0;
-        continue;
-      }
+      xet_jobs.push_back({k - 1, dst});
     } else {
       out << " [regular]\n" << std::flush;
       try {
@@ -165,6 +172,44 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
         continue;
       }
     }
+  }
+  // Xet files: up to ZEST_FILE_CONCURRENCY (default 4) at once.  Their terms share the
+  // downloader's `concurrency` slots, so a file's tail overlaps the next file's terms, and the
+  // snapshot writes spread over several files (concurrent pwrites to ONE file serialize on its
+  // inode: Llama-3.1-8B from one HBM peer spent 13 s of 34 thread-seconds in pwrite at 3.75 GB/s,
+  // profiles/host_pull_trace_r2.md).
+  {
+    const char* fc = std::getenv("ZEST_FILE_CONCURRENCY");
+    const size_t nfile_threads = std::max<size_t>(1, std::min<size_t>(fc ? std::strtoul(fc, nullptr, 10) : 4,
+                                                                       xet_jobs.size()));
+    std::atomic<size_t> next{0};
+    std::atomic<uint64_t> bytes{0};
+    std::mutex io_mu;
+    auto run = [&]() {
+      for (size_t j; (j = next.fetch_add(1)) < xet_jobs.size();) {
+        const XetJob& job = xet_jobs[j];
+        const hub::RepoFile& f = files[job.file];
+        try {
+          trace::Span fs("pull", "xet file");
+          FileResult r = dl.reconstruct_to_file(*f.xet_hash, job.dst, opt.verify);
+          bytes += r.bytes;
+          if (r.verified) storage::write_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, job.dst);
+          if (r.resumed_terms) {
+            std::lock_guard<std::mutex> g(io_mu);
+            out << "  " << f.path << ": resumed " << r.resumed_terms << "/" << r.terms << " terms\n";
+          }
+        } catch (const Error& e) {
+          std::lock_guard<std::mutex> g(io_mu);
+          err << "  Parallel download error (" << f.path << ": " << e.what() << ")\n";
+          ok[job.file] = 0;
+        }
+      }
+    };
+    std::vector<std::thread> fts;
+    for (size_t t = 1; t < nfile_threads; ++t) fts.emplace_back(run);
+    run();
+    for (auto& t : fts) t.join();
+    S.bytes += bytes.load();
   }
   try {
     storage::write_ref(cfg, opt.repo_id, opt.revision, S.commit);

@@ -37,6 +37,8 @@ def main() -> int:
     ap.add_argument("--model", default="llama-3.1-8b")
     ap.add_argument("--skip-host", action="store_true")
     ap.add_argument("--skip-gpu-cli", action="store_true")
+    ap.add_argument("--skip-direct", action="store_true")
+    ap.add_argument("--trace-host", default=None, help="ZEST_TRACE=<file.json> for the host zest pull")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -64,34 +66,37 @@ def main() -> int:
            "source": "HBM seeder over BEP XET (loopback TCP)",
            "data": "synthetic random-byte weights, real tensor shapes"}
     try:
-        # warm-up on the smallest Xet file (connections, allocator, kernels)
-        zest_amd._init()
-        torch.cuda.synchronize()
-        t0 = time.time()
-        out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
-        torch.cuda.synchronize()
-        dt = time.time() - t0
-        n = sum(v.numel() * v.element_size() for v in out.values())
-        res.update(direct_s=round(dt, 3), direct_gbps=round(total / dt / 1e9, 3), tensors=len(out),
-                   tensor_bytes=n, cdn_xorb_gets=hub.counters.get("xorb_missing", 0) + hub.counters.get("xorb_get", 0))
-        print(f"[direct] network -> HBM, GPU decode + BLAKE3/Merkle verify: {total / dt / 1e9:.2f} GB/s "
-              f"({dt:.1f}s, {len(out)} tensors)", flush=True)
-        del out
-        torch.cuda.empty_cache()
-        # same, without keeping the fetched runs in the disk xorb cache (pure network -> HBM)
-        os.environ.update(hub.env(str(work / "direct_nocache")))
-        os.environ["ZEST_CACHE_WRITES"] = "0"
-        t0 = time.time()
-        out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
-        torch.cuda.synchronize()
-        dt = time.time() - t0
-        os.environ.pop("ZEST_CACHE_WRITES")
-        res.update(direct_nocache_s=round(dt, 3), direct_nocache_gbps=round(total / dt / 1e9, 3))
-        print(f"[direct, ZEST_CACHE_WRITES=0] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
-        del out
-        torch.cuda.empty_cache()
+        if not a.skip_direct:
+            # warm-up on the smallest Xet file (connections, allocator, kernels)
+            zest_amd._init()
+            torch.cuda.synchronize()
+            t0 = time.time()
+            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            n = sum(v.numel() * v.element_size() for v in out.values())
+            res.update(direct_s=round(dt, 3), direct_gbps=round(total / dt / 1e9, 3), tensors=len(out),
+                       tensor_bytes=n, cdn_xorb_gets=hub.counters.get("xorb_missing", 0) + hub.counters.get("xorb_get", 0))
+            print(f"[direct] network -> HBM, GPU decode + BLAKE3/Merkle verify: {total / dt / 1e9:.2f} GB/s "
+                  f"({dt:.1f}s, {len(out)} tensors)", flush=True)
+            del out
+            torch.cuda.empty_cache()
+            # same, without keeping the fetched runs in the disk xorb cache (pure network -> HBM)
+            os.environ.update(hub.env(str(work / "direct_nocache")))
+            os.environ["ZEST_CACHE_WRITES"] = "0"
+            t0 = time.time()
+            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            os.environ.pop("ZEST_CACHE_WRITES")
+            res.update(direct_nocache_s=round(dt, 3), direct_nocache_gbps=round(total / dt / 1e9, 3))
+            print(f"[direct, ZEST_CACHE_WRITES=0] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
+            del out
+            torch.cuda.empty_cache()
         if not a.skip_host:
             env = dict(os.environ, **hub.env(str(work / "host")))
+            if a.trace_host:
+                env["ZEST_TRACE"] = a.trace_host
             t0 = time.time()
             r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
                                 "--no-dht"], env=env, capture_output=True, text=True, timeout=3600)

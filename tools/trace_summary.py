@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Aggregate a ZEST_TRACE Chrome trace: per (category, span) count, summed and mean duration, and
+the trace's wall span.  `python tools/trace_summary.py trace.json [--top 25]`"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    ev = json.load(open(a.trace))
+    ev = ev["traceEvents"] if isinstance(ev, dict) else ev
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    ts = []
+    threads = set()
+    for e in ev:
+        if e.get("ph") != "X":
+            continue
+        k = (e.get("cat", ""), e.get("name", ""))
+        agg[k][0] += 1
+        agg[k][1] += e.get("dur", 0) / 1e3
+        ts += [e["ts"], e["ts"] + e.get("dur", 0)]
+        threads.add(e.get("tid"))
+    wall = (max(ts) - min(ts)) / 1e3 if ts else 0.0
+    print(f"wall span {wall:.1f} ms, {len(threads)} threads")
+    print(f"{'category':10s} {'span':34s} {'count':>7s} {'sum ms':>10s} {'mean ms':>9s}")
+    for (c, n), (cnt, ms) in sorted(agg.items(), key=lambda x: -x[1][1])[:a.top]:
+        print(f"{c:10s} {n:34s} {cnt:7d} {ms:10.1f} {ms / cnt:9.2f}")
+
+
+if __name__ == "__main__":
+    main()
