@@ -77,15 +77,19 @@ void pwritev_all(int fd, std::vector<iovec>& iov, uint64_t off) {
 
 }  // namespace
 
-void ParallelDownloader::acquire_slot() {
+ParallelDownloader::RunBuffer* ParallelDownloader::acquire_slot() {
   std::unique_lock<std::mutex> g(gate_mu_);
   gate_cv_.wait(g, [&] { return free_ > 0; });
   --free_;
+  RunBuffer* b = bufs_.back().release();
+  bufs_.pop_back();
+  return b;
 }
 
-void ParallelDownloader::release_slot() {
+void ParallelDownloader::release_slot(RunBuffer* b) {
   {
     std::lock_guard<std::mutex> g(gate_mu_);
+    bufs_.emplace_back(b);
     ++free_;
   }
   gate_cv_.notify_one();
@@ -166,9 +170,9 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
     bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i] != 0, false);
     pending[i] = 0;
   };
-  auto do_term = [&](size_t i, const FetchOptions& opt) {
+  auto do_term = [&](size_t i, const FetchOptions& opt, RunBuffer* buf) {
     const cas::Term& t = rec.terms[i];
-    XorbFetchResult f = bridge_.fetch_term(t, rec, opt);
+    XorbFetchResult f = bridge_.fetch_term(t, rec, opt, [buf](size_t nbytes) { return buf->get(nbytes); });
     src[i] = f.source;  // recorded before decoding so a bad peer copy can be attributed
     peer[i] = f.peer;
     run_off[i] = f.run_offset;
@@ -231,20 +235,20 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       const size_t i = next.fetch_add(1);
       if (i >= n) return;
       if (done[i]) continue;
-      acquire_slot();
       struct Slot {
         ParallelDownloader* d;
-        ~Slot() { d->release_slot(); }
-      } slot{this};
+        RunBuffer* buf;
+        ~Slot() { d->release_slot(buf); }
+      } slot{this, acquire_slot()};
       try {
-        do_term(i, FetchOptions{});
+        do_term(i, FetchOptions{}, slot.buf);
         if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
       } catch (const std::exception& e) {
         // A peer/cache copy that does not decode: retry straight from the CDN once.
         ZTRACE("download", "term " << i << " via " << int(src[i]) << " failed (" << e.what() << "), CDN retry");
         try {
           if (src[i] != Source::Cdn) reject(i);
-          do_term(i, FetchOptions{false, false, /*repair=*/src[i] != Source::Cdn});
+          do_term(i, FetchOptions{false, false, /*repair=*/src[i] != Source::Cdn}, slot.buf);
           if (sc.fd >= 0) sc.append(uint32_t(i), hashes[i]);
         } catch (const std::exception& e2) {
           std::lock_guard<std::mutex> g(err_mu);
@@ -279,11 +283,12 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       // Repair: every term not fetched from the CDN in this run — peer runs, cache hits and terms
       // restored from the resume sidecar — is refetched from the CDN, replacing its cached copy.
       bridge_.stats().verify_failures++;
+      RunBuffer repair_buf;
       try {
         for (size_t i = 0; i < n; ++i) {
           if (src[i] == Source::Cdn) continue;
           reject(i);
-          do_term(i, FetchOptions{false, false, /*repair=*/true});
+          do_term(i, FetchOptions{false, false, /*repair=*/true}, &repair_buf);
           bridge_.stats().refetches++;
         }
       } catch (...) {  // the CDN failed too: keep the sidecar (resumed terms are re-checked next run)
@@ -292,10 +297,8 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
           if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
         throw;
       }
-      {
       trace::Span vs("download", "file hash verify");
       ok = file_hash_now() == hex;
-    }
     }
     if (!ok) {
       ::close(fd);

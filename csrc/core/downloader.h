@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -35,7 +36,9 @@ struct FileResult {
 class ParallelDownloader {
  public:
   ParallelDownloader(XetBridge& bridge, int concurrency)
-      : bridge_(bridge), concurrency_(concurrency), free_(size_t(std::max(1, concurrency))) {}
+      : bridge_(bridge), concurrency_(concurrency), free_(size_t(std::max(1, concurrency))) {
+    for (size_t i = 0; i < free_; ++i) bufs_.push_back(std::make_unique<RunBuffer>());
+  }
   // Optional hook: called with every verified-in-order byte range (file offset, bytes) after the
   // file hash check, e.g. to stage the file into device memory.
   using RangeHook = std::function<void(uint64_t, const uint8_t*, size_t)>;
@@ -46,14 +49,29 @@ class ParallelDownloader {
   FileResult reconstruct_to_file(const std::string& file_hash_hex, const std::string& out_path, bool verify = true);
 
  private:
-  void acquire_slot();
-  void release_slot();
+  // One receive buffer per term slot, kept across terms and files: a fetched run (up to a 64 MiB
+  // xorb) lands in memory whose pages were faulted in once, instead of a fresh mmap'd allocation
+  // per term whose every page faults and is zeroed on first touch.
+  struct RunBuffer {
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0;
+    uint8_t* get(size_t n) {
+      if (n > cap) {
+        p.reset(new uint8_t[n]);
+        cap = n;
+      }
+      return p.get();
+    }
+  };
+  RunBuffer* acquire_slot();
+  void release_slot(RunBuffer* b);
 
   XetBridge& bridge_;
   int concurrency_;
   std::mutex gate_mu_;
   std::condition_variable gate_cv_;
   size_t free_;
+  std::vector<std::unique_ptr<RunBuffer>> bufs_;  // the free slots' buffers
 };
 
 }  // namespace zest
