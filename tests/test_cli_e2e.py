@@ -422,3 +422,29 @@ def test_seed_hbm_cache_option(nodes, tmp_path):
                "PYTHONPATH": str(ROOT)})
     assert json.loads(log.read_text()) == ["--port", "7001", "--device", "cuda:3", "--max-gb", "12.5"]
     assert "--hbm-cache-gb" in n.run("help").stdout
+
+
+@pytest.mark.parametrize("file_concurrency", ["1", "3"])
+def test_p2p_many_xet_files_concurrently(hub, nodes, file_concurrency):
+    """Several Xet files pulled at once (ZEST_FILE_CONCURRENCY) with their terms sharing the
+    downloader's slots and receive buffers (-j 2: fewer slots than files): every file is exact and
+    every byte came from the peer."""
+    import numpy as np
+
+    rng = np.random.default_rng(17)
+    files = {f"model-{i:05d}-of-00005.safetensors": rng.integers(0, 256, 700_000 + 91_000 * i, dtype=np.uint8).tobytes()
+             for i in range(5)}
+    files["config.json"] = b'{"model_type": "llama"}'
+    a, commit = _seed_node(hub, nodes, files)
+    srv = a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
+    a.wait_healthy()
+    b = nodes("leecher")
+    before = hub.counters.get("xorb_get", 0)
+    out = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{a.listen_port}", "--no-dht", "-j", "2",
+                env={"ZEST_FILE_CONCURRENCY": file_concurrency}).stdout
+    assert "5 Xet-backed files, 6 total files" in out
+    assert p2p_ratio(out) == 100.0
+    assert hub.counters.get("xorb_get", 0) == before, "leecher touched the CDN"
+    assert_snapshot(b, REPO_ID, commit, files)
+    a.run("stop")
+    srv.wait(timeout=10)
