@@ -37,7 +37,7 @@ def _expected(world):
     return out
 
 
-def _worker(rank, world_size, port, repo, q):
+def _worker(rank, world_size, port, repo, q, peers=None):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -46,7 +46,7 @@ def _worker(rank, world_size, port, repo, q):
         from zest_amd.parallel import swarm_pull
         st = {}
         try:
-            t = swarm_pull(repo, p2p=False, dht=False, stats=st)
+            t = swarm_pull(repo, p2p=bool(peers), peers=peers, dht=False, stats=st)
             q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
         except Exception as e:
             q.put((rank, type(e).__name__, str(e), st))
@@ -54,11 +54,11 @@ def _worker(rank, world_size, port, repo, q):
         dist.destroy_process_group()
 
 
-def _run(world_size, repo):
+def _run(world_size, repo, peers=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world_size, port, repo, q)) for r in range(world_size)]
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, repo, q, peers)) for r in range(world_size)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
@@ -111,3 +111,31 @@ def test_swarm_pull_failed_owner_fails_every_rank(hub_env, victim_index):
     res = _run(3, world.spec.repo_id)
     assert all(r[1] == "SwarmPullError" for r in res), res
     assert sum("rank" in r[2] for r in res) == 3
+
+
+def test_swarm_pull_from_another_node(hub_env, tmp_path):
+    """SURVEY §4.4 item 7, multi-node without a cluster: "node B" is a `zest serve` process with the
+    model in its xorb cache; "node A" is 2 ranks running swarm_pull with B as their BEP XET peer over
+    TCP loopback.  Every file crosses the inter-node link once (owner rank, 100 % from the peer, no
+    CDN), is then broadcast inside node A, and every rank ends with every tensor."""
+    from e2e_util import Node
+
+    world, hub = hub_env
+    b = Node(hub, tmp_path, "node_b")
+    try:
+        b.run("pull", world.spec.repo_id, "--no-p2p", "--no-serve", timeout=300)
+        b.spawn("serve", "--listen-port", str(b.listen_port), "--http-port", str(b.http_port))
+        b.wait_healthy()
+        want = _expected(world)
+        before = hub.counters.get("xorb_get", 0)
+        res = _run(2, world.spec.repo_id, peers=[f"127.0.0.1:{b.listen_port}"])
+        assert [r[1] for r in res] == ["ok", "ok"], res
+        for _, _, got, _ in res:
+            assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert hub.counters.get("xorb_get", 0) == before, "node A touched the CDN"
+        total = sum(f.size for f in world.xet_files)
+        assert sum(r[3]["fetched_bytes"] for r in res) == total
+        st = __import__("json").loads(b.api("/v1/status")[1])
+        assert st["bytes_served"] > 0
+    finally:
+        b.close()
