@@ -170,6 +170,9 @@ http::ServerResponse ApiServer::route(const http::Request& r) {
     m << "# TYPE zest_chunks_served_total counter\nzest_chunks_served_total " << s.chunks_served << "\n";
     m << "# TYPE zest_bytes_served_total counter\nzest_bytes_served_total " << s.bytes_served << "\n";
     m << "# TYPE zest_bt_peers gauge\nzest_bt_peers " << s.active_peers << "\n";
+    m << "# TYPE zest_bt_peers_total counter\nzest_bt_peers_total " << s.total_peers << "\n";
+    m << "# TYPE zest_bt_rejected_total counter\nzest_bt_rejected_total " << s.rejected << "\n";
+    m << "# TYPE zest_chunk_not_found_total counter\nzest_chunk_not_found_total " << s.not_found << "\n";
     m << "# TYPE zest_xorbs_cached gauge\nzest_xorbs_cached " << (registry_ ? registry_->count() : 0) << "\n";
     m << "# TYPE zest_http_requests_total counter\nzest_http_requests_total " << server_->requests() << "\n";
     resp.content_type = "text/plain; version=0.0.4";

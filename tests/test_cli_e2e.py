@@ -328,7 +328,9 @@ def test_http_api_and_pull_job(hub, nodes):
     models = json.loads(a.api("/v1/models")[1])
     assert {"name": REPO_ID, "files": 3} in models
     assert json.loads(a.api("/v1/status")[1])["xorbs_cached"] > 0
-    assert b"zest_chunks_served_total" in a.api("/metrics")[1]
+    metrics = a.api("/metrics")[1]
+    for name in (b"zest_chunks_served_total", b"zest_bt_rejected_total", b"zest_chunk_not_found_total"):
+        assert name in metrics
     assert json.loads(a.api("/v1/stop", "POST")[1]) == {"status": "shutting down"}
     srv.wait(timeout=10)
     out = srv.stdout.read()
