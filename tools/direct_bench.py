@@ -71,7 +71,7 @@ def main() -> int:
             zest_amd._init()
             torch.cuda.synchronize()
             t0 = time.time()
-            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
+            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False, threads=a.threads)
             torch.cuda.synchronize()
             dt = time.time() - t0
             n = sum(v.numel() * v.element_size() for v in out.values())
@@ -85,7 +85,7 @@ def main() -> int:
             os.environ.update(hub.env(str(work / "direct_nocache")))
             os.environ["ZEST_CACHE_WRITES"] = "0"
             t0 = time.time()
-            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False)
+            out = zest_amd.pull(spec.repo_id, device="cuda:0", direct=True, peers=[peer], dht=False, threads=a.threads)
             torch.cuda.synchronize()
             dt = time.time() - t0
             os.environ.pop("ZEST_CACHE_WRITES")

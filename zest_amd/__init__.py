@@ -56,7 +56,7 @@ def disable() -> None:
 def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = False, verify: bool = True,
          p2p: bool = True, peers=None, tracker=None, dht: bool = True, dht_bootstrap=None, include=None,
          group=None, repo_type: str = "model", verbose: bool = False, direct: bool = False,
-         save_snapshot: bool = False):
+         save_snapshot: bool = False, threads: int = 16, staging_bytes: int = 1 << 30):
     """Download `repo@revision` via zest.
 
     * default: returns the HF-cache snapshot directory (reference behaviour).
@@ -65,7 +65,8 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
     * device="all": collective over `group` (default WORLD) — every rank gets all tensors on its
       own GPU while each file is read/pushed by one owner rank and replicated over xGMI (RCCL).
     * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
-      cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct).
+      cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct);
+      `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.
     """
     _init()
     kw = dict(p2p=p2p, peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, include=include,
@@ -87,7 +88,8 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
         from .direct import pull_to_device
 
         return pull_to_device(repo, revision, device or "cuda:0", p2p=p2p, peers=peers, tracker=tracker, dht=dht,
-                              dht_bootstrap=dht_bootstrap, repo_type=repo_type, save_snapshot=save_snapshot)
+                              dht_bootstrap=dht_bootstrap, repo_type=repo_type, save_snapshot=save_snapshot,
+                              threads=threads, staging_bytes=staging_bytes)
     from .device import load_snapshot
 
     res = _client.pull_detailed(repo, revision, **kw)
