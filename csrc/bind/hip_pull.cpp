@@ -169,6 +169,7 @@ class DeviceXetPull {
       if (attempt == 0) bridge_->stats().refetches += again.size();
       todo = std::move(again);
     }
+    if (cfg_.cache_max_gb > 0) cache_->trim(uint64_t(cfg_.cache_max_gb * 1e9));  // ZEST_CACHE_MAX_GB
     for (size_t f : todo)
       throw Error("HashMismatch", "device bytes hash " + got[f] + " != " + std::get<0>(files[f]));
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

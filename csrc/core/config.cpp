@@ -1,5 +1,7 @@
 #include "config.h"
 
+#include <algorithm>
+
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -67,6 +69,7 @@ Config Config::from_env() {
   c.listen_port = port_env("ZEST_LISTEN_PORT", kDefaultListenPort);
   c.dht_port = port_env("ZEST_DHT_PORT", kDefaultDhtPort);
   if (const char* v = env("ZEST_MAX_PEERS")) c.max_peers = uint32_t(std::strtoul(v, nullptr, 10));
+  if (const char* v = env("ZEST_CACHE_MAX_GB")) c.cache_max_gb = std::max(0.0, std::strtod(v, nullptr));
   if (const char* v = env("ZEST_MAX_INBOUND")) c.max_inbound = uint32_t(std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_PEER_CONNECTIONS")) c.peer_connections = uint32_t(std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_CONCURRENCY")) c.concurrency = std::max(1ul, std::strtoul(v, nullptr, 10));

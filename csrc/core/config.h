@@ -54,6 +54,7 @@ struct Config {
   bool trace = false;       // ZEST_TRACE
   std::string fault;        // ZEST_FAULT ("drop:p,corrupt:p,delay:ms")
   bool cache_writes = true; // ZEST_CACHE_WRITES=0: do not keep fetched runs in the xorb cache
+  double cache_max_gb = 0;  // ZEST_CACHE_MAX_GB: trim the xorb cache (least recently used runs) to this size; 0 = unbounded
 
   static Config from_env();
   std::string repo_dir(const std::string& repo_id) const;  // models--org--name

@@ -211,6 +211,11 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
     for (auto& t : fts) t.join();
     S.bytes += bytes.load();
   }
+  if (cfg.cache_max_gb > 0) {  // size-bounded xorb cache: drop least recently used runs
+    const uint64_t cut = cache.trim(uint64_t(cfg.cache_max_gb * 1e9));
+    if (cut) out << "Trimmed the xorb cache by " << std::fixed << std::setprecision(1) << double(cut) / 1e6
+                 << " MB (ZEST_CACHE_MAX_GB=" << cfg.cache_max_gb << ")\n";
+  }
   try {
     storage::write_ref(cfg, opt.repo_id, opt.revision, S.commit);
   } catch (const Error& e) {

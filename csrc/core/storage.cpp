@@ -157,6 +157,10 @@ void XorbRegistry::add(const std::string& key) {
   std::lock_guard<std::mutex> g(mu_);
   keys_.insert(key);
 }
+void XorbRegistry::remove(const std::string& key) {
+  std::lock_guard<std::mutex> g(mu_);
+  keys_.erase(key);
+}
 bool XorbRegistry::has(const std::string& key) const {
   std::lock_guard<std::mutex> g(mu_);
   return keys_.count(key) > 0;
@@ -256,7 +260,8 @@ std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, 
   // Closest preceding run first: most likely to be the one that was fetched for this range.
   for (auto it = offs.rbegin(); it != offs.rend(); ++it) {
     if (*it > start) continue;
-    auto m = map_file(cfg_.xorb_cache_path(*it == 0 ? hex : hex + "." + std::to_string(*it)));
+    const std::string path = cfg_.xorb_cache_path(*it == 0 ? hex : hex + "." + std::to_string(*it));
+    auto m = map_file(path);
     if (!m) continue;
     const uint8_t* base = static_cast<const uint8_t*>(m->p);
     std::vector<xet::ChunkEntry> idx;
@@ -276,6 +281,7 @@ std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, 
     h.ext = base + lo;
     h.ext_len = hi - lo;
     h.keep = m;
+    (void)::utimensat(AT_FDCWD, path.c_str(), nullptr, 0);  // recently used: trim() keeps it longer
     return h;
   }
   return std::nullopt;
@@ -325,6 +331,56 @@ void XorbCache::discard_pending(const std::string& hex, uint32_t chunk_offset) {
 }
 
 void XorbCache::evict(const std::string& hex, uint32_t chunk_offset) { remove_file(run_path(hex, chunk_offset)); }
+
+uint64_t XorbCache::trim(uint64_t max_bytes) {
+  struct Run {
+    int64_t mtime_ns;
+    uint64_t size;
+    std::string hex, path;
+  };
+  std::vector<Run> runs;
+  uint64_t total = 0;
+  DIR* d = ::opendir(cfg_.xorb_cache_dir.c_str());
+  if (!d) return 0;
+  while (dirent* e = ::readdir(d)) {
+    const std::string pfx = e->d_name;
+    if (pfx.size() != 2) continue;
+    const std::string sub = cfg_.xorb_cache_dir + "/" + pfx;
+    DIR* sd = ::opendir(sub.c_str());
+    if (!sd) continue;
+    while (dirent* f = ::readdir(sd)) {
+      const std::string n = f->d_name;
+      if (n.size() < 64 || n.compare(0, 2, pfx) != 0) continue;
+      const bool run = n.size() == 64 ||
+                       (n[64] == '.' && n.size() > 65 && std::all_of(n.begin() + 65, n.end(), ::isdigit));
+      if (!run) continue;  // quarantined (.unverified) and temporary files stay
+      struct stat st;
+      const std::string path = sub + "/" + n;
+      if (::stat(path.c_str(), &st) != 0) continue;
+      runs.push_back({int64_t(st.st_mtim.tv_sec) * 1000000000ll + st.st_mtim.tv_nsec, uint64_t(st.st_size),
+                      n.substr(0, 64), path});
+      total += uint64_t(st.st_size);
+    }
+    ::closedir(sd);
+  }
+  ::closedir(d);
+  if (total <= max_bytes) return 0;
+  std::sort(runs.begin(), runs.end(), [](const Run& a, const Run& b) { return a.mtime_ns < b.mtime_ns; });
+  const uint64_t target = max_bytes - max_bytes / 10;
+  uint64_t removed = 0;
+  std::set<std::string> touched;
+  for (const Run& r : runs) {
+    if (total - removed <= target) break;
+    if (::unlink(r.path.c_str()) == 0) {
+      removed += r.size;
+      touched.insert(r.hex);
+    }
+  }
+  if (registry_)
+    for (const auto& hex : touched)
+      if (run_offsets(hex).empty()) registry_->remove(hex);
+  return removed;
+}
 
 uint64_t XorbCache::bytes_on_disk() const {
   uint64_t t = 0;

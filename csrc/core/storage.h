@@ -81,6 +81,7 @@ std::string xet_hash_of_file(const std::string& file, int threads = 0);
 class XorbRegistry {
  public:
   void add(const std::string& key);
+  void remove(const std::string& key);
   bool has(const std::string& key) const;
   size_t count() const;
   void scan(const Config& cfg);
@@ -125,6 +126,11 @@ class XorbCache {
   }
   std::vector<uint32_t> run_offsets(const std::string& hex) const;  // offsets of cached runs
   uint64_t bytes_on_disk() const;
+  // Size bound (ZEST_CACHE_MAX_GB): when the published runs exceed `max_bytes`, delete the least
+  // recently used ones (cache hits refresh a run's mtime) down to 90 % of it; xorbs with no run
+  // left leave the registry, so they are no longer seeded.  Quarantined and temporary files are
+  // never touched.  Returns the bytes removed.  The reference's cache only grows.
+  uint64_t trim(uint64_t max_bytes);
 
  private:
   std::string run_path(const std::string& hex, uint32_t chunk_offset) const;

@@ -450,3 +450,30 @@ def test_p2p_many_xet_files_concurrently(hub, nodes, file_concurrency):
     assert_snapshot(b, REPO_ID, commit, files)
     a.run("stop")
     srv.wait(timeout=10)
+
+
+def test_cache_size_bound(hub, nodes):
+    """ZEST_CACHE_MAX_GB: after a pull the xorb cache is trimmed (least recently used runs first) to
+    90 % of the bound; the snapshot stays exact, and a later pull refetches what was dropped."""
+    import numpy as np
+
+    rng = np.random.default_rng(29)
+    files = {f"w{i}.safetensors": rng.integers(0, 256, 900_000, dtype=np.uint8).tobytes() for i in range(4)}
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
+    a = nodes("a")
+    bound = 2_000_000
+    env = {"ZEST_CACHE_MAX_GB": str(bound / 1e9)}
+    out = a.run("pull", REPO_ID, "--no-p2p", "--no-serve", env=env).stdout
+    assert "Trimmed the xorb cache by" in out
+    assert_snapshot(a, REPO_ID, commit, files)
+    cached = sum(p.stat().st_size for p in a.xorb_files())
+    assert 0 < cached <= bound * 0.9, cached
+    # without the cached copies of the trimmed runs, a re-pull goes back to the CDN and is exact
+    snap = a.snapshot(REPO_ID, commit)
+    for name in files:
+        (snap / name).unlink()
+    gets = hub.counters.get("xorb_get", 0)
+    a.run("pull", REPO_ID, "--no-p2p", "--no-serve", env=env)
+    assert_snapshot(a, REPO_ID, commit, files)
+    assert hub.counters.get("xorb_get", 0) > gets
+    assert sum(p.stat().st_size for p in a.xorb_files()) <= bound * 0.9
