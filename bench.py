@@ -216,6 +216,7 @@ def main() -> None:
                    "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
                    "verify": "blake3 of every chunk on every rank + merkle file hashes",
                    "numa_bound_cpus": len(numa_cpus), "hip_graph": bool(graph),
+                   "pipeline": getattr(puller, "pipeline", "cpu"),
                    "backend": backend if world_size > 1 else "none"},
     }
     if rank == 0:

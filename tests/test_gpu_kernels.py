@@ -535,12 +535,15 @@ def test_device_puller_host_header_walk_matches_device_walk():
     want = arena.clone()
     pullers = []
     for host in ("1", "0"):
-        os.environ["ZEST_HOST_INDEX"] = host
+        # the host walk runs in the "lanes" pipeline (a compressed world defaults to "copy", which
+        # keeps the device walk)
+        os.environ.update(ZEST_HOST_INDEX=host, ZEST_PIPELINE="lanes")
         try:
             p = DevicePuller(w, arena, 0, 1, round_bytes=256 << 10)
         finally:
             os.environ.pop("ZEST_HOST_INDEX", None)
-        assert p.host_index == (host == "1")
+            os.environ.pop("ZEST_PIPELINE", None)
+        assert p.host_index == (host == "1") and p.pipeline == "lanes"
         p.build_origin()
         for _ in range(3):  # both parities of the host record tables
             arena.fill_(0x5A)
@@ -561,3 +564,37 @@ def test_device_puller_host_header_walk_matches_device_walk():
     assert ei.value.code == 1
     for q in pullers:
         q.close()
+
+
+@pytest.mark.parametrize("pipeline", ["copy", "lanes"])
+@pytest.mark.parametrize("mode,compression", [("bf16", "bg4"), ("random", "none")])
+def test_device_puller_pipelines(pipeline, mode, compression):
+    """Both engine pipeline shapes ("copy": one H2D stream gated by slot events, the default for
+    compressed worlds; "lanes": H2D on the compute lanes, the default for raw ones) pull every byte
+    exactly over several steps."""
+    import os
+
+    from zest_amd import ops
+    from zest_amd.engine import DevicePuller
+    from zest_amd.synthetic import SyntheticWorld
+    dev = torch.device("cuda:0")
+    w = SyntheticWorld("llama-tiny", seed=13, mode=mode, max_xorb_bytes=256 << 10, compression=compression)
+    arena = ops.padded_empty(w.arena_bytes, dev)
+    w.generate_on_device(arena)
+    w.build_on_device(arena)
+    want = arena.clone()
+    os.environ["ZEST_PIPELINE"] = pipeline
+    try:
+        p = DevicePuller(w, arena, 0, 1, round_bytes=256 << 10, slots=4)
+    finally:
+        os.environ.pop("ZEST_PIPELINE", None)
+    assert p.pipeline == pipeline and p.n_rounds >= 4
+    p.build_origin()
+    for _ in range(3):
+        arena.fill_(0x3C)
+        p.err.zero_()
+        p.step()
+    torch.cuda.synchronize()
+    p.check()
+    for f in w.xet_files:  # (the arena also holds alignment gaps that belong to no file)
+        assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size])

@@ -234,6 +234,21 @@ class DevicePuller:
                 hi = -1
             self.lane_stream = torch.cuda.Stream(self.device, priority=hi)
             self.side_stream = torch.cuda.Stream(self.device, priority=hi)
+            # Pipeline shape.  "lanes": each round's H2D copy rides its compute lane (above; best when
+            # the kernels are short next to the copy: raw chunks, 56.9 vs 56.2 GB/s).  "copy": one
+            # copy stream issues every round's H2D back to back, gated only by slot-free events, so
+            # PCIe never waits behind a lane's kernels -- needed when rounds decode LZ4/BG4 (a 1 GiB
+            # bf16 round decodes in ~13 ms against ~16 ms of H2D; in "lanes" the two lanes drift
+            # into copying together and decoding together, leaving PCIe idle: 54.3 vs 64.3 GB/s).
+            # Default: "copy" when any chunk is stored compressed; ZEST_PIPELINE overrides.
+            compressed = bool(np.any(world.chunk_clen < world.chunk_len))
+            self.pipeline = os.environ.get("ZEST_PIPELINE", "copy" if compressed else "lanes")
+            if self.pipeline not in ("lanes", "copy"):
+                raise ValueError(f"ZEST_PIPELINE={self.pipeline!r}: expected 'lanes' or 'copy'")
+            if self.pipeline == "copy":
+                self.copy_stream = torch.cuda.Stream(self.device, priority=hi)
+                self.h2d_done = [torch.cuda.Event() for _ in self.staging]
+                self.slot_free = [torch.cuda.Event() for _ in self.staging]
         # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
         # and returns, so a caller looping over step() without syncing queues thousands of commands
         # over many steps, and past ~10 steps queued the HIP runtime fed the device measurably slower
@@ -248,7 +263,11 @@ class DevicePuller:
         # pointer chase per 1 GiB round and the largest kernel in the profile).  Pinned record
         # tables alternate by step parity, which is race-free while at most one earlier step is in
         # flight (steps_ahead == 1); otherwise, and inside a HIP graph, the device walk runs.
-        self.host_index = (self.is_cuda and self.steps_ahead == 1
+        # The copy pipeline keeps the device walk: a round's small record upload (host walk) would sit
+        # on a lane or the copy stream between 1 GiB transfers, and the host blocked on it, leaving
+        # one copy in flight at a time (BG4 bf16 70B: 53.5 / 59.2 GB/s with host records on the
+        # copy stream / the lane, vs 64.3 with the device walk; profiles/pipeline_ab_r2.md).
+        self.host_index = (self.is_cuda and self.steps_ahead == 1 and getattr(self, "pipeline", "lanes") == "lanes"
                            and os.environ.get("ZEST_HOST_INDEX", "1") != "0")
         if self.host_index:
             nbytes = max(1, sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize)
@@ -563,27 +582,35 @@ class DevicePuller:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
-    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int) -> None:
-        """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes."""
+    def _host_records(self, rw: RoundWork) -> int:
+        """Host header walk of round rw's runs in the pinned origin into this step's pinned record
+        table (error word set stream-ordered on the current stream); returns the records' address."""
+        tab = self._tables[self._step_no & 1]
+        rec_ptr = tab.data_ptr() + rw.table_off
+        e = _core.index_runs(self.origin.ptr + rw.span_off, rw.span_len, rw.terms_host.ctypes.data,
+                             rw.term_b - rw.term_a, rec_ptr, rw.n_chunks)
+        if e:
+            self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
+        return rec_ptr
+
+    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int, chunks=None) -> None:
+        """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes.
+        `chunks`: device chunk records already uploaded for this round (copy pipeline)."""
         if rw.term_b <= rw.term_a:
             return
         nbytes = rw.n_chunks * ops.CHUNK_DTYPE.itemsize
-        if self.host_index and not self._capturing:
-            tab = self._tables[self._step_no & 1]
-            rec_ptr = tab.data_ptr() + rw.table_off
-            e = _core.index_runs(self.origin.ptr + rw.span_off, rw.span_len, rw.terms_host.ctypes.data,
-                                 rw.term_b - rw.term_a, rec_ptr, rw.n_chunks)
-            if e:
-                self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
-            H.memcpy_async(ws.chunks.data_ptr(), rec_ptr, nbytes, st)
-        else:
-            ws.chunks[:nbytes].zero_()
-            H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, ws.chunks.data_ptr(),
-                          self.err.data_ptr(), st)
-        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(),
+        if chunks is None:
+            chunks = ws.chunks
+            if self.host_index and not self._capturing:
+                H.memcpy_async(chunks.data_ptr(), self._host_records(rw), nbytes, st)
+            else:
+                chunks[:nbytes].zero_()
+                H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, chunks.data_ptr(),
+                              self.err.data_ptr(), st)
+        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(),
                        rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
         sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
-        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), ws.chunks.data_ptr(), rw.n_chunks,
+        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(), rw.n_chunks,
                       self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
 
     def capture_graph(self) -> bool:
@@ -644,10 +671,23 @@ class DevicePuller:
                 st = comp.cuda_stream
                 if self._rx:
                     _core.trace.roctx_push(f"engine: round {k}")
+                copy_mode = self.pipeline == "copy" and not self._capturing
+                if copy_mode:
+                    slot = k % len(self.staging)
+                    with torch.cuda.stream(self.copy_stream):
+                        self.copy_stream.wait_event(self.slot_free[slot])  # no-op before first use
+                        if rw.span_len:
+                            H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
+                                           self.copy_stream.cuda_stream)
+                        self.h2d_done[slot].record(self.copy_stream)
                 with torch.cuda.stream(comp):
-                    if rw.span_len:
+                    if copy_mode:
+                        comp.wait_event(self.h2d_done[slot])
+                    elif rw.span_len:
                         H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, st)
                     self._ingest_round(H, rw, src, ws, st)
+                    if copy_mode:
+                        self.slot_free[slot].record(comp)
                     if self.n_ranks > 1:
                         if self.exchange in PEER_MAPPED_MODES:
                             # peers read round k once its kernels are done; wait for that only after
