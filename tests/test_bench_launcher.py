@@ -1,0 +1,65 @@
+"""bench.py contract on CPU: `python bench.py --gpus N` launches its own ranks (torchrun child),
+prints one JSON line, and a rank that hangs ends the run with a non-zero status instead of a
+silent empty record (per-phase watchdog, launcher timeout)."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.update(env_extra or {})
+    t0 = time.time()
+    p = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--model", "llama-tiny", *args],
+                       capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    return p, time.time() - t0
+
+
+def _json_lines(text):
+    return [json.loads(ln) for ln in text.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_prints_one_json_line(gpus):
+    p, _ = _run(["--gpus", str(gpus), "--steps", "2", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    out = lines[0]
+    assert out["n_gpus"] == gpus and out["steps"] == 2 and out["warmup"] == 1
+    assert out["metric"].startswith("aggregate pull GB/s")
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    # both data modes measured; the first (bf16) is the headline
+    assert out["config"]["modes"] == ["bf16", "random"]
+    assert out["extra"]["bf16_GBps"] == out["value"] and out["extra"]["random_GBps"] > 0
+    if gpus > 1:
+        assert out["config"]["backend"] == "gloo" and 0 < out["p2p_ratio"] < 1
+        assert "launching 2 ranks" in p.stderr
+
+
+def test_bench_hung_rank_fails_fast():
+    """Rank 1 stops in the warm-up phase: its watchdog dumps the stack and exits, torchrun tears
+    rank 0 down, and the launcher returns non-zero well before any driver timeout."""
+    p, dt = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--modes", "random"],
+                 {"ZEST_BENCH_WATCHDOG": "8", "ZEST_BENCH_FAULT": "hang:1:warmup", "ZEST_BENCH_PG_TIMEOUT": "20"})
+    assert p.returncode != 0
+    assert not _json_lines(p.stdout)
+    assert "Timeout" in p.stderr or "most recent call first" in p.stderr, p.stderr[-3000:]
+    assert dt < 150
+
+
+def test_bench_launcher_timeout_kills_group():
+    """Watchdog disabled: the launcher's own deadline kills the whole rank group (exit 124)."""
+    p, dt = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--modes", "random"],
+                 {"ZEST_BENCH_WATCHDOG": "0", "ZEST_BENCH_FAULT": "hang:1:timed", "ZEST_BENCH_TIMEOUT": "25"})
+    assert p.returncode == 124, p.stderr[-2000:]
+    assert dt < 90
