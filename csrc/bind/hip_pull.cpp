@@ -150,10 +150,13 @@ class DeviceXetPull {
         settle_all(at, recs, todo, [](size_t) { return false; });
         throw Error("DownloadFailed", at.fetch_err);
       }
+      // A file is bad only when its own Merkle root misses: the roots are computed from the bytes
+      // that landed in HBM, so a decode error in one file (the error word is shared by the batch)
+      // cannot pass as good data, and it no longer evicts the cache runs of every other file.
       std::vector<size_t> bad;
       for (size_t j = 0; j < todo.size(); ++j) {
         got[todo[j]] = at.roots[j];
-        if (at.ingest_err || at.roots[j] != std::get<0>(files[todo[j]])) bad.push_back(j);
+        if (at.roots[j] != std::get<0>(files[todo[j]])) bad.push_back(j);
       }
       settle_all(at, recs, todo, [&](size_t j) { return std::find(bad.begin(), bad.end(), j) == bad.end(); });
       if (bad.empty()) {
@@ -196,7 +199,7 @@ class DeviceXetPull {
   struct TermSource {
     Source src = Source::Cdn;
     uint32_t run_offset = 0;
-    bool pending = false;
+    std::string pending;  // quarantine file of a peer run (empty: none)
   };
   struct Attempt {
     std::vector<std::string> roots;  // per file of the attempt: Merkle root (Xet hex)

@@ -82,8 +82,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         if (cache_ && cfg_.cache_writes) {
           try {
             trace::Span sp("cache", "put_pending");
-            cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
-            out.pending = true;
+            out.pending = cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
             out.run_offset = r->chunk_offset;
           } catch (const Error&) {
           }
@@ -130,12 +129,13 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   return out;
 }
 
-void XetBridge::settle(const std::string& xorb_hex, Source src, uint32_t run_offset, bool pending, bool ok) {
+void XetBridge::settle(const std::string& xorb_hex, Source src, uint32_t run_offset, const std::string& pending,
+                       bool ok) {
   if (!cache_) return;
   try {
-    if (src == Source::Peer && pending) {
-      if (ok) cache_->promote(xorb_hex, run_offset);
-      else cache_->discard_pending(xorb_hex, run_offset);
+    if (src == Source::Peer && !pending.empty()) {
+      if (ok) cache_->promote(xorb_hex, run_offset, pending);
+      else cache_->discard_pending(pending);
     } else if (src == Source::Cache && !ok) {
       cache_->evict(xorb_hex, run_offset);
     }

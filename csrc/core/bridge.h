@@ -44,10 +44,10 @@ struct XorbFetchResult {
   Source source = Source::Cdn;
   std::string peer;
   // Cache bookkeeping for verification: Cache -> the run the hit came from (evicted when the file
-  // fails verification); Peer -> the run quarantined with put_pending (`pending` true), published by
-  // XetBridge::settle once the file hash checked out.
+  // fails verification); Peer -> the run quarantined with put_pending (`pending` = its quarantine
+  // file, unique to this fetch), published by XetBridge::settle once the file hash checked out.
   uint32_t run_offset = 0;
-  bool pending = false;
+  std::string pending;
   // With a sink: the run was written to sink memory instead of `data`.
   uint8_t* ext = nullptr;
   size_t ext_len = 0;
@@ -71,7 +71,7 @@ class XetBridge {
   // run quarantined by fetch_term; on failure also evict the cached run a cache hit came from, so
   // the repair refetch cannot read the same bad bytes again.
   void settle(const std::string& xorb_hex, const XorbFetchResult& r, bool ok);
-  void settle(const std::string& xorb_hex, Source src, uint32_t run_offset, bool pending, bool ok);
+  void settle(const std::string& xorb_hex, Source src, uint32_t run_offset, const std::string& pending, bool ok);
   FetchStats& stats() { return stats_; }
   void print_stats(std::ostream& w) const;
   std::string stats_json() const;

@@ -116,7 +116,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   std::vector<Source> src(n, Source::Cdn);
   std::vector<std::string> peer(n);
   std::vector<uint32_t> run_off(n, 0);
-  std::vector<uint8_t> pending(n, 0);
+  std::vector<std::string> pending(n);  // quarantine file of a peer run, until settled
   size_t resumed = 0;
   // ---- resume from sidecar
   if (storage::exists(tmp) && storage::exists(side)) {
@@ -167,8 +167,8 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   // it and blame the peer that served it.
   auto reject = [&](size_t i) {
     if (src[i] == Source::Peer && !peer[i].empty() && bridge_.swarm()) bridge_.swarm()->report_bad_peer(peer[i]);
-    bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i] != 0, false);
-    pending[i] = 0;
+    bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], false);
+    pending[i].clear();
   };
   auto do_term = [&](size_t i, const FetchOptions& opt, RunBuffer* buf) {
     const cas::Term& t = rec.terms[i];
@@ -265,7 +265,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   if (failed) {
     ::close(fd);
     for (size_t i = 0; i < n; ++i)
-      if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
+      if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], false);
     throw Error("DownloadFailed", first_err);
   }
   bool ok = true;
@@ -294,7 +294,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       } catch (...) {  // the CDN failed too: keep the sidecar (resumed terms are re-checked next run)
         ::close(fd);
         for (size_t i = 0; i < n; ++i)
-          if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, false);
+          if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], false);
         throw;
       }
       trace::Span vs("download", "file hash verify");
@@ -308,7 +308,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   }
   // The file checked out (or the caller skipped verification): publish the quarantined peer runs.
   for (size_t i = 0; i < n; ++i)
-    if (pending[i]) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], true, true);
+    if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], true);
   ::fdatasync(fd);
   ::close(fd);
   if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);

@@ -215,6 +215,8 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
     const uint64_t cut = cache.trim(uint64_t(cfg.cache_max_gb * 1e9));
     if (cut) out << "Trimmed the xorb cache by " << std::fixed << std::setprecision(1) << double(cut) / 1e6
                  << " MB (ZEST_CACHE_MAX_GB=" << cfg.cache_max_gb << ")\n";
+  } else {
+    cache.sweep_pending();  // quarantine runs orphaned by pulls that died
   }
   try {
     storage::write_ref(cfg, opt.repo_id, opt.revision, S.commit);

@@ -4,6 +4,8 @@
 #include <thread>
 
 #include <dirent.h>
+#include <signal.h>
+#include <ctime>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -252,6 +254,22 @@ std::shared_ptr<Mapping> map_file(const std::string& path) {
 }
 }  // namespace
 
+// A quarantine file `{run}.p{pid}-{seq}.unverified` is stale when its writer is gone (no process
+// with that pid) or it is older than `max_age_s` (pid reuse; a pull never holds a run that long).
+bool stale_pending(const std::string& path, int64_t max_age_s) {
+  const std::string suffix = XorbCache::kPendingSuffix;
+  if (path.size() < suffix.size() || path.compare(path.size() - suffix.size(), suffix.size(), suffix) != 0)
+    return false;
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0) return false;
+  if (max_age_s >= 0 && ::time(nullptr) - st.st_mtim.tv_sec > max_age_s) return true;
+  const size_t p = path.rfind(".p");
+  if (p == std::string::npos) return true;  // pre-round-3 name without a pid: nobody owns it
+  const long pid = std::strtol(path.c_str() + p + 2, nullptr, 10);
+  if (pid <= 0) return true;
+  return ::kill(pid_t(pid), 0) != 0 && errno == ESRCH;
+}
+
 // Zero-copy: the hit views the page-cache mapping of the run file (cache files are only ever
 // replaced by rename, never truncated in place, so a live mapping stays valid).  Only the chunk
 // headers are touched to validate coverage.
@@ -305,15 +323,21 @@ void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uin
   if (registry_) registry_->add(hex);
 }
 
-void XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
-  write_file_atomic(run_path(hex, chunk_offset) + kPendingSuffix, data, n, /*durable=*/false);
+std::string XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+  // One quarantine file per fetch: `{run}.p{pid}-{seq}.unverified`.  Files are reconstructed
+  // concurrently, so two fetches of the same run (from different peers) must not share a name:
+  // promote() publishes exactly the bytes that belonged to the file that verified.
+  static std::atomic<uint64_t> seq{0};
+  const std::string path = run_path(hex, chunk_offset) + ".p" + std::to_string(::getpid()) + "-" +
+                           std::to_string(seq.fetch_add(1)) + kPendingSuffix;
+  write_file_atomic(path, data, n, /*durable=*/false);
+  return path;
 }
 
-bool XorbCache::promote(const std::string& hex, uint32_t chunk_offset) {
+bool XorbCache::promote(const std::string& hex, uint32_t chunk_offset, const std::string& pending) {
+  if (pending.empty() || !exists(pending)) return false;
   const std::string path = run_path(hex, chunk_offset);
-  const std::string pending = path + kPendingSuffix;
   const uint64_t n = file_size(pending);
-  if (!exists(pending)) return false;
   if (exists(path) && file_size(path) >= n) {  // a published run at least as long already exists
     remove_file(pending);
     return true;
@@ -326,13 +350,13 @@ bool XorbCache::promote(const std::string& hex, uint32_t chunk_offset) {
   return true;
 }
 
-void XorbCache::discard_pending(const std::string& hex, uint32_t chunk_offset) {
-  remove_file(run_path(hex, chunk_offset) + kPendingSuffix);
+void XorbCache::discard_pending(const std::string& pending) {
+  if (!pending.empty()) remove_file(pending);
 }
 
 void XorbCache::evict(const std::string& hex, uint32_t chunk_offset) { remove_file(run_path(hex, chunk_offset)); }
 
-uint64_t XorbCache::trim(uint64_t max_bytes) {
+uint64_t XorbCache::trim(uint64_t max_bytes, int64_t pending_max_age_s) {
   struct Run {
     int64_t mtime_ns;
     uint64_t size;
@@ -353,7 +377,10 @@ uint64_t XorbCache::trim(uint64_t max_bytes) {
       if (n.size() < 64 || n.compare(0, 2, pfx) != 0) continue;
       const bool run = n.size() == 64 ||
                        (n[64] == '.' && n.size() > 65 && std::all_of(n.begin() + 65, n.end(), ::isdigit));
-      if (!run) continue;  // quarantined (.unverified) and temporary files stay
+      if (!run) {  // quarantined (.unverified) runs left behind by a pull that died are removed
+        if (stale_pending(sub + "/" + n, pending_max_age_s)) ::unlink((sub + "/" + n).c_str());
+        continue;  // live quarantine and temporary files stay
+      }
       struct stat st;
       const std::string path = sub + "/" + n;
       if (::stat(path.c_str(), &st) != 0) continue;
@@ -379,6 +406,26 @@ uint64_t XorbCache::trim(uint64_t max_bytes) {
   if (registry_)
     for (const auto& hex : touched)
       if (run_offsets(hex).empty()) registry_->remove(hex);
+  return removed;
+}
+
+size_t XorbCache::sweep_pending(int64_t max_age_s) {
+  size_t removed = 0;
+  DIR* d = ::opendir(cfg_.xorb_cache_dir.c_str());
+  if (!d) return 0;
+  while (dirent* e = ::readdir(d)) {
+    const std::string pfx = e->d_name;
+    if (pfx.size() != 2) continue;
+    const std::string sub = cfg_.xorb_cache_dir + "/" + pfx;
+    DIR* sd = ::opendir(sub.c_str());
+    if (!sd) continue;
+    while (dirent* f = ::readdir(sd)) {
+      const std::string path = sub + "/" + f->d_name;
+      if (stale_pending(path, max_age_s) && ::unlink(path.c_str()) == 0) ++removed;
+    }
+    ::closedir(sd);
+  }
+  ::closedir(d);
   return removed;
 }
 

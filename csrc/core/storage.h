@@ -78,6 +78,9 @@ bool check_verified_marker(const Config& cfg, const std::string& repo_id, const 
 // Xet file hash of a file on disk (CDC + keyed BLAKE3 chunk hashes + Merkle), multi-threaded.
 std::string xet_hash_of_file(const std::string& file, int threads = 0);
 
+// A quarantine file whose writer died (pid gone) or older than max_age_s.
+bool stale_pending(const std::string& path, int64_t max_age_s);
+
 class XorbRegistry {
  public:
   void add(const std::string& key);
@@ -114,9 +117,10 @@ class XorbCache {
   // checked out, promote() publishes the run (keeping an existing longer one); otherwise
   // discard_pending() drops it.  The reference caches peer runs unverified (swarm.zig:416-420) and
   // then serves them on; it caches only CDN bytes in the bridge (xet_bridge.zig:203-208).
-  void put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
-  bool promote(const std::string& hex, uint32_t chunk_offset);
-  void discard_pending(const std::string& hex, uint32_t chunk_offset);
+  // put_pending returns the quarantine file's path (unique per call), which promote/discard take.
+  std::string put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  bool promote(const std::string& hex, uint32_t chunk_offset, const std::string& pending);
+  void discard_pending(const std::string& pending);
   // Drop a published run (a cached copy whose bytes failed verification).
   void evict(const std::string& hex, uint32_t chunk_offset);
   static constexpr const char* kPendingSuffix = ".unverified";
@@ -128,9 +132,14 @@ class XorbCache {
   uint64_t bytes_on_disk() const;
   // Size bound (ZEST_CACHE_MAX_GB): when the published runs exceed `max_bytes`, delete the least
   // recently used ones (cache hits refresh a run's mtime) down to 90 % of it; xorbs with no run
-  // left leave the registry, so they are no longer seeded.  Quarantined and temporary files are
-  // never touched.  Returns the bytes removed.  The reference's cache only grows.
-  uint64_t trim(uint64_t max_bytes);
+  // left leave the registry, so they are no longer seeded.  Live quarantine and temporary files are
+  // never touched; quarantine files whose writer process is gone, or older than
+  // `pending_max_age_s` (< 0: no age limit), are deleted.  Returns the bytes of published runs
+  // removed.  The reference's cache only grows.
+  uint64_t trim(uint64_t max_bytes, int64_t pending_max_age_s = 24 * 3600);
+  // Delete stale quarantine files only (see stale_pending); returns how many.  Runs after every
+  // pull, so runs orphaned by a killed pull do not pile up outside the cache bound.
+  size_t sweep_pending(int64_t max_age_s = 24 * 3600);
 
  private:
   std::string run_path(const std::string& hex, uint32_t chunk_offset) const;

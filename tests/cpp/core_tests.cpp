@@ -314,6 +314,44 @@ TEST(xorb_cache_runs) {
   CHECK(storage::list_cached_xorbs(cfg).size() == 1);
 }
 
+TEST(xorb_cache_quarantine_per_fetch) {
+  // Two concurrent fetches of the same run (e.g. two files, two peers) quarantine under distinct
+  // names; promote() publishes exactly the copy of the file that verified, discard() drops the
+  // other; a quarantine file whose writer is gone is swept, a live one stays.
+  char tmpl[] = "/tmp/zest_cpp_q_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  setenv("ZEST_CACHE_DIR", dir, 1);
+  Config cfg = Config::from_env();
+  storage::XorbCache cache(cfg);
+  xet::XorbBuilder b(xet::CompressionPolicy::None);
+  for (uint32_t i = 0; i < 3; ++i) {
+    Bytes c = rnd(9000, 40 + i);
+    b.add_chunk(c.data(), c.size());
+  }
+  const std::string hx = xet::to_hex(b.hash());
+  Bytes good = b.body(), bad = good;
+  bad[100] ^= 1;
+  const std::string p_bad = cache.put_pending(hx, 0, bad.data(), bad.size());
+  const std::string p_good = cache.put_pending(hx, 0, good.data(), good.size());
+  CHECK(p_bad != p_good && storage::exists(p_bad) && storage::exists(p_good));
+  CHECK(!cache.find(hx, 0, 3).has_value());  // quarantined runs are invisible
+  CHECK(storage::list_cached_xorbs(cfg).empty());
+  CHECK(cache.promote(hx, 0, p_good));
+  cache.discard_pending(p_bad);
+  auto h = cache.find(hx, 0, 3);
+  CHECK(h.has_value() && h->size() == good.size() && std::memcmp(h->bytes(), good.data(), good.size()) == 0);
+  CHECK(!storage::exists(p_bad) && !storage::exists(p_good));
+  // stale sweep: a live writer's file stays, a dead writer's (pid that cannot exist) goes
+  const std::string live = cache.put_pending(hx, 1, good.data(), good.size());
+  const std::string dead = live.substr(0, live.rfind(".p")) + ".p999999999-0.unverified";
+  storage::write_file_atomic(dead, good.data(), good.size(), false);
+  CHECK(!storage::stale_pending(live, 3600) && storage::stale_pending(dead, 3600));
+  CHECK(cache.sweep_pending(3600) == 1);
+  CHECK(storage::exists(live) && !storage::exists(dead));
+  CHECK(storage::stale_pending(live, -1) == false && storage::stale_pending(live, 0) == false);
+}
+
 TEST(peer_pool_leases) {
   // Lease accounting of the connection pool against a loopback seeding server: a lease raises its
   // session's user count by exactly one for its lifetime, busy sessions make the pool open more
