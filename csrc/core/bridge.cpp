@@ -173,6 +173,10 @@ std::string XetBridge::stats_json() const {
   w.key("bytes_from_peer").num_u(stats_.bytes_from_peer).key("bytes_from_cdn").num_u(stats_.bytes_from_cdn);
   w.key("p2p_ratio").num(total_bytes ? double(stats_.bytes_from_peer) / double(total_bytes) : 0.0, 4);
   w.key("verify_failures").num_u(stats_.verify_failures).key("refetches").num_u(stats_.refetches);
+  w.key("peer_bytes").obj();
+  if (swarm_)
+    for (const auto& [addr, b] : swarm_->peer_bytes()) w.key(addr).num_u(b);
+  w.end();
   w.end();
   return w.out();
 }

@@ -1,5 +1,6 @@
 #include "swarm.h"
 
+#include <algorithm>
 #include <cstring>
 #include <set>
 #include <iomanip>
@@ -89,10 +90,26 @@ std::vector<net::Addr> SwarmDownloader::discover(const Sha1Digest& ih) {
   return peers;
 }
 
-// Peers are tried in two rounds: first the direct peers plus every peer that already served this
-// session (one seeder usually holds the whole repo, so its address is reused for the next xorb),
-// then — only if none of them had the range — the per-xorb DHT / tracker discovery.  The reference
-// runs discovery for every xorb (swarm.zig:363-394), serialised behind one lock.
+void SwarmDownloader::remember(const net::Addr& a) {
+  if (known_keys_.insert(a.str()).second) known_.push_back(a);
+}
+
+std::map<std::string, uint64_t> SwarmDownloader::peer_bytes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::map<std::string, uint64_t> out;
+  for (const auto& [k, l] : load_)
+    if (l.bytes) out[k] = l.bytes;
+  return out;
+}
+
+// Peers are tried in two rounds: first the direct peers plus every peer this session already knows
+// (served something, or was discovered for another xorb: one seeder usually holds the whole repo),
+// then -- only if none of them had the range -- the per-xorb DHT / tracker discovery.  Within a
+// round the terms are striped: each attempt picks the untried candidate with the fewest requests in
+// flight (peers that keep answering NOT_FOUND sink to the back), starting from a rotation by the
+// xorb hash so equally loaded peers share the load evenly.  With k seeders and 16 term workers every
+// seeder serves ~1/k of the bytes.  The reference runs discovery for every xorb behind one lock and
+// tries peers in fixed order (swarm.zig:363-394).
 std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash, uint32_t start, uint32_t end,
                                                           const bt::PayloadSink& sink) {
   if (!enabled_) return std::nullopt;
@@ -102,53 +119,90 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
   req.range_start = start;
   req.range_end = end;
   req.sink = sink;
+  uint64_t h0 = 0;
+  std::memcpy(&h0, hash.data(), 8);
+  const uint64_t rot = h0 ^ (uint64_t(start) * 0x9E3779B97F4A7C15ull);
   std::set<std::string> tried;
-  auto attempt = [&](const std::vector<net::Addr>& cands) -> std::optional<bt::ChunkResult> {
-    for (const auto& a : cands) {
+  // Pick the best untried candidate and count the request against it, under one lock.
+  auto pick = [&](const std::vector<net::Addr>& cands) -> std::optional<net::Addr> {
+    std::lock_guard<std::mutex> g(mu_);
+    const size_t n = cands.size();
+    std::optional<size_t> best;
+    std::pair<int, int> best_key{0, 0};
+    for (size_t j = 0; j < n; ++j) {
+      const net::Addr& a = cands[(rot + j) % n];
       const std::string key = a.str();
-      if (!tried.insert(key).second) continue;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        auto it = score_.find(key);
-        if (it != score_.end() && it->second >= 3) continue;  // banned / repeatedly failing
+      if (tried.count(key)) continue;
+      auto sc = score_.find(key);
+      if (sc != score_.end() && sc->second >= 3) continue;  // banned / repeatedly failing
+      const PeerLoad& l = load_[key];
+      const std::pair<int, int> k{l.misses > l.hits + 2 ? 1 : 0, l.inflight};
+      if (!best || k < best_key) {
+        best = (rot + j) % n;
+        best_key = k;
       }
+    }
+    if (!best) return std::nullopt;
+    const net::Addr& a = cands[*best];
+    tried.insert(a.str());
+    load_[a.str()].inflight++;
+    return a;
+  };
+  auto attempt = [&](const std::vector<net::Addr>& cands) -> std::optional<bt::ChunkResult> {
+    while (auto pa = pick(cands)) {
+      const net::Addr a = *pa;
+      const std::string key = a.str();
+      bool hit = false, miss = false;
+      uint64_t got = 0;
+      std::optional<bt::ChunkResult> out;
       try {
         auto s = pool_->get_or_connect(a, ih);
-        if (!s->supports_xet()) continue;
-        trace::Span sp("peer", "request");
-        bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
-        r.peer = key;
-        {
-          std::lock_guard<std::mutex> g(mu_);
-          if (served_by_.insert(r.peer).second) {
-            stats_.peers_connected++;
-            known_.push_back(a);
+        if (s->supports_xet()) {
+          trace::Span sp("peer", "request");
+          bt::ChunkResult r = s->request(req, cfg_.io_timeout_ms);
+          r.peer = key;
+          hit = true;
+          got = r.size();
+          ZTRACE("swarm", "peer " << r.peer << " served " << xet::to_hex(hash) << " [" << start << "," << end
+                                  << ") offset " << r.chunk_offset << " bytes " << r.size());
+          stats_.peer_xorbs++;
+          stats_.peer_bytes += r.size();
+          stats_.total_bytes += r.size();
+          stats_.total_xorbs++;
+          if (dht_) {
+            {
+              std::lock_guard<std::mutex> g(aq_mu_);
+              announce_q_.push_back(ih);
+            }
+            aq_cv_.notify_one();
           }
+          out = std::move(r);
         }
-        ZTRACE("swarm", "peer " << r.peer << " served " << xet::to_hex(hash) << " [" << start << "," << end
-                                << ") offset " << r.chunk_offset << " bytes " << r.size());
-        stats_.peer_xorbs++;
-        stats_.peer_bytes += r.size();
-        stats_.total_bytes += r.size();
-        stats_.total_xorbs++;
-        if (dht_) {
-          {
-            std::lock_guard<std::mutex> g(aq_mu_);
-            announce_q_.push_back(ih);
-          }
-          aq_cv_.notify_one();
-        }
-        return r;
       } catch (const Error& e) {
         stats_.peer_failures++;
         ZTRACE("swarm", "peer " << key << " failed " << xet::to_hex(hash) << " [" << start << "," << end
                                 << "): " << e.what());
-        if (e.code() != "ChunkNotFound" && e.code() != "ChunkError") {
+        if (e.code() == "ChunkNotFound" || e.code() == "ChunkError") {
+          miss = true;
+        } else {
           pool_->remove(a);
           std::lock_guard<std::mutex> g(mu_);
           score_[key]++;
         }
       }
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        PeerLoad& l = load_[key];
+        l.inflight--;
+        l.bytes += got;
+        l.hits += hit;
+        l.misses += miss;
+        if (hit) {
+          if (served_by_.insert(key).second) stats_.peers_connected++;
+          remember(a);
+        }
+      }
+      if (out) return out;
     }
     return std::nullopt;
   };
@@ -156,11 +210,17 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
   {
     std::lock_guard<std::mutex> g(mu_);
     first = direct_;
-    first.insert(first.end(), known_.begin(), known_.end());
+    for (const auto& k : known_)
+      if (std::find(first.begin(), first.end(), k) == first.end()) first.push_back(k);
   }
   if (auto r = attempt(first)) return r;
   if (!dht_ && !tracker_) return std::nullopt;
-  return attempt(discover(ih));
+  const std::vector<net::Addr> found = discover(ih);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& a : found) remember(a);  // striping candidates for the following xorbs too
+  }
+  return attempt(found);
 }
 
 void SwarmDownloader::report_bad_peer(const std::string& addr) {
@@ -200,6 +260,9 @@ void SwarmDownloader::print_stats(std::ostream& w) const {
     const double pct = double(stats_.peer_bytes.load()) / double(stats_.total_bytes.load()) * 100.0;
     w << "  P2P ratio:       " << std::fixed << std::setprecision(1) << pct << "%\n";
   }
+  const auto per_peer = peer_bytes();
+  if (per_peer.size() > 1)
+    for (const auto& [addr, b] : per_peer) w << "  Peer " << addr << ": " << b << " bytes\n";
 }
 
 }  // namespace zest

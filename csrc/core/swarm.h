@@ -7,7 +7,9 @@
 // announceToSwarm (:458-470), printStats (:472-485).  Differences: counters are atomics (the
 // reference mutates stats from concurrent tasks without a lock, SURVEY §5.2 a/b), the cached peer
 // list is copied under the lock before iteration (§5.2 c), peers that time out or serve corrupt
-// data are scored down and skipped, and candidates can be raced (`race` > 1).
+// data are scored down and skipped, and terms are striped over every known peer: each request goes
+// to the candidate with the fewest requests in flight (the reference tries peers in fixed order,
+// first success wins, so one seeder serves everything, swarm.zig:371-394).
 #pragma once
 
 #include <atomic>
@@ -53,6 +55,8 @@ class SwarmDownloader {
   void report_bad_peer(const std::string& addr);
   DownloadStats& stats() { return stats_; }
   void print_stats(std::ostream& os) const;
+  // Bytes each peer served this session ("addr" -> bytes), for stats / striping checks.
+  std::map<std::string, uint64_t> peer_bytes() const;
   dht::Dht* dht() { return dht_.get(); }
 
  private:
@@ -62,7 +66,7 @@ class SwarmDownloader {
   std::unique_ptr<dht::Dht> dht_;
   std::unique_ptr<bt::PeerPool> pool_;
   std::vector<net::Addr> direct_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   struct Cached {
     std::vector<net::Addr> peers;
     std::chrono::steady_clock::time_point at;
@@ -70,7 +74,16 @@ class SwarmDownloader {
   std::map<std::string, Cached> discovered_;
   std::map<std::string, int> score_;  // addr -> failures
   std::set<std::string> served_by_;   // distinct peers that served data ("Peers connected")
-  std::vector<net::Addr> known_;      // the same peers, tried before per-xorb discovery
+  std::vector<net::Addr> known_;      // peers that served or were discovered, tried before per-xorb discovery
+  std::set<std::string> known_keys_;
+  // Per-peer load for striping: requests in flight, bytes served, range hits and misses.
+  struct PeerLoad {
+    int inflight = 0;
+    uint64_t bytes = 0;
+    uint32_t hits = 0, misses = 0;
+  };
+  std::map<std::string, PeerLoad> load_;
+  void remember(const net::Addr& a);  // caller holds mu_
   std::mutex disc_mu_;
   DownloadStats stats_;
   // DHT re-announce of xorbs fetched from peers: queued and drained by an owned worker thread

@@ -175,6 +175,41 @@ def test_p2p_loopback_direct_peer(hub, nodes):
     srv_b.wait(timeout=10)
 
 
+def test_p2p_terms_striped_across_seeders(hub, nodes):
+    """Three warm seeders: the leecher spreads its terms over all of them (least requests in flight
+    per peer) instead of taking everything from the first that answers (reference: sequential
+    first-success, swarm.zig:371-394).  Every seeder serves >= 20 % of the bytes."""
+    import shutil
+    files = {"model.safetensors": sample_files(big=24_000_000)["model.safetensors"]}
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=1)
+    assert len(hub.xorbs) >= 12
+    a = nodes("s0")
+    a.run("pull", REPO_ID, "--no-p2p")
+    seeders = [a]
+    for name in ("s1", "s2"):
+        s = nodes(name)
+        shutil.copytree(a.root / "zest" / "xorbs", s.root / "zest" / "xorbs")
+        seeders.append(s)
+    for s in seeders:
+        s.spawn("serve", "--listen-port", str(s.listen_port), "--http-port", str(s.http_port))
+    for s in seeders:
+        s.wait_healthy()
+    b = nodes("leecher")
+    before = hub.counters.get("xorb_get", 0)
+    args = ["pull", REPO_ID, "--no-dht"]
+    for s in seeders:
+        args += ["--peer", f"127.0.0.1:{s.listen_port}"]
+    out = b.run(*args).stdout
+    assert p2p_ratio(out) == 100.0 and hub.counters.get("xorb_get", 0) == before
+    assert_snapshot(b, REPO_ID, commit, files)
+    served = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
+    total = sum(served)
+    assert total > 0
+    assert all(x >= 0.2 * total for x in served), served
+    # the leecher reports the per-peer split too
+    assert sum(1 for ln in out.splitlines() if ln.strip().startswith("Peer 127.0.0.1:")) == 3, out
+
+
 def test_p2p_corrupt_peer_falls_back_to_cdn(hub, nodes):
     files = sample_files()
     a, commit = _seed_node(hub, nodes, files)
