@@ -190,8 +190,11 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         assert int(lo.item()) == int(hi.item()), "ranks disagree on the synthetic repository"
     seeders = a.seeders if a.seeders > 0 else world_size
+    # Pin once for every data mode: the origin of a raw world is the largest (+8 B per chunk header),
+    # and a share is within one 64 MiB xorb term of 1/seeders of it.
+    reserve = (int(world.model_bytes * 1.002) // seeders + (256 << 20)) if rank < seeders else 0
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
-                          seeders=seeders)
+                          seeders=seeders, origin_reserve=reserve)
     ipc = False
     if world_size > 1 and cuda:
         # The peer-mapped exchanges are opt-in under auto (ZEST_EXCHANGE_IPC=1): a 16 GB arena
@@ -385,6 +388,9 @@ def rank_main(a) -> None:
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if cuda:
+        from zest_amd.engine import release_pinned_pool
+        release_pinned_pool()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -394,6 +394,8 @@ int cmd_seed(const std::string& exe, const std::vector<std::string>& a) {
     }
   }
   SwarmDownloader swarm(cfg, tracker, true, true, boot);
+  // default routers bootstrap in the background: give them a bounded moment before announcing
+  for (int i = 0; i < 500 && !swarm.bootstrap_done(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   swarm.announce(hashes);
   std::cout << "Announced " << hashes.size() << " xorbs via BT protocol\n";
   std::cout << "  Peer ID: " << peer_id::kClientPrefix << "...\n";
@@ -519,7 +521,10 @@ int cmd_serve(const std::vector<std::string>& a) {
   if (run_dht) {
     node = std::make_unique<dht::Dht>(cfg.dht_port);
     node->start();
-    if (!boot.empty()) node->bootstrap(boot);
+    if (boot.empty())  // default public routers, each resolved with a deadline (offline: skipped)
+      for (const std::string& r : cfg.dht_routers)
+        if (auto ra = net::resolve_with_deadline(r, 6881, 1500)) boot.push_back(*ra);
+    if (!boot.empty()) node->bootstrap(boot, 1500);
     std::cout << "  DHT port:       " << node->port() << "\n";
   }
   std::cout << "\nServer running. Press Ctrl+C to stop.\n" << std::flush;

@@ -68,6 +68,20 @@ Config Config::from_env() {
   c.http_port = port_env("ZEST_HTTP_PORT", kDefaultHttpPort);
   c.listen_port = port_env("ZEST_LISTEN_PORT", kDefaultListenPort);
   c.dht_port = port_env("ZEST_DHT_PORT", kDefaultDhtPort);
+  if (const char* b = std::getenv("ZEST_DHT_BOOTSTRAP")) {
+    const std::string v = b;
+    if (v != "none") {
+      size_t p = 0;
+      while (p < v.size()) {
+        size_t e = v.find(',', p);
+        if (e == std::string::npos) e = v.size();
+        if (e > p) c.dht_routers.push_back(v.substr(p, e - p));
+        p = e + 1;
+      }
+    }
+  } else {
+    for (const char* r : kDefaultDhtRouters) c.dht_routers.push_back(r);
+  }
   if (const char* v = env("ZEST_MAX_PEERS")) c.max_peers = uint32_t(std::strtoul(v, nullptr, 10));
   if (const char* v = env("ZEST_CACHE_MAX_GB")) c.cache_max_gb = std::max(0.0, std::strtod(v, nullptr));
   if (const char* v = env("ZEST_MAX_INBOUND")) c.max_inbound = uint32_t(std::strtoul(v, nullptr, 10));
@@ -104,6 +118,9 @@ std::string Config::to_json() const {
   w.obj();
   w.key("version").str(kVersion).key("hub_url").str(hub_url).key("hf_cache_dir").str(hf_cache_dir);
   w.key("cache_dir").str(cache_dir).key("xorb_cache_dir").str(xorb_cache_dir).key("chunk_cache_dir").str(chunk_cache_dir);
+  w.key("dht_routers").arr();
+  for (const auto& r : dht_routers) w.str(r);
+  w.end();
   w.key("pid_file").str(pid_file).key("dht_port").num(int64_t(dht_port)).key("listen_port").num(int64_t(listen_port));
   w.key("http_port").num(int64_t(http_port)).key("max_peers").num(int64_t(max_peers)).key("max_inbound").num(int64_t(max_inbound));
   w.key("peer_connections").num(int64_t(peer_connections)).key("cache_writes").boolean(cache_writes);

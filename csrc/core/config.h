@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <optional>
 #include <string>
+#include <vector>
 
 #include "sha1.h"
 
@@ -26,6 +27,10 @@ constexpr uint16_t kDefaultHttpPort = 9847;
 constexpr uint32_t kDefaultMaxPeers = 50;
 constexpr uint32_t kDefaultChunkTarget = 65536;
 constexpr uint32_t kDefaultConcurrency = 16;
+// Public BitTorrent DHT routers (reference: config.zig:14-18 and dht.zig:32-36 list them but never
+// bootstrap from them; router.utorrent.com added).
+constexpr const char* kDefaultDhtRouters[] = {"router.bittorrent.com:6881", "dht.transmissionbt.com:6881",
+                                              "router.utorrent.com:6881"};
 
 struct Config {
   std::string home;
@@ -48,6 +53,9 @@ struct Config {
   int connect_timeout_ms = 5000;
   int io_timeout_ms = 30000;
   int discovery_ttl_s = 30;
+  // DHT bootstrap routers used when no --dht-bootstrap is given; ZEST_DHT_BOOTSTRAP="h:p,..."
+  // replaces them ("none" = no default bootstrap).
+  std::vector<std::string> dht_routers;
   // MI355X extensions
   int gpus = 0;             // ZEST_GPUS (0 = CPU verify path)
   double hbm_cache_gb = 0;  // ZEST_HBM_CACHE_GB

@@ -8,6 +8,12 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cstring>
 
 namespace zest::net {
@@ -84,6 +90,50 @@ Addr Addr::resolve(std::string_view host, uint16_t port) {
   if (a.ss.ss_family == AF_INET) reinterpret_cast<sockaddr_in*>(&a.ss)->sin_port = htons(port);
   else reinterpret_cast<sockaddr_in6*>(&a.ss)->sin6_port = htons(port);
   return a;
+}
+
+std::optional<Addr> resolve_with_deadline(const std::string& host_port, uint16_t default_port, int timeout_ms) {
+  if (const char* m = std::getenv("ZEST_DHT_HOSTS")) {
+    const std::string map = m;
+    const std::string host = host_port.substr(0, host_port.rfind(':'));
+    size_t p = 0;
+    while (p <= map.size()) {
+      size_t e = map.find(',', p);
+      if (e == std::string::npos) e = map.size();
+      const std::string item = map.substr(p, e - p);
+      const size_t eq = item.find('=');
+      if (eq != std::string::npos && (item.substr(0, eq) == host || item.substr(0, eq) == host_port)) {
+        try {
+          return Addr::parse(item.substr(eq + 1), default_port);
+        } catch (const Error&) {
+          return std::nullopt;
+        }
+      }
+      p = e + 1;
+    }
+  }
+  struct State {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    std::optional<Addr> addr;
+  };
+  auto st = std::make_shared<State>();
+  // Detached: it owns only `st`, so a resolver that outlives the deadline touches nothing of ours.
+  std::thread([st, host_port, default_port] {
+    std::optional<Addr> a;
+    try {
+      a = Addr::parse(host_port, default_port);
+    } catch (const Error&) {
+    }
+    std::lock_guard<std::mutex> g(st->mu);
+    st->addr = a;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  std::unique_lock<std::mutex> lk(st->mu);
+  st->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return st->done; });
+  return st->done ? st->addr : std::nullopt;
 }
 
 Addr Addr::ipv4(const uint8_t ip[4], uint16_t port) {

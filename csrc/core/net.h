@@ -10,6 +10,7 @@
 #include <sys/uio.h>
 
 #include <cstdint>
+#include <optional>
 #include <string>
 #include <string_view>
 
@@ -35,6 +36,11 @@ struct Addr {
   bool operator==(const Addr& o) const;
   bool operator!=(const Addr& o) const { return !(*this == o); }
 };
+
+// Resolve "host:port" with a deadline: a hosts override (ZEST_DHT_HOSTS="name=ip:port,...", for
+// air-gapped labs and tests) first, then getaddrinfo on a helper thread (getaddrinfo itself has no
+// timeout; an offline resolver can block for many seconds).  nullopt when unresolved in time.
+std::optional<Addr> resolve_with_deadline(const std::string& host_port, uint16_t default_port, int timeout_ms);
 
 class Socket {
  public:

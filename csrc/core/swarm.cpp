@@ -19,7 +19,14 @@ SwarmDownloader::SwarmDownloader(const Config& cfg, std::optional<std::string> t
     dht_ = std::make_unique<dht::Dht>(cfg.dht_port);
     if (!dht_->has_socket()) dht_ = std::make_unique<dht::Dht>(0);  // port taken: ephemeral
     dht_->start();
-    if (!dht_bootstrap.empty()) dht_->bootstrap(dht_bootstrap, 1500);
+    if (!dht_bootstrap.empty()) {
+      dht_->bootstrap(dht_bootstrap, 1500);  // explicit nodes: synchronous, so discovery can use them at once
+    } else if (!cfg.dht_routers.empty()) {
+      // Default public routers: resolved and queried in the background with deadlines, so an
+      // offline machine pays nothing and a pull never waits on DNS (the reference lists these
+      // routers but never bootstraps, leaving its DHT inert: SURVEY §2.A #7).
+      boot_thread_ = std::thread([this] { bootstrap_default(); });
+    }
     aq_thread_ = std::thread([this] { announce_worker(); });
   }
 }
@@ -31,7 +38,26 @@ SwarmDownloader::~SwarmDownloader() {
   }
   aq_cv_.notify_all();
   if (aq_thread_.joinable()) aq_thread_.join();
+  if (boot_thread_.joinable()) boot_thread_.join();
   if (dht_) dht_->stop();
+}
+
+void SwarmDownloader::bootstrap_default() {
+  for (const std::string& r : cfg_.dht_routers) {
+    {
+      std::lock_guard<std::mutex> g(aq_mu_);
+      if (aq_stop_) return;
+    }
+    auto a = net::resolve_with_deadline(r, 6881, 1500);
+    if (!a) {
+      ZTRACE("dht", "bootstrap router " << r << " did not resolve");
+      continue;
+    }
+    const size_t n = dht_->bootstrap({*a}, 1500);
+    ZTRACE("dht", "bootstrap via " << r << " (" << a->str() << "): routing table " << n);
+    if (n >= 8) break;  // enough to start iterative lookups
+  }
+  boot_done_ = true;
 }
 
 void SwarmDownloader::announce_worker() {
@@ -72,6 +98,8 @@ std::vector<net::Addr> SwarmDownloader::discover(const Sha1Digest& ih) {
       return it->second.peers;
   }
   std::lock_guard<std::mutex> dg(disc_mu_);  // one discovery at a time (swarm.zig:320-355)
+  // The first lookup waits (bounded) for the background bootstrap from the default routers.
+  for (int i = 0; dht_ && i < 300 && !bootstrap_done(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   std::vector<net::Addr> peers;
   if (dht_ && dht_->table().size() > 0) {
     stats_.dht_lookups++;

@@ -58,6 +58,8 @@ class SwarmDownloader {
   // Bytes each peer served this session ("addr" -> bytes), for stats / striping checks.
   std::map<std::string, uint64_t> peer_bytes() const;
   dht::Dht* dht() { return dht_.get(); }
+  // The background bootstrap from the default routers finished (or there was none to run).
+  bool bootstrap_done() const { return boot_done_ || !boot_thread_.joinable(); }
 
  private:
   const Config& cfg_;
@@ -89,6 +91,9 @@ class SwarmDownloader {
   // DHT re-announce of xorbs fetched from peers: queued and drained by an owned worker thread
   // (never a detached thread holding `this`).
   void announce_worker();
+  void bootstrap_default();
+  std::thread boot_thread_;
+  std::atomic<bool> boot_done_{false};
   std::mutex aq_mu_;
   std::condition_variable aq_cv_;
   std::vector<Sha1Digest> announce_q_;

@@ -316,6 +316,37 @@ def test_dht_discovery(hub, nodes):
         boot.stop()
 
 
+def test_dht_default_bootstrap_routers(hub, nodes):
+    """No --dht-bootstrap: seeder and leecher bootstrap from the default public routers
+    (router.bittorrent.com, dht.transmissionbt.com, router.utorrent.com).  The resolver is stubbed
+    with ZEST_DHT_HOSTS so "router.bittorrent.com" is a local DHT node; the routing tables fill from
+    it and discovery works end to end (the reference lists those routers but never bootstraps)."""
+    files = sample_files()
+    a, commit = _seed_node(hub, nodes, files)
+    boot = _core.dht.Node(0)
+    try:
+        hosts = {"ZEST_DHT_HOSTS": f"router.bittorrent.com=127.0.0.1:{boot.port}"}
+        assert "ZEST_DHT_BOOTSTRAP" not in a.env
+        seed = a.spawn("seed", "--dht-port", str(a.dht_port), "--listen", str(a.listen_port), env=hosts)
+        info_hashes = [_core.info_hash(_core.from_xet_hex(x.hash_hex)) for x in hub.xorbs]
+        t0 = time.time()
+        while time.time() - t0 < 20 and not all(boot.stored_peers(ih) for ih in info_hashes):
+            time.sleep(0.1)
+        assert all(boot.stored_peers(ih) for ih in info_hashes), "seeder did not bootstrap from the default routers"
+        assert boot.routing_size() >= 1  # the seeder's node is known to the router now
+        b = nodes("leecher")
+        out = b.run("pull", REPO_ID, env=hosts).stdout
+        assert p2p_ratio(out) == 100.0
+        assert_snapshot(b, REPO_ID, commit, files)
+        seed.terminate()
+        seed.wait(timeout=10)
+    finally:
+        boot.stop()
+    # the default list is what the config reports; ZEST_DHT_BOOTSTRAP=none turns it off
+    assert json.loads(_core.config_json())["dht_routers"] == [
+        "router.bittorrent.com:6881", "dht.transmissionbt.com:6881", "router.utorrent.com:6881"]
+
+
 def test_resume_after_failed_term(hub, nodes):
     files = {"model.safetensors": sample_files(big=6_000_000)["model.safetensors"]}
     commit = hub.add_repo(REPO_ID, files, xet_min_size=1)

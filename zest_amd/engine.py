@@ -63,16 +63,38 @@ class RoundWork:
     table_off: int = 0                     # byte offset of the round's chunk records in a host table
 
 
-class OriginStore:
-    """Pinned host memory holding the CDN response bytes for this rank's terms."""
+# Pinned allocations kept for reuse by the next OriginStore of this process (capacity, pointer).
+# Pinning ~141 GB again after freeing it ran the following pull's H2D at 53.1 instead of 56.9 GB/s
+# (bench.py, second data mode; profiles/bench70b_modes_r3.md), so a process that pulls several
+# worlds pins once, sized by `reserve`.
+_PINNED_POOL: list[tuple[int, int]] = []
 
-    def __init__(self, nbytes: int, device: torch.device):
+
+def release_pinned_pool() -> None:
+    """Free the pinned buffers kept by closed OriginStores."""
+    H = ops.hip() if _PINNED_POOL else None
+    while _PINNED_POOL:
+        H.host_free(_PINNED_POOL.pop()[1])
+
+
+class OriginStore:
+    """Pinned host memory holding the CDN response bytes for this rank's terms.  `reserve` (bytes)
+    over-allocates so a later store of another world can reuse the same pinned pages."""
+
+    def __init__(self, nbytes: int, device: torch.device, reserve: int = 0):
         self.n = int(nbytes)
         self.device = device
         if device.type == "cuda":
             self._H = ops.hip()
-            self.ptr = self._H.host_malloc(max(1, self.n))
-            self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.n)).from_address(self.ptr))
+            need = max(1, self.n)
+            hit = next((i for i, (cap, _) in enumerate(_PINNED_POOL) if cap >= need), None)
+            if hit is not None:
+                self.cap, self.ptr = _PINNED_POOL.pop(hit)
+            else:
+                release_pinned_pool()  # too small: give the pages back before pinning more
+                self.cap = max(need, int(reserve))
+                self.ptr = self._H.host_malloc(self.cap)
+            self.array = np.ctypeslib.as_array((ctypes.c_uint8 * need).from_address(self.ptr))
         else:
             self._H = None
             self.array = np.empty(max(1, self.n), dtype=np.uint8)
@@ -80,7 +102,10 @@ class OriginStore:
 
     def close(self):
         if self._H is not None and self.ptr:
-            self._H.host_free(self.ptr)
+            if os.environ.get("ZEST_PIN_POOL", "1") != "0":
+                _PINNED_POOL.append((self.cap, self.ptr))
+            else:
+                self._H.host_free(self.ptr)
             self.ptr = 0
 
     def __del__(self):
@@ -149,7 +174,7 @@ def split_rounds(world: SyntheticWorld, a: int, b: int, weights) -> list[tuple[i
 class DevicePuller:
     def __init__(self, world: SyntheticWorld, arena: torch.Tensor, rank: int = 0, n_ranks: int = 1,
                  round_bytes: int = 1 << 30, slots: int = 3, group=None, exchange: str = "p2p",
-                 seeders: int | None = None):
+                 seeders: int | None = None, origin_reserve: int = 0):
         self.world = world
         self.arena = arena
         self.device = arena.device
@@ -173,7 +198,7 @@ class DevicePuller:
         a_r, b_r = self.rank_terms[rank]
         ser_len = T["ser_len"][a_r:b_r].astype(np.int64)
         self.term_origin_off = np.concatenate([[0], np.cumsum(ser_len)]).astype(np.int64)  # relative to a_r
-        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device)
+        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device, origin_reserve)
         self.rounds: list[RoundWork] = []
         max_span, max_terms, max_chunks = 0, 1, 1
         for k in range(self.n_rounds):
