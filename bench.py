@@ -147,7 +147,7 @@ class Watchdog:
 # ------------------------------------------------------------------------------------------------
 # One rank
 # ------------------------------------------------------------------------------------------------
-def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=None) -> dict:
+def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=None, arenas=None) -> dict:
     """Build the synthetic world of one data mode, pull it a.warmup + a.steps times; returns the
     measured numbers (every rank) plus the puller's exchange choice."""
     import numpy as np
@@ -168,7 +168,14 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
               f"arena {world.arena_bytes / 1e9:.2f} GB; ranks {world_size}")
     contents = None
     if cuda:
-        arena = ops.padded_empty(world.arena_bytes, device)
+        # One arena for every data mode (the layout depends only on the model's files): freeing and
+        # re-allocating 141 GB between modes is avoidable churn in the HBM allocator.
+        if arenas is not None and arenas.get("arena") is not None and arenas["arena"].numel() == world.arena_bytes:
+            arena = arenas["arena"]
+        else:
+            arena = ops.padded_empty(world.arena_bytes, device)
+            if arenas is not None:
+                arenas["arena"] = arena
         world.generate_on_device(arena)
         world.build_on_device(arena)
         torch.cuda.synchronize()
@@ -291,8 +298,6 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     }
     puller.close()
     del puller, arena
-    if cuda:
-        torch.cuda.empty_cache()
     return res
 
 
@@ -345,9 +350,9 @@ def rank_main(a) -> None:
             from zest_amd.parallel import nccl_options
             dist.init_process_group("nccl", device_id=device, pg_options=nccl_options(), timeout=timeout)
     spec = models.get(a.model)
-    results, pick = [], None
+    results, pick, arenas = [], None, {}
     for mode in a.modes:
-        r = run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=pick)
+        r = run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=pick, arenas=arenas)
         pick = r["exchange"] if world_size > 1 else None
         log(rank, f"[{mode}] {r['value']:.3f} GB/s aggregate, {r['step_s'] * 1e3:.1f} ms/step, "
                   f"exchange {r['exchange']}")

@@ -38,13 +38,15 @@ Result measure(const char* name, uint32_t runs, F&& body) {
   r.name = name;
   r.runs = per * batches;
   for (uint32_t i = 0; i < std::min<uint32_t>(per, 64); ++i) keep(body());  // warm caches/tables
-  std::vector<uint64_t> per_run;
+  // Per-batch time per operation, in fractional ns: a frame write takes well under 1 ns, so an
+  // integer division reported it as 0 (round 2).
+  std::vector<double> per_run;
   for (uint32_t b = 0; b < batches; ++b) {
     const uint64_t t0 = now_ns();
     for (uint32_t i = 0; i < per; ++i) r.bytes_processed += body();
     const uint64_t dt = now_ns() - t0;
     r.total_ns += dt;
-    per_run.push_back(dt / per);
+    per_run.push_back(double(dt) / double(per));
   }
   std::nth_element(per_run.begin(), per_run.begin() + per_run.size() / 2, per_run.end());
   r.median_ns = per_run[per_run.size() / 2];
@@ -174,8 +176,8 @@ void write_text(std::ostream& os, const std::vector<Result>& r) {
                 "------------", "------------");
   os << line;
   for (auto& x : r) {
-    std::snprintf(line, sizeof line, "%22s %10u %12llu %12.1f\n", x.name.c_str(), x.runs,
-                  (unsigned long long)x.median_ns, x.throughput_mbps());
+    std::snprintf(line, sizeof line, "%22s %10u %12.2f %12.1f\n", x.name.c_str(), x.runs,
+                  x.median_ns, x.throughput_mbps());
     os << line;
   }
   os << "\n";
@@ -186,8 +188,8 @@ void write_json(std::ostream& os, const std::vector<Result>& r) {
   char buf[256];
   for (size_t i = 0; i < r.size(); ++i) {
     std::snprintf(buf, sizeof buf,
-                  "%s{\"name\":\"%s\",\"runs\":%u,\"median_ns\":%llu,\"throughput_mbps\":%.1f,\"bytes_processed\":%llu}",
-                  i ? "," : "", r[i].name.c_str(), r[i].runs, (unsigned long long)r[i].median_ns,
+                  "%s{\"name\":\"%s\",\"runs\":%u,\"median_ns\":%.3f,\"throughput_mbps\":%.1f,\"bytes_processed\":%llu}",
+                  i ? "," : "", r[i].name.c_str(), r[i].runs, r[i].median_ns,
                   r[i].throughput_mbps(), (unsigned long long)r[i].bytes_processed);
     os << buf;
   }

@@ -18,7 +18,7 @@ namespace zest::bench {
 struct Result {
   std::string name;
   uint32_t runs = 0;
-  uint64_t median_ns = 0;
+  double median_ns = 0;  // per-operation median over batches; fractional for sub-ns operations
   uint64_t total_ns = 0;
   uint64_t bytes_processed = 0;
   double throughput_mbps() const;  // MiB/s

@@ -95,7 +95,8 @@ void ParallelDownloader::release_slot(RunBuffer* b) {
   gate_cv_.notify_one();
 }
 
-FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const std::string& out_path, bool verify) {
+FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const std::string& out_path, bool verify,
+                                                   const std::function<void(uint64_t, Source)>& on_term) {
   const auto t0 = std::chrono::steady_clock::now();
   std::optional<trace::Span> rec_span(std::in_place, "download", "get_reconstruction");
   cas::Reconstruction rec = bridge_.get_reconstruction(hex);
@@ -228,6 +229,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       pwritev_all(fd, iov, off - skip);
     }
     hashes[i] = std::move(hs);
+    if (on_term) on_term(total, f.source);
   };
 
   auto worker = [&]() {

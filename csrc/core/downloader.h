@@ -46,7 +46,9 @@ class ParallelDownloader {
   // concurrently).  Their workers share one gate of `concurrency` term slots, so at most that many
   // terms are in flight in total, and one file's tail (its last few terms) is filled with the next
   // file's terms instead of idle workers.
-  FileResult reconstruct_to_file(const std::string& file_hash_hex, const std::string& out_path, bool verify = true);
+  // `on_term(bytes, source)` (optional) is called as each term lands in the file.
+  FileResult reconstruct_to_file(const std::string& file_hash_hex, const std::string& out_path, bool verify = true,
+                                 const std::function<void(uint64_t, Source)>& on_term = {});
 
  private:
   // One receive buffer per term slot, kept across terms and files: a fetched run (up to a 64 MiB

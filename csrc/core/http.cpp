@@ -464,7 +464,7 @@ void Server::serve(net::Socket s, net::Addr peer) {
   const uint64_t len = r.stream ? r.stream_len : r.body.size();
   std::string head = "HTTP/1.1 " + std::to_string(r.status) + " " + status_text(r.status) + "\r\n";
   head += "Content-Type: " + r.content_type + "\r\n";
-  head += "Content-Length: " + std::to_string(len) + "\r\n";
+  if (!(r.stream && r.stream_len == ServerResponse::kUntilClose)) head += "Content-Length: " + std::to_string(len) + "\r\n";
   for (auto& h : r.extra) head += h.first + ": " + h.second + "\r\n";
   head += "Connection: close\r\n\r\n";
   s.write_all(head.data(), head.size());

@@ -81,8 +81,10 @@ struct ServerResponse {
   std::string body;
   Headers extra;
   // Optional streamed body (e.g. a file range): producer writes to the socket via the callback.
+  // stream_len == kUntilClose: no Content-Length, the body ends when the connection closes (SSE).
   std::function<void(net::Socket&)> stream;
   uint64_t stream_len = 0;
+  static constexpr uint64_t kUntilClose = ~uint64_t(0);
 };
 
 using Handler = std::function<ServerResponse(const Request&)>;

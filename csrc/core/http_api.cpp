@@ -91,6 +91,131 @@ std::string ApiServer::models_json() const {
   return w.out();
 }
 
+std::shared_ptr<PullJob> ApiServer::start_job(const http::Request& r, int* status, std::string* err) {
+  json::Value body;
+  try {
+    body = r.body.empty() ? json::Value() : json::Value::parse(r.body);
+  } catch (const Error&) {
+    *status = 400;
+    *err = "{\"error\":\"invalid json\"}";
+    return nullptr;
+  }
+  auto job = std::make_shared<PullJob>();
+  job->repo = body.str_or("repo", "");
+  job->revision = body.str_or("revision", "main");
+  if (job->repo.empty()) {
+    *status = 400;
+    *err = "{\"error\":\"missing repo\"}";
+    return nullptr;
+  }
+  PullOptions opt;
+  opt.repo_id = job->repo;
+  opt.revision = job->revision;
+  opt.p2p = !(body["no_p2p"].type() == json::Value::Type::Bool && body["no_p2p"].as_bool());
+  opt.autostart_server = false;
+  opt.progress = job->progress;
+  for (auto& pe : body["peers"].array())
+    if (pe.is_string()) opt.peers.push_back(pe.as_string());
+  {
+    std::lock_guard<std::mutex> g(jobs_mu_);
+    job->id = std::to_string(jobs_.size() + 1);
+    jobs_[job->id] = job;
+  }
+  std::lock_guard<std::mutex> g(jobs_mu_);
+  job_threads_.emplace_back([this, job, opt] {
+    job->phase = 1;
+    std::ostringstream out, err;
+    try {
+      Config c = cfg_;
+      PullSummary s = run_pull(c, opt, out, err);
+      {
+        std::lock_guard<std::mutex> jg(job->mu);
+        job->snapshot = s.snapshot_dir;
+        job->stats_json = s.stats_json;
+        if (s.failed_files) job->error = std::to_string(s.failed_files) + " file(s) failed";
+        job->log = out.str() + err.str();
+      }
+      if (registry_) registry_->scan(cfg_);
+      job->phase = s.failed_files ? 3 : 2;
+    } catch (const std::exception& e) {
+      {
+        std::lock_guard<std::mutex> jg(job->mu);
+        job->error = e.what();
+        job->log = out.str() + err.str();
+      }
+      job->phase = 3;
+    }
+  });
+  return job;
+}
+
+http::ServerResponse ApiServer::sse(std::shared_ptr<PullJob> job) {
+  http::ServerResponse resp;
+  resp.content_type = "text/event-stream";
+  resp.extra.emplace_back("Cache-Control", "no-cache");
+  resp.stream_len = http::ServerResponse::kUntilClose;
+  resp.stream = [this, job](net::Socket& s) {
+    auto send = [&](const char* ev, const std::string& data) {
+      const std::string m = std::string("event: ") + ev + "\ndata: " + data + "\n\n";
+      s.write_all(m.data(), m.size());
+    };
+    PullProgress& pr = *job->progress;
+    std::vector<int> seen;
+    uint64_t last_bytes = ~uint64_t(0);
+    try {
+      {
+        json::Writer w;
+        w.obj().key("job").str(job->id).key("repo").str(job->repo).key("revision").str(job->revision).end();
+        send("job", w.out());
+      }
+      while (true) {
+        const int ph = job->phase.load();  // read before the counters: a finished job's are final
+        if (pr.listed.load()) {
+          std::lock_guard<std::mutex> g(pr.mu);
+          seen.resize(pr.files.size(), 0);
+          for (size_t i = 0; i < pr.files.size(); ++i) {
+            const int st = pr.files[i]->state.load();
+            if (st == seen[i]) continue;
+            seen[i] = st;
+            static const char* names[] = {"queued", "running", "done", "failed", "cached"};
+            json::Writer w;
+            w.obj().key("path").str(pr.files[i]->path).key("size").num_u(pr.files[i]->size);
+            w.key("index").num(int64_t(i + 1)).key("total").num(int64_t(pr.files.size()));
+            w.key("state").str(names[st]).end();
+            send("file", w.out());
+          }
+        }
+        const uint64_t b = pr.bytes.load();
+        if (b != last_bytes && pr.listed.load()) {
+          last_bytes = b;
+          json::Writer w;
+          w.obj().key("bytes").num_u(b).key("total").num_u(pr.total.load());
+          w.key("source").str(PullProgress::source_name(pr.last_source.load()));
+          w.key("peers").num_u(pr.peers.load()).key("from_peer").num_u(pr.from_peer.load());
+          w.key("from_cdn").num_u(pr.from_cdn.load()).key("from_cache").num_u(pr.from_cache.load()).end();
+          send("progress", w.out());
+        }
+        if (ph >= 2) {
+          json::Writer w;
+          std::lock_guard<std::mutex> g(job->mu);
+          if (ph == 2) {
+            w.obj().key("path").str(job->snapshot).key("stats").raw(job->stats_json).end();
+            send("complete", w.out());
+          } else {
+            w.obj().key("error").str(job->error).key("path").str(job->snapshot).end();
+            send("error", w.out());
+          }
+          return;
+        }
+        if (stop_.load()) return;
+        std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      }
+    } catch (const Error&) {  // client went away
+    }
+  };
+  return resp;
+}
+
 http::ServerResponse ApiServer::route(const http::Request& r) {
   http::ServerResponse resp;
   const std::string& p = r.path;
@@ -107,47 +232,22 @@ http::ServerResponse ApiServer::route(const http::Request& r) {
   } else if (p == "/v1/config") {
     resp.body = cfg_.to_json();
   } else if (p == "/v1/pull" && r.method == "POST") {
-    json::Value body = r.body.empty() ? json::Value() : json::Value::parse(r.body);
-    auto job = std::make_shared<PullJob>();
-    job->repo = body.str_or("repo", "");
-    job->revision = body.str_or("revision", "main");
-    if (job->repo.empty()) {
-      resp.status = 400;
-      resp.body = "{\"error\":\"missing repo\"}";
+    int status = 200;
+    std::string err;
+    auto job = start_job(r, &status, &err);
+    if (!job) {
+      resp.status = status;
+      resp.body = err;
       return resp;
     }
-    PullOptions opt;
-    opt.repo_id = job->repo;
-    opt.revision = job->revision;
-    opt.p2p = !(body["no_p2p"].type() == json::Value::Type::Bool && body["no_p2p"].as_bool());
-    opt.autostart_server = false;
-    for (auto& pe : body["peers"].array())
-      if (pe.is_string()) opt.peers.push_back(pe.as_string());
-    {
-      std::lock_guard<std::mutex> g(jobs_mu_);
-      job->id = std::to_string(jobs_.size() + 1);
-      jobs_[job->id] = job;
-    }
-    job_threads_.emplace_back([this, job, opt] {
-      job->state = "running";
-      std::ostringstream out, err;
-      try {
-        Config c = cfg_;
-        PullSummary s = run_pull(c, opt, out, err);
-        job->snapshot = s.snapshot_dir;
-        job->stats_json = s.stats_json;
-        job->state = "done";
-        job->progress = 1.0;
-        if (registry_) registry_->scan(cfg_);
-      } catch (const std::exception& e) {
-        job->state = "error";
-        job->error = e.what();
-      }
-      job->log = out.str() + err.str();
-    });
+    auto it = r.query.find("stream");
+    if (r.header("accept").find("text/event-stream") != std::string::npos || (it != r.query.end() && it->second == "1"))
+      return sse(job);
     resp.body = "{\"status\":\"started\",\"job\":\"" + job->id + "\"}";
-  } else if (p.rfind("/v1/pull", 0) == 0) {
-    std::string id = p.size() > 9 ? p.substr(9) : "";
+  } else if (p.rfind("/v1/pull/", 0) == 0) {
+    std::string id = p.substr(9);
+    const bool events = id.size() > 7 && id.compare(id.size() - 7, 7, "/events") == 0;
+    if (events) id.resize(id.size() - 7);
     std::shared_ptr<PullJob> job;
     {
       std::lock_guard<std::mutex> g(jobs_mu_);
@@ -157,11 +257,22 @@ http::ServerResponse ApiServer::route(const http::Request& r) {
     if (!job) {
       resp.status = 404;
       resp.body = "{\"error\":\"no such pull job\"}";
+    } else if (events) {
+      return sse(job);
     } else {
+      const PullProgress& pr = *job->progress;
+      const uint64_t bytes = pr.bytes.load(), total = pr.total.load();
+      const int ph = job->phase.load();
       json::Writer w;
+      std::lock_guard<std::mutex> g(job->mu);
       w.obj().key("job").str(job->id).key("repo").str(job->repo).key("revision").str(job->revision);
-      w.key("state").str(job->state).key("progress").num(job->progress, 2).key("snapshot").str(job->snapshot);
-      w.key("error").str(job->error).key("stats").raw(job->stats_json).key("log").str(job->log).end();
+      w.key("state").str(job->state());
+      w.key("progress").num(ph == 2 ? 1.0 : total ? double(bytes) / double(total) : 0.0, 4);
+      w.key("bytes").num_u(bytes).key("total").num_u(total);
+      w.key("from_peer").num_u(pr.from_peer.load()).key("from_cdn").num_u(pr.from_cdn.load());
+      w.key("from_cache").num_u(pr.from_cache.load()).key("peers").num_u(pr.peers.load());
+      w.key("snapshot").str(job->snapshot).key("error").str(job->error).key("stats").raw(job->stats_json);
+      w.key("log").str(job->log).end();
       resp.body = w.out();
     }
   } else if (p == "/metrics") {

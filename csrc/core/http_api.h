@@ -5,7 +5,9 @@
 // "bt_port"} (:120-136), /v1/stop (:144-149), /v1/pull* (a stub there, :138-142), /v1/models
 // (:152-210), / and /ui dashboard (:212-221, :235-351), 404 {"error":"not found"}.
 // Here /v1/pull really pulls (POST {"repo","revision",...} -> background job, GET /v1/pull/{id}
-// for progress), the server is multi-threaded, xorb counts are live, and /metrics exports
+// for byte progress; with `Accept: text/event-stream` (or ?stream=1) the POST answers with the
+// job's SSE stream as DESIGN.md:317-338 specifies, and GET /v1/pull/{id}/events streams an
+// existing job), the server is multi-threaded, xorb counts are live, and /metrics exports
 // Prometheus counters.  Keys of the reference's status JSON are kept; GPU/seeding fields are added.
 #pragma once
 
@@ -20,15 +22,22 @@
 #include "bt_server.h"
 #include "config.h"
 #include "http.h"
+#include "pull.h"
 #include "storage.h"
 
 namespace zest {
 
 struct PullJob {
-  std::string id, repo, revision, state = "queued", error, snapshot;
-  double progress = 0;
+  std::string id, repo, revision, error, snapshot;
+  std::atomic<int> phase{0};  // 0 queued, 1 running, 2 done, 3 error (strings via state())
   std::string log;
   std::string stats_json = "{}";
+  std::shared_ptr<PullProgress> progress = std::make_shared<PullProgress>();
+  std::mutex mu;  // guards the strings written when the job ends
+  const char* state() const {
+    static const char* names[] = {"queued", "running", "done", "error"};
+    return names[phase.load()];
+  }
 };
 
 class ApiServer {
@@ -45,6 +54,10 @@ class ApiServer {
 
  private:
   http::ServerResponse route(const http::Request& r);
+  // Server-Sent Events of one pull job: `file` (a file started or finished), `progress` (bytes,
+  // total, source, peers; at most every 200 ms while bytes move) and a final `complete` / `error`.
+  http::ServerResponse sse(std::shared_ptr<PullJob> job);
+  std::shared_ptr<PullJob> start_job(const http::Request& r, int* status, std::string* err);
   std::string status_json() const;
   std::string models_json() const;
   Config& cfg_;

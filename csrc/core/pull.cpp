@@ -27,6 +27,30 @@ extern char** environ;
 
 namespace zest {
 
+void PullProgress::add(size_t file, uint64_t n, int source) {
+  if (file < files.size()) {  // a repair refetch re-adds terms: clamp each file at its size
+    File& f = *files[file];
+    uint64_t cur = f.done.load();
+    uint64_t next;
+    do {
+      next = std::min<uint64_t>(f.size ? f.size : cur + n, cur + n);
+    } while (!f.done.compare_exchange_weak(cur, next));
+    bytes += next - cur;
+  } else {
+    bytes += n;
+  }
+  (source == 1 ? from_cache : source == 2 ? from_peer : from_cdn) += n;
+  last_source = source;
+}
+
+const char* PullProgress::source_name(int s) {
+  return s == 1 ? "cache" : s == 2 ? "peer" : s == 3 ? "cdn" : "none";
+}
+
+namespace {
+int source_code(Source s) { return s == Source::Cache || s == Source::Resumed ? 1 : s == Source::Peer ? 2 : 3; }
+}  // namespace
+
 bool server_healthy(uint16_t http_port, int timeout_ms) {
   try {
     http::RequestOptions o;
@@ -88,6 +112,21 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
     if (f.xet_hash) S.xet_files++;
   out << "  " << S.xet_files << " Xet-backed files, " << files.size() << " total files\n";
   S.files = files.size();
+  PullProgress* prog = opt.progress.get();
+  if (prog) {
+    std::lock_guard<std::mutex> g(prog->mu);
+    for (auto& f : files) {
+      auto pf = std::make_unique<PullProgress::File>();
+      pf->path = f.path;
+      pf->size = f.size;
+      prog->total += f.size;
+      prog->files.push_back(std::move(pf));
+    }
+    prog->listed = true;
+  }
+  auto set_state = [&](size_t i, int st) {
+    if (prog && i < prog->files.size()) prog->files[i]->state = st;
+  };
 
   std::vector<net::Addr> boot;
   for (auto& b : opt.dht_bootstrap) {
@@ -149,6 +188,8 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
       if (good) {
         out << " (cached)\n";
         S.cached_files++;
+        set_state(k - 1, 4);
+        if (prog) prog->add(k - 1, f.size, 1);
         continue;
       }
       out << " (cached copy failed verification, downloading again)";
@@ -164,11 +205,16 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
       xet_jobs.push_back({k - 1, dst});
     } else {
       out << " [regular]\n" << std::flush;
+      set_state(k - 1, 1);
       try {
-        S.bytes += hub::download_regular(cfg, opt.repo_id, S.commit == opt.revision ? opt.revision : S.commit, f.path, dst);
+        const uint64_t n = hub::download_regular(cfg, opt.repo_id, S.commit == opt.revision ? opt.revision : S.commit, f.path, dst);
+        S.bytes += n;
+        if (prog) prog->add(k - 1, n, 3);
+        set_state(k - 1, 2);
       } catch (const Error& e) {
         err << "  Error downloading: " << e.what() << "\n";
         file_ok = 0;
+        set_state(k - 1, 3);
         continue;
       }
     }
@@ -191,7 +237,15 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
         const hub::RepoFile& f = files[job.file];
         try {
           trace::Span fs("pull", "xet file");
-          FileResult r = dl.reconstruct_to_file(*f.xet_hash, job.dst, opt.verify);
+          set_state(job.file, 1);
+          std::function<void(uint64_t, Source)> on_term;
+          if (prog)
+            on_term = [prog, &job, &swarm](uint64_t n, Source src) {
+              prog->add(job.file, n, source_code(src));
+              prog->peers = uint32_t(swarm.stats().peers_connected.load());
+            };
+          FileResult r = dl.reconstruct_to_file(*f.xet_hash, job.dst, opt.verify, on_term);
+          set_state(job.file, 2);
           bytes += r.bytes;
           if (r.verified) storage::write_verified_marker(cfg, opt.repo_id, S.commit, f.path, *f.xet_hash, job.dst);
           if (r.resumed_terms) {
@@ -202,6 +256,7 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
           std::lock_guard<std::mutex> g(io_mu);
           err << "  Parallel download error (" << f.path << ": " << e.what() << ")\n";
           ok[job.file] = 0;
+          set_state(job.file, 3);
         }
       }
     };

@@ -7,6 +7,9 @@
 // files must also match their size (a crashed run leaves `.incomplete`, never a final name).
 #pragma once
 
+#include <atomic>
+#include <memory>
+#include <mutex>
 #include <optional>
 #include <ostream>
 #include <string>
@@ -16,6 +19,25 @@
 #include "net.h"
 
 namespace zest {
+
+// Live progress of one pull (read by the REST API's /v1/pull SSE stream while the pull runs).
+struct PullProgress {
+  struct File {
+    std::string path;
+    uint64_t size = 0;
+    std::atomic<uint64_t> done{0};
+    std::atomic<int> state{0};  // 0 queued, 1 running, 2 done, 3 failed, 4 cached
+  };
+  std::atomic<bool> listed{false};
+  std::atomic<uint64_t> bytes{0}, total{0};
+  std::atomic<uint64_t> from_peer{0}, from_cdn{0}, from_cache{0};
+  std::atomic<int> last_source{0};  // 0 none, 1 cache, 2 peer, 3 cdn (source of the latest term)
+  std::atomic<uint32_t> peers{0};
+  std::mutex mu;                     // guards `files` growth (set once after listing)
+  std::vector<std::unique_ptr<File>> files;
+  void add(size_t file, uint64_t n, int source);
+  static const char* source_name(int s);
+};
 
 struct PullOptions {
   std::string repo_id;
@@ -30,6 +52,7 @@ struct PullOptions {
   int concurrency = 0;                      // 0 = cfg.concurrency
   bool autostart_server = true;
   std::vector<std::string> include;         // optional path filters (suffix match)
+  std::shared_ptr<PullProgress> progress;   // optional live progress sink
 };
 
 struct PullSummary {

@@ -405,6 +405,60 @@ def test_http_api_and_pull_job(hub, nodes):
         assert s in out
 
 
+def _read_sse(resp):
+    """Parse a text/event-stream body into [(event, data_dict)] until the server closes it."""
+    events, ev, data = [], None, []
+    for raw in resp:
+        line = raw.decode().rstrip("\n")
+        if line.startswith("event: "):
+            ev = line[7:]
+        elif line.startswith("data: "):
+            data.append(line[6:])
+        elif line == "" and ev is not None:
+            events.append((ev, json.loads("\n".join(data))))
+            ev, data = None, []
+    return events
+
+
+def test_http_pull_sse_progress(hub, nodes):
+    """POST /v1/pull with Accept: text/event-stream answers with the job's SSE stream
+    (reference DESIGN.md:317-338: file / progress / complete events; its code is a stub,
+    http_api.zig:138-142).  A slowed CDN makes the pull long enough to see bytes in flight."""
+    import urllib.request
+    files = {"model.safetensors": sample_files(big=12_000_000)["model.safetensors"],
+             "config.json": b'{"model_type": "llama"}'}
+    commit = hub.add_repo(REPO_ID, files, xet_min_size=1000)
+    hub.xorb_delay_s = 0.15
+    a = nodes("a")
+    a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
+    a.wait_healthy()
+    req = urllib.request.Request(f"http://127.0.0.1:{a.http_port}/v1/pull", method="POST",
+                                 data=json.dumps({"repo": REPO_ID, "no_p2p": True}).encode(),
+                                 headers={"Accept": "text/event-stream"})
+    with urllib.request.urlopen(req, timeout=120) as r:
+        assert r.headers["Content-Type"].startswith("text/event-stream")
+        events = _read_sse(r)
+    kinds = [e for e, _ in events]
+    assert kinds[0] == "job" and kinds[-1] == "complete", kinds
+    fev = [d for e, d in events if e == "file"]
+    assert {d["path"] for d in fev} == set(files) and all(d["total"] == 2 for d in fev)
+    assert {d["state"] for d in fev if d["path"] == "model.safetensors"} >= {"running", "done"}
+    prog = [d for e, d in events if e == "progress"]
+    total = sum(len(v) for v in files.values())
+    assert all(d["total"] == total for d in prog)
+    assert any(0 < d["bytes"] < d["total"] for d in prog), prog
+    assert prog[-1]["bytes"] == total and prog[-1]["source"] in ("cdn", "cache", "peer")
+    assert events[-1][1]["path"].endswith(commit)
+    assert_snapshot(a, REPO_ID, commit, files)
+    # the job endpoint reports byte progress; the events of a finished job replay to the end
+    job = events[0][1]["job"]
+    js = json.loads(a.api(f"/v1/pull/{job}")[1])
+    assert js["state"] == "done" and js["bytes"] == js["total"] == total and js["progress"] == 1.0
+    with urllib.request.urlopen(f"http://127.0.0.1:{a.http_port}/v1/pull/{job}/events", timeout=30) as r:
+        again = _read_sse(r)
+    assert again[-1][0] == "complete"
+
+
 def test_start_stop(nodes):
     a = nodes("a")
     r = a.run("stop", check=False)

@@ -70,8 +70,24 @@ class RoundWork:
 _PINNED_POOL: list[tuple[int, int]] = []
 
 
+# Device staging buffers of closed pullers, reused by the next one (same process, same device).
+_STAGING_POOL: list[torch.Tensor] = []
+
+
+def _staging_take(nbytes: int, device: torch.device) -> torch.Tensor:
+    """A staging buffer of at least nbytes (rounded up to 64 MiB so worlds of nearly equal round
+    sizes share the buffers)."""
+    nbytes = -(-max(1, nbytes) // (64 << 20)) * (64 << 20)
+    if device.type == "cuda":
+        for i, t in enumerate(_STAGING_POOL):
+            if t.device == device and t.numel() >= nbytes:
+                return _STAGING_POOL.pop(i)
+    return ops.padded_empty(nbytes, device)
+
+
 def release_pinned_pool() -> None:
     """Free the pinned buffers kept by closed OriginStores."""
+    _STAGING_POOL.clear()
     H = ops.hip() if _PINNED_POOL else None
     while _PINNED_POOL:
         H.host_free(_PINNED_POOL.pop()[1])
@@ -233,7 +249,7 @@ class DevicePuller:
         # tools/step_times.py), while round k+1's kernels fill the CUs left idle in the tail of
         # round k's decode (a 1 GiB round is ~2 chunks per resident wave).
         self.slots = max(2, slots + (slots & 1))
-        self.staging = [ops.padded_empty(max_span, self.device) for _ in range(min(self.slots, self.n_rounds))]
+        self.staging = [_staging_take(max_span, self.device) for _ in range(min(self.slots, self.n_rounds))]
         self.ws_lanes = [ops.IngestWorkspace(self.device, max_terms, max_chunks) for _ in range(2)]
         self.hashes = torch.zeros((world.n_chunks, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.from_numpy(world.chunk_len.astype(np.int64)).to(self.device)
@@ -793,3 +809,6 @@ class DevicePuller:
 
     def close(self):
         self.origin.close()
+        if self.is_cuda:
+            _STAGING_POOL.extend(self.staging)  # the next puller of this process reuses them
+            self.staging = []

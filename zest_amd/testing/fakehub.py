@@ -107,6 +107,7 @@ class FakeHub:
         self.fail_xorbs: set[str] = set()      # xorb hex -> 500
         self.corrupt_xorbs: set[str] = set()   # xorb hex -> flipped byte in the body
         self.ignore_range = False
+        self.xorb_delay_s = 0.0                # slow CDN: sleep before each xorb response
         self.tracker_peers: dict[bytes, dict[str, float]] = {}
         self._srv: ThreadingHTTPServer | None = None
         self._thr: threading.Thread | None = None
@@ -540,6 +541,8 @@ class FakeHub:
         if hx in self.fail_xorbs:
             self._count("xorb_fail")
             return self._json(h, {"error": "injected failure"}, 500)
+        if self.xorb_delay_s:
+            time.sleep(self.xorb_delay_s)
         data = self.xorbs[idx].data
         if data is None:  # metadata-only world: the bytes live with the peers
             self._count("xorb_missing")
