@@ -1,513 +1,40 @@
-// Device-direct pull: fetch a Xet file's reconstruction terms through the native cache -> P2P ->
-// CDN waterfall into pinned staging buffers and ingest them on the GPU (LZ4/BG4 decode, BLAKE3
-// chunk hashes; the chunk records come from the header index the fetch workers build anyway while
-// validating each run, so the GPU has no header walk to do) straight into a caller-provided HBM
-// buffer, then verify the file's
-// Xet hash with the Merkle kernel.  The host only moves compressed bytes; decompression and
-// verification never touch the CPU (the host pull path, csrc/core/downloader.cpp, does both on
-// the CPU).  North-star path for `zest_amd.pull(..., device=...)`.
-//
-// Pipeline: batches of terms fill one of two pinned buffers (fetch threads that run on across
-// batch boundaries) while the previous batch's H2D + kernels run on a private HIP stream; a buffer
-// is refilled only after its stream event completed.
-#include <hip/hip_runtime.h>
+// pybind11 face of the native device-direct pull (csrc/gpurt/device_pull.{h,cpp}): fetch a Xet
+// file's terms through the cache -> P2P -> CDN waterfall into pinned staging and decode + BLAKE3 +
+// Merkle-verify them on the GPU into caller-provided HBM.  North-star path for
+// `zest_amd.pull(..., device=...)` and the owner fetch of `parallel.swarm_pull`.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <cstring>
-#include <memory>
-#include <mutex>
-#include <string>
-#include <thread>
-#include <vector>
-
-#include "../gpu/zgpu.h"
-#include "bridge.h"
-#include "config.h"
-#include "storage.h"
-#include "swarm.h"
-#include "trace.h"
-#include "xet_hash.h"
-#include "xorb.h"
+#include "../gpurt/device_pull.h"
 
 namespace py = pybind11;
-using namespace zest;
+using zest::gpurt::DeviceXetPull;
+using zest::gpurt::DevicePullOptions;
+using zest::gpurt::PullRequest;
 
 namespace {
 
-void hip_check(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw Error("HipError", std::string(what) + ": " + hipGetErrorString(e));
+py::list pull_files_py(DeviceXetPull& self, const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
+  std::vector<PullRequest> req;
+  for (const auto& f : files) req.push_back({std::get<0>(f), std::get<1>(f), std::get<2>(f)});
+  std::vector<zest::gpurt::PullFileStats> st;
+  {
+    py::gil_scoped_release nogil;  // the fetch may talk to a hub served from this process
+    st = self.pull_files(req);
+  }
+  py::list out;
+  for (auto& s : st) {
+    py::dict d;
+    d["bytes"] = s.bytes;
+    d["terms"] = s.terms;
+    d["chunks"] = s.chunks;
+    d["seconds"] = s.seconds;
+    d["fetched_bytes"] = s.fetched_bytes;
+    d["chunk_lens"] = py::bytes(reinterpret_cast<const char*>(s.chunk_lens.data()), 4 * s.chunk_lens.size());
+    out.append(d);
+  }
+  return out;
 }
-
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  void ensure(size_t count) {
-    if (count <= n) return;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    hip_check(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T) + 4096), "hipMalloc");
-    n = count;
-  }
-};
-
-struct Slot {
-  uint8_t* host = nullptr;  // pinned
-  DevBuf<uint8_t> dev;      // device staging (padded)
-  DevBuf<ZgChunk> chunks_dev;
-  std::vector<ZgChunk> chunks_host;  // chunk records of the batch, built by the fetch workers
-  hipEvent_t done = nullptr;
-};
-
-class DeviceXetPull {
- public:
-  DeviceXetPull(const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
-                std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
-                std::vector<std::string> dht_bootstrap, int device, size_t staging_bytes, int threads)
-      : cfg_(Config::from_env()), device_(device), cap_(staging_bytes), threads_(threads > 0 ? threads : 16) {
-    registry_.scan(cfg_);
-    cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
-    std::vector<net::Addr> boot;
-    for (auto& b : dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
-    swarm_ = std::make_unique<SwarmDownloader>(cfg_, tracker, p2p, dht && p2p, boot);
-    for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
-    bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
-    bridge_->authenticate(repo, repo_type, revision);
-    hip_check(hipSetDevice(device_), "hipSetDevice");
-    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    for (auto& s : slots_) {
-      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cap_ + 4096, hipHostMallocDefault), "hipHostMalloc");
-      s.dev.ensure(cap_);
-      hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
-    }
-    err_.ensure(1);
-  }
-
-  ~DeviceXetPull() {
-    if (stream_) (void)hipStreamSynchronize(stream_);
-    for (auto& s : slots_) {
-      if (s.host) (void)hipHostFree(s.host);
-      if (s.done) (void)hipEventDestroy(s.done);
-    }
-    if (stream_) (void)hipStreamDestroy(stream_);
-  }
-
-  py::dict pull_file(const std::string& hex, uintptr_t dst_ptr, uint64_t dst_size) {
-    py::list r = pull_files({std::make_tuple(hex, dst_ptr, dst_size)});
-    return r[0].cast<py::dict>();
-  }
-
-  // Pull several Xet files (hash, device pointer, size) through ONE pipeline: staging batches
-  // cross file boundaries, so there is no per-file drain; every file's Merkle hash is checked in a
-  // single kernel launch at the end.  Term destinations are device addresses relative to the
-  // lowest destination pointer.
-  //
-  // Peer runs are quarantined in the disk cache until their file verified; a file that fails
-  // (Merkle mismatch, or any device decode error) has its peer runs dropped and its cache runs
-  // evicted, then is pulled once more straight from the CDN with the refetched runs replacing the
-  // cached ones — so one corrupt copy costs one refetch, not a permanently failing pull.
-  py::list pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
-    const auto t0 = std::chrono::steady_clock::now();
-    const size_t nf = files.size();
-    std::vector<cas::Reconstruction> recs(nf);
-    {
-      py::gil_scoped_release nogil;
-      std::vector<std::string> errs(nf);
-      std::atomic<size_t> k{0};
-      auto w = [&]() {
-        for (size_t f; (f = k.fetch_add(1)) < nf;) {
-          try {
-            recs[f] = bridge_->get_reconstruction(std::get<0>(files[f]));
-          } catch (const std::exception& e) {
-            errs[f] = e.what();
-          }
-        }
-      };
-      std::vector<std::thread> ts;
-      for (size_t t = 0; t < std::min<size_t>(nf, 8); ++t) ts.emplace_back(w);
-      for (auto& t : ts) t.join();
-      for (size_t f = 0; f < nf; ++f)
-        if (!errs[f].empty()) throw Error("DownloadFailed", std::get<0>(files[f]) + ": " + errs[f]);
-    }
-    std::vector<size_t> todo(nf);
-    for (size_t f = 0; f < nf; ++f) todo[f] = f;
-    std::vector<std::string> got(nf);
-    uint64_t fetched = 0;
-    for (int attempt = 0; attempt < 2 && !todo.empty(); ++attempt) {
-      FetchOptions opt;
-      opt.repair = attempt > 0;
-      Attempt at = run_once(files, recs, todo, opt);
-      fetched += at.fetched;
-      if (!at.fetch_err.empty()) {
-        settle_all(at, recs, todo, [](size_t) { return false; });
-        throw Error("DownloadFailed", at.fetch_err);
-      }
-      // A file is bad only when its own Merkle root misses: the roots are computed from the bytes
-      // that landed in HBM, so a decode error in one file (the error word is shared by the batch)
-      // cannot pass as good data, and it no longer evicts the cache runs of every other file.
-      std::vector<size_t> bad;
-      for (size_t j = 0; j < todo.size(); ++j) {
-        got[todo[j]] = at.roots[j];
-        if (at.roots[j] != std::get<0>(files[todo[j]])) bad.push_back(j);
-      }
-      settle_all(at, recs, todo, [&](size_t j) { return std::find(bad.begin(), bad.end(), j) == bad.end(); });
-      if (bad.empty()) {
-        todo.clear();
-        break;
-      }
-      if (attempt == 0) bridge_->stats().verify_failures += bad.size();
-      else if (at.ingest_err)
-        throw Error("IngestError", "code " + std::to_string(at.ingest_err >> 32) + " at " +
-                                       std::to_string(at.ingest_err & 0xFFFFFFFFu));
-      std::vector<size_t> again;
-      for (size_t j : bad) again.push_back(todo[j]);
-      if (attempt == 0) bridge_->stats().refetches += again.size();
-      todo = std::move(again);
-    }
-    if (cfg_.cache_max_gb > 0) cache_->trim(uint64_t(cfg_.cache_max_gb * 1e9));  // ZEST_CACHE_MAX_GB
-    for (size_t f : todo)
-      throw Error("HashMismatch", "device bytes hash " + got[f] + " != " + std::get<0>(files[f]));
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    py::list out;
-    for (size_t f = 0; f < nf; ++f) {
-      uint64_t nck = 0;
-      for (auto& t : recs[f].terms) nck += t.range.end - t.range.start;
-      py::dict d;
-      d["bytes"] = std::get<2>(files[f]);
-      d["terms"] = recs[f].terms.size();
-      d["chunks"] = nck;
-      d["seconds"] = secs;
-      d["fetched_bytes"] = fetched;  // for the whole call
-      out.append(d);
-    }
-    return out;
-  }
-
-  std::string stats_json() const { return bridge_->stats_json(); }
-
-  size_t staging_bytes() const { return cap_; }
-
- private:
-  struct TermSource {
-    Source src = Source::Cdn;
-    uint32_t run_offset = 0;
-    std::string pending;  // quarantine file of a peer run (empty: none)
-  };
-  struct Attempt {
-    std::vector<std::string> roots;  // per file of the attempt: Merkle root (Xet hex)
-    std::vector<std::vector<TermSource>> sources;  // per file, per term
-    unsigned long long ingest_err = 0;
-    std::string fetch_err;
-    uint64_t fetched = 0;
-  };
-
-  // Publish (ok) or drop/evict (!ok) the cache runs behind every term of the attempt's files.
-  template <typename OkFn>
-  void settle_all(const Attempt& at, const std::vector<cas::Reconstruction>& recs, const std::vector<size_t>& todo,
-                  OkFn ok) {
-    for (size_t j = 0; j < todo.size(); ++j) {
-      const auto& rec = recs[todo[j]];
-      const bool good = ok(j);
-      for (size_t i = 0; i < at.sources[j].size() && i < rec.terms.size(); ++i) {
-        const TermSource& ts = at.sources[j][i];
-        bridge_->settle(rec.terms[i].hash_hex, ts.src, ts.run_offset, ts.pending, good);
-      }
-    }
-  }
-
-  // One pass over files[todo]: fetch (+ chunk records) -> staging -> H2D -> place/hash -> Merkle roots.
-  Attempt run_once(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& all_files,
-                   const std::vector<cas::Reconstruction>& all_recs, const std::vector<size_t>& todo,
-                   const FetchOptions& opt) {
-    const size_t nf = todo.size();
-    Attempt at;
-    at.sources.resize(nf);
-    // Global term list in file order; chunk indices are global (one hash array for all files).
-    struct GTerm {
-      size_t file, term;
-      uint64_t dst;    // device address offset from `base`
-      uint64_t chunk;  // global index of the term's first chunk
-      uint32_t nchunks;
-      uint64_t ulen;
-    };
-    std::vector<GTerm> gt;
-    std::vector<uint64_t> file_chunk0(nf + 1, 0);
-    uintptr_t base = UINTPTR_MAX, top_addr = 0;
-    for (size_t f = 0; f < nf; ++f) {
-      const auto& fl = all_files[todo[f]];
-      base = std::min(base, std::get<1>(fl));
-      top_addr = std::max<uintptr_t>(top_addr, std::get<1>(fl) + std::get<2>(fl));
-    }
-    for (size_t f = 0; f < nf; ++f) {
-      const auto& fl = all_files[todo[f]];
-      const auto& rec = all_recs[todo[f]];
-      if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
-      at.sources[f].resize(rec.terms.size());
-      uint64_t off = 0, c = file_chunk0[f];
-      for (size_t i = 0; i < rec.terms.size(); ++i) {
-        const auto& t = rec.terms[i];
-        const uint32_t n = uint32_t(t.range.end - t.range.start);
-        gt.push_back({f, i, std::get<1>(fl) - base + off, c, n, t.unpacked_length});
-        off += t.unpacked_length;
-        c += n;
-      }
-      if (off != std::get<2>(fl)) throw Error("SizeMismatch", std::get<0>(fl) + " is " + std::to_string(off) + " bytes");
-      file_chunk0[f + 1] = c;
-    }
-    const uint64_t nck = file_chunk0[nf];
-    const size_t n = gt.size();
-    hashes_.ensure(nck ? nck * 32 : 32);
-    sizes_.ensure(nck ? nck : 1);
-    uint8_t* dst = reinterpret_cast<uint8_t*>(base);
-    const uint64_t dst_size = nf ? uint64_t(top_addr - base) : 0;
-    hip_check(hipMemsetAsync(err_.p, 0, sizeof(unsigned long long), stream_), "hipMemset");
-    std::string& fetch_err = at.fetch_err;
-    {
-      py::gil_scoped_release nogil;
-      // Batches: consecutive terms whose fetched-size bounds fit one staging slot, so every term
-      // has a reserved region of the pinned buffer (no refetch, no second copy pass: workers
-      // receive / copy their run straight into place).  Batch b fills slot b % 2.
-      uint64_t max_bound = 0;
-      for (size_t i = 0; i < n; ++i) max_bound = std::max(max_bound, term_bound(gt[i].ulen, gt[i].nchunks));
-      if (max_bound > cap_) grow_staging(max_bound);  // one huge term: enlarge both slots
-      struct Batch {
-        size_t begin = 0, end = 0;
-        std::vector<uint64_t> off, len, src_at;  // per term: region, fetched bytes, run start
-      };
-      std::vector<Batch> batches;
-      std::vector<uint32_t> batch_of(n);
-      for (size_t next = 0; next < n;) {
-        Batch bt;
-        bt.begin = next;
-        uint64_t pos = 0;
-        size_t end = next;
-        while (end < n) {
-          const uint64_t bound = term_bound(gt[end].ulen, gt[end].nchunks);
-          if (pos + bound > cap_ && end > next) break;
-          bt.off.push_back(pos);
-          pos += bound;
-          batch_of[end++] = uint32_t(batches.size());
-        }
-        bt.end = end;
-        bt.len.assign(end - next, 0);
-        bt.src_at.assign(end - next, 0);
-        batches.push_back(std::move(bt));
-        next = end;
-      }
-      const size_t nb = batches.size();
-      auto chunk_lo = [&](size_t b) { return gt[batches[b].begin].chunk; };
-      auto chunk_hi = [&](size_t b) { return batches[b].end < n ? gt[batches[b].end].chunk : nck; };
-      // Continuous pipeline: the fetch workers take terms in order across batch boundaries, so the
-      // next batch's terms are already in flight while the current batch's slowest transfers finish
-      // (a per-batch join left the connections ~45 % idle: tools/direct_bench.py under ZEST_TRACE).
-      // A worker may fill slot b % 2 for batch b once ready[b % 2] >= b, i.e. once the GPU work of
-      // batch b - 2 on that slot has completed; the submitting thread (this one) waits for each
-      // batch's last term, queues its H2D + kernels, and frees the slot when they are done.
-      std::mutex mu;
-      std::condition_variable cv;
-      size_t ready[2] = {0, 1};
-      std::vector<size_t> remaining(nb);
-      for (size_t b = 0; b < nb; ++b) remaining[b] = batches[b].end - batches[b].begin;
-      bool abort = false;
-      for (size_t b = 0; b < std::min<size_t>(2, nb); ++b)
-        slots_[b].chunks_host.assign(size_t(chunk_hi(b) - chunk_lo(b)), ZgChunk{});
-      std::atomic<size_t> k{0};
-      auto fail = [&](const std::string& what) {
-        std::lock_guard<std::mutex> g(mu);
-        if (fetch_err.empty()) fetch_err = what;
-        abort = true;
-        cv.notify_all();
-      };
-      auto worker = [&]() {
-        while (true) {
-          const size_t i = k.fetch_add(1);
-          if (i >= n) return;
-          const size_t b = batch_of[i];
-          Batch& bt = batches[b];
-          Slot& s = slots_[b & 1];
-          {
-            std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return abort || ready[b & 1] >= b; });
-            if (abort) return;
-          }
-          const size_t j = i - bt.begin;
-          try {
-            const auto& rec = all_recs[todo[gt[i].file]];
-            // The run is received straight into this term's region of the pinned buffer when it
-            // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
-            uint8_t* region = s.host + bt.off[j];
-            const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
-            auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-            XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
-            at.sources[gt[i].file][gt[i].term] = TermSource{r.source, r.run_offset, r.pending};
-            auto idx = xet::index_chunks(r.bytes(), r.size());
-            if (r.local_end > idx.size() || r.local_start >= r.local_end)
-              throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
-            const uint64_t a = idx[r.local_start].header_off;
-            const uint64_t e_end = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
-            if (r.ext) {
-              bt.src_at[j] = bt.off[j] + a;  // already in place
-            } else {
-              if (e_end - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
-              std::memcpy(region, r.data.data() + a, e_end - a);
-              bt.src_at[j] = bt.off[j];
-            }
-            bt.len[j] = e_end - a;
-            // the device records of this term's chunks; a term that does not match its plan keeps
-            // zero (no-op) records, so its file fails the Merkle check and takes the repair path
-            ZgChunk* cr = s.chunks_host.data() + (gt[i].chunk - chunk_lo(b));
-            const uint64_t run0 = bt.src_at[j];
-            uint64_t uoff = 0;
-            bool ok = r.local_end - r.local_start == gt[i].nchunks;
-            for (uint32_t c = r.local_start; ok && c < r.local_end; ++c) {
-              const xet::ChunkEntry& e = idx[c];
-              const uint32_t sc = uint32_t(e.scheme);
-              if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
-                ok = false;
-                break;
-              }
-              cr[c - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
-                                               e.clen, e.ulen, sc, uint32_t(j)};
-              uoff += e.ulen;
-            }
-            if (!ok || uoff != gt[i].ulen) std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
-          } catch (const std::exception& e) {
-            fail(e.what());
-            return;
-          }
-          std::lock_guard<std::mutex> g(mu);
-          if (--remaining[b] == 0) cv.notify_all();
-        }
-      };
-      std::vector<std::thread> ts;
-      const int nt = int(std::min<size_t>(size_t(threads_), n));
-      for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
-      try {
-        for (size_t b = 0; b < nb; ++b) {
-          {
-            trace::Span sp("device", "wait fetch batch");
-            std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return abort || remaining[b] == 0; });
-            if (abort) break;
-          }
-          const Batch& bt = batches[b];
-          Slot& s = slots_[b & 1];
-          uint64_t top = 0;
-          for (size_t j = 0; j < bt.len.size(); ++j) {
-            at.fetched += bt.len[j];
-            top = std::max<uint64_t>(top, bt.src_at[j] + bt.len[j]);
-          }
-          const uint64_t c0 = chunk_lo(b);
-          const int nchunks = int(chunk_hi(b) - c0);
-          s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
-          trace::Span submit_span("device", "H2D + place/hash");
-          submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
-          hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
-          if (nchunks)
-            hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
-                                     hipMemcpyHostToDevice, stream_),
-                      "H2D chunk records");
-          hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
-                                    stream_),
-                    "place");
-          uint64_t ubytes = 0;
-          for (size_t i = bt.begin; i < bt.end; ++i) ubytes += gt[i].ulen;
-          const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
-          hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
-          hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
-                                   hash_scratch_.p, hs_bytes, stream_),
-                    "hash");
-          hip_check(hipEventRecord(s.done, stream_), "event");
-          // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
-          hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
-          if (b + 2 < nb) s.chunks_host.assign(size_t(chunk_hi(b + 2) - chunk_lo(b + 2)), ZgChunk{});
-          std::lock_guard<std::mutex> g(mu);
-          ready[b & 1] = b + 2;
-          cv.notify_all();
-        }
-      } catch (const std::exception& e) {
-        fail(e.what());
-        for (auto& t : ts) t.join();
-        (void)hipStreamSynchronize(stream_);
-        throw;
-      }
-      for (auto& t : ts) t.join();
-      hip_check(hipStreamSynchronize(stream_), "sync");
-    }
-    if (!fetch_err.empty()) return at;
-    hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
-    // Merkle roots of every file in one launch
-    trace::Span merkle_span("device", "merkle verify");
-    std::vector<ZgMerkleJob> jobs(nf);
-    uint64_t max_leaves = 1;
-    for (size_t f = 0; f < nf; ++f) {
-      jobs[f] = ZgMerkleJob{file_chunk0[f], file_chunk0[f + 1] - file_chunk0[f], 1, 0};
-      max_leaves = std::max<uint64_t>(max_leaves, jobs[f].n_leaves);
-    }
-    std::vector<uint8_t> roots(32 * std::max<size_t>(nf, 1));
-    if (nf) {
-      merkle_job_.ensure(nf);
-      hip_check(hipMemcpyAsync(merkle_job_.p, jobs.data(), sizeof(ZgMerkleJob) * nf, hipMemcpyHostToDevice, stream_),
-                "job H2D");
-      const size_t sb = zg_merkle_scratch_bytes(max_leaves, int(nf));
-      merkle_scratch_.ensure(sb);
-      root_.ensure(32 * nf);
-      hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, int(nf), root_.p, merkle_scratch_.p, sb, stream_),
-                "merkle");
-      hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
-      hip_check(hipStreamSynchronize(stream_), "sync");
-    }
-    for (size_t f = 0; f < nf; ++f) {
-      xet::Hash h;
-      std::memcpy(h.data(), roots.data() + 32 * f, 32);
-      at.roots.push_back(xet::to_hex(h));
-    }
-    return at;
-  }
-
-  // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does
-  // not help, so the payload is <= its unpacked size plus LZ4 frame overhead; + 8-byte headers.
-  static uint64_t term_bound(uint64_t unpacked, uint64_t nchunks) {
-    return unpacked + unpacked / 128 + 80 * nchunks + 4096;
-  }
-
-  void grow_staging(uint64_t bytes) {
-    hip_check(hipStreamSynchronize(stream_), "sync");  // no copy still reads the old buffers
-    for (auto& s : slots_) {
-      if (s.host) (void)hipHostFree(s.host);
-      s.host = nullptr;
-      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), bytes + 4096, hipHostMallocDefault), "hipHostMalloc");
-      s.dev.ensure(bytes);
-    }
-    cap_ = bytes;
-  }
-
-  Config cfg_;
-  int device_;
-  size_t cap_;
-  int threads_;
-  storage::XorbRegistry registry_;
-  std::unique_ptr<storage::XorbCache> cache_;
-  std::unique_ptr<SwarmDownloader> swarm_;
-  std::unique_ptr<XetBridge> bridge_;
-  hipStream_t stream_ = nullptr;
-  Slot slots_[2];
-  DevBuf<unsigned long long> err_;
-  DevBuf<uint8_t> hashes_;
-  DevBuf<uint64_t> sizes_;
-  DevBuf<ZgMerkleJob> merkle_job_;
-  DevBuf<uint8_t> merkle_scratch_;
-  DevBuf<uint8_t> hash_scratch_;
-  DevBuf<uint8_t> root_;
-};
 
 }  // namespace
 
@@ -516,18 +43,34 @@ void bind_hip_pull(py::module_& m) {
       .def(py::init([](const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
                        std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
                        std::vector<std::string> boot, int device, size_t staging, int threads) {
+             DevicePullOptions o;
+             o.repo = repo;
+             o.revision = revision;
+             o.repo_type = repo_type;
+             o.p2p = p2p;
+             o.peers = std::move(peers);
+             o.tracker = std::move(tracker);
+             o.dht = dht;
+             o.dht_bootstrap = std::move(boot);
+             o.device = device;
+             o.staging_bytes = staging;
+             o.threads = threads;
              // Authentication talks HTTP: release the GIL (the hub may be served from this process).
              py::gil_scoped_release nogil;
-             return new DeviceXetPull(repo, revision, repo_type, p2p, std::move(peers), std::move(tracker), dht,
-                                      std::move(boot), device, staging, threads);
+             return new DeviceXetPull(o);
            }),
            py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model", py::arg("p2p") = true,
            py::arg("peers") = std::vector<std::string>{}, py::arg("tracker") = std::nullopt, py::arg("dht") = true,
            py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("device") = 0,
            py::arg("staging_bytes") = size_t(1) << 30, py::arg("threads") = 16)
-      .def("pull_file", &DeviceXetPull::pull_file, py::arg("xet_hash"), py::arg("dst_ptr"), py::arg("dst_size"))
-      .def("pull_files", &DeviceXetPull::pull_files, py::arg("files"),
-           "[(xet_hash, dst_ptr, size), ...] through one pipeline; returns one stats dict per file")
+      .def("pull_file",
+           [](DeviceXetPull& self, const std::string& hex, uintptr_t dst, uint64_t size) {
+             return pull_files_py(self, {std::make_tuple(hex, dst, size)})[0].cast<py::dict>();
+           },
+           py::arg("xet_hash"), py::arg("dst_ptr"), py::arg("dst_size"))
+      .def("pull_files", &pull_files_py, py::arg("files"),
+           "[(xet_hash, dst_ptr, size), ...] through one pipeline; returns one stats dict per file "
+           "(chunk_lens: uint32 chunk sizes in file order)")
       .def("stats_json", &DeviceXetPull::stats_json)
       .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

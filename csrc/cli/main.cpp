@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <iomanip>
 
 #include <algorithm>
 #include <atomic>
@@ -30,6 +31,7 @@
 #include "dht.h"
 #include "http.h"
 #include "http_api.h"
+#include "hub.h"
 #include "json.h"
 #include "pull.h"
 #include "storage.h"
@@ -154,53 +156,92 @@ std::vector<xet::Hash> cached_xorb_hashes(const Config& cfg) {
 
 int cmd_pull(const std::string& exe, const std::vector<std::string>& a);
 
-// One attempt of `zest pull --gpus N`: `python -m torch.distributed.run --nproc-per-node N -m
-// zest_amd.multigpu <args>` as a child process of this CLI (one worker per GPU; N = 1 runs
-// `python -m zest_amd.multigpu` directly).  Rank 0 writes
-// `status_path` once the whole job ran to the end (every rank alive through the final all-reduce).
-int spawn_gpu_workers(const std::vector<std::string>& pass, int gpus, int attempt, const std::string& status_path) {
+// One attempt of `zest pull --gpus N`: N independent worker processes, worker r pinned to
+// devices[r] through HIP_VISIBLE_DEVICES.  Files are independent, so there is no rendezvous, no
+// torchrun agent and no RCCL communicator: each worker takes its LPT share of the Xet files
+// (ZEST_GPU_RANK / ZEST_GPU_WORLD) and writes `{status_base}.{r}` when it ran to the end.  The
+// worker is the native `zest-gpu-worker` next to this binary (no Python start-up on the path);
+// ZEST_GPU_WORKER_MODULE substitutes `python -m <module>` (tests use a stub).
+struct WorkerResult {
+  int rc = 0;
+  bool complete = false;
+  json::Value status;
+};
+
+std::vector<WorkerResult> spawn_gpu_workers(const std::string& exe, const std::vector<std::string>& pass,
+                                            const std::vector<std::string>& devices, const std::string& status_base) {
   const char* py = std::getenv("ZEST_PYTHON");
-  const char* mod = std::getenv("ZEST_GPU_WORKER_MODULE");  // tests substitute a stub worker
-  const std::string module = mod && *mod ? mod : "zest_amd.multigpu";
-  std::vector<std::string> args = {py ? py : "python3", "-m"};
-  if (gpus == 1) {
-    // One GPU needs no rendezvous: run the worker itself (no torchrun agent process and no RCCL
-    // communicator to start; `zest pull --gpus 1` of Llama-3.1-8B spent ~9 s of 13 before its worker
-    // began, profiles/gpu_cli_pull_r2.md).
-    args.push_back(module);
-  } else {
-    for (const std::string& s : {std::string("torch.distributed.run"), std::string("--nnodes"), std::string("1"),
-                                 std::string("--nproc-per-node"), std::to_string(gpus), std::string("--master-addr"),
-                                 std::string("127.0.0.1"), std::string("--master-port"),
-                                 std::to_string(29400 + (::getpid() * 7 + attempt * 131) % 2000), std::string("-m"),
-                                 module})
-      args.push_back(s);
+  const char* mod = std::getenv("ZEST_GPU_WORKER_MODULE");
+  const std::string native = exe.substr(0, exe.rfind('/') + 1) + "zest-gpu-worker";
+  std::vector<std::string> base;
+  if (mod && *mod) base = {py ? py : "python3", "-m", mod};
+  else if (::access(native.c_str(), X_OK) == 0) base = {native};
+  else base = {py ? py : "python3", "-m", "zest_amd.multigpu"};
+  std::string all;
+  for (size_t i = 0; i < devices.size(); ++i) all += (i ? "," : "") + devices[i];
+  const int n = int(devices.size());
+  std::vector<pid_t> pids(static_cast<size_t>(n), 0);
+  std::vector<WorkerResult> out(static_cast<size_t>(n));
+  for (int r = 0; r < n; ++r) {
+    std::vector<std::string> args = base;
+    args.insert(args.end(), pass.begin(), pass.end());
+    std::vector<std::string> env_s;
+    for (char** e = environ; *e; ++e) {
+      const std::string kv = *e;
+      const std::string k = kv.substr(0, kv.find('='));
+      if (k == "HIP_VISIBLE_DEVICES" || k == "ZEST_GPU_RANK" || k == "ZEST_GPU_WORLD" || k == "ZEST_GPU_STATUS" ||
+          k == "ZEST_GPU_DEVICES" || k == "RANK" || k == "WORLD_SIZE" || k == "LOCAL_RANK")
+        continue;
+      env_s.push_back(kv);
+    }
+    const std::string st = status_base + "." + std::to_string(r);
+    ::unlink(st.c_str());
+    env_s.push_back("HIP_VISIBLE_DEVICES=" + devices[size_t(r)]);
+    env_s.push_back("ZEST_GPU_RANK=" + std::to_string(r));
+    env_s.push_back("ZEST_GPU_WORLD=" + std::to_string(n));
+    env_s.push_back("ZEST_GPU_STATUS=" + st);
+    env_s.push_back("ZEST_GPU_DEVICES=" + all);
+    std::vector<char*> argv, envp;
+    for (auto& x : args) argv.push_back(const_cast<char*>(x.c_str()));
+    argv.push_back(nullptr);
+    for (auto& x : env_s) envp.push_back(const_cast<char*>(x.c_str()));
+    envp.push_back(nullptr);
+    if (posix_spawnp(&pids[size_t(r)], argv[0], nullptr, nullptr, argv.data(), envp.data()) != 0) {
+      std::cerr << "Error: cannot start " << argv[0] << " for --gpus\n";
+      pids[size_t(r)] = 0;
+      out[size_t(r)].rc = 127;
+    }
   }
-  args.insert(args.end(), pass.begin(), pass.end());
-  ::setenv("ZEST_GPU_STATUS", status_path.c_str(), 1);
-  std::vector<char*> argv;
-  for (auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
-  argv.push_back(nullptr);
-  pid_t pid = 0;
-  if (posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) {
-    std::cerr << "Error: cannot start " << argv[0] << " for --gpus\n";
-    return 127;
+  for (int r = 0; r < n; ++r) {
+    if (!pids[size_t(r)]) continue;
+    int status = 0;
+    while (::waitpid(pids[size_t(r)], &status, 0) < 0 && errno == EINTR) {
+    }
+    out[size_t(r)].rc = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+    const std::string st = status_base + "." + std::to_string(r);
+    if (auto b = storage::read_file(st)) {
+      try {
+        out[size_t(r)].status = json::Value::parse(std::string(b->begin(), b->end()));
+        out[size_t(r)].complete = out[size_t(r)].status["complete"].type() == json::Value::Type::Bool &&
+                                  out[size_t(r)].status["complete"].as_bool();
+      } catch (const Error&) {
+      }
+    }
+    ::unlink(st.c_str());
   }
-  int status = 0;
-  while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
-  }
-  return WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+  return out;
 }
 
-// `zest pull <repo> --gpus N`: N GPU decode/verify workers, elastic over worker loss.  An attempt
-// that dies before the end (a worker crashed, a device or the RCCL communicator failed; torchrun then
-// stops the other ranks) is retried on one GPU fewer.  Files verified by earlier attempts stay on disk
-// and are skipped, so each retry pulls only what is missing; after the single-GPU attempt the host
-// pipeline finishes the job (ZEST_GPU_HOST_FALLBACK=0 turns that off).  An attempt that ran to the end
-// but failed files (rank 0 wrote its status) is final: fewer GPUs would not fix the data.  SURVEY
-// §5.3 ("elastic world size 8 -> 7"); the reference has no GPU path and no retry (main.zig:233-256).
+// `zest pull <repo> --gpus N`: N GPU decode/verify workers, elastic over worker loss.  While the
+// workers pull the Xet files, this process fetches the regular files (config, tokenizer) on the
+// host.  An attempt in which a worker dies before the end (crash, lost device) is retried on one GPU
+// fewer -- the failed devices are dropped first -- and files verified by earlier attempts are
+// skipped, so each retry pulls only what is missing; after the single-GPU attempt the host pipeline
+// finishes the job (ZEST_GPU_HOST_FALLBACK=0 turns that off).  An attempt whose workers all ran to
+// the end but failed files is final: fewer GPUs would not fix the data.  SURVEY §5.3 ("elastic world
+// size 8 -> 7"); the reference has no GPU path and no retry (main.zig:233-256).
 int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int gpus, const std::vector<int>& devices) {
-  // exe = <pkg>/_bin/zest -> PYTHONPATH = parent of the package directory
+  // exe = <pkg>/_bin/zest -> PYTHONPATH = parent of the package directory (Python workers)
   std::string pkg_parent = exe;
   for (int i = 0; i < 3; ++i) {
     const size_t s = pkg_parent.rfind('/');
@@ -210,38 +251,131 @@ int pull_on_gpus(const std::string& exe, const std::vector<std::string>& a, int 
   if (const char* old = std::getenv("PYTHONPATH")) pp += std::string(":") + old;
   ::setenv("PYTHONPATH", pp.c_str(), 1);
   std::vector<std::string> pass;
+  std::string repo, revision = "main", repo_type = "model";
+  bool p2p = true;
   for (size_t i = 0; i < a.size(); ++i) {
     if (a[i] == "--gpus") {
       ++i;
       continue;
     }
+    if ((a[i] == "--revision" || a[i] == "-r") && i + 1 < a.size()) revision = a[i + 1];
+    if (a[i] == "--repo-type" && i + 1 < a.size()) repo_type = a[i + 1];
+    if (a[i] == "--no-p2p") p2p = false;
+    if (repo.empty() && !a[i].empty() && a[i][0] != '-' && (i == 0 || a[i - 1].rfind("-", 0) != 0)) repo = a[i];
     pass.push_back(a[i]);
   }
+  if (repo.empty()) {
+    std::cerr << "Error: missing repository ID\n";
+    return 1;
+  }
+  // Device list: --gpus 0,2,5; else the first N of an inherited HIP_VISIBLE_DEVICES; else 0..N-1.
+  std::vector<std::string> devs;
+  if (!devices.empty()) {
+    for (int d : devices) devs.push_back(std::to_string(d));
+  } else {
+    std::vector<std::string> vis;
+    if (const char* v = std::getenv("HIP_VISIBLE_DEVICES")) {
+      std::string s = v;
+      for (size_t p = 0; p <= s.size();) {
+        size_t e = s.find(',', p);
+        if (e == std::string::npos) e = s.size();
+        if (e > p) vis.push_back(s.substr(p, e - p));
+        p = e + 1;
+      }
+    }
+    for (int i = 0; i < gpus; ++i) devs.push_back(size_t(i) < vis.size() ? vis[size_t(i)] : std::to_string(i));
+  }
+  Config cfg = Config::from_env();
+  std::cout << "zest pull " << repo << " (revision: " << revision << ") on " << devs.size() << " GPU(s)\n" << std::flush;
+  // Regular files on the host, concurrently with the GPU workers.
+  std::string commit = revision, snap;
+  size_t regular_failed = 0, regular_files = 0;
+  std::thread host_files([&] {
+    try {
+      auto files = hub::list_files(cfg, repo, revision, repo_type);
+      commit = hub::resolve_commit(cfg, repo, revision, repo_type).value_or(revision);
+      snap = cfg.snapshot_dir(repo, commit);
+      for (auto& f : files) {
+        if (f.xet_hash) continue;
+        ++regular_files;
+        const std::string dst = snap + "/" + f.path;
+        if (storage::exists(dst) && storage::file_size(dst) == f.size) continue;
+        try {
+          hub::download_regular(cfg, repo, commit, f.path, dst);
+        } catch (const Error& e) {
+          std::cerr << "  Error downloading " << f.path << ": " << e.what() << "\n";
+          ++regular_failed;
+        }
+      }
+    } catch (const Error& e) {
+      std::cerr << "  Error listing " << repo << ": " << e.what() << "\n";
+      ++regular_failed;
+    }
+  });
   const char* tmp = std::getenv("TMPDIR");
   const std::string status = std::string(tmp && *tmp ? tmp : "/tmp") + "/zest-gpu-pull-" + std::to_string(::getpid()) +
                              ".json";
+  const auto t0 = std::chrono::steady_clock::now();
   int rc = 1;
-  for (int n = gpus, attempt = 0; n >= 1; --n, ++attempt) {
-    if (!devices.empty()) {  // an explicit device list: the first n of it (retries drop the last)
-      std::string vis;
-      for (int i = 0; i < n; ++i) vis += (i ? "," : "") + std::to_string(devices[size_t(i)]);
-      ::setenv("HIP_VISIBLE_DEVICES", vis.c_str(), 1);
+  bool finished = false;
+  std::vector<WorkerResult> res;
+  while (!devs.empty()) {
+    res = spawn_gpu_workers(exe, pass, devs, status);
+    std::vector<std::string> alive, dead;
+    for (size_t r = 0; r < res.size(); ++r) (res[r].complete ? alive : dead).push_back(devs[r]);
+    if (dead.empty()) {
+      finished = true;
+      rc = 0;
+      for (auto& w : res)
+        if (w.rc != 0) rc = w.rc;
+      break;
     }
-    ::unlink(status.c_str());
-    rc = spawn_gpu_workers(pass, n, attempt, status);
-    const bool finished = ::access(status.c_str(), F_OK) == 0;
-    ::unlink(status.c_str());
-    if (rc == 0) return 0;
-    if (finished) return rc;
-    std::cerr << "zest: GPU pull on " << n << " GPU(s) stopped before the end (exit " << rc << ")";
+    const size_t n = devs.size();
+    std::cerr << "zest: GPU pull on " << n << " GPU(s) stopped before the end (" << dead.size() << " worker(s) lost";
+    for (auto& w : res)
+      if (!w.complete) std::cerr << ", exit " << w.rc;
+    std::cerr << ")";
     if (n > 1) std::cerr << "; retrying on " << n - 1 << " GPU(s), keeping verified files";
     std::cerr << "\n";
+    devs = alive;
+    devs.insert(devs.end(), dead.begin(), dead.end());
+    devs.resize(n - 1);
   }
-  const char* fb = std::getenv("ZEST_GPU_HOST_FALLBACK");
-  if (fb && std::string(fb) == "0") return rc;
-  std::cerr << "zest: finishing the pull on the host\n";
-  ::unsetenv("ZEST_GPUS");  // the host pass must not start GPU workers again
-  return cmd_pull(exe, pass);
+  host_files.join();
+  if (!finished) {
+    const char* fb = std::getenv("ZEST_GPU_HOST_FALLBACK");
+    if (fb && std::string(fb) == "0") return rc;
+    std::cerr << "zest: finishing the pull on the host\n";
+    ::unsetenv("ZEST_GPUS");  // the host pass must not start GPU workers again
+    return cmd_pull(exe, pass);
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t bytes = 0, failed = regular_failed, peer = 0, cdn = 0, cache = 0;
+  for (auto& w : res) {
+    bytes += uint64_t(w.status["bytes"].as_double());
+    failed += uint64_t(w.status["failed_files"].as_double());
+    const json::Value& st = w.status["stats"];
+    peer += uint64_t(st["bytes_from_peer"].as_double());
+    cdn += uint64_t(st["bytes_from_cdn"].as_double());
+    cache += uint64_t(st["bytes_from_cache"].as_double());
+  }
+  if (!failed) {
+    try {
+      storage::write_ref(cfg, repo, revision, commit);
+    } catch (const Error& e) {
+      std::cerr << "Warning: failed to write ref: " << e.what() << "\n";
+    }
+  }
+  const uint64_t src = peer + cdn + cache;
+  std::cout << std::fixed << std::setprecision(1);
+  std::cout << "\nXorb fetch stats:\n  From peers:   " << peer / 1e6 << " MB\n  From CDN:     " << cdn / 1e6
+            << " MB\n  From cache:   " << cache / 1e6 << " MB\n  P2P ratio:    "
+            << (src ? 100.0 * double(peer) / double(src) : 0.0) << "%\n";
+  std::cout << std::setprecision(2) << "\n" << bytes / 1e9 << " GB verified on " << res.size() << " GPU(s) in " << dt
+            << "s (" << (dt > 0 ? bytes / dt / 1e9 : 0.0) << " GB/s)\n";
+  std::cout << "\nDone! Model available at:\n  " << snap << "\n" << std::flush;
+  if (failed) std::cerr << "zest: " << failed << " file(s) failed\n";
+  return failed ? 1 : rc;
 }
 
 // `--gpus` value: a count ("4") or a device list ("0,2,5", also "3," for the single device 3).

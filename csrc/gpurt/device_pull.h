@@ -1,0 +1,64 @@
+// Device-direct Xet pull (native GPU runtime, no Python): fetch a file's reconstruction terms through
+// the cache -> P2P -> CDN waterfall into pinned staging, then decode (LZ4/BG4), BLAKE3-hash and
+// Merkle-verify them on the GPU straight into a caller-provided HBM buffer.  Used by the pybind
+// module (`_hip.DeviceXetPull`, zest_amd.direct / swarm_pull) and by the native per-GPU worker of
+// `zest pull --gpus N` (csrc/gpurt/gpu_worker.cpp).
+//
+// Reference: the host equivalent is xet_bridge.zig:149-264 + parallel_download.zig:91-204 (fetch,
+// then XorbReader.extractChunkRange on the CPU); here the CPU only moves compressed bytes.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <string>
+#include <vector>
+
+namespace zest::gpurt {
+
+struct DevicePullOptions {
+  std::string repo;
+  std::string revision = "main";
+  std::string repo_type = "model";
+  bool p2p = true;
+  std::vector<std::string> peers;
+  std::optional<std::string> tracker;
+  bool dht = true;
+  std::vector<std::string> dht_bootstrap;
+  int device = 0;
+  size_t staging_bytes = size_t(1) << 30;  // per pinned slot (two slots)
+  int threads = 16;                        // fetch workers
+};
+
+struct PullRequest {
+  std::string xet_hash;  // Xet file hash (hex)
+  uintptr_t dst = 0;     // device pointer
+  uint64_t size = 0;     // file size (bytes)
+};
+
+struct PullFileStats {
+  uint64_t bytes = 0, terms = 0, chunks = 0;
+  double seconds = 0;          // whole call
+  uint64_t fetched_bytes = 0;  // whole call (compressed bytes moved)
+  std::vector<uint32_t> chunk_lens;  // uncompressed size of every chunk, in file order
+};
+
+class DeviceXetPull {
+ public:
+  explicit DeviceXetPull(const DevicePullOptions& opt);
+  ~DeviceXetPull();
+  DeviceXetPull(const DeviceXetPull&) = delete;
+  DeviceXetPull& operator=(const DeviceXetPull&) = delete;
+  // Pull several files through ONE pipeline (staging batches cross file boundaries; one Merkle
+  // launch verifies all of them).  Throws zest::Error ("HashMismatch", "DownloadFailed", ...) when a
+  // file cannot be verified after its CDN repair pass.
+  std::vector<PullFileStats> pull_files(const std::vector<PullRequest>& files);
+  std::string stats_json() const;
+  size_t staging_bytes() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+}  // namespace zest::gpurt

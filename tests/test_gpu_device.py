@@ -3,6 +3,7 @@ compared against the host (C++) Xet implementation, which is itself pinned to hf
 from __future__ import annotations
 
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -155,21 +156,32 @@ def test_cli_bench_gpu(tmp_path):
         assert row["median_ns"] > 0 and row["throughput_mbps"] > 0
 
 
-def test_cli_pull_gpus(tmp_path):
-    """`zest pull <repo> --gpus 1`: CLI spawns a torchrun GPU worker that decodes + verifies every Xet
-    file on the GPU and writes the HF snapshot (single-command multi-GPU UX)."""
+@pytest.mark.parametrize("worker,gpus", [("native", "1"), ("python", "1"), ("native", "0,0")])
+def test_cli_pull_gpus(tmp_path, worker, gpus):
+    """`zest pull <repo> --gpus N`: the CLI starts one worker per device (the native
+    zest-gpu-worker, or the Python fallback) that decodes + verifies its Xet files on the GPU and
+    writes them into the HF snapshot, while the CLI fetches the regular files.  `0,0` runs two
+    workers on the one GPU of the test box (LPT split of the files, two status files)."""
     from e2e_util import Node, assert_snapshot, sample_files
 
     hub = FakeHub(policy="auto", max_xorb_bytes=1 << 20)
     hub.start()
     try:
         files = sample_files(seed=6)
+        files["model-00002.safetensors"] = sample_files(seed=7, big=2_000_000)["model.safetensors"]
         commit = hub.add_repo("org/gpus", files, xet_min_size=100_000)
         n = Node(hub, tmp_path, "a")
-        r = n.run("pull", "org/gpus", "--gpus", "1", "--no-p2p", timeout=300)
-        assert "verified on 1 GPU(s)" in r.stdout and "Done! Model available at:" in r.stdout
+        env = {"ZEST_GPU_WORKER_MODULE": "zest_amd.multigpu", "ZEST_PYTHON": sys.executable} if worker == "python" else {}
+        r = n.run("pull", "org/gpus", "--gpus", gpus, "--no-p2p", timeout=300, env=env)
+        n_gpus = len(gpus.split(","))
+        assert f"verified on {n_gpus} GPU(s)" in r.stdout and "Done! Model available at:" in r.stdout, r.stdout + r.stderr
+        if worker == "native":
+            assert "[xet]" in r.stdout and "verified on the GPU" in r.stdout
         assert_snapshot(n, "org/gpus", commit, files)
         assert (n.root / "hf/hub/models--org--gpus/refs/main").read_text().strip() == commit
+        # a second pull finds every Xet file verified in the cache
+        r = n.run("pull", "org/gpus", "--gpus", gpus, "--no-p2p", timeout=300, env=env)
+        assert r.stdout.count("(cached)") >= 2, r.stdout
         n.close()
     finally:
         hub.stop()

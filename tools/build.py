@@ -143,10 +143,19 @@ def build(only: str | None = None, jobs: int | None = None, debug: bool = False,
         gpu_objs = b.compile(gpu_srcs, "gpu", hip=True)
         hbind = b.compile(sorted((CSRC / "bind").glob("hip_*.cpp")), "hbind", hip=True,
                           extra=[f"-I{_pybind_include()}", f"-I{_py_include()}", "-fvisibility=hidden"])
+        # native GPU runtime (device-direct pull): shared by the pybind module and the worker binary
+        rt_srcs = sorted(p for p in (CSRC / "gpurt").glob("*.cpp") if p.name != "gpu_worker.cpp")
+        rt_objs = b.compile(rt_srcs, "gpurt", hip=True)
+        hip_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"] + ssl_libs
         out = PKG / f"_hip{EXT}"
-        b.link(gpu_objs + hbind + core_objs, out, shared=True,
-               libs=[f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"] + ssl_libs, hip=True)
+        b.link(gpu_objs + rt_objs + hbind + core_objs, out, shared=True, libs=hip_libs, hip=True)
         built["hip"] = out
+        worker = CSRC / "gpurt" / "gpu_worker.cpp"
+        if worker.exists():  # `zest pull --gpus N` worker: one process per GPU, no Python on its path
+            w_objs = b.compile([worker], "gpurt", hip=True)
+            out = PKG / "_bin" / "zest-gpu-worker"
+            b.link(w_objs + rt_objs + gpu_objs + core_objs, out, shared=False, libs=hip_libs, hip=True)
+            built["gpu_worker"] = out
     if only in (None, "cli"):
         cli_srcs = sorted((CSRC / "cli").glob("*.cpp"))
         if cli_srcs:

@@ -85,6 +85,22 @@ def _staging_take(nbytes: int, device: torch.device) -> torch.Tensor:
     return ops.padded_empty(nbytes, device)
 
 
+# The puller's streams, created once per process and role.  torch hands out streams from a
+# round-robin pool and HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 here); a
+# second DevicePuller in the same process drew other pool streams, its two compute lanes shared a
+# queue, and its pull ran at 52.9 instead of 56.9 GB/s (bf16 -> random in one bench run; 47.6
+# instead of 64.3 the other way round; profiles/bench70b_modes_r3.md).  Reusing the first puller's
+# streams keeps the lane/copy layout that was measured.
+_STREAMS: dict = {}
+
+
+def _role_stream(device: torch.device, role: str, priority: int = 0):
+    key = (device.index, role)
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(device, priority=priority)
+    return _STREAMS[key]
+
+
 def release_pinned_pool() -> None:
     """Free the pinned buffers kept by closed OriginStores."""
     _STAGING_POOL.clear()
@@ -273,8 +289,9 @@ class DevicePuller:
                 hi = int(torch.cuda.Stream.priority_range()[1])  # (least, greatest); lower = more urgent
             except Exception:
                 hi = -1
-            self.lane_stream = torch.cuda.Stream(self.device, priority=hi)
-            self.side_stream = torch.cuda.Stream(self.device, priority=hi)
+            self.lane_stream = _role_stream(self.device, "lane", hi)
+            self.side_stream = _role_stream(self.device, "side", hi)
+            copy_stream = _role_stream(self.device, "copy", hi)  # created in a fixed order for every world
             # Pipeline shape.  "lanes": each round's H2D copy rides its compute lane (above; best when
             # the kernels are short next to the copy: raw chunks, 56.9 vs 56.2 GB/s).  "copy": one
             # copy stream issues every round's H2D back to back, gated only by slot-free events, so
@@ -287,7 +304,7 @@ class DevicePuller:
             if self.pipeline not in ("lanes", "copy"):
                 raise ValueError(f"ZEST_PIPELINE={self.pipeline!r}: expected 'lanes' or 'copy'")
             if self.pipeline == "copy":
-                self.copy_stream = torch.cuda.Stream(self.device, priority=hi)
+                self.copy_stream = copy_stream
                 self.h2d_done = [torch.cuda.Event() for _ in self.staging]
                 self.slot_free = [torch.cuda.Event() for _ in self.staging]
         # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
@@ -329,7 +346,7 @@ class DevicePuller:
         if self.is_cuda and n_ranks > 1:
             self.chunk_off_dev = torch.from_numpy(world.chunk_off.astype(np.int64)).to(self.device)
             self.chunk_len_dev = torch.from_numpy(world.chunk_len.astype(np.int32)).to(self.device)
-            self.verify_stream = torch.cuda.Stream(self.device)
+            self.verify_stream = _role_stream(self.device, "verify")
             self._verify_scratch = ops.HashScratch(self.device)
             self._chunk_len_csum = np.concatenate([[0], np.cumsum(world.chunk_len, dtype=np.int64)])
         self.bytes_received = sum(hi - lo for k in range(self.n_rounds) for r, (lo, hi) in
@@ -472,7 +489,7 @@ class DevicePuller:
                                  for _ in range(2)]
             self._gather_used = [False, False]
             if self.is_cuda:
-                self._unpack_stream = torch.cuda.Stream(self.device)
+                self._unpack_stream = _role_stream(self.device, "unpack")
                 self._unpacked = [torch.cuda.Event() for _ in range(2)]
         b = k % 2
         buf = self._gather_bufs[b][: self.n_ranks * slab]
@@ -543,7 +560,7 @@ class DevicePuller:
         if not int(flag.item()):
             return False
         self._peer_arenas = peers
-        self._ipc_streams = [torch.cuda.Stream(self.device) for _ in range(min(self.n_ranks - 1, 4))]
+        self._ipc_streams = [_role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
         self._ipc_done = {}
         return True
 

@@ -1,11 +1,18 @@
-"""`zest pull <repo> --gpus N`: pull a repository with N GPUs as decode/verify engines.
+"""Python GPU pull worker: pull a repository's Xet files with one GPU as decode/verify engine.
 
-Launched by the CLI as `python -m torch.distributed.run --nproc-per-node N -m zest_amd.multigpu ...`
-(N = 1: `python -m zest_amd.multigpu ...`, no rendezvous; one process per GPU, SURVEY §7.3 item 6: single-command UX over per-rank workers).  Xet files are
-assigned to ranks by size (LPT); each rank fetches its files' compressed runs through the native
-cache -> P2P -> CDN waterfall, decodes and verifies them on its own GPU (`_hip.DeviceXetPull`) and
-writes them into the HF-cache snapshot (file i's write overlaps file i + 1's pull); rank 0 fetches
-the regular files and writes the ref.
+`zest pull <repo> --gpus N` runs the native worker (`zest_amd/_bin/zest-gpu-worker`,
+csrc/gpurt/gpu_worker.cpp) when it is built; this module is the fallback and the library form.
+Two launch shapes:
+
+* independent (what the CLI does): one process per device, ZEST_GPU_RANK / ZEST_GPU_WORLD /
+  ZEST_GPU_STATUS set, HIP_VISIBLE_DEVICES pinned; no process group -- files are independent, and
+  each worker writes its own status JSON; the CLI fetches the regular files and writes the ref.
+* torchrun (`python -m torch.distributed.run --nproc-per-node N -m zest_amd.multigpu ...`): ranks
+  all-reduce their byte counts and rank 0 fetches the regular files and writes the ref.
+
+Xet files are assigned by size (LPT); each worker fetches its files' compressed runs through the
+native cache -> P2P -> CDN waterfall, decodes and verifies them on its GPU (`_hip.DeviceXetPull`)
+and writes them into the HF-cache snapshot (file i's write overlaps file i + 1's pull).
 """
 from __future__ import annotations
 
@@ -95,8 +102,13 @@ def main(argv=None) -> int:
                     help="pinned staging ring per GPU worker, MB (network -> staging -> HBM)")
     # the reference ignores unknown flags (main.zig:98-119); so do the GPU workers
     a, _unknown = ap.parse_known_args(argv)
-    rank, world, local, dev = init_from_env()
-    if world == 1 and "RANK" not in os.environ:  # started directly by the CLI for one GPU (no torchrun)
+    independent = "ZEST_GPU_RANK" in os.environ and "RANK" not in os.environ
+    if independent:  # one worker per device, started by the CLI; no process group
+        rank, world = int(os.environ["ZEST_GPU_RANK"]), int(os.environ.get("ZEST_GPU_WORLD", "1"))
+        dev = torch.device("cuda", 0)
+    else:
+        rank, world, local, dev = init_from_env()
+    if independent or (world == 1 and "RANK" not in os.environ):
         torch.cuda.set_device(dev)
         bind_local_numa(dev)
     t0 = time.time()
@@ -177,10 +189,20 @@ def main(argv=None) -> int:
         stats = json.loads(dp.stats_json())
     else:
         stats = {}
-    if rank == 0 and regular:
+    if rank == 0 and regular and not independent:  # independent workers: the CLI fetches these
         r = _core.pull(a.repo, a.revision, p2p, a.peer, a.tracker, not a.no_dht, a.dht_bootstrap, regular, True, 0,
                        a.repo_type)
         failed += r["failed_files"]
+    if independent:
+        dt = time.time() - t0
+        status = os.environ.get("ZEST_GPU_STATUS")
+        if status:
+            with open(status, "w") as fh:
+                json.dump({"complete": True, "rank": rank, "world": world, "failed_files": failed, "bytes": done_bytes,
+                           "seconds": round(dt, 3), "stats": stats}, fh)
+        print(f"[gpu {rank}] {done_bytes / 1e9:.2f} GB in {dt:.1f}s (worker start {startup:.1f}s, device pulls "
+              f"{t_pull:.1f}s, writes {t_write:.1f}s overlapped)", flush=True)
+        return 1 if failed else 0
     if rank == 0:
         _core.write_ref(a.repo, a.revision, commit, a.repo_type)
     tot = torch.tensor([float(done_bytes), float(failed), float(stats.get("bytes_from_peer", 0)),
