@@ -8,6 +8,9 @@
 #include <memory>
 #include <sstream>
 
+#include "swarm.h"
+#include "bridge.h"
+#include "downloader.h"
 #include "bench.h"
 #include "bencode.h"
 #include "bind_extra.h"
@@ -145,6 +148,56 @@ struct PySeeder {
 };
 
 }  // namespace
+
+// In-memory host fetch of Xet files (see HostXetFetcher binding below).
+class HostXetFetcher {
+ public:
+  HostXetFetcher(const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
+                 std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
+                 std::vector<std::string> boot, int concurrency)
+      : cfg_(Config::from_env()) {
+    registry_.scan(cfg_);
+    cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
+    std::vector<net::Addr> b;
+    for (auto& x : boot) b.push_back(net::Addr::parse(x, 6881));
+    swarm_ = std::make_unique<SwarmDownloader>(cfg_, std::move(tracker), p2p, dht && p2p, b);
+    for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
+    bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
+    bridge_->authenticate(repo, repo_type, revision);
+    dl_ = std::make_unique<ParallelDownloader>(*bridge_, concurrency > 0 ? concurrency : int(cfg_.concurrency));
+  }
+  std::vector<FileResult> fetch(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
+    std::vector<FileResult> out(files.size());
+    std::vector<std::string> errs(files.size());
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < files.size();) {
+        try {
+          out[i] = dl_->reconstruct_to_memory(std::get<0>(files[i]), reinterpret_cast<uint8_t*>(std::get<1>(files[i])),
+                                              std::get<2>(files[i]), true);
+        } catch (const std::exception& e) {
+          errs[i] = e.what();
+        }
+      }
+    };
+    std::vector<std::thread> ts;
+    for (size_t t = 1; t < std::min<size_t>(4, files.size()); ++t) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+    for (size_t i = 0; i < files.size(); ++i)
+      if (!errs[i].empty()) throw Error("DownloadFailed", std::get<0>(files[i]) + ": " + errs[i]);
+    return out;
+  }
+  std::string stats_json() const { return bridge_->stats_json(); }
+
+ private:
+  Config cfg_;
+  storage::XorbRegistry registry_;
+  std::unique_ptr<storage::XorbCache> cache_;
+  std::unique_ptr<SwarmDownloader> swarm_;
+  std::unique_ptr<XetBridge> bridge_;
+  std::unique_ptr<ParallelDownloader> dl_;
+};
 
 void bind_extra(py::module_& m) {
   // ---------------- bencode ----------------
@@ -542,6 +595,43 @@ void bind_extra(py::module_& m) {
         }
         return py::make_tuple(total, failed);
       }, py::arg("hashes"), py::arg("starts"), py::arg("ends"), py::arg("timeout_ms") = 60000);
+
+  // ---------------- in-memory Xet fetch (host waterfall, no snapshot) ----------------
+  // The host twin of _hip.DeviceXetPull: Xet files reconstructed through the cache -> P2P -> CDN
+  // waterfall and verified against their file hash, written into caller memory (e.g. a CPU tensor)
+  // instead of the HF cache.  Kept alive across calls so peer connections and the CAS session carry
+  // over (swarm_pull rounds on CPU process groups).
+  py::class_<HostXetFetcher>(m, "HostXetFetcher")
+      .def(py::init([](const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
+                       std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
+                       std::vector<std::string> boot, int concurrency) {
+             py::gil_scoped_release nogil;
+             return new HostXetFetcher(repo, revision, repo_type, p2p, std::move(peers), std::move(tracker), dht,
+                                       std::move(boot), concurrency);
+           }),
+           py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model", py::arg("p2p") = true,
+           py::arg("peers") = std::vector<std::string>{}, py::arg("tracker") = std::nullopt, py::arg("dht") = true,
+           py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("concurrency") = 0)
+      .def("fetch_files",
+           [](HostXetFetcher& self, const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
+             std::vector<FileResult> rs;
+             {
+               py::gil_scoped_release nogil;
+               rs = self.fetch(files);
+             }
+             py::list out;
+             for (auto& r : rs) {
+               py::dict d;
+               d["bytes"] = r.bytes;
+               d["terms"] = r.terms;
+               d["seconds"] = r.seconds;
+               d["chunk_lens"] = py::bytes(reinterpret_cast<const char*>(r.chunk_lens.data()), 4 * r.chunk_lens.size());
+               out.append(d);
+             }
+             return out;
+           },
+           py::arg("files"), "[(xet_hash, ptr, size), ...] -> one dict per file (chunk_lens: uint32 sizes)")
+      .def("stats_json", &HostXetFetcher::stats_json);
 
   // ---------------- pull ----------------
   m.def("pull", [](std::string repo, std::string revision, bool p2p, std::vector<std::string> peers,

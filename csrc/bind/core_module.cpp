@@ -1,4 +1,6 @@
 // pybind11 bindings for the zest host core (`zest_amd._core`).
+#include <thread>
+#include <atomic>
 #include <pybind11/pybind11.h>
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
@@ -172,6 +174,41 @@ PYBIND11_MODULE(_core, m) {
         leaves.push_back({xet::chunk_hash(s.data + prev, e - prev), e - prev});
         prev = e;
       }
+      h = xet::file_hash(leaves);
+    }
+    return to_bytes(h);
+  });
+
+  // Xet file hash with the chunk boundaries given (uint32 chunk sizes, e.g. the ones the owner of a
+  // swarm piece parsed from the xorb headers): chunk hashes + Merkle + salt, no CDC pass.  Wrong
+  // boundaries give a different hash, so they need no trust.
+  m.def("xet_file_hash_lens", [](py::buffer b, py::buffer lens_b) {
+    ByteSpan s = span_of(b);
+    ByteSpan lb = span_of(lens_b);
+    if (lb.size % 4) throw Error("InvalidArgument", "chunk lens must be uint32");
+    const size_t n = lb.size / 4;
+    std::vector<uint32_t> lens(n);
+    std::memcpy(lens.data(), lb.data, lb.size);
+    uint64_t total = 0;
+    for (uint32_t l : lens) total += l;
+    if (total != s.size) return py::bytes();  // boundaries do not cover the buffer: no hash
+    xet::Hash h;
+    {
+      py::gil_scoped_release nogil;
+      std::vector<xet::HashSize> leaves(n);
+      std::vector<uint64_t> off(n + 1, 0);
+      for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + lens[i];
+      std::atomic<size_t> next{0};
+      auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(64)) < n;)
+          for (size_t j = i; j < std::min(n, i + 64); ++j)
+            leaves[j] = {xet::chunk_hash(s.data + off[j], lens[j]), lens[j]};
+      };
+      std::vector<std::thread> ts;
+      const size_t nt = std::min<size_t>(8, std::max<size_t>(1, n / 64));
+      for (size_t t = 1; t < nt; ++t) ts.emplace_back(work);
+      work();
+      for (auto& t : ts) t.join();
       h = xet::file_hash(leaves);
     }
     return to_bytes(h);

@@ -97,6 +97,19 @@ void ParallelDownloader::release_slot(RunBuffer* b) {
 
 FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const std::string& out_path, bool verify,
                                                    const std::function<void(uint64_t, Source)>& on_term) {
+  return reconstruct(hex, out_path, nullptr, 0, verify, on_term);
+}
+
+FileResult ParallelDownloader::reconstruct_to_memory(const std::string& hex, uint8_t* dst, uint64_t cap, bool verify,
+                                                     const std::function<void(uint64_t, Source)>& on_term) {
+  if (!dst && cap) throw Error("InvalidArgument", "null destination");
+  return reconstruct(hex, std::string(), dst, cap, verify, on_term);
+}
+
+FileResult ParallelDownloader::reconstruct(const std::string& hex, const std::string& out_path, uint8_t* mem,
+                                           uint64_t mem_cap, bool verify,
+                                           const std::function<void(uint64_t, Source)>& on_term) {
+  const bool to_mem = out_path.empty();
   const auto t0 = std::chrono::steady_clock::now();
   std::optional<trace::Span> rec_span(std::in_place, "download", "get_reconstruction");
   cas::Reconstruction rec = bridge_.get_reconstruction(hex);
@@ -106,10 +119,11 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   for (size_t i = 0; i < n; ++i) offs[i + 1] = offs[i] + rec.terms[i].unpacked_length;
   const uint64_t skip = rec.offset_into_first_range;
   const uint64_t total = offs[n] - skip;
+  if (to_mem && total > mem_cap) throw Error("SizeMismatch", "file " + hex + " is larger than its buffer");
   const size_t slash = out_path.rfind('/');
-  if (slash != std::string::npos) storage::ensure_dir(out_path.substr(0, slash));
-  const std::string tmp = out_path + ".incomplete";
-  const std::string side = out_path + ".zest-resume";
+  if (!to_mem && slash != std::string::npos) storage::ensure_dir(out_path.substr(0, slash));
+  const std::string tmp = to_mem ? std::string() : out_path + ".incomplete";
+  const std::string side = to_mem ? std::string() : out_path + ".zest-resume";
 
   std::vector<std::vector<xet::HashSize>> hashes(n);
   std::vector<uint8_t> done(n, 0);
@@ -120,7 +134,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   std::vector<std::string> pending(n);  // quarantine file of a peer run, until settled
   size_t resumed = 0;
   // ---- resume from sidecar
-  if (storage::exists(tmp) && storage::exists(side)) {
+  if (!to_mem && storage::exists(tmp) && storage::exists(side)) {
     if (auto b = storage::read_file(side); b && b->size() >= 4 + 64 + 4 && std::memcmp(b->data(), kResumeMagic, 4) == 0 &&
                                          std::string(reinterpret_cast<char*>(b->data()) + 4, 64) == hex &&
                                          load_le32(b->data() + 68) == n) {
@@ -141,16 +155,19 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       }
     }
   }
-  if (!resumed) storage::remove_file(side);
-  int fd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
-  if (fd < 0) throw Error("IoError", tmp + ": " + std::strerror(errno));
-  if (::ftruncate(fd, off_t(total)) != 0) {
-    ::close(fd);
-    throw Error("IoError", "ftruncate");
-  }
+  if (!resumed && !to_mem) storage::remove_file(side);
+  int fd = -1;
   Sidecar sc;
-  const bool fresh = !storage::exists(side);
-  sc.fd = ::open(side.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+  if (!to_mem) {
+    fd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+    if (fd < 0) throw Error("IoError", tmp + ": " + std::strerror(errno));
+    if (::ftruncate(fd, off_t(total)) != 0) {
+      ::close(fd);
+      throw Error("IoError", "ftruncate");
+    }
+  }
+  const bool fresh = !to_mem && !storage::exists(side);
+  if (!to_mem) sc.fd = ::open(side.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
   if (sc.fd >= 0 && fresh) {
     Bytes h(72);
     std::memcpy(h.data(), kResumeMagic, 4);
@@ -224,7 +241,15 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       }
       off = skip;
     }
-    {
+    if (to_mem) {
+      trace::Span sp("download", "copy");
+      uint64_t o = off - skip;
+      for (const iovec& v : iov) {
+        if (o + v.iov_len > mem_cap) throw Error("SizeMismatch", "term past the end of the buffer");
+        std::memcpy(mem + o, v.iov_base, v.iov_len);
+        o += v.iov_len;
+      }
+    } else {
       trace::Span sp("download", "pwrite");
       pwritev_all(fd, iov, off - skip);
     }
@@ -264,8 +289,12 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
   std::vector<std::thread> ts;
   for (int k = 0; k < nthreads; ++k) ts.emplace_back(worker);
   for (auto& t : ts) t.join();
+  auto close_fd = [&] {
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+  };
   if (failed) {
-    ::close(fd);
+    close_fd();
     for (size_t i = 0; i < n; ++i)
       if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], false);
     throw Error("DownloadFailed", first_err);
@@ -294,7 +323,7 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
           bridge_.stats().refetches++;
         }
       } catch (...) {  // the CDN failed too: keep the sidecar (resumed terms are re-checked next run)
-        ::close(fd);
+        close_fd();
         for (size_t i = 0; i < n; ++i)
           if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], false);
         throw;
@@ -303,19 +332,24 @@ FileResult ParallelDownloader::reconstruct_to_file(const std::string& hex, const
       ok = file_hash_now() == hex;
     }
     if (!ok) {
-      ::close(fd);
-      storage::remove_file(side);
+      close_fd();
+      if (!to_mem) storage::remove_file(side);
       throw Error("HashMismatch", "file " + hex);
     }
   }
   // The file checked out (or the caller skipped verification): publish the quarantined peer runs.
   for (size_t i = 0; i < n; ++i)
     if (!pending[i].empty()) bridge_.settle(rec.terms[i].hash_hex, src[i], run_off[i], pending[i], true);
-  ::fdatasync(fd);
-  ::close(fd);
-  if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);
-  storage::remove_file(side);
   FileResult r;
+  if (to_mem) {
+    for (auto& h : hashes)
+      for (auto& x : h) r.chunk_lens.push_back(uint32_t(x.size));
+  } else {
+    ::fdatasync(fd);
+    close_fd();
+    if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);
+    storage::remove_file(side);
+  }
   r.bytes = total;
   r.terms = n;
   r.resumed_terms = resumed;

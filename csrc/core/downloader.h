@@ -31,6 +31,7 @@ struct FileResult {
   size_t resumed_terms = 0;
   bool verified = false;
   double seconds = 0;
+  std::vector<uint32_t> chunk_lens;  // uncompressed chunk sizes in file order (memory targets)
 };
 
 class ParallelDownloader {
@@ -49,8 +50,14 @@ class ParallelDownloader {
   // `on_term(bytes, source)` (optional) is called as each term lands in the file.
   FileResult reconstruct_to_file(const std::string& file_hash_hex, const std::string& out_path, bool verify = true,
                                  const std::function<void(uint64_t, Source)>& on_term = {});
+  // Same waterfall + verification into caller memory (`cap` >= the file size); no file, no resume
+  // sidecar.  FileResult::chunk_lens carries the chunk boundaries (e.g. for a swarm receiver).
+  FileResult reconstruct_to_memory(const std::string& file_hash_hex, uint8_t* dst, uint64_t cap, bool verify = true,
+                                   const std::function<void(uint64_t, Source)>& on_term = {});
 
  private:
+  FileResult reconstruct(const std::string& hex, const std::string& out_path, uint8_t* mem, uint64_t mem_cap,
+                         bool verify, const std::function<void(uint64_t, Source)>& on_term);
   // One receive buffer per term slot, kept across terms and files: a fetched run (up to a 64 MiB
   // xorb) lands in memory whose pages were faulted in once, instead of a fresh mmap'd allocation
   // per term whose every page faults and is zeroed on first touch.

@@ -139,3 +139,68 @@ def test_swarm_pull_from_another_node(hub_env, tmp_path):
         assert st["bytes_served"] > 0
     finally:
         b.close()
+
+
+def _api_worker(rank, world_size, port, repo, q, fault):
+    """zest_amd.pull(repo, device="all") on a CPU process group (gloo)."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if fault:
+        os.environ["ZEST_SWARM_FAULT"] = fault
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        import zest_amd
+        from zest_amd.parallel import swarm_pull
+        st = {}
+        try:
+            if fault:  # the stats of the re-shard are only visible through swarm_pull itself
+                t = swarm_pull(repo, p2p=False, dht=False, stats=st)
+            else:
+                t = zest_amd.pull(repo, device="all", p2p=False, dht=False)
+            q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
+        except Exception as e:
+            q.put((rank, type(e).__name__, str(e), st))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_api(world_size, repo, fault=""):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_api_worker, args=(r, world_size, port, repo, q, fault)) for r in range(world_size)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_pull_device_all_is_a_swarm_pull_without_snapshot(hub_env, tmp_path):
+    """The public API's device="all" runs the swarm pull: every rank gets every tensor, each file
+    is fetched once by its owner into memory, and no rank writes an HF snapshot."""
+    world, hub = hub_env
+    want = _expected(world)
+    res = _run_api(3, world.spec.repo_id)
+    assert [r[1] for r in res] == ["ok"] * 3, res
+    for _, _, got, _ in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+    snaps = list((tmp_path / "hf").rglob("snapshots/*/*")) if (tmp_path / "hf").exists() else []
+    assert not snaps, snaps
+
+
+def test_swarm_pull_reshards_a_failed_fetch(hub_env):
+    """Rank 1's first-round fetch fails (injected): its file is reassigned to another owner and
+    every rank still ends with every tensor (SURVEY §5.3 re-shard), instead of all ranks raising."""
+    world, hub = hub_env
+    want = _expected(world)
+    res = _run_api(3, world.spec.repo_id, fault="1:0")
+    assert [r[1] for r in res] == ["ok"] * 3, res
+    for _, _, got, _ in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+    assert all(r[3]["reassigned"] >= 1 for r in res)
+    total = sum(f.size for f in world.xet_files)
+    assert sum(r[3]["fetched_bytes"] for r in res) == total  # every file landed once

@@ -63,7 +63,9 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
     * device="cuda:N" (or as_tensors=True): also loads every *.safetensors file into that GPU's HBM,
       verifies each against its Xet file hash on the GPU, and returns {tensor_name: tensor}.
     * device="all": collective over `group` (default WORLD) — every rank gets all tensors on its
-      own GPU while each file is read/pushed by one owner rank and replicated over xGMI (RCCL).
+      own GPU (CPU process groups: host memory).  Each Xet file is fetched once, device-direct, by
+      one owner rank and seeded to the others over xGMI (RCCL broadcasts), re-verified on every
+      receiver; no snapshot is written (zest_amd.parallel.swarm_pull).
     * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
       cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct);
       `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.
@@ -74,16 +76,11 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
     if device is None and not as_tensors:
         return _client.pull(repo, revision, **kw)
     if device == "all":
-        import torch.distributed as dist
+        from .parallel import swarm_pull
 
-        from .parallel import swarm_load
-
-        # rank 0 pulls (P2P/CDN), the others wait; then the snapshot is swarm-loaded into HBM.
-        res = _client.pull_detailed(repo, revision, **kw) if dist.get_rank(group) == 0 else None
-        obj = [None if res is None else (res.snapshot_dir, res.xet_hashes())]
-        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        snap, hashes = obj[0]
-        return swarm_load(snap, group=group, xet_hashes=hashes if verify else None)
+        return swarm_pull(repo, revision, group=group, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
+                          dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify,
+                          staging_bytes=staging_bytes, threads=threads)
     if direct:
         from .direct import pull_to_device
 
