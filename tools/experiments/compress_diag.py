@@ -1,7 +1,7 @@
 """Per-input GPU vs host LZ4/BG4 compressed sizes (diagnostic for the K7b kernel)."""
 import sys
 from pathlib import Path
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import numpy as np
 import torch
 from zest_amd import _core, ops

@@ -1,4 +1,4 @@
-"""Bisect the DevicePuller HIP-graph capture crash: python tools/graph_probe2.py <level>
+"""Bisect the DevicePuller HIP-graph capture crash: python tools/experiments/graph_probe2.py <level>
 level 0: H2D copies + events + torch memsets only (engine kernels stubbed out), 1: + index_terms,
 2: + place_chunks, 3: + hash_chunks, 4: + merkle/compare (the full step)."""
 import faulthandler
@@ -7,7 +7,7 @@ from pathlib import Path
 
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from zest_amd import ops  # noqa: E402
 from zest_amd.engine import DevicePuller  # noqa: E402
 from zest_amd.synthetic import SyntheticWorld  # noqa: E402

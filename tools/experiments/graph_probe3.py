@@ -1,5 +1,5 @@
 """Minimal HIP-graph capture shapes of the engine step (no engine code):
-python tools/graph_probe3.py <variant>  A full shape, B no memsets on the lanes, C one lane,
+python tools/experiments/graph_probe3.py <variant>  A full shape, B no memsets on the lanes, C one lane,
 D copies issued on the lanes (no copy stream), E copy stream only (no lanes), P = A on
 high-priority streams (as the engine creates them), X = A + the copy stream waiting on lane events."""
 import faulthandler
@@ -8,7 +8,7 @@ from pathlib import Path
 
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from zest_amd import ops  # noqa: E402
 
 faulthandler.enable()

@@ -1,5 +1,5 @@
 """Bisect the engine-step capture crash with the engine's own buffers and streams, re-issuing the
-step's stream/event structure by hand: python tools/graph_probe4.py <flags>
+step's stream/event structure by hand: python tools/experiments/graph_probe4.py <flags>
 flags: e = eager pass before capture (as capture_graph does), z = hashes.zero_() on the capture
 stream, c = ws.chunks zero_ per round, r = the engine's lane streams (else fresh default-priority ones).
 (Reproduces the copy-stream pipeline the engine used before round 2's per-lane copies.)"""
@@ -9,7 +9,7 @@ from pathlib import Path
 
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from zest_amd import ops  # noqa: E402
 from zest_amd.engine import DevicePuller  # noqa: E402
 from zest_amd.synthetic import SyntheticWorld  # noqa: E402

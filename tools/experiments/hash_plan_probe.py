@@ -1,12 +1,12 @@
 """Probe: leaf-flat K1 kernels with a device sync between launches (kernel-trace durations without
-back-to-back queueing effects).  python tools/hash_plan_probe.py [n_chunks] [chunk_bytes]"""
+back-to-back queueing effects).  python tools/experiments/hash_plan_probe.py [n_chunks] [chunk_bytes]"""
 import sys
 from pathlib import Path
 
 import numpy as np
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from zest_amd import ops  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384

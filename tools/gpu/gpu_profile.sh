@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: kernel tests + rocprofv3 kernel-trace/stats of the pull bench (Llama-3.1-8B, 1 GPU).
-# Usage (from this container): gpurun --timeout 1100 -- 'bash tools/gpu_profile.sh'
+# Usage (from this container): gpurun --timeout 1100 -- 'bash tools/gpu/gpu_profile.sh'
 export ZEST_SKIP_BUILD=1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof

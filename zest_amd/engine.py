@@ -607,7 +607,7 @@ class DevicePuller:
         modes = tuple(m for m in modes if m not in PEER_MAPPED_MODES or self._peer_arenas is not None)
         if self.is_cuda and self._backend() == "gloo":
             # gloo moves device tensors only through its collectives; a batched isend/irecv of
-            # device tensors never completed (2-rank rehearsal on one GPU, tools/gpu_check_r2.sh)
+            # device tensors never completed (2-rank rehearsal on one GPU, tools/experiments/gpu_check_r2.sh)
             modes = tuple(m for m in modes if m != "p2p")
         full = [k for k, w in enumerate(self.round_weights) if w == 1.0]  # time full-size rounds
         rounds = (full or list(range(self.n_rounds)))[:max_rounds]
@@ -680,7 +680,7 @@ class DevicePuller:
 
         The step's stream shape captures as is: every round lives on one lane, so the graph has no
         cross-stream events (an earlier pipeline whose copy stream and lanes waited on each other
-        crashed hipStreamEndCapture, ROCm 7: tools/graph_probe3.py X).  Host cost per step drops from
+        crashed hipStreamEndCapture, ROCm 7: tools/experiments/graph_probe3.py X).  Host cost per step drops from
         ~1300 Python-issued HIP calls to one launch, but the graph's copy nodes ran slower (70B pull:
         51.2 GB/s, the same shape issued eagerly 56.9; profiles/hip_graph_r2.md), so bench.py uses it
         only with ZEST_GRAPH=1."""
