@@ -1,0 +1,92 @@
+"""Host `zest pull` throughput from 1 vs 3 warm loopback seeders (term striping).
+
+Every "machine" is a cache root + port set on 127.0.0.1 (tests/e2e_util.Node).  Seeder 0 pulls the
+repo from the fake CDN; seeders 1-2 get a copy of its xorb cache; all three run `zest serve`.  A
+fresh leecher then pulls with `--peer` = seeder 0 only, and another with all three.  Reports wall
+time, GB/s and each seeder's share of the bytes served (from its /v1/status).
+
+    python tools/stripe_bench.py [--mb 2048] [--out profiles/stripe_bench.json]
+
+Reference target: "Lab with 5 warm peers: 15 sec (parallel LAN), 20x" (DESIGN.md:570); the
+reference itself tries peers sequentially, first success wins (swarm.zig:371-394).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import shutil
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+from e2e_util import Node, p2p_ratio  # noqa: E402
+from zest_amd.testing import FakeHub  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", type=int, default=2048, help="repo size (MB of random weights, 4 shards)")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    rng = np.random.default_rng(1)
+    shard = a.mb * 1_000_000 // 4
+    files = {f"model-0000{i}-of-00004.safetensors": rng.integers(0, 256, shard, dtype=np.uint8).tobytes()
+             for i in range(1, 5)}
+    files["config.json"] = b'{"model_type": "llama"}'
+    total = sum(len(v) for v in files.values())
+    hub = FakeHub(policy="none")
+    hub.start()
+    work = Path(tempfile.mkdtemp(prefix="zest-stripe-"))
+    nodes = []
+    res = {"bytes": total, "repo": "org/stripe", "data": "random bytes, 4 Xet shards, raw chunks"}
+    try:
+        hub.add_repo("org/stripe", files, xet_min_size=1000)
+        seeders = [Node(hub, work, "s0")]
+        nodes += seeders
+        seeders[0].run("pull", "org/stripe", "--no-p2p", "--no-serve", timeout=1800)
+        for k in (1, 2):
+            s = Node(hub, work, f"s{k}")
+            shutil.copytree(seeders[0].root / "zest" / "xorbs", s.root / "zest" / "xorbs")
+            seeders.append(s)
+            nodes.append(s)
+        for s in seeders:
+            s.spawn("serve", "--listen-port", str(s.listen_port), "--http-port", str(s.http_port))
+        for s in seeders:
+            s.wait_healthy(timeout=30)
+        for label, use in (("1_seeder", seeders[:1]), ("3_seeders", seeders)):
+            before = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
+            leech = Node(hub, work, f"leech_{label}")
+            nodes.append(leech)
+            args = ["pull", "org/stripe", "--no-dht", "--no-serve"]
+            for s in use:
+                args += ["--peer", f"127.0.0.1:{s.listen_port}"]
+            t0 = time.time()
+            r = leech.run(*args, timeout=1800)
+            dt = time.time() - t0
+            after = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
+            served = [b - a_ for a_, b in zip(before, after)]
+            res[label] = {"seconds": round(dt, 3), "GBps": round(total / dt / 1e9, 3), "p2p_ratio": p2p_ratio(r.stdout),
+                          "served_share": [round(x / max(1, sum(served)), 3) for x in served]}
+            print(f"[{label}] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s), P2P {p2p_ratio(r.stdout):.0f}%, "
+                  f"seeder shares {res[label]['served_share']}", flush=True)
+        res["speedup_3_vs_1"] = round(res["1_seeder"]["seconds"] / res["3_seeders"]["seconds"], 3)
+        print(json.dumps(res), flush=True)
+        if a.out:
+            Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
+        return 0
+    finally:
+        for n in nodes:
+            n.close()
+        hub.stop()
+        shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
