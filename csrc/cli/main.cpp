@@ -7,6 +7,7 @@
 // main.zig:361-369), re-announcing every `--reannounce` seconds; `serve` can also run a DHT node;
 // xorb hashes are parsed with the Xet word-order hex (the reference's seed parses bytewise,
 // main.zig:349-356, which yields info-hashes no puller computes).
+#include <fcntl.h>
 #include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>
@@ -61,7 +62,7 @@ void print_usage(std::ostream& w) {
        "  zest pull <repo_id> [options]    Download a model\n"
        "  zest seed [options]              Seed cached xorbs to peers\n"
        "  zest serve [options]             Run server (BT + HTTP API)\n"
-       "  zest start                       Start server in background\n"
+       "  zest start [--open|--no-open]    Start server in background (and open the dashboard)\n"
        "  zest stop                        Stop background server\n"
        "  zest status                      Show background server status\n"
        "  zest bench [options]             Run benchmarks\n"
@@ -685,10 +686,44 @@ int cmd_serve(const std::vector<std::string>& a) {
   return 0;
 }
 
-int cmd_start(const std::string& exe) {
+// Open the dashboard in a browser (xdg-open / open), detached; false when no opener could start.
+bool open_dashboard(const std::string& url) {
+#ifdef __APPLE__
+  const char* opener = "open";
+#else
+  const char* opener = "xdg-open";
+#endif
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);
+  posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
+  const char* argv[] = {opener, url.c_str(), nullptr};
+  pid_t pid = 0;
+  const int rc = posix_spawnp(&pid, opener, &fa, nullptr, const_cast<char* const*>(argv), environ);
+  posix_spawn_file_actions_destroy(&fa);
+  return rc == 0;
+}
+
+// `zest start [--open | --no-open]`: start the background server.  The reference always runs
+// xdg-open/open on the dashboard (main.zig:485-529); here that happens only with --open, or by
+// default when a desktop session is present (DISPLAY / WAYLAND_DISPLAY), so headless GPU servers
+// never try to launch a browser.  ZEST_OPEN_DASHBOARD=0/1 sets the default.
+int cmd_start(const std::string& exe, const std::vector<std::string>& a) {
   Config cfg = Config::from_env();
+  auto set = [](const char* k) {
+    const char* v = std::getenv(k);
+    return v && *v;
+  };
+  bool open = set("DISPLAY") || set("WAYLAND_DISPLAY");
+  if (const char* e = std::getenv("ZEST_OPEN_DASHBOARD")) open = std::string(e) == "1";
+  for (auto& f : a) {
+    if (f == "--open") open = true;
+    else if (f == "--no-open") open = false;
+  }
+  const std::string url = "http://localhost:" + std::to_string(cfg.http_port);
   if (server_healthy(cfg.http_port, 500)) {
     std::cerr << "zest server is already running on port " << cfg.http_port << ".\n";
+    if (open && !open_dashboard(url)) std::cerr << "Could not open a browser; dashboard: " << url << "\n";
     return 0;
   }
   if (!spawn_background_server(exe, cfg.http_port)) {
@@ -698,7 +733,11 @@ int cmd_start(const std::string& exe) {
   for (int i = 0; i < 50 && !server_healthy(cfg.http_port, 200); ++i)
     std::this_thread::sleep_for(std::chrono::milliseconds(100));
   std::cout << "Seeding in background (BT :" << cfg.listen_port << ", HTTP :" << cfg.http_port << ")\n";
-  std::cout << "Dashboard: http://localhost:" << cfg.http_port << "\n";
+  std::cout << "Dashboard: " << url << "\n";
+  if (open) {
+    if (open_dashboard(url)) std::cout << "Opened the dashboard in a browser\n";
+    else std::cerr << "Could not open a browser (no xdg-open); dashboard: " << url << "\n";
+  }
   return 0;
 }
 
@@ -758,7 +797,7 @@ int main(int argc, char** argv) {
     if (cmd == "seed") return cmd_seed(exe, rest);
     if (cmd == "bench") return cmd_bench(exe, rest);
     if (cmd == "serve") return cmd_serve(rest);
-    if (cmd == "start") return cmd_start(exe);
+    if (cmd == "start") return cmd_start(exe, rest);
     if (cmd == "stop") return cmd_stop();
     if (cmd == "status") return cmd_status();
     if (cmd == "version" || cmd == "--version" || cmd == "-V") {

@@ -480,6 +480,29 @@ def test_start_stop(nodes):
         raise AssertionError("server still up after stop")
 
 
+def test_start_opens_dashboard(nodes, tmp_path):
+    """`zest start --open` launches the dashboard in a browser like the reference (main.zig:485-529,
+    xdg-open); headless default (no DISPLAY) does not.  xdg-open is stubbed to record its URL."""
+    a = nodes("a")
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    opened = tmp_path / "opened.txt"
+    (bindir / "xdg-open").write_text(f"#!/bin/sh\necho \"$1\" >> {opened}\n")
+    (bindir / "xdg-open").chmod(0o755)
+    env = {"PATH": f"{bindir}:{os.environ['PATH']}", "DISPLAY": ""}
+    env_headless = {k: v for k, v in a.env.items() if k not in ("DISPLAY", "WAYLAND_DISPLAY")}
+    env_headless["PATH"] = env["PATH"]
+    r = subprocess.run([ZEST, "start"], env=env_headless, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "Opened the dashboard" not in r.stdout
+    a.wait_healthy()
+    r = a.run("start", "--open", env=env)
+    t0 = time.time()
+    while not opened.exists() and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert opened.read_text().strip() == f"http://localhost:{a.http_port}"
+    a.run("stop")
+
+
 def test_p2p_cluster_script_local(tmp_path):
     """scripts/p2p_cluster_test.sh --local 3 (the reference's hetzner / docker P2P suites): CDN-only
     baseline, two seeders, pulls from both and from one — each snapshot identical, 100 % P2P."""
