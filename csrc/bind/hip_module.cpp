@@ -137,6 +137,17 @@ PYBIND11_MODULE(_hip, m) {
           "zg_hash_chunks");
   }, py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"), py::arg("hashes"), py::arg("sizes"),
      py::arg("base"), py::arg("stream"), py::arg("scratch") = 0, py::arg("scratch_bytes") = 0);
+  m.def("ingest_chunks", [](uintptr_t src, uint64_t src_n, uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n,
+                            bool has_compressed, uintptr_t err, uintptr_t hashes, uintptr_t sizes, uint32_t base,
+                            uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {
+    check(zg_ingest_chunks(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n,
+                           has_compressed ? 1 : 0, P<unsigned long long>(err), P<uint8_t>(hashes), P<uint64_t>(sizes),
+                           base, P<uint8_t>(scratch), scratch_bytes, S(st)),
+          "zg_ingest_chunks");
+  }, py::arg("src"), py::arg("src_n"), py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"),
+     py::arg("has_compressed"), py::arg("err"), py::arg("hashes"), py::arg("sizes"), py::arg("base"), py::arg("stream"),
+     py::arg("scratch"), py::arg("scratch_bytes"),
+     "fused ingest: LZ4/BG4 decode of compressed chunks, then one pass that places raw chunks and hashes all");
   m.def("hash_ranges", [](uintptr_t buf, uintptr_t offs, uintptr_t lens, int n, uintptr_t out, int key_mode,
                           uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {
     check(zg_hash_ranges(P<const uint8_t>(buf), P<const uint64_t>(offs), P<const uint32_t>(lens), n,

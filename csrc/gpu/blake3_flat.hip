@@ -64,37 +64,75 @@ __host__ __device__ inline Layout layout(uint8_t* s, int n, uint32_t cap) {
   return l;
 }
 
-// Descriptor sources: byte offset + length of message c, or bad (hashed as described per source).
+// Descriptor sources: the bytes + length of message c, or bad (hashed as described per source).
 struct ChunkSrc {  // placed Xet chunks (k_hash_chunks semantics: a bad descriptor hashes as empty)
   const ZgChunk* chunks;
+  const uint8_t* buf;
   uint64_t dst_n;
   static constexpr bool kBadIsFF = false;
-  __device__ __forceinline__ void get(int c, uint64_t& off, uint32_t& len, bool& bad) const {
-    off = chunks[c].dst;
+  static constexpr bool kPlace = false;
+  __device__ __forceinline__ void get(int c, const uint8_t*& p, uint32_t& len, bool& bad) const {
+    uint64_t off = chunks[c].dst;
     len = chunks[c].ulen;
     bad = false;
     if (off + len > dst_n || len > kMaxChunk) off = 0, len = 0;
+    p = buf + off;
   }
 };
 
 struct RangeSrc {  // raw (offset, len) messages (k_hash_ranges semantics: > 128 KiB -> all-ones hash)
   const uint64_t* offs;
   const uint32_t* lens;
+  const uint8_t* buf;
   static constexpr bool kBadIsFF = true;
-  __device__ __forceinline__ void get(int c, uint64_t& off, uint32_t& len, bool& bad) const {
-    off = offs[c];
+  static constexpr bool kPlace = false;
+  __device__ __forceinline__ void get(int c, const uint8_t*& p, uint32_t& len, bool& bad) const {
+    uint64_t off = offs[c];
     len = lens[c];
     bad = len > kMaxChunk;
     if (bad) off = 0, len = 0;
+    p = buf + off;
+  }
+};
+
+// Fused place + hash of one ingest launch (K3a + K1 in one pass): uncompressed (scheme 0) chunks
+// are still in the staging buffer; each leaf wave first copies the raw bytes of its 64 leaves
+// staging -> arena (wave_copy: 16-byte aligned stores, coalesced), then hashes them from staging,
+// whose lines the copy just pulled into L2.  Compressed chunks were decoded into the arena by the
+// LZ4 kernel before this launch and are hashed from there.  The arena is written once and never
+// read back, where place-then-hash read it again (round 2: k_place_raw 28 % + k_hash_leaves 22 % of
+// the pull's kernel time, profiles/bench70b_n1_kernels_r2c.md).
+struct PlaceSrc {
+  const ZgChunk* chunks;
+  const uint8_t* src;
+  uint64_t src_n;
+  uint8_t* dst;
+  uint64_t dst_n;
+  static constexpr bool kBadIsFF = false;
+  static constexpr bool kPlace = true;
+  __device__ __forceinline__ bool raw_ok(const ZgChunk& ch) const {
+    return ch.src + ch.ulen <= src_n && ch.dst + ch.ulen <= dst_n && ch.ulen <= kMaxChunk;
+  }
+  __device__ __forceinline__ void get(int c, const uint8_t*& p, uint32_t& len, bool& bad) const {
+    const ZgChunk ch = chunks[c];
+    bad = false;
+    len = ch.ulen;
+    if (ch.scheme == 0) {
+      if (!raw_ok(ch)) len = 0;
+      p = src + (len ? ch.src : 0);
+    } else {
+      if (ch.dst + len > dst_n || len > kMaxChunk) len = 0;
+      p = dst + (len ? ch.dst : 0);
+    }
   }
 };
 
 template <class Src>
 __device__ __forceinline__ uint32_t n_leaves(const Src& s, int c) {
-  uint64_t off;
+  const uint8_t* p;
   uint32_t len;
   bool bad;
-  s.get(c, off, len, bad);
+  s.get(c, p, len, bad);
   return len == 0 ? 1u : (len + 1023u) >> 10;
 }
 
@@ -172,10 +210,25 @@ __global__ void __launch_bounds__(kPlanThreads) k_hash_plan(Src s, int n, uint8_
   }
 }
 
+// The raw bytes of wave task `task` (leaves 64 task .. 64 task + 63, chunks lo_c..hi_c) go
+// staging -> arena; wave-uniform loop over the (at most ~9) chunks the task touches.
+__device__ __forceinline__ void place_task(const PlaceSrc& s, const Layout& l, uint32_t task, int lo_c, int hi_c,
+                                           uint32_t lane) {
+  const uint32_t g0 = task * kWave, g1 = g0 + kWave;
+  for (int c = lo_c; c <= hi_c; ++c) {
+    const ZgChunk ch = s.chunks[c];
+    if (__builtin_amdgcn_readfirstlane(ch.scheme) != 0 || !s.raw_ok(ch)) continue;
+    const uint32_t p0 = __builtin_amdgcn_readfirstlane(l.P[c]), p1 = __builtin_amdgcn_readfirstlane(l.P[c + 1]);
+    const uint32_t a = max(p0, g0) - p0, b = min(p1, g1) - p0;  // leaf range of this chunk in the task
+    if (a >= b) continue;
+    const uint64_t lo = uint64_t(a) << 10, hi = min(uint64_t(b) << 10, uint64_t(ch.ulen));
+    if (lo < hi) zwv::wave_copy(s.dst + ch.dst + lo, s.src + ch.src + lo, hi - lo, lane);
+  }
+}
+
 template <class Src>
-__global__ void __launch_bounds__(256) k_hash_leaves(Src s, const uint8_t* __restrict__ buf, int n, int key_mode,
-                                                     uint8_t* scratch, uint32_t cap, uint8_t* __restrict__ out,
-                                                     uint64_t* __restrict__ sizes) {
+__global__ void __launch_bounds__(256) k_hash_leaves(Src s, int n, int key_mode, uint8_t* scratch, uint32_t cap,
+                                                     uint8_t* __restrict__ out, uint64_t* __restrict__ sizes) {
   const Layout l = layout(scratch, n, cap);
   const PlanHdr* h = reinterpret_cast<const PlanHdr*>(scratch);
   const uint32_t T = __builtin_amdgcn_readfirstlane(h->tasks);
@@ -190,6 +243,7 @@ __global__ void __launch_bounds__(256) k_hash_leaves(Src s, const uint8_t* __res
     // the owner of leaf g lies in [WF[task], WF[task + 1]]: binary search of P over that range
     int lo = int(__builtin_amdgcn_readfirstlane(l.WF[task]));
     int hi = task + 1 < T ? int(__builtin_amdgcn_readfirstlane(l.WF[task + 1])) : n - 1;
+    if constexpr (Src::kPlace) place_task(s, l, task, lo, hi, lane);
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (l.P[mid] <= g) lo = mid;
@@ -199,13 +253,13 @@ __global__ void __launch_bounds__(256) k_hash_leaves(Src s, const uint8_t* __res
     const int c = lo;
     const uint32_t b = g - l.P[c];
     const uint32_t nb = l.P[c + 1] - l.P[c];
-    uint64_t off;
+    const uint8_t* p;
     uint32_t len;
     bool bad;
-    s.get(c, off, len, bad);
+    s.get(c, p, len, bad);
     const uint32_t seg = len > (b << 10) ? min(len - (b << 10), 1024u) : 0u;
     uint32_t cv[8];
-    zg::hash_leaf(buf + off + (uint64_t(b) << 10), seg, b, key, mode, nb == 1, cv);
+    zg::hash_leaf(p + (uint64_t(b) << 10), seg, b, key, mode, nb == 1, cv);
     if (nb == 1) {
       if (Src::kBadIsFF && bad) {
 #pragma unroll
@@ -294,15 +348,15 @@ uint32_t cap_of(int n, size_t bytes) {
 }
 
 template <class Src>
-hipError_t launch_flat(Src s, const uint8_t* buf, int n, int key_mode, uint8_t* out, uint64_t* sizes,
-                       uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
+hipError_t launch_flat(Src s, int n, int key_mode, uint8_t* out, uint64_t* sizes, uint8_t* scratch,
+                       size_t scratch_bytes, hipStream_t stream) {
   const uint32_t cap = cap_of(n, scratch_bytes);
   if (cap == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_hash_plan<Src>), dim3(1), dim3(kPlanThreads), 0, stream, s, n, scratch, cap);
   const uint64_t task_bound = (uint64_t(cap) + 63) / 64;
   const uint32_t waves = uint32_t(task_bound < kLeafMaxWaves ? task_bound : kLeafMaxWaves);
-  hipLaunchKernelGGL((k_hash_leaves<Src>), dim3((waves + 3) / 4), dim3(256), 0, stream, s, buf, n, key_mode, scratch,
-                     cap, out, sizes);
+  hipLaunchKernelGGL((k_hash_leaves<Src>), dim3((waves + 3) / 4), dim3(256), 0, stream, s, n, key_mode, scratch, cap,
+                     out, sizes);
   const int groups = (n + kTreeG - 1) / kTreeG;
   hipLaunchKernelGGL(k_hash_tree, dim3((groups + 3) / 4), dim3(256), 0, stream, n, key_mode, scratch, cap, out);
   return hipGetLastError();
@@ -321,13 +375,20 @@ size_t zg_hash_scratch_bytes(int n, uint64_t total_bytes) {
 hipError_t zg_hash_chunks_flat(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
                                uint8_t* hashes, uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes,
                                hipStream_t stream) {
-  return launch_flat(ChunkSrc{chunks, dst_n}, dst, n_chunks, 0, hashes, sizes, scratch, scratch_bytes, stream);
+  return launch_flat(ChunkSrc{chunks, dst, dst_n}, n_chunks, 0, hashes, sizes, scratch, scratch_bytes, stream);
+}
+
+hipError_t zg_place_hash_flat(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                              int n_chunks, uint8_t* hashes, uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes,
+                              hipStream_t stream) {
+  return launch_flat(PlaceSrc{chunks, src, src_n, dst, dst_n}, n_chunks, 0, hashes, sizes, scratch, scratch_bytes,
+                     stream);
 }
 
 hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,
                                uint8_t* hashes, int key_mode, uint8_t* scratch, size_t scratch_bytes,
                                hipStream_t stream) {
-  return launch_flat(RangeSrc{offsets, lens}, buf, n, key_mode, hashes, nullptr, scratch, scratch_bytes, stream);
+  return launch_flat(RangeSrc{offsets, lens, buf}, n, key_mode, hashes, nullptr, scratch, scratch_bytes, stream);
 }
 
 }  // extern "C"

@@ -11,6 +11,7 @@
 
 #include "blake3_dev.h"
 #include "lz4win.h"
+#include "wave64.h"
 #include "zgpu.h"
 
 namespace {
@@ -98,49 +99,7 @@ __global__ void k_index_terms(const uint8_t* __restrict__ src, const ZgTerm* __r
   if (off != tm.src_len || (tm.ulen != 0 && uoff != tm.ulen)) report(err, ZG_ERR_COUNT, uint32_t(t));
 }
 
-// --------------------------------------------------------------------------------------------
-// Wave-cooperative byte-exact copy between arbitrarily aligned addresses: 16-byte aligned
-// dwordx4 stores; the source is read as aligned dwords and funnel-shifted (v_alignbyte_b32).
-// --------------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_copy(uint8_t* d, const uint8_t* s, uint64_t n, uint32_t lane) {
-  const uint64_t da = reinterpret_cast<uintptr_t>(d);
-  uint64_t head = (16 - (da & 15)) & 15;
-  if (head > n) head = n;
-  if (lane < head) d[lane] = s[lane];
-  d += head;
-  s += head;
-  n -= head;
-  const uint64_t nvec = n >> 4;
-  const uintptr_t sa = reinterpret_cast<uintptr_t>(s);
-  const uint32_t k = uint32_t(sa & 3);
-  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
-  uint4* dv = reinterpret_cast<uint4*>(d);
-  if (k == 0) {
-    for (uint64_t v = lane; v < nvec; v += kWave) {
-      const uint32_t* p = sw + 4 * v;
-      uint4 o;
-      o.x = p[0];
-      o.y = p[1];
-      o.z = p[2];
-      o.w = p[3];
-      dv[v] = o;
-    }
-  } else {
-    for (uint64_t v = lane; v < nvec; v += kWave) {
-      const uint32_t* p = sw + 4 * v;
-      const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
-      uint4 o;
-      o.x = __builtin_amdgcn_alignbyte(w1, w0, k);
-      o.y = __builtin_amdgcn_alignbyte(w2, w1, k);
-      o.z = __builtin_amdgcn_alignbyte(w3, w2, k);
-      o.w = __builtin_amdgcn_alignbyte(w4, w3, k);
-      dv[v] = o;
-    }
-  }
-  const uint64_t done = nvec << 4;
-  const uint64_t rem = n - done;
-  if (lane < rem) d[done + lane] = s[done + lane];
-}
+using zwv::wave_copy;  // wave64.h
 
 // K3a: place uncompressed chunks (scheme 0): one wave per chunk, clipped to [clip_lo, clip_hi).
 __global__ void __launch_bounds__(256) k_place_raw(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -736,6 +695,20 @@ hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chu
   hipLaunchKernelGGL(k_hash_chunks, dim3((n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, stream, dst,
                      chunks, n_chunks, hashes, sizes, hash_index_base, dst_n);
   return hipGetLastError();
+}
+
+hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                            int n_chunks, int has_compressed, unsigned long long* err, uint8_t* hashes,
+                            uint64_t* sizes, uint32_t hash_index_base, uint8_t* scratch, size_t scratch_bytes,
+                            hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  if (!scratch) return hipErrorInvalidValue;
+  if (has_compressed) {
+    const hipError_t e = zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
+    if (e != hipSuccess) return e;
+  }
+  return zg_place_hash_flat(src, src_n, dst, dst_n, chunks, n_chunks, hashes + 32 * uint64_t(hash_index_base),
+                            sizes ? sizes + hash_index_base : nullptr, scratch, scratch_bytes, stream);
 }
 
 hipError_t zg_hash_ranges(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n, uint8_t* hashes,

@@ -87,6 +87,18 @@ hipError_t zg_hash_chunks_flat(const uint8_t* dst, uint64_t dst_n, const ZgChunk
 hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,
                                uint8_t* hashes, int key_mode, uint8_t* scratch, size_t scratch_bytes,
                                hipStream_t stream);
+// Fused K3a + K1: uncompressed chunks are copied src -> dst by the hashing waves themselves (and
+// hashed from src); compressed ones must already be decoded into dst.
+hipError_t zg_place_hash_flat(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                              int n_chunks, uint8_t* hashes, uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes,
+                              hipStream_t stream);
+// One ingest launch sequence for an unclipped batch: LZ4/BG4 decode of the compressed chunks (only
+// when `has_compressed`), then the fused place + hash (hashes[hash_index_base + c]).  Replaces
+// zg_place_chunks + zg_hash_chunks (2 passes over the arena) with one pass; `scratch` is required.
+hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                            int n_chunks, int has_compressed, unsigned long long* err, uint8_t* hashes,
+                            uint64_t* sizes, uint32_t hash_index_base, uint8_t* scratch, size_t scratch_bytes,
+                            hipStream_t stream);
 hipError_t zg_merkle(const uint8_t* leaf_hashes, const uint64_t* leaf_sizes, const ZgMerkleJob* jobs,
                      int n_jobs, uint8_t* roots, uint8_t* scratch, uint64_t scratch_bytes,
                      hipStream_t stream);

@@ -409,16 +409,17 @@ struct DeviceXetPull::Impl {
             hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
                                      hipMemcpyHostToDevice, stream_),
                       "H2D chunk records");
-          hip_check(zg_place_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, 0, dst_size, nullptr, err_.p,
-                                    stream_),
-                    "place");
           uint64_t ubytes = 0;
           for (size_t i = bt.begin; i < bt.end; ++i) ubytes += gt[i].ulen;
+          bool compressed = false;
+          for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.chunks_host[size_t(c)].scheme != 0;
           const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
           hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
-          hip_check(zg_hash_chunks(dst, dst_size, s.chunks_dev.p, nchunks, hashes_.p + 32 * c0, sizes_.p + c0, 0,
-                                   hash_scratch_.p, hs_bytes, stream_),
-                    "hash");
+          // decode (when the batch has compressed chunks) + one fused pass placing raw chunks and
+          // hashing every chunk (csrc/gpu/blake3_flat.hip PlaceSrc)
+          hip_check(zg_ingest_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, compressed ? 1 : 0, err_.p,
+                                     hashes_.p + 32 * c0, sizes_.p + c0, 0, hash_scratch_.p, hs_bytes, stream_),
+                    "ingest");
           hip_check(hipEventRecord(s.done, stream_), "event");
           // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
           hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");

@@ -158,8 +158,11 @@ def _make_runs(policy, seed=0):
     return data, ends, b
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("policy", ["none", "lz4", "bg4", "auto"])
-def test_ingest_matches_cpu(policy):
+def test_ingest_matches_cpu(policy, fused):
+    """Ingest (decode + place + hash) vs the host builder, at odd src/dst offsets; `fused`: the one-
+    pass place+hash (zg_ingest_chunks, raw chunks copied by the hashing waves) vs place then hash."""
     data, ends, b = _make_runs(policy)
     body = b.serialize(False)
     nck = len(ends)
@@ -185,7 +188,7 @@ def test_ingest_matches_cpu(policy):
     dst = ops.padded_empty(len(data) + 2 * dst_gap, DEV)
     dst.fill_(0xAB)
     hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=DEV)
-    ops.ingest_terms(src, dst, terms, hashes)
+    ops.ingest_terms(src, dst, terms, hashes, fused=fused, has_compressed=policy != "none")
     torch.cuda.synchronize()
     out = dst.cpu().numpy().tobytes()
     assert out[dst_gap:dst_gap + len(data)] == data

@@ -162,8 +162,9 @@ def main():
         emit(kernel="hash_chunks[flat]", bytes=n, ms=ms, gbps=n / ms / 1e6)
         del body, dst
 
-    def ingest_case(name, raw, policy, iters):
-        """Pack `raw` into xorb runs with `policy`, then time index+place/decode+hash on the GPU."""
+    def ingest_case(name, raw, policy, iters, fused=None):
+        """Pack `raw` into xorb runs with `policy`, then time index+place/decode+hash on the GPU
+        (fused: one place+hash pass; None = the ZEST_FUSED_INGEST default)."""
         m = len(raw)
         ends = C.chunk_ends(raw)
         b = C.XorbBuilder(policy)
@@ -198,10 +199,13 @@ def main():
         nck2 = int(terms["n_chunks"].sum())
         hashes = torch.empty((nck2, 32), dtype=torch.uint8, device=dev)
         ws = ops.IngestWorkspace(dev, len(terms), nck2)
-        ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), iters)
+        comp = policy != "none"
+        ms = timed(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False, fused=fused,
+                                            has_compressed=comp), iters)
         ops.raise_on_error(ws.err)
         ok = dst[:m].cpu().numpy().tobytes() == raw
-        emit(kernel=f"ingest_{policy}({name})", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
+        tag = "" if fused is None else ("[fused]" if fused else "[place+hash]")
+        emit(kernel=f"ingest_{policy}({name}){tag}", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
              chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
         assert ok, name
         del src, dst, hashes, ws
@@ -221,6 +225,20 @@ def main():
         raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
         del w
         ingest_case("bf16_1g", raw, "bg4", max(3, a.iters // 4))
+        del raw
+
+    if want("fuse"):
+        # a bench round of raw chunks (1 GiB random bytes): place then hash vs the fused one pass,
+        # and the same for a BG4 bf16 round (decode + place/hash)
+        m = 1 << 30
+        raw = np.random.default_rng(2).integers(0, 256, m, dtype=np.uint8).tobytes()
+        for fused in (False, True):
+            ingest_case("random_1g", raw, "none", max(3, a.iters), fused=fused)
+        w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
+        raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+        del w
+        for fused in (False, True):
+            ingest_case("bf16_1g", raw, "bg4", max(3, a.iters // 4), fused=fused)
         del raw
 
     if want("lz4paths"):

@@ -61,6 +61,7 @@ class RoundWork:
     terms_dev: torch.Tensor | None = None  # TERM_DTYPE records (src relative to the staging slot)
     terms_host: np.ndarray | None = None   # the same records on the host (host header walk)
     table_off: int = 0                     # byte offset of the round's chunk records in a host table
+    compressed: bool = True                # any chunk of the round stored LZ4/BG4 (decoder launch needed)
 
 
 # Pinned allocations kept for reuse by the next OriginStore of this process (capacity, pointer).
@@ -251,8 +252,9 @@ class DevicePuller:
                 terms_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
             else:
                 c0, nck, rec, region, terms_dev = 0, 0, None, (0, 0), None
+            comp = bool(world.chunk_scheme is not None and b > a and world.chunk_scheme[c0:c0 + nck].any())
             self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev, rec,
-                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize))
+                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize, comp))
             max_span = max(max_span, span_len)
             max_terms = max(max_terms, b - a)
             max_chunks = max(max_chunks, nck)
@@ -665,9 +667,15 @@ class DevicePuller:
                 chunks[:nbytes].zero_()
                 H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, chunks.data_ptr(),
                               self.err.data_ptr(), st)
+        sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
+        if ops.FUSED_INGEST:
+            # decode (compressed rounds only) + ONE pass that places raw chunks and hashes every chunk
+            H.ingest_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(),
+                            rw.n_chunks, rw.compressed, self.err.data_ptr(), self.hashes.data_ptr() + 32 * rw.c0, 0, 0,
+                            st, sp, sb)
+            return
         H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(),
                        rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
-        sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
         H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(), rw.n_chunks,
                       self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
 

@@ -11,6 +11,7 @@ K5 cdc_candidates, K7 pack_chunks.
 from __future__ import annotations
 
 import functools
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -178,9 +179,12 @@ class IngestWorkspace:
         return self._clip_scratch.data_ptr()
 
 
+FUSED_INGEST = os.environ.get("ZEST_FUSED_INGEST", "1") != "0"
+
+
 def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes: torch.Tensor,
                  hash_base: int = 0, clip=None, ws: IngestWorkspace | None = None,
-                 check: bool = True) -> None:
+                 check: bool = True, fused: bool | None = None, has_compressed: bool = True) -> None:
     """Decode + place + hash a batch of fetched runs.
 
     src: uint8 staging buffer holding the runs (padded); dst: uint8 arena (padded).
@@ -188,6 +192,8 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     clip: optional (lo, hi) arena byte window this rank owns: bytes outside are not written, and
     the hashes of chunks not entirely inside the window are unspecified.
     LZ4 chunks take the batched decoder (lz4seq.hip) unless clipped (LDS-ring decoder).
+    fused (default: ZEST_FUSED_INGEST != 0): unclipped batches run decode + one fused place/hash
+    pass (zg_ingest_chunks) instead of place then hash; `has_compressed=False` skips the decoder.
     """
     terms = np.ascontiguousarray(terms, dtype=TERM_DTYPE)
     nt = len(terms)
@@ -228,11 +234,15 @@ def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes
     ws.chunks[: n_chunks * CHUNK_DTYPE.itemsize].zero_()  # gaps between terms become no-op descriptors
     H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(), ws.err.data_ptr(), st)
     clipped = lo > 0 or hi < dst_n
-    H.place_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, lo, hi,
-                   ws.err.data_ptr(), st, ws.clip_scratch() if clipped else 0)
     hptr = hashes.data_ptr() + 32 * hash_base
     sp, sb = ws.hash_scratch.get(n_chunks, int(terms["ulen"].sum()))
-    H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st, sp, sb)
+    if (FUSED_INGEST if fused is None else fused) and not clipped:
+        H.ingest_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks,
+                        has_compressed, ws.err.data_ptr(), hptr, 0, 0, st, sp, sb)
+    else:
+        H.place_chunks(src.data_ptr(), src_n, dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, lo, hi,
+                       ws.err.data_ptr(), st, ws.clip_scratch() if clipped else 0)
+        H.hash_chunks(dst8.data_ptr(), dst_n, ws.chunks.data_ptr(), n_chunks, hptr, 0, 0, st, sp, sb)
     if check:
         raise_on_error(ws.err)
 
