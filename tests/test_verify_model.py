@@ -153,3 +153,46 @@ def test_zest_from_pretrained_direct_to_hbm(hub_with_gpt2, gpt2_checkpoint, tmp_
     with torch.no_grad():
         out = model(ids.cuda()).logits.cpu()
     assert torch.allclose(out, logits, atol=1e-4, rtol=1e-4)
+
+
+def _fp_all_worker(rank, world, port, env, ref, q):
+    import torch.distributed as dist
+
+    os.environ.update(env)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import zest_amd
+        ids, logits, gen = torch.load(ref, weights_only=True)
+        m = zest_amd.from_pretrained(REPO, device="all", p2p=False, dht=False)
+        with torch.no_grad():
+            ok = torch.equal(m(ids).logits, logits) and torch.equal(
+                m.generate(ids[:1], max_new_tokens=8, do_sample=False, pad_token_id=0), gen)
+        q.put((rank, ok, ""))
+    except Exception as e:  # reported to the parent
+        q.put((rank, False, f"{type(e).__name__}: {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zest_from_pretrained_all_ranks(hub_with_gpt2, gpt2_checkpoint, tmp_path):
+    """from_pretrained(device="all") on a 2-rank CPU process group: the weights come from the swarm
+    pull (each file fetched by one rank, broadcast to the other, re-verified), every rank gets a
+    working model with the uploaded model's logits and generation."""
+    import torch.multiprocessing as mp
+
+    hub, commit = hub_with_gpt2
+    _, ids, logits, gen = gpt2_checkpoint
+    ref = tmp_path / "ref.pt"
+    torch.save((ids, logits, gen), ref)
+    env = dict(hub.env(str(tmp_path)), ZEST_LISTEN_PORT=str(free_port()))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_fp_all_worker, args=(r, 2, port, env, str(ref), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res

@@ -40,26 +40,48 @@ def model_class(config, auto_class="AutoModelForCausalLM"):
 
 def from_pretrained(repo: str, revision: str = "main", *, device="cuda:0", direct: bool = True,
                     auto_class="AutoModelForCausalLM", p2p: bool = True, peers=None, tracker=None, dht: bool = True,
-                    dht_bootstrap=None, repo_type: str = "model", verify: bool = True, **model_kwargs):
+                    dht_bootstrap=None, repo_type: str = "model", verify: bool = True, group=None, **model_kwargs):
     """A transformers model whose parameters are zest-pulled, hash-verified tensors on `device`.
 
     direct=True (GPU only): Xet files go network -> pinned staging -> HBM with GPU decode + Merkle
     verification and never touch the disk; otherwise the files land in the HF cache first and are
-    streamed to `device` and verified there.  Extra keyword arguments go to the model class's
-    `from_pretrained` (e.g. attn_implementation); a `dtype` different from the checkpoint's makes
-    transformers convert (copy) the weights.
+    streamed to `device` and verified there.  device="all": collective over `group` (one process per
+    GPU): the weights come from the intra-node swarm pull (each file fetched once by one rank,
+    seeded to the others over xGMI, re-verified everywhere) and every rank gets a model on its own
+    device; rank 0 alone fetches the config / tokenizer files.  Extra keyword arguments go to the
+    model class's `from_pretrained` (e.g. attn_implementation); a `dtype` different from the
+    checkpoint's makes transformers convert (copy) the weights.
     """
     import torch
     import transformers
 
     from . import pull
 
-    dev = torch.device(device)
-    snap = snapshot_without_weights(repo, revision, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
-                                    dht_bootstrap=dht_bootstrap, repo_type=repo_type)
-    config = transformers.AutoConfig.from_pretrained(snap)
-    weights = pull(repo, revision, device=dev, direct=direct and dev.type == "cuda", verify=verify, p2p=p2p,
-                   peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, repo_type=repo_type)
+    if device == "all":
+        import torch.distributed as dist
+
+        obj = [None]
+        if dist.get_rank(group) == 0:
+            try:
+                obj[0] = ("ok", snapshot_without_weights(repo, revision, p2p=p2p, peers=peers, tracker=tracker,
+                                                         dht=dht, dht_bootstrap=dht_bootstrap, repo_type=repo_type))
+            except Exception as e:  # every rank leaves the same way
+                obj[0] = ("err", f"{type(e).__name__}: {e}")
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if obj[0][0] != "ok":
+            raise RuntimeError(f"{repo}@{revision}: config files: {obj[0][1]}")
+        snap = obj[0][1]
+        weights = pull(repo, revision, device="all", group=group, verify=verify, p2p=p2p, peers=peers,
+                       tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, repo_type=repo_type)
+        dev = next(iter(weights.values())).device if weights else torch.device("cpu")
+        config = transformers.AutoConfig.from_pretrained(snap)
+    else:
+        dev = torch.device(device)
+        snap = snapshot_without_weights(repo, revision, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
+                                        dht_bootstrap=dht_bootstrap, repo_type=repo_type)
+        config = transformers.AutoConfig.from_pretrained(snap)
+        weights = pull(repo, revision, device=dev, direct=direct and dev.type == "cuda", verify=verify, p2p=p2p,
+                       peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, repo_type=repo_type)
     cls = model_class(config, auto_class)
     # place the model where the weights already are (without a device_map transformers would
     # materialise it on the CPU and copy the tensors there)
