@@ -232,16 +232,24 @@ int run(int argc, char** argv) {
     gpurt::DeviceXetPull dp(o);
     uint64_t max_size = 1;
     for (auto& f : todo) max_size = std::max(max_size, f.size);
-    // Two device buffers: file i is written back from one while file i+1 is pulled into the other.
-    uint8_t* bufs[2] = {nullptr, nullptr};
-    for (auto& b : bufs) hip_ok(hipMalloc(reinterpret_cast<void**>(&b), max_size + 4096), "hipMalloc");
-    Writer writer(size_t(256) << 20, 4);
+    // Device buffer pool: file i is pulled into a free buffer while earlier files are written back
+    // by `nwriters` threads, each on a different file (concurrent pwrites to ONE file serialize on
+    // its inode; the host pull writes 4 files at once for the same reason).  As many buffers as
+    // half the free HBM holds, capped by the file count: a 70B repo (30 x 4.7 GB) fits whole.
+    size_t free_b = 0, total_b = 0;
+    hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    const size_t nbuf = std::max<size_t>(2, std::min<size_t>(todo.size(), (free_b / 2) / (max_size + 4096)));
+    const int nwriters = int(std::min<size_t>(size_t(std::max(1, env_int("ZEST_GPU_WRITERS", 4))), todo.size()));
+    std::vector<uint8_t*> bufs(std::min(nbuf, todo.size()), nullptr);
+    for (auto& bp : bufs) hip_ok(hipMalloc(reinterpret_cast<void**>(&bp), max_size + 4096), "hipMalloc");
+    std::vector<int> free_bufs;
+    for (int k = int(bufs.size()) - 1; k >= 0; --k) free_bufs.push_back(k);
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::pair<size_t, int>> queue;  // (file, buffer) verified in HBM, waiting for write-back
-    bool buf_busy[2] = {false, false}, closing = false;
-    std::string write_err;
-    std::thread wt([&] {
+    bool closing = false;
+    auto write_loop = [&] {
+      Writer writer(size_t(256) << 20, 2);  // own D2H stream + pinned slots per writer thread
       while (true) {
         std::pair<size_t, int> job;
         {
@@ -257,7 +265,7 @@ int run(int argc, char** argv) {
         try {
           const size_t slash = dst.rfind('/');
           storage::ensure_dir(dst.substr(0, slash));
-          writer.write(bufs[job.second], f.size, dst + ".incomplete");
+          writer.write(bufs[size_t(job.second)], f.size, dst + ".incomplete");
           if (::rename((dst + ".incomplete").c_str(), dst.c_str()) != 0) throw Error("IoError", "rename " + dst);
           storage::write_verified_marker(cfg, a.repo, commit, f.path, *f.xet_hash, dst);  // verified on the GPU
           std::lock_guard<std::mutex> g(mu);
@@ -271,25 +279,28 @@ int run(int argc, char** argv) {
           ++failed;
         }
         std::lock_guard<std::mutex> g(mu);
-        buf_busy[job.second] = false;
+        free_bufs.push_back(job.second);
         cv.notify_all();
       }
-    });
+    };
+    std::vector<std::thread> writers;
+    for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
     const double tp = now_s();
     for (size_t i = 0; i < todo.size(); ++i) {
-      const int b = int(i & 1);
+      int b;
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return !buf_busy[b]; });
-        buf_busy[b] = true;
+        cv.wait(g, [&] { return !free_bufs.empty(); });
+        b = free_bufs.back();
+        free_bufs.pop_back();
       }
       try {
-        dp.pull_files({{*todo[i].xet_hash, reinterpret_cast<uintptr_t>(bufs[b]), todo[i].size}});
+        dp.pull_files({{*todo[i].xet_hash, reinterpret_cast<uintptr_t>(bufs[size_t(b)]), todo[i].size}});
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu);
         std::cerr << "[gpu " << rank << "] " << todo[i].path << ": error " << e.what() << "\n";
         ++failed;
-        buf_busy[b] = false;
+        free_bufs.push_back(b);
         continue;
       }
       std::lock_guard<std::mutex> g(mu);
@@ -302,8 +313,8 @@ int run(int argc, char** argv) {
       closing = true;
       cv.notify_all();
     }
-    wt.join();
-    for (auto& b : bufs) (void)hipFree(b);
+    for (auto& t : writers) t.join();
+    for (auto& bp : bufs) (void)hipFree(bp);
     stats = dp.stats_json();
   }
   const double dt = now_s() - t0;

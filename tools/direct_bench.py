@@ -115,7 +115,7 @@ def main() -> int:
                   f"{total / (t2 - t1) / 1e9:.2f} GB/s -> end to end {total / (t2 - t0) / 1e9:.2f} GB/s", flush=True)
             del tensors
         if not a.skip_gpu_cli:
-            # `zest pull --gpus 1`: the CLI's GPU worker (zest_amd.multigpu) pulls device-direct,
+            # `zest pull --gpus 1`: the CLI's GPU worker (native zest-gpu-worker) pulls device-direct,
             # decodes + verifies on the GPU and writes the HF-cache snapshot
             env = dict(os.environ, **hub.env(str(work / "gpucli")))
             t0 = time.time()
@@ -125,8 +125,11 @@ def main() -> int:
             if r.returncode != 0:
                 raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
             tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
+            workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and " GB in " in ln]
             res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
-                       gpu_cli_summary=tail[-1] if tail else "")
+                       gpu_cli_summary=tail[-1] if tail else "", gpu_cli_workers=workers)
+            for ln in workers:
+                print(f"[gpu cli worker] {ln}", flush=True)
             print(f"[gpu cli] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s; {tail[-1] if tail else ''})",
                   flush=True)
         res["seeder"] = srv.stats()
