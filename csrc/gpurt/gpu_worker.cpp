@@ -239,7 +239,8 @@ int run(int argc, char** argv) {
     size_t free_b = 0, total_b = 0;
     hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
     const size_t nbuf = std::max<size_t>(2, std::min<size_t>(todo.size(), (free_b / 2) / (max_size + 4096)));
-    const int nwriters = int(std::min<size_t>(size_t(std::max(1, env_int("ZEST_GPU_WRITERS", 4))), todo.size()));
+    const int nwriters = int(std::min<size_t>(size_t(std::max(1, env_int("ZEST_GPU_WRITERS", 2))), todo.size()));
+    const int wslots = std::max(2, env_int("ZEST_GPU_WRITE_SLOTS", 3));
     std::vector<uint8_t*> bufs(std::min(nbuf, todo.size()), nullptr);
     for (auto& bp : bufs) hip_ok(hipMalloc(reinterpret_cast<void**>(&bp), max_size + 4096), "hipMalloc");
     std::vector<int> free_bufs;
@@ -249,7 +250,7 @@ int run(int argc, char** argv) {
     std::deque<std::pair<size_t, int>> queue;  // (file, buffer) verified in HBM, waiting for write-back
     bool closing = false;
     auto write_loop = [&] {
-      Writer writer(size_t(256) << 20, 2);  // own D2H stream + pinned slots per writer thread
+      Writer writer(size_t(256) << 20, wslots);  // own D2H stream + pinned slots per writer thread
       while (true) {
         std::pair<size_t, int> job;
         {
@@ -283,8 +284,12 @@ int run(int argc, char** argv) {
         cv.notify_all();
       }
     };
+    // ZEST_GPU_WRITE_AFTER=1: write back only after every pull finished (needs a buffer per file;
+    // measures the two legs separately).
+    const bool write_after = env_int("ZEST_GPU_WRITE_AFTER", 0) == 1 && bufs.size() >= todo.size();
     std::vector<std::thread> writers;
-    for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
+    if (!write_after)
+      for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
     const double tp = now_s();
     for (size_t i = 0; i < todo.size(); ++i) {
       int b;
@@ -308,6 +313,8 @@ int run(int argc, char** argv) {
       cv.notify_all();
     }
     t_pull = now_s() - tp;
+    if (write_after)
+      for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
     {
       std::lock_guard<std::mutex> g(mu);
       closing = true;
@@ -319,7 +326,8 @@ int run(int argc, char** argv) {
   }
   const double dt = now_s() - t0;
   std::cout << "[gpu " << rank << "] " << done_bytes / 1e9 << " GB in " << dt << " s (start " << t_ready - t0
-            << " s, device pulls " << t_pull << " s, writes " << t_write << " s overlapped)\n"
+            << " s, device pulls " << t_pull << " s, writes " << t_write << " s summed over writer threads, "
+            << "overlapped)\n"
             << std::flush;
   if (status_path) {
     json::Writer w;

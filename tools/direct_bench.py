@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--skip-direct", action="store_true")
     ap.add_argument("--trace-host", default=None, help="ZEST_TRACE=<file.json> for the host zest pull")
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--cli-configs", default="",
+                    help="';'-separated env settings for repeated `zest pull --gpus 1` runs, e.g. "
+                         "'ZEST_GPU_WRITERS=1;ZEST_GPU_WRITERS=2,ZEST_GPU_WRITE_SLOTS=3'")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -117,21 +120,27 @@ def main() -> int:
         if not a.skip_gpu_cli:
             # `zest pull --gpus 1`: the CLI's GPU worker (native zest-gpu-worker) pulls device-direct,
             # decodes + verifies on the GPU and writes the HF-cache snapshot
-            env = dict(os.environ, **hub.env(str(work / "gpucli")))
-            t0 = time.time()
-            r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
-                                "--no-dht", "--gpus", "1"], env=env, capture_output=True, text=True, timeout=3600)
-            dt = time.time() - t0
-            if r.returncode != 0:
-                raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
-            tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
-            workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and " GB in " in ln]
-            res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
-                       gpu_cli_summary=tail[-1] if tail else "", gpu_cli_workers=workers)
-            for ln in workers:
-                print(f"[gpu cli worker] {ln}", flush=True)
-            print(f"[gpu cli] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s; {tail[-1] if tail else ''})",
-                  flush=True)
+            configs = [c for c in a.cli_configs.split(";")] if a.cli_configs else [""]
+            for ci, cfg in enumerate(configs):
+                extra = dict(kv.split("=", 1) for kv in cfg.split(",") if kv)
+                env = dict(os.environ, **hub.env(str(work / f"gpucli{ci}")), **extra)
+                t0 = time.time()
+                r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
+                                    "--no-dht", "--gpus", "1"], env=env, capture_output=True, text=True, timeout=3600)
+                dt = time.time() - t0
+                if r.returncode != 0:
+                    raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
+                tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
+                workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and " GB in " in ln]
+                key = "gpu_cli" if not cfg else f"gpu_cli[{cfg}]"
+                res[key] = {"s": round(dt, 3), "gbps": round(total / dt / 1e9, 3), "workers": workers}
+                if not cfg:
+                    res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
+                               gpu_cli_summary=tail[-1] if tail else "", gpu_cli_workers=workers)
+                for ln in workers:
+                    print(f"[gpu cli worker {cfg}] {ln}", flush=True)
+                print(f"[gpu cli {cfg}] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
+                subprocess.run(["rm", "-rf", str(work / f"gpucli{ci}")])
         res["seeder"] = srv.stats()
         print(json.dumps(res), flush=True)
         if a.out:

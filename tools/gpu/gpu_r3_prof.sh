@@ -14,3 +14,5 @@ DB=$(find $OUT/prof -name "*.db" | head -1)
 python tools/rocpd_summary.py "$DB" --title "70B bench, bf16 then random, fused ingest (round 3)" > $OUT/b70_kernels.md 2>&1
 head -30 $OUT/b70_kernels.md
 rm -f "$DB"
+ZEST_BENCH_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 4 --model llama-3.1-8b --steps 2 --warmup 1 > $OUT/bench_n4_gloo.log 2>&1 || { tail -40 $OUT/bench_n4_gloo.log; exit 1; }
+grep -h "aggregate" $OUT/bench_n4_gloo.log
