@@ -129,10 +129,18 @@ struct PlaceSrc {
 
 template <class Src>
 __device__ __forceinline__ uint32_t n_leaves(const Src& s, int c) {
-  const uint8_t* p;
   uint32_t len;
-  bool bad;
-  s.get(c, p, len, bad);
+  if constexpr (Src::kPlace) {
+    // the plan needs only the size: one 4-byte load instead of the 32-byte record (the single-
+    // workgroup plan is latency-bound).  A record that later fails its bounds check in get() hashes
+    // as empty leaves, so its chunk hash -- and the file's Merkle check -- fails as it should.
+    len = s.chunks[c].ulen;
+    if (len > kMaxChunk) len = 0;
+  } else {
+    const uint8_t* p;
+    bool bad;
+    s.get(c, p, len, bad);
+  }
   return len == 0 ? 1u : (len + 1023u) >> 10;
 }
 
