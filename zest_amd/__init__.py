@@ -68,7 +68,8 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
       receiver; no snapshot is written (zest_amd.parallel.swarm_pull).
     * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
       cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct);
-      `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.
+      `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.  With
+      device="cpu" the same pull lands in CPU tensors (host decode + verification, no disk).
     """
     _init()
     kw = dict(p2p=p2p, peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, include=include,

@@ -2,6 +2,10 @@
 GPU-side decode and verification (`_hip.DeviceXetPull`); the host only moves compressed bytes.
 
     tensors = pull_to_device("meta-llama/Llama-3.1-8B", device="cuda:0")
+    tensors = pull_to_device("meta-llama/Llama-3.1-8B", device="cpu")   # in memory, no disk
+
+device="cpu": the same fetch through the host waterfall straight into CPU tensors
+(`_core.HostXetFetcher`: CPU decode + BLAKE3/Merkle verification, no snapshot written).
 
 Non-Xet files of the repo (config, tokenizer, small safetensors) are fetched by the native host
 pull (`include=` filter) and loaded like the disk path.  With `save_snapshot=True` the verified
@@ -22,14 +26,23 @@ def pull_to_device(repo: str, revision: str = "main", device="cuda:0", *, p2p: b
                    tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
                    save_snapshot: bool = False, staging_bytes: int = 1 << 30, threads: int = 16):
     dev = torch.device(device)
-    if dev.type != "cuda":
-        raise ValueError("pull_to_device needs a GPU device")
+    if dev.type not in ("cuda", "cpu"):
+        raise ValueError("pull_to_device needs a GPU or the CPU")
     commit, files = _core.list_repo_files(repo, revision, repo_type)
     st_files = [f for f in files if f["path"].endswith(".safetensors")]
     xet = [f for f in st_files if f["xet_hash"]]
     plain = [f for f in st_files if not f["xet_hash"]]
     out: dict[str, torch.Tensor] = {}
-    if xet:
+    if xet and dev.type == "cpu":
+        hf = _core.HostXetFetcher(repo, revision, repo_type, p2p, list(peers or []), tracker, dht,
+                                  list(dht_bootstrap or []), threads)
+        bufs = [torch.empty(f["size"], dtype=torch.uint8) for f in xet]
+        hf.fetch_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(xet, bufs)])
+        for f, buf in zip(xet, bufs):
+            _add_views(out, buf, f["path"])
+            if save_snapshot:
+                _save(repo, commit or revision, f["path"], buf)
+    elif xet:
         dp = ops.hip().DeviceXetPull(repo, revision, repo_type, p2p, list(peers or []), tracker, dht,
                                      list(dht_bootstrap or []), dev.index or 0, staging_bytes, threads)
         bufs = [ops.padded_empty(f["size"], dev)[:f["size"]] for f in xet]
