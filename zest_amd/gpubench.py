@@ -139,7 +139,8 @@ def run(mib: int = 1024, runs: int = 5, device="cuda:0") -> list[dict]:
         dst = ops.padded_empty(len(raw), dev)
         hashes = torch.empty((nck, 32), dtype=torch.uint8, device=dev)
         ws = ops.IngestWorkspace(dev, len(terms), nck)
-        ns = _time(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False), runs)
+        comp = policy != "none"
+        ns = _time(lambda: ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False, has_compressed=comp), runs)
         ops.raise_on_error(ws.err)
         if dst[:len(raw)].cpu().numpy().tobytes() != raw:
             raise RuntimeError(f"{name}: decoded bytes differ from the input")
