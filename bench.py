@@ -41,6 +41,8 @@ BASELINE_METRIC = "aggregate pull GB/s + P2P ratio, Llama-3.1-70B at 1/2/4/8 MI3
 MODES = ("bf16", "random")
 
 # Per-phase watchdog limits (seconds) for N > 1; ZEST_BENCH_WATCHDOG=<s> overrides all, =0 disables.
+# "1": --exchange auto also maps the peers' arenas and times the ipc / xgmi exchanges
+IPC_AUTO = "0"
 PHASE_LIMITS = {"init": 180, "setup": 420, "ipc": 90, "autotune": 180, "warmup": 240, "timed": 420,
                 "report": 120}
 
@@ -158,6 +160,11 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     from zest_amd.synthetic import SyntheticWorld
 
     cuda = device.type == "cuda"
+    # The peer-mapped exchanges (ipc DMA copies / xgmi K8 kernel) are tried under auto too; a failed
+    # or timed-out mapping falls back to the RCCL exchanges.  ZEST_EXCHANGE_IPC=0 turns them off.
+    want_ipc = world_size > 1 and cuda and (
+        a.exchange in ("ipc", "xgmi") or (a.exchange == "auto" and os.environ.get("ZEST_EXCHANGE_IPC", IPC_AUTO) != "0"))
+    mapped = arenas.get("peers") if arenas is not None else None
     wd.arm("setup")
     t_setup = time.time()
     # bf16 mode stores chunks the way Xet stores real checkpoints: BG4-LZ4 frames (compressed on the
@@ -176,6 +183,16 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
             arena = ops.padded_empty(world.arena_bytes, device)
             if arenas is not None:
                 arenas["arena"] = arena
+            if want_ipc:
+                # map the peers' arenas while they are fresh allocations, before any kernel wrote
+                # them (imports of a built arena were seen to hang, docs/PARITY.md)
+                from zest_amd.engine import map_peer_arenas
+                wd.arm("ipc")
+                mapped = map_peer_arenas(arena, rank, world_size)
+                wd.arm("setup")
+                if arenas is not None:
+                    arenas["peers"] = mapped
+                log(rank, f"peer arenas mapped over HIP IPC before the build: {mapped is not None}")
         world.generate_on_device(arena)
         world.build_on_device(arena)
         torch.cuda.synchronize()
@@ -203,15 +220,8 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
                           seeders=seeders, origin_reserve=reserve)
     ipc = False
-    if world_size > 1 and cuda:
-        # The peer-mapped exchanges are opt-in under auto (ZEST_EXCHANGE_IPC=1): a 16 GB arena
-        # import once hung inside hipIpcOpenMemHandle in a 2-rank rehearsal on one GPU (docs/PARITY.md).
-        want_ipc = a.exchange in ("ipc", "xgmi") or (a.exchange == "auto" and os.environ.get("ZEST_EXCHANGE_IPC") == "1")
-        if want_ipc:
-            wd.arm("ipc")
-            ipc = puller.enable_ipc()
-            wd.arm("setup")
-        log(rank, f"peer arenas mapped over HIP IPC: {ipc}")
+    if want_ipc:
+        ipc = mapped is not None and puller.enable_ipc(mapped)
         if a.exchange in ("ipc", "xgmi") and not ipc:
             raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
     if cuda:

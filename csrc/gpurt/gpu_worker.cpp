@@ -24,6 +24,7 @@
 #include <cstring>
 #include <deque>
 #include <iostream>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -183,6 +184,41 @@ int run(int argc, char** argv) {
   const int rank = env_int("ZEST_GPU_RANK", 0), world = std::max(1, env_int("ZEST_GPU_WORLD", 1));
   const char* status_path = std::getenv("ZEST_GPU_STATUS");
   Config cfg = Config::from_env();
+  // HIP runtime start-up and the device pipeline (Xet auth, pinned staging) come up on a side
+  // thread while this one lists the repository: both are a few hundred ms on a fresh process.
+  std::unique_ptr<gpurt::DeviceXetPull> dp;
+  std::string init_err;
+  double t_init = 0;
+  std::thread init([&] {
+    try {
+      int dev_count = 0;
+      hip_ok(hipGetDeviceCount(&dev_count), "hipGetDeviceCount");
+      if (dev_count < 1) throw Error("NoDevice", "no GPU visible to this worker");
+      hip_ok(hipSetDevice(0), "hipSetDevice");  // the CLI pinned this worker with HIP_VISIBLE_DEVICES
+      gpurt::DevicePullOptions o;
+      o.repo = a.repo;
+      o.revision = a.revision;
+      o.repo_type = a.repo_type;
+      o.p2p = a.p2p;
+      o.peers = a.peers;
+      o.tracker = a.tracker;
+      o.dht = a.dht;
+      o.dht_bootstrap = a.dht_bootstrap;
+      o.device = 0;
+      o.staging_bytes = a.staging_mb << 20;
+      o.threads = a.threads;
+      dp = std::make_unique<gpurt::DeviceXetPull>(o);
+    } catch (const std::exception& e) {
+      init_err = e.what();
+    }
+    t_init = now_s();
+  });
+  struct Join {
+    std::thread& t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } join_init{init};
   std::vector<hub::RepoFile> files = hub::list_files(cfg, a.repo, a.revision, a.repo_type);
   const std::string commit = hub::resolve_commit(cfg, a.repo, a.revision, a.repo_type).value_or(a.revision);
   const std::string snap = cfg.snapshot_dir(a.repo, commit);
@@ -213,29 +249,17 @@ int run(int argc, char** argv) {
       todo.push_back(xet[i]);
     }
   }
-  int dev_count = 0;
-  hip_ok(hipGetDeviceCount(&dev_count), "hipGetDeviceCount");
-  if (dev_count < 1) throw Error("NoDevice", "no GPU visible to this worker");
-  hip_ok(hipSetDevice(0), "hipSetDevice");  // the CLI pinned this worker with HIP_VISIBLE_DEVICES
+  // largest first: the write-back of the file pulled last is the un-overlapped tail
+  std::stable_sort(todo.begin(), todo.end(), [](const hub::RepoFile& x, const hub::RepoFile& y) { return x.size > y.size; });
+  const double t_list = now_s();
+  init.join();
+  if (!init_err.empty()) throw Error("DeviceInit", init_err);
   const double t_ready = now_s();
   uint64_t done_bytes = 0;
   size_t failed = 0;
   std::string stats = "{}";
-  double t_pull = 0, t_write = 0;
+  double t_pull = 0, t_write = 0, t_bufs = t_ready, t_last_pull = t_ready, t_last_write = t_ready;
   if (!todo.empty()) {
-    gpurt::DevicePullOptions o;
-    o.repo = a.repo;
-    o.revision = a.revision;
-    o.repo_type = a.repo_type;
-    o.p2p = a.p2p;
-    o.peers = a.peers;
-    o.tracker = a.tracker;
-    o.dht = a.dht;
-    o.dht_bootstrap = a.dht_bootstrap;
-    o.device = 0;
-    o.staging_bytes = a.staging_mb << 20;
-    o.threads = a.threads;
-    gpurt::DeviceXetPull dp(o);
     uint64_t max_size = 1;
     for (auto& f : todo) max_size = std::max(max_size, f.size);
     // Device buffer pool: file i is pulled into a free buffer while earlier files are written back
@@ -249,6 +273,7 @@ int run(int argc, char** argv) {
     const int wslots = std::max(2, env_int("ZEST_GPU_WRITE_SLOTS", 3));
     std::vector<uint8_t*> bufs(std::min(nbuf, todo.size()), nullptr);
     for (auto& bp : bufs) hip_ok(hipMalloc(reinterpret_cast<void**>(&bp), max_size + 4096), "hipMalloc");
+    t_bufs = now_s();
     std::vector<int> free_bufs;
     for (int k = int(bufs.size()) - 1; k >= 0; --k) free_bufs.push_back(k);
     std::mutex mu;
@@ -277,7 +302,8 @@ int run(int argc, char** argv) {
           storage::write_verified_marker(cfg, a.repo, commit, f.path, *f.xet_hash, dst);  // verified on the GPU
           std::lock_guard<std::mutex> g(mu);
           done_bytes += f.size;
-          t_write += now_s() - tw;
+          t_last_write = now_s();
+          t_write += t_last_write - tw;
           std::cout << "[gpu " << rank << "] " << f.path << " [xet] " << f.size / 1e6 << " MB verified on the GPU\n"
                     << std::flush;
         } catch (const std::exception& e) {
@@ -306,7 +332,7 @@ int run(int argc, char** argv) {
         free_bufs.pop_back();
       }
       try {
-        dp.pull_files({{*todo[i].xet_hash, reinterpret_cast<uintptr_t>(bufs[size_t(b)]), todo[i].size}});
+        dp->pull_files({{*todo[i].xet_hash, reinterpret_cast<uintptr_t>(bufs[size_t(b)]), todo[i].size}});
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu);
         std::cerr << "[gpu " << rank << "] " << todo[i].path << ": error " << e.what() << "\n";
@@ -315,6 +341,7 @@ int run(int argc, char** argv) {
         continue;
       }
       std::lock_guard<std::mutex> g(mu);
+      t_last_pull = now_s();
       queue.emplace_back(i, b);
       cv.notify_all();
     }
@@ -328,19 +355,24 @@ int run(int argc, char** argv) {
     }
     for (auto& t : writers) t.join();
     for (auto& bp : bufs) (void)hipFree(bp);
-    stats = dp.stats_json();
+    stats = dp->stats_json();
   }
   const double dt = now_s() - t0;
   std::cout << "[gpu " << rank << "] " << done_bytes / 1e9 << " GB in " << dt << " s (start " << t_ready - t0
             << " s, device pulls " << t_pull << " s, writes " << t_write << " s summed over writer threads, "
-            << "overlapped)\n"
+            << "overlapped)\n";
+  auto rel = [&](double t) { return std::to_string(int((t - t0) * 1000)); };
+  std::cout << "[gpu " << rank << "] timeline ms: listed " << rel(t_list) << ", device ready " << rel(t_init)
+            << ", buffers " << rel(t_bufs) << ", last pull " << rel(t_last_pull) << ", last write "
+            << rel(t_last_write) << ", end " << rel(now_s()) << "\n"
             << std::flush;
   if (status_path) {
     json::Writer w;
     w.obj().key("complete").boolean(true).key("rank").num(int64_t(rank)).key("world").num(int64_t(world));
     w.key("failed_files").num_u(failed).key("bytes").num_u(done_bytes).key("files").num_u(todo.size());
     w.key("cached_files").num_u(cached).key("seconds").num(dt, 3).key("pull_s").num(t_pull, 3);
-    w.key("write_s").num(t_write, 3).key("stats").raw(stats).end();
+    w.key("write_s").num(t_write, 3).key("init_s").num(t_init - t0, 3).key("list_s").num(t_list - t0, 3);
+    w.key("stats").raw(stats).end();
     storage::write_file_atomic(status_path, w.out() + "\n", true);
   }
   return failed ? 1 : 0;

@@ -43,6 +43,8 @@ def main() -> int:
     ap.add_argument("--cli-configs", default="",
                     help="';'-separated env settings for repeated `zest pull --gpus 1` runs, e.g. "
                          "'ZEST_GPU_WRITERS=1;ZEST_GPU_WRITERS=2,ZEST_GPU_WRITE_SLOTS=3'")
+    ap.add_argument("--host-after", action="store_true",
+                    help="time the host pull again after the GPU CLI configs (order check)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -96,16 +98,28 @@ def main() -> int:
             print(f"[direct, ZEST_CACHE_WRITES=0] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
             del out
             torch.cuda.empty_cache()
-        if not a.skip_host:
-            env = dict(os.environ, **hub.env(str(work / "host")))
+
+        def settle():
+            # every timed pull starts with no dirty page cache of an earlier one still being written
+            t = time.time()
+            os.sync()
+            return round(time.time() - t, 3)
+
+        def host_pull(tag):
+            env = dict(os.environ, **hub.env(str(work / tag)))
             if a.trace_host:
                 env["ZEST_TRACE"] = a.trace_host
+            synced = settle()
             t0 = time.time()
             r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
                                 "--no-dht"], env=env, capture_output=True, text=True, timeout=3600)
             t1 = time.time()
             if r.returncode != 0:
                 raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
+            return t0, t1, synced
+
+        if not a.skip_host:
+            t0, t1, synced = host_pull("host")
             snap = work / "host" / "hf" / "hub" / ("models--" + spec.repo_id.replace("/", "--")) / "snapshots" / commit
             hashes = {f.path: world.file_hash_hex(i) for i, f in enumerate(world.xet_files)}
             tensors = zdev.load_snapshot(str(snap), dev, hashes)
@@ -113,10 +127,12 @@ def main() -> int:
             t2 = time.time()
             res.update(host_pull_s=round(t1 - t0, 3), host_pull_gbps=round(total / (t1 - t0) / 1e9, 3),
                        load_verify_s=round(t2 - t1, 3), load_verify_gbps=round(total / (t2 - t1) / 1e9, 3),
-                       host_path_gbps=round(total / (t2 - t0) / 1e9, 3), host_tensors=len(tensors))
+                       host_path_gbps=round(total / (t2 - t0) / 1e9, 3), host_tensors=len(tensors),
+                       host_presync_s=synced)
             print(f"[host] zest pull to disk {total / (t1 - t0) / 1e9:.2f} GB/s, then load + GPU verify "
                   f"{total / (t2 - t1) / 1e9:.2f} GB/s -> end to end {total / (t2 - t0) / 1e9:.2f} GB/s", flush=True)
             del tensors
+            subprocess.run(["rm", "-rf", str(work / "host")])
         if not a.skip_gpu_cli:
             # `zest pull --gpus 1`: the CLI's GPU worker (native zest-gpu-worker) pulls device-direct,
             # decodes + verifies on the GPU and writes the HF-cache snapshot
@@ -124,6 +140,7 @@ def main() -> int:
             for ci, cfg in enumerate(configs):
                 extra = dict(kv.split("=", 1) for kv in cfg.split(",") if kv)
                 env = dict(os.environ, **hub.env(str(work / f"gpucli{ci}")), **extra)
+                synced = settle()
                 t0 = time.time()
                 r = subprocess.run([str(ROOT / "zest_amd" / "_bin" / "zest"), "pull", spec.repo_id, "--peer", peer,
                                     "--no-dht", "--gpus", "1"], env=env, capture_output=True, text=True, timeout=3600)
@@ -133,7 +150,7 @@ def main() -> int:
                 tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
                 workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and " GB in " in ln]
                 key = "gpu_cli" if not cfg else f"gpu_cli[{cfg}]"
-                res[key] = {"s": round(dt, 3), "gbps": round(total / dt / 1e9, 3), "workers": workers}
+                res[key] = {"s": round(dt, 3), "gbps": round(total / dt / 1e9, 3), "workers": workers, "presync_s": synced}
                 if not cfg:
                     res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
                                gpu_cli_summary=tail[-1] if tail else "", gpu_cli_workers=workers)
@@ -141,6 +158,11 @@ def main() -> int:
                     print(f"[gpu cli worker {cfg}] {ln}", flush=True)
                 print(f"[gpu cli {cfg}] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
                 subprocess.run(["rm", "-rf", str(work / f"gpucli{ci}")])
+        if a.host_after:
+            t0, t1, synced = host_pull("host_after")
+            res.update(host_after_s=round(t1 - t0, 3), host_after_gbps=round(total / (t1 - t0) / 1e9, 3))
+            print(f"[host, again] zest pull to disk {total / (t1 - t0) / 1e9:.2f} GB/s", flush=True)
+            subprocess.run(["rm", "-rf", str(work / "host_after")])
         res["seeder"] = srv.stats()
         print(json.dumps(res), flush=True)
         if a.out:

@@ -204,6 +204,79 @@ def split_rounds(world: SyntheticWorld, a: int, b: int, weights) -> list[tuple[i
     return [(int(cuts[k]), int(cuts[k + 1])) for k in range(n_rounds)]
 
 
+@dataclass
+class PeerArenas:
+    """Every peer's arena mapped into this process (``peers[rank]`` is None), plus the gloo group the
+    ``ipc`` exchange's host barriers use."""
+    arena: "torch.Tensor"
+    peers: list
+    host_group: object
+
+
+def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: float | None = None):
+    """Collective: export this rank's arena with HIP IPC and import every peer's.  Returns a
+    :class:`PeerArenas`, or None unless every rank mapped every peer (MIN-reduced).
+
+    Best called right after the arena is allocated, before any kernel has written it: imports of a
+    16 GB arena that already held a built synthetic model were seen to hang in
+    ``hipIpcOpenMemHandle`` (2 ranks on one GPU, docs/PARITY.md).  ``deadline_s`` (default
+    ``ZEST_IPC_DEADLINE`` = 60 s) bounds each import: a rank whose import does not return in time
+    reports failure, and the caller falls back to an RCCL exchange."""
+    import threading
+
+    import torch.distributed as dist
+    from torch.multiprocessing.reductions import reduce_tensor
+    if arena.device.type != "cuda" or n_ranks == 1:
+        return None
+    if deadline_s is None:
+        deadline_s = float(os.environ.get("ZEST_IPC_DEADLINE", "60"))
+    try:
+        mine = reduce_tensor(arena)
+    except Exception:
+        mine = None
+    objs = [None] * n_ranks
+    dist.all_gather_object(objs, mine, group=group)
+    # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
+    host_group = dist.new_group(backend="gloo")
+    peers = [None] * n_ranks
+    ok = 1
+    # One rank imports at a time: two processes opening each other's large dmabuf handles at the
+    # same moment deadlocked inside hipIpcOpenMemHandle (16 GB arenas, 2 ranks on one MI355X); an
+    # exporter that is idle in a barrier answers at once.
+    for turn in range(n_ranks):
+        if turn == rank:
+            res: dict = {}
+
+            def imp():
+                try:
+                    H = ops.hip()
+                    for p, o in enumerate(objs):
+                        if p != rank:
+                            if o is None:
+                                raise RuntimeError(f"rank {p} could not export its arena")
+                            fn, args = o
+                            t = fn(*args)
+                            if t.device != arena.device and not H.enable_peer_access(t.device.index):
+                                raise RuntimeError(f"no peer access to {t.device}")
+                            res[p] = t
+                except Exception as e:  # noqa: BLE001
+                    res["error"] = e
+            th = threading.Thread(target=imp, daemon=True)
+            th.start()
+            th.join(deadline_s)
+            if th.is_alive() or "error" in res:
+                ok = 0  # a hung import stays parked in its daemon thread; this rank reports failure
+            else:
+                for p in range(n_ranks):
+                    peers[p] = res.get(p)
+        dist.barrier(group=host_group)
+    flag = torch.tensor([ok], dtype=torch.int32, device=arena.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if not int(flag.item()):
+        return None
+    return PeerArenas(arena, peers, host_group)
+
+
 class DevicePuller:
     def __init__(self, world: SyntheticWorld, arena: torch.Tensor, rank: int = 0, n_ranks: int = 1,
                  round_bytes: int = 1 << 30, slots: int = 3, group=None, exchange: str = "p2p",
@@ -524,44 +597,19 @@ class DevicePuller:
         self._gather_used[b] = True
         return [_StreamJoin(self._unpack_stream)]
 
-    def enable_ipc(self) -> bool:
-        """Map every peer's arena into this process (HIP IPC over dmabuf) for the ``ipc`` exchange.
-        Collective; returns True only if every rank mapped every peer (MIN-reduced)."""
-        import torch.distributed as dist
-        from torch.multiprocessing.reductions import reduce_tensor
+    def enable_ipc(self, mapped: "PeerArenas | None" = None) -> bool:
+        """Map every peer's arena into this process (HIP IPC over dmabuf) for the ``ipc`` / ``xgmi``
+        exchanges.  ``mapped``: the result of :func:`map_peer_arenas` done earlier (right after the
+        arena was allocated); otherwise the mapping is done now.  Collective; True only if every rank
+        mapped every peer."""
         if not self.is_cuda or self.n_ranks == 1:
             return False
-        try:
-            mine = reduce_tensor(self.arena)
-        except Exception:
-            mine = None
-        objs = [None] * self.n_ranks
-        dist.all_gather_object(objs, mine, group=self.group)
-        # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
-        self._host_group = dist.new_group(backend="gloo")
-        peers = [None] * self.n_ranks
-        ok = 1
-        # One rank imports at a time: two processes opening each other's large dmabuf handles at
-        # the same moment deadlock inside hipIpcOpenMemHandle (seen with 16 GB arenas, 2 ranks on
-        # one MI355X: both stuck in the open); an exporter that is idle in a barrier answers at once.
-        for turn in range(self.n_ranks):
-            if turn == self.rank:
-                try:
-                    H = ops.hip()
-                    for p, o in enumerate(objs):
-                        if p != self.rank:
-                            fn, args = o
-                            peers[p] = fn(*args)
-                            if peers[p].device != self.device and not H.enable_peer_access(peers[p].device.index):
-                                ok = 0
-                except Exception:
-                    ok = 0
-            dist.barrier(group=self._host_group)
-        flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        if not int(flag.item()):
+        if mapped is None:
+            mapped = map_peer_arenas(self.arena, self.rank, self.n_ranks, self.group)
+        if mapped is None or mapped.arena.data_ptr() != self.arena.data_ptr():
             return False
-        self._peer_arenas = peers
+        self._host_group = mapped.host_group
+        self._peer_arenas = mapped.peers
         self._ipc_streams = [_role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
         self._ipc_done = {}
         return True
