@@ -71,14 +71,24 @@ struct DeviceXetPull::Impl {
     const auto& peers = o.peers;
     const auto& tracker = o.tracker;
     const auto& dht_bootstrap = o.dht_bootstrap;
-    registry_.scan(cfg_);
-    cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
+    {
+      trace::Span sp("device", "init: cache scan");
+      registry_.scan(cfg_);
+      cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
+    }
     std::vector<net::Addr> boot;
     for (auto& b : dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
-    swarm_ = std::make_unique<SwarmDownloader>(cfg_, tracker, p2p, dht && p2p, boot);
-    for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
+    {
+      trace::Span sp("device", "init: swarm");
+      swarm_ = std::make_unique<SwarmDownloader>(cfg_, tracker, p2p, dht && p2p, boot);
+      for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
+    }
     bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
-    bridge_->authenticate(repo, repo_type, revision);
+    {
+      trace::Span sp("device", "init: xet auth");
+      bridge_->authenticate(repo, repo_type, revision);
+    }
+    trace::Span sp("device", "init: staging alloc");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& s : slots_) {
@@ -112,6 +122,7 @@ struct DeviceXetPull::Impl {
     const size_t nf = files.size();
     std::vector<cas::Reconstruction> recs(nf);
     {
+      trace::Span sp("device", "reconstructions");
       std::vector<std::string> errs(nf);
       std::atomic<size_t> k{0};
       auto w = [&]() {
@@ -137,6 +148,7 @@ struct DeviceXetPull::Impl {
     for (int attempt = 0; attempt < 2 && !todo.empty(); ++attempt) {
       FetchOptions opt;
       opt.repair = attempt > 0;
+      attempt_ = attempt;
       Attempt at = run_once(files, recs, todo, opt);
       fetched += at.fetched;
       if (!at.fetch_err.empty()) {
@@ -188,6 +200,9 @@ struct DeviceXetPull::Impl {
 
   size_t staging_bytes() const { return cap_; }
 
+  PullProgressFn progress_;  // set for the duration of one pull_files call
+  int attempt_ = 0;
+
   struct TermSource {
     Source src = Source::Cdn;
     uint32_t run_offset = 0;
@@ -232,7 +247,7 @@ struct DeviceXetPull::Impl {
       uint64_t ulen;
     };
     std::vector<GTerm> gt;
-    std::vector<uint64_t> file_chunk0(nf + 1, 0);
+    std::vector<uint64_t> file_chunk0(nf + 1, 0), file_dst0(nf, 0);
     uintptr_t base = UINTPTR_MAX, top_addr = 0;
     for (size_t f = 0; f < nf; ++f) {
       const auto& fl = all_files[todo[f]];
@@ -244,6 +259,7 @@ struct DeviceXetPull::Impl {
       const auto& rec = all_recs[todo[f]];
       if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
       at.sources[f].resize(rec.terms.size());
+      file_dst0[f] = std::get<1>(fl) - base;
       uint64_t off = 0, c = file_chunk0[f];
       for (size_t i = 0; i < rec.terms.size(); ++i) {
         const auto& t = rec.terms[i];
@@ -424,9 +440,18 @@ struct DeviceXetPull::Impl {
           // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
           hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
           if (b + 2 < nb) s.chunks_host.assign(size_t(chunk_hi(b + 2) - chunk_lo(b + 2)), ZgChunk{});
-          std::lock_guard<std::mutex> g(mu);
-          ready[b & 1] = b + 2;
-          cv.notify_all();
+          {
+            std::lock_guard<std::mutex> g(mu);
+            ready[b & 1] = b + 2;
+            cv.notify_all();
+          }
+          if (progress_) {
+            // batches run in term order, and terms are in file order: each touched file's bytes
+            // are complete up to the end of its last term in this batch
+            for (size_t i = bt.begin; i < bt.end; ++i)
+              if (i + 1 == bt.end || gt[i + 1].file != gt[i].file)
+                progress_(todo[gt[i].file], attempt_, gt[i].dst + gt[i].ulen - file_dst0[gt[i].file]);
+          }
         }
       } catch (const std::exception& e) {
         fail(e.what());
@@ -509,10 +534,16 @@ struct DeviceXetPull::Impl {
 DeviceXetPull::DeviceXetPull(const DevicePullOptions& opt) : impl_(std::make_unique<Impl>(opt)) {}
 DeviceXetPull::~DeviceXetPull() = default;
 
-std::vector<PullFileStats> DeviceXetPull::pull_files(const std::vector<PullRequest>& files) {
+std::vector<PullFileStats> DeviceXetPull::pull_files(const std::vector<PullRequest>& files,
+                                                     const PullProgressFn& progress) {
   std::vector<std::tuple<std::string, uintptr_t, uint64_t>> f;
   f.reserve(files.size());
   for (const auto& r : files) f.emplace_back(r.xet_hash, r.dst, r.size);
+  impl_->progress_ = progress;
+  struct Reset {
+    PullProgressFn& p;
+    ~Reset() { p = nullptr; }
+  } reset{impl_->progress_};
   return impl_->pull_files(f);
 }
 

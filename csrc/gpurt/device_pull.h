@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <optional>
 #include <string>
@@ -43,6 +44,12 @@ struct PullFileStats {
   std::vector<uint32_t> chunk_lens;  // uncompressed size of every chunk, in file order
 };
 
+// Called on the pipeline's submit thread after a staging batch's kernels completed: file `file`
+// (index into the request list) now holds its verified-or-not bytes [0, bytes) in HBM.  `attempt` is
+// 0 for the first pass and 1 for the CDN repair pass of files whose Merkle root missed (which
+// overwrites their bytes).  Keep it cheap: the next batch waits for it.
+using PullProgressFn = std::function<void(size_t file, int attempt, uint64_t bytes)>;
+
 class DeviceXetPull {
  public:
   explicit DeviceXetPull(const DevicePullOptions& opt);
@@ -52,7 +59,7 @@ class DeviceXetPull {
   // Pull several files through ONE pipeline (staging batches cross file boundaries; one Merkle
   // launch verifies all of them).  Throws zest::Error ("HashMismatch", "DownloadFailed", ...) when a
   // file cannot be verified after its CDN repair pass.
-  std::vector<PullFileStats> pull_files(const std::vector<PullRequest>& files);
+  std::vector<PullFileStats> pull_files(const std::vector<PullRequest>& files, const PullProgressFn& progress = {});
   std::string stats_json() const;
   size_t staging_bytes() const;
 

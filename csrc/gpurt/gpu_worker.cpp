@@ -4,9 +4,10 @@
 // talk to each other; the CLI aggregates their status files).
 //
 //   list files (Hub API) -> this worker's Xet files (LPT by size over ZEST_GPU_WORLD workers)
-//   -> skip verified cached files -> device-direct pull (DeviceXetPull: fetch -> pinned -> H2D ->
-//   GPU decode + BLAKE3 + Merkle verify into HBM) -> snapshot write-back (D2H in 256 MiB pieces
-//   into pinned slots on a side stream, pwrite threads), overlapped with the next file's pull.
+//   -> skip verified cached files -> device-direct pull of all of them in one call (DeviceXetPull:
+//   fetch -> pinned -> H2D -> GPU decode + BLAKE3 + Merkle verify into HBM) -> snapshot write-back
+//   streaming behind the pull (64 MiB pieces, D2H + pwrite threads, into `.incomplete` files that
+//   are renamed once the pull verified them).
 //
 // Environment: ZEST_GPU_RANK / ZEST_GPU_WORLD (this worker's index and the worker count),
 // ZEST_GPU_STATUS (path of this worker's JSON status: written only when the worker ran to the end).
@@ -26,6 +27,7 @@
 #include <iostream>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -35,6 +37,7 @@
 #include "hub.h"
 #include "json.h"
 #include "storage.h"
+#include "trace.h"
 
 using namespace zest;
 
@@ -68,83 +71,144 @@ std::vector<int> assign_owners(const std::vector<uint64_t>& sizes, int world) {
   return owner;
 }
 
-// Device buffer -> file: D2H of piece k+1 (side stream, pinned slot) overlaps the pwrite of piece k
-// (`writers` threads).  The snapshot write is the slow leg of a GPU pull (page cache), so it runs on
-// several threads and overlaps the next file's device pull.
-class Writer {
+// Snapshot write-back that streams while the device pull runs: the pull reports, after each
+// staging batch, how much of each file is in HBM (PullProgressFn); those bytes are queued as pieces,
+// and `threads` writers each copy a piece to a pinned buffer (own stream) and pwrite it into the
+// file's `.incomplete` temp file.  The file is renamed into the snapshot only once the whole pull
+// call verified it.  A buffered pwrite holds the file's inode lock, so one file takes ~10 GB/s on
+// the box (profiles/write_probe_box_r3.jsonl) -- below the ~14 GB/s the pull delivers -- but the
+// files of a pull arrive one after the other and their writes overlap each other.
+class WriteBack {
  public:
-  Writer(size_t piece, int slots) : piece_(piece) {
-    hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    slots_.resize(size_t(slots));
-    for (auto& s : slots_) {
-      hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.host), piece_, hipHostMallocDefault), "hipHostMalloc");
-      hip_ok(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
-    }
-  }
-  ~Writer() {
-    (void)hipStreamSynchronize(stream_);
-    for (auto& s : slots_) {
-      if (s.host) (void)hipHostFree(s.host);
-      if (s.ev) (void)hipEventDestroy(s.ev);
-    }
-    (void)hipStreamDestroy(stream_);
-  }
-
-  // ZEST_GPU_ODIRECT=1: whole 4 KiB-multiple pieces go to the file with O_DIRECT straight from the
-  // pinned slot (DMA, no CPU copy into the page cache; the tail piece is written buffered).
-  void write(const uint8_t* dev, uint64_t n, const std::string& path) {
-    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    if (fd < 0) throw Error("IoError", "open " + path + ": " + std::strerror(errno));
-    int dfd = -1;
-    if (env_int("ZEST_GPU_ODIRECT", 0) == 1) dfd = ::open(path.c_str(), O_WRONLY | O_DIRECT | O_CLOEXEC);
+  struct File {
+    std::string dst, tmp;
+    const uint8_t* dev = nullptr;
+    uint64_t size = 0, queued = 0;
+    int fd = -1;
+    bool repaired = false;  // a repair pass overwrote its bytes: written again after the pull
     std::string err;
-    std::vector<std::thread> th;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<int> busy(slots_.size(), 0);
-    bool failed = false;
-    for (uint64_t off = 0, k = 0; off < n && !failed; off += piece_, ++k) {
-      const size_t s = size_t(k % slots_.size());
-      {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return !busy[s] || failed; });
-        if (failed) break;
-        busy[s] = 1;
-      }
-      const uint64_t m = std::min<uint64_t>(piece_, n - off);
-      hip_ok(hipMemcpyAsync(slots_[s].host, dev + off, m, hipMemcpyDeviceToHost, stream_), "D2H");
-      hip_ok(hipEventRecord(slots_[s].ev, stream_), "event");
-      th.emplace_back([&, s, m, off] {
-        std::string e;
-        if (hipEventSynchronize(slots_[s].ev) != hipSuccess) e = "D2H failed";
-        const int wfd = (dfd >= 0 && m % 4096 == 0 && off % 4096 == 0) ? dfd : fd;
-        for (uint64_t done = 0; e.empty() && done < m;) {
-          const ssize_t w = ::pwrite(wfd, slots_[s].host + done, size_t(m - done), off_t(off + done));
-          if (w < 0 && errno == EINTR) continue;
-          if (w <= 0) e = std::string("pwrite: ") + std::strerror(errno);
-          else done += uint64_t(w);
-        }
-        std::lock_guard<std::mutex> g(mu);
-        if (!e.empty() && err.empty()) err = e, failed = true;
-        busy[s] = 0;
-        cv.notify_all();
-      });
+  };
+
+  WriteBack(int threads, size_t piece) : piece_(piece) {
+    for (int t = 0; t < threads; ++t) {
+      Lane l;
+      hip_ok(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreate");
+      hip_ok(hipHostMalloc(reinterpret_cast<void**>(&l.host), piece_, hipHostMallocDefault), "hipHostMalloc");
+      lanes_.push_back(l);
     }
-    for (auto& t : th) t.join();
-    if (dfd >= 0) ::close(dfd);
-    ::close(fd);
-    if (!err.empty()) throw Error("IoError", path + ": " + err);
+  }
+  ~WriteBack() { stop(); }  // pinned buffers and streams go with the process (the worker _Exits)
+
+  void start(std::vector<File>* files) {
+    files_ = files;
+    closing_ = false;
+    for (size_t t = 0; t < lanes_.size(); ++t) threads_.emplace_back([this, t] { loop(lanes_[t]); });
+  }
+  // PullProgressFn: file f holds [0, bytes) in HBM after a batch of attempt `attempt`
+  void progress(size_t f, int attempt, uint64_t bytes) {
+    std::lock_guard<std::mutex> g(mu_);
+    File& fl = (*files_)[f];
+    if (attempt > 0) {
+      fl.repaired = true;
+      return;
+    }
+    post_locked(f, fl.queued, bytes);
+    fl.queued = std::max(fl.queued, bytes);
+  }
+  void post(size_t f, uint64_t lo, uint64_t hi) {
+    std::lock_guard<std::mutex> g(mu_);
+    post_locked(f, lo, hi);
+  }
+  void drain() {
+    std::unique_lock<std::mutex> g(mu_);
+    idle_.wait(g, [&] { return pending_ == 0; });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      closing_ = true;
+      work_.notify_all();
+    }
+    for (auto& t : threads_) t.join();
+    threads_.clear();
   }
 
  private:
-  struct Slot {
+  struct Lane {
+    hipStream_t stream = nullptr;
     uint8_t* host = nullptr;
-    hipEvent_t ev = nullptr;
   };
+  struct Piece {
+    size_t file;
+    uint64_t off, len;
+  };
+  void post_locked(size_t f, uint64_t lo, uint64_t hi) {
+    for (uint64_t o = lo; o < hi; o += piece_) {
+      q_.push_back({f, o, std::min<uint64_t>(piece_, hi - o)});
+      ++pending_;
+    }
+    work_.notify_all();
+  }
+  void loop(Lane& l) {
+    while (true) {
+      Piece p;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        work_.wait(g, [&] { return closing_ || !q_.empty(); });
+        if (q_.empty()) return;
+        p = q_.front();
+        q_.pop_front();
+      }
+      File& fl = (*files_)[p.file];
+      std::string e;
+      {
+        trace::Span sp("write", "D2H piece");
+        if (hipMemcpyAsync(l.host, fl.dev + p.off, p.len, hipMemcpyDeviceToHost, l.stream) != hipSuccess ||
+            hipStreamSynchronize(l.stream) != hipSuccess)
+          e = "D2H failed";
+      }
+      trace::Span sp("write", "pwrite piece");
+      for (uint64_t done = 0; e.empty() && done < p.len;) {
+        const ssize_t w = ::pwrite(fl.fd, l.host + done, size_t(p.len - done), off_t(p.off + done));
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) e = std::string("pwrite: ") + std::strerror(errno);
+        else done += uint64_t(w);
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      if (!e.empty() && fl.err.empty()) fl.err = e;
+      if (--pending_ == 0) idle_.notify_all();
+    }
+  }
+
   size_t piece_;
-  hipStream_t stream_ = nullptr;
-  std::vector<Slot> slots_;
+  std::vector<Lane> lanes_;
+  std::vector<std::thread> threads_;
+  std::vector<File>* files_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable work_, idle_;
+  std::deque<Piece> q_;
+  size_t pending_ = 0;
+  bool closing_ = false;
 };
+
+// One stats object for the status file: the pipelines' byte and xorb counters summed.
+std::string merged_stats(const std::vector<std::unique_ptr<gpurt::DeviceXetPull>>& dps) {
+  static const char* keys[] = {"xorbs_from_cache", "xorbs_from_peer", "xorbs_from_cdn", "bytes_from_cache",
+                               "bytes_from_peer",  "bytes_from_cdn",  "verify_failures", "refetches"};
+  double sum[8] = {0};
+  for (auto& d : dps) {
+    if (!d) continue;
+    const json::Value v = json::Value::parse(d->stats_json());
+    for (int i = 0; i < 8; ++i) sum[i] += v[keys[i]].as_double();
+  }
+  json::Writer w;
+  w.obj();
+  for (int i = 0; i < 8; ++i) w.key(keys[i]).num_u(uint64_t(sum[i]));
+  const double total = sum[3] + sum[4] + sum[5];
+  w.key("p2p_ratio").num(total > 0 ? sum[4] / total : 0.0, 4).key("pipelines").num_u(dps.size());
+  w.end();
+  return w.out();
+}
 
 struct Args {
   std::string repo, revision = "main", repo_type = "model";
@@ -152,7 +216,7 @@ struct Args {
   std::optional<std::string> tracker;
   bool p2p = true, dht = true;
   int threads = 16;
-  size_t staging_mb = 1024;
+  size_t staging_mb = size_t(std::max(16, env_int("ZEST_GPU_STAGING_MB", 512)));
 };
 
 Args parse(int argc, char** argv) {
@@ -179,6 +243,9 @@ Args parse(int argc, char** argv) {
 
 int run(int argc, char** argv) {
   const double t0 = now_s();
+  // ZEST_GPU_TRACE=<file.json>: this worker's Chrome trace (ZEST_TRACE would be shared with the CLI)
+  if (const char* tp = std::getenv("ZEST_GPU_TRACE"); tp && *tp)
+    trace::set_output(std::string(tp) + "." + std::to_string(env_int("ZEST_GPU_RANK", 0)));
   const Args a = parse(argc, argv);
   if (a.repo.empty()) throw Error("Usage", "zest-gpu-worker <repo_id> [pull options]");
   const int rank = env_int("ZEST_GPU_RANK", 0), world = std::max(1, env_int("ZEST_GPU_WORLD", 1));
@@ -186,15 +253,24 @@ int run(int argc, char** argv) {
   Config cfg = Config::from_env();
   // HIP runtime start-up and the device pipeline (Xet auth, pinned staging) come up on a side
   // thread while this one lists the repository: both are a few hundred ms on a fresh process.
-  std::unique_ptr<gpurt::DeviceXetPull> dp;
+  // ZEST_GPU_PIPES device pipelines pull different files at the same time, so the write-back
+  // always has several files (inodes) to write into at once.
+  const int npipes = std::max(1, env_int("ZEST_GPU_PIPES", 2));
+  std::vector<std::unique_ptr<gpurt::DeviceXetPull>> dps(static_cast<size_t>(npipes));
+  // Write-back: `nwriters` threads, each with its own D2H stream and a pinned piece buffer.
+  const int nwriters = std::max(1, env_int("ZEST_GPU_WRITERS", 4));
+  const size_t piece = size_t(std::max(4, env_int("ZEST_GPU_PIECE_MB", 64))) << 20;
+  std::unique_ptr<WriteBack> wb;
   std::string init_err;
-  double t_init = 0;
+  double t_init = 0, t_hip = 0, t_dp = 0;
   std::thread init([&] {
     try {
       int dev_count = 0;
       hip_ok(hipGetDeviceCount(&dev_count), "hipGetDeviceCount");
       if (dev_count < 1) throw Error("NoDevice", "no GPU visible to this worker");
       hip_ok(hipSetDevice(0), "hipSetDevice");  // the CLI pinned this worker with HIP_VISIBLE_DEVICES
+      hip_ok(hipFree(nullptr), "hipFree");      // runtime + device context up
+      t_hip = now_s();
       gpurt::DevicePullOptions o;
       o.repo = a.repo;
       o.revision = a.revision;
@@ -207,7 +283,21 @@ int run(int argc, char** argv) {
       o.device = 0;
       o.staging_bytes = a.staging_mb << 20;
       o.threads = a.threads;
-      dp = std::make_unique<gpurt::DeviceXetPull>(o);
+      std::vector<std::string> errs(dps.size());
+      std::vector<std::thread> mk;
+      for (size_t k = 0; k < dps.size(); ++k)
+        mk.emplace_back([&, k] {
+          try {
+            dps[k] = std::make_unique<gpurt::DeviceXetPull>(o);
+          } catch (const std::exception& e) {
+            errs[k] = e.what();
+          }
+        });
+      for (auto& t : mk) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) throw Error("DeviceInit", e);
+      t_dp = now_s();
+      wb = std::make_unique<WriteBack>(nwriters, piece);
     } catch (const std::exception& e) {
       init_err = e.what();
     }
@@ -219,6 +309,8 @@ int run(int argc, char** argv) {
       if (t.joinable()) t.join();
     }
   } join_init{init};
+  std::optional<trace::Span> phase;
+  phase.emplace("worker", "list files");
   std::vector<hub::RepoFile> files = hub::list_files(cfg, a.repo, a.revision, a.repo_type);
   const std::string commit = hub::resolve_commit(cfg, a.repo, a.revision, a.repo_type).value_or(a.revision);
   const std::string snap = cfg.snapshot_dir(a.repo, commit);
@@ -252,7 +344,9 @@ int run(int argc, char** argv) {
   // largest first: the write-back of the file pulled last is the un-overlapped tail
   std::stable_sort(todo.begin(), todo.end(), [](const hub::RepoFile& x, const hub::RepoFile& y) { return x.size > y.size; });
   const double t_list = now_s();
+  phase.emplace("worker", "wait device init");
   init.join();
+  phase.reset();
   if (!init_err.empty()) throw Error("DeviceInit", init_err);
   const double t_ready = now_s();
   uint64_t done_bytes = 0;
@@ -260,109 +354,111 @@ int run(int argc, char** argv) {
   std::string stats = "{}";
   double t_pull = 0, t_write = 0, t_bufs = t_ready, t_last_pull = t_ready, t_last_write = t_ready;
   if (!todo.empty()) {
-    uint64_t max_size = 1;
-    for (auto& f : todo) max_size = std::max(max_size, f.size);
-    // Device buffer pool: file i is pulled into a free buffer while earlier files are written back
-    // by `nwriters` threads, each on a different file (concurrent pwrites to ONE file serialize on
-    // its inode; the host pull writes 4 files at once for the same reason).  As many buffers as
-    // half the free HBM holds, capped by the file count: a 70B repo (30 x 4.7 GB) fits whole.
+    // Files go to the device in groups that fit half the free HBM (a 70B repo on one MI355X is one
+    // or two groups); each group is ONE pull call -- one pipeline, no drain between files -- and is
+    // written back while it is pulled.
     size_t free_b = 0, total_b = 0;
     hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
-    const size_t nbuf = std::max<size_t>(2, std::min<size_t>(todo.size(), (free_b / 2) / (max_size + 4096)));
-    const int nwriters = int(std::min<size_t>(size_t(std::max(1, env_int("ZEST_GPU_WRITERS", 2))), todo.size()));
-    const int wslots = std::max(2, env_int("ZEST_GPU_WRITE_SLOTS", 3));
-    std::vector<uint8_t*> bufs(std::min(nbuf, todo.size()), nullptr);
-    for (auto& bp : bufs) hip_ok(hipMalloc(reinterpret_cast<void**>(&bp), max_size + 4096), "hipMalloc");
+    auto padded = [](uint64_t n) { return (n + 4095) / 4096 * 4096; };
+    uint64_t max_size = 0;
+    for (auto& f : todo) max_size = std::max<uint64_t>(max_size, padded(f.size));
+    const uint64_t budget = std::max<uint64_t>(max_size, free_b / 2);
+    std::vector<std::pair<size_t, size_t>> groups;  // [begin, end) of todo
+    uint64_t gmax = 0;
+    for (size_t i = 0; i < todo.size();) {
+      uint64_t sum = 0;
+      size_t j = i;
+      while (j < todo.size() && (j == i || sum + padded(todo[j].size) <= budget)) sum += padded(todo[j++].size);
+      groups.emplace_back(i, j);
+      gmax = std::max(gmax, sum);
+      i = j;
+    }
+    uint8_t* dbuf = nullptr;
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&dbuf), gmax + 4096), "hipMalloc");
     t_bufs = now_s();
-    std::vector<int> free_bufs;
-    for (int k = int(bufs.size()) - 1; k >= 0; --k) free_bufs.push_back(k);
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<std::pair<size_t, int>> queue;  // (file, buffer) verified in HBM, waiting for write-back
-    bool closing = false;
-    auto write_loop = [&] {
-      Writer writer(size_t(256) << 20, wslots);  // own D2H stream + pinned slots per writer thread
-      while (true) {
-        std::pair<size_t, int> job;
-        {
-          std::unique_lock<std::mutex> g(mu);
-          cv.wait(g, [&] { return closing || !queue.empty(); });
-          if (queue.empty()) return;
-          job = queue.front();
-          queue.pop_front();
+    const double tp = now_s();
+    for (auto [g0, g1] : groups) {
+      std::vector<WriteBack::File> out(g1 - g0);
+      std::vector<gpurt::PullRequest> reqs;
+      uint64_t off = 0;
+      for (size_t i = g0; i < g1; ++i) {
+        WriteBack::File& f = out[i - g0];
+        f.dst = snap + "/" + todo[i].path;
+        f.tmp = f.dst + ".incomplete";
+        f.dev = dbuf + off;
+        f.size = todo[i].size;
+        storage::ensure_dir(f.dst.substr(0, f.dst.rfind('/')));
+        f.fd = ::open(f.tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (f.fd < 0) throw Error("IoError", "open " + f.tmp + ": " + std::strerror(errno));
+        reqs.push_back({*todo[i].xet_hash, reinterpret_cast<uintptr_t>(f.dev), f.size});
+        off += padded(f.size);
+      }
+      wb->start(&out);
+      // deal the group's files to the pipelines, largest first to the least-loaded one
+      std::vector<std::vector<size_t>> share(dps.size());
+      {
+        std::vector<uint64_t> load(dps.size(), 0);
+        for (size_t k = 0; k < out.size(); ++k) {
+          const size_t p = size_t(std::min_element(load.begin(), load.end()) - load.begin());
+          share[p].push_back(k);
+          load[p] += out[k].size;
         }
-        const hub::RepoFile& f = todo[job.first];
-        const std::string dst = snap + "/" + f.path;
-        const double tw = now_s();
-        try {
-          const size_t slash = dst.rfind('/');
-          storage::ensure_dir(dst.substr(0, slash));
-          writer.write(bufs[size_t(job.second)], f.size, dst + ".incomplete");
-          if (::rename((dst + ".incomplete").c_str(), dst.c_str()) != 0) throw Error("IoError", "rename " + dst);
-          storage::write_verified_marker(cfg, a.repo, commit, f.path, *f.xet_hash, dst);  // verified on the GPU
-          std::lock_guard<std::mutex> g(mu);
+      }
+      std::vector<std::string> pipe_err(dps.size());
+      std::vector<std::thread> pipes;
+      for (size_t p = 0; p < dps.size(); ++p) {
+        if (share[p].empty()) continue;
+        pipes.emplace_back([&, p] {
+          std::vector<gpurt::PullRequest> mine;
+          for (size_t k : share[p]) mine.push_back(reqs[k]);
+          try {
+            dps[p]->pull_files(mine, [&](size_t f, int attempt, uint64_t bytes) {
+              wb->progress(share[p][f], attempt, bytes);
+            });
+          } catch (const std::exception& e) {
+            pipe_err[p] = e.what();
+          }
+        });
+      }
+      for (auto& t : pipes) t.join();
+      std::vector<std::string> file_err(out.size());
+      for (size_t p = 0; p < dps.size(); ++p)
+        for (size_t k : share[p]) file_err[k] = pipe_err[p];
+      t_last_pull = now_s();
+      wb->drain();
+      for (size_t k = 0; k < out.size(); ++k)
+        if (out[k].repaired && file_err[k].empty()) wb->post(k, 0, out[k].size);  // the repair pass replaced its bytes
+      wb->drain();
+      wb->stop();
+      t_last_write = now_s();
+      for (size_t k = 0; k < out.size(); ++k) {
+        WriteBack::File& f = out[k];
+        const hub::RepoFile& rf = todo[g0 + k];
+        ::close(f.fd);
+        const std::string err = !file_err[k].empty() ? file_err[k] : f.err;
+        if (err.empty() && ::rename(f.tmp.c_str(), f.dst.c_str()) == 0) {
+          storage::write_verified_marker(cfg, a.repo, commit, rf.path, *rf.xet_hash, f.dst);  // verified on the GPU
           done_bytes += f.size;
-          t_last_write = now_s();
-          t_write += t_last_write - tw;
-          std::cout << "[gpu " << rank << "] " << f.path << " [xet] " << f.size / 1e6 << " MB verified on the GPU\n"
-                    << std::flush;
-        } catch (const std::exception& e) {
-          std::lock_guard<std::mutex> g(mu);
-          std::cerr << "[gpu " << rank << "] " << f.path << ": write failed: " << e.what() << "\n";
+          std::cout << "[gpu " << rank << "] " << rf.path << " [xet] " << f.size / 1e6 << " MB verified on the GPU\n";
+        } else {
+          ::unlink(f.tmp.c_str());
+          std::cerr << "[gpu " << rank << "] " << rf.path << ": " << (err.empty() ? "rename failed" : err) << "\n";
           ++failed;
         }
-        std::lock_guard<std::mutex> g(mu);
-        free_bufs.push_back(job.second);
-        cv.notify_all();
       }
-    };
-    // ZEST_GPU_WRITE_AFTER=1: write back only after every pull finished (needs a buffer per file;
-    // measures the two legs separately).
-    const bool write_after = env_int("ZEST_GPU_WRITE_AFTER", 0) == 1 && bufs.size() >= todo.size();
-    std::vector<std::thread> writers;
-    if (!write_after)
-      for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
-    const double tp = now_s();
-    for (size_t i = 0; i < todo.size(); ++i) {
-      int b;
-      {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return !free_bufs.empty(); });
-        b = free_bufs.back();
-        free_bufs.pop_back();
-      }
-      try {
-        dp->pull_files({{*todo[i].xet_hash, reinterpret_cast<uintptr_t>(bufs[size_t(b)]), todo[i].size}});
-      } catch (const std::exception& e) {
-        std::lock_guard<std::mutex> g(mu);
-        std::cerr << "[gpu " << rank << "] " << todo[i].path << ": error " << e.what() << "\n";
-        ++failed;
-        free_bufs.push_back(b);
-        continue;
-      }
-      std::lock_guard<std::mutex> g(mu);
-      t_last_pull = now_s();
-      queue.emplace_back(i, b);
-      cv.notify_all();
+      std::cout << std::flush;
     }
-    t_pull = now_s() - tp;
-    if (write_after)
-      for (int w = 0; w < nwriters; ++w) writers.emplace_back(write_loop);
-    {
-      std::lock_guard<std::mutex> g(mu);
-      closing = true;
-      cv.notify_all();
-    }
-    for (auto& t : writers) t.join();
-    for (auto& bp : bufs) (void)hipFree(bp);
-    stats = dp->stats_json();
+    t_pull = t_last_pull - tp;
+    t_write = t_last_write - t_last_pull;  // write-back tail after the last pull call returned
+    stats = merged_stats(dps);
   }
   const double dt = now_s() - t0;
   std::cout << "[gpu " << rank << "] " << done_bytes / 1e9 << " GB in " << dt << " s (start " << t_ready - t0
-            << " s, device pulls " << t_pull << " s, writes " << t_write << " s summed over writer threads, "
-            << "overlapped)\n";
+            << " s, device pulls " << t_pull << " s with the write-back streaming behind them, write tail "
+            << t_write << " s)\n";
   auto rel = [&](double t) { return std::to_string(int((t - t0) * 1000)); };
-  std::cout << "[gpu " << rank << "] timeline ms: listed " << rel(t_list) << ", device ready " << rel(t_init)
+  std::cout << "[gpu " << rank << "] timeline ms: listed " << rel(t_list) << ", hip " << rel(t_hip) << ", pipeline "
+            << rel(t_dp) << ", device ready " << rel(t_init)
             << ", buffers " << rel(t_bufs) << ", last pull " << rel(t_last_pull) << ", last write "
             << rel(t_last_write) << ", end " << rel(now_s()) << "\n"
             << std::flush;
@@ -375,7 +471,12 @@ int run(int argc, char** argv) {
     w.key("stats").raw(stats).end();
     storage::write_file_atomic(status_path, w.out() + "\n", true);
   }
-  return failed ? 1 : 0;
+  // Every file is written and renamed and the status is on disk: leave without unwinding ~25 GB of
+  // device buffers and pinned pieces one free at a time (the OS reclaims them with the process).
+  trace::flush();
+  std::cout << std::flush;
+  std::cerr << std::flush;
+  std::_Exit(failed ? 1 : 0);
 }
 
 }  // namespace

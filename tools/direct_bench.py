@@ -148,7 +148,7 @@ def main() -> int:
                 if r.returncode != 0:
                     raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
                 tail = [ln for ln in r.stdout.splitlines() if "verified on" in ln]
-                workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and " GB in " in ln]
+                workers = [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu") and (" GB in " in ln or "timeline" in ln)]
                 key = "gpu_cli" if not cfg else f"gpu_cli[{cfg}]"
                 res[key] = {"s": round(dt, 3), "gbps": round(total / dt / 1e9, 3), "workers": workers, "presync_s": synced}
                 if not cfg:

@@ -11,6 +11,7 @@ snapshot files.  This probe times the candidate write strategies on 4 files x `-
   mmap16    16 threads, 4 per file, memcpy into a MAP_SHARED mapping of a pre-sized file
   direct4   O_DIRECT, 4 threads one file each
   direct16  O_DIRECT, 16 threads 4 per file, fallocate'd file
+  one1/one4 ONE file (gb/4) written by 1 / 4 threads (does the inode lock serialize writers?)
 
 `write_s` is the time until the last write call returned (what a pull waits for); `sync_s` the
 time the following `sync` took (writeback the kernel still owed).
@@ -67,6 +68,24 @@ def _mmap_range(mm: mmap.mmap, src: memoryview, lo: int, hi: int) -> None:
 
 
 def run_case(case: str, d: str, size: int, src: memoryview) -> dict:
+    if case in ("one1", "one4"):  # ONE file: does a second writer help (inode lock)?
+        p = os.path.join(d, "one.bin")
+        fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        os.ftruncate(fd, size)
+        parts = _ranges(size, 1 if case == "one1" else 4)
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=_pwrite_range, args=(fd, src, lo, hi)) for lo, hi in parts]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        t1 = time.perf_counter()
+        os.close(fd)
+        os.sync()
+        t2 = time.perf_counter()
+        os.unlink(p)
+        return {"case": case, "threads": len(parts), "GB": round(size / 1e9, 2), "write_s": round(t1 - t0, 3),
+                "GBps": round(size / (t1 - t0) / 1e9, 2), "sync_s": round(t2 - t1, 3)}
     paths = [os.path.join(d, f"f{i}.bin") for i in range(4)]
     jobs = []  # (callable)
     fds, maps = [], []

@@ -16,6 +16,7 @@ def main() -> None:
     ev = json.load(open(a.trace))
     ev = ev["traceEvents"] if isinstance(ev, dict) else ev
     agg = collections.defaultdict(lambda: [0, 0.0])
+    span = {}  # (cat, name) -> [first start, last end] in us
     ts = []
     threads = set()
     for e in ev:
@@ -25,12 +26,16 @@ def main() -> None:
         agg[k][0] += 1
         agg[k][1] += e.get("dur", 0) / 1e3
         ts += [e["ts"], e["ts"] + e.get("dur", 0)]
+        lo, hi = span.get(k, (e["ts"], e["ts"] + e.get("dur", 0)))
+        span[k] = (min(lo, e["ts"]), max(hi, e["ts"] + e.get("dur", 0)))
         threads.add(e.get("tid"))
     wall = (max(ts) - min(ts)) / 1e3 if ts else 0.0
     print(f"wall span {wall:.1f} ms, {len(threads)} threads")
-    print(f"{'category':10s} {'span':34s} {'count':>7s} {'sum ms':>10s} {'mean ms':>9s}")
+    t0 = min(ts) if ts else 0
+    print(f"{'category':10s} {'span':34s} {'count':>7s} {'sum ms':>10s} {'mean ms':>9s} {'first..last ms':>16s}")
     for (c, n), (cnt, ms) in sorted(agg.items(), key=lambda x: -x[1][1])[:a.top]:
-        print(f"{c:10s} {n:34s} {cnt:7d} {ms:10.1f} {ms / cnt:9.2f}")
+        lo, hi = span[(c, n)]
+        print(f"{c:10s} {n:34s} {cnt:7d} {ms:10.1f} {ms / cnt:9.2f} {(lo - t0) / 1e3:7.1f}..{(hi - t0) / 1e3:<7.1f}")
 
 
 if __name__ == "__main__":
