@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../gpu/zgpu.h"
+#include "pinned.h"
 #include "bridge.h"
 #include "config.h"
 #include "storage.h"
@@ -52,7 +53,8 @@ struct DevBuf {
 };
 
 struct Slot {
-  uint8_t* host = nullptr;  // pinned
+  PinnedBuf pin;
+  uint8_t* host = nullptr;  // = pin.data()
   DevBuf<uint8_t> dev;      // device staging (padded)
   DevBuf<ZgChunk> chunks_dev;
   std::vector<ZgChunk> chunks_host;  // chunk records of the batch, built by the fetch workers
@@ -92,7 +94,8 @@ struct DeviceXetPull::Impl {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& s : slots_) {
-      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cap_ + 4096, hipHostMallocDefault), "hipHostMalloc");
+      if (!s.pin.alloc(cap_ + 4096)) throw Error("HipError", "pinning the staging buffer failed");
+      s.host = s.pin.data();
       s.dev.ensure(cap_);
       hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
     }
@@ -102,7 +105,7 @@ struct DeviceXetPull::Impl {
   ~Impl() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (auto& s : slots_) {
-      if (s.host) (void)hipHostFree(s.host);
+      s.pin.reset();
       if (s.done) (void)hipEventDestroy(s.done);
     }
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -503,9 +506,9 @@ struct DeviceXetPull::Impl {
   void grow_staging(uint64_t bytes) {
     hip_check(hipStreamSynchronize(stream_), "sync");  // no copy still reads the old buffers
     for (auto& s : slots_) {
-      if (s.host) (void)hipHostFree(s.host);
       s.host = nullptr;
-      hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), bytes + 4096, hipHostMallocDefault), "hipHostMalloc");
+      if (!s.pin.alloc(bytes + 4096)) throw Error("HipError", "pinning the staging buffer failed");
+      s.host = s.pin.data();
       s.dev.ensure(bytes);
     }
     cap_ = bytes;

@@ -36,6 +36,7 @@
 #include "device_pull.h"
 #include "hub.h"
 #include "json.h"
+#include "pinned.h"
 #include "storage.h"
 #include "trace.h"
 
@@ -93,7 +94,9 @@ class WriteBack {
     for (int t = 0; t < threads; ++t) {
       Lane l;
       hip_ok(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreate");
-      hip_ok(hipHostMalloc(reinterpret_cast<void**>(&l.host), piece_, hipHostMallocDefault), "hipHostMalloc");
+      l.pin = std::make_shared<gpurt::PinnedBuf>();
+      if (!l.pin->alloc(piece_)) throw Error("HipError", "pinning a write-back buffer failed");
+      l.host = l.pin->data();
       lanes_.push_back(l);
     }
   }
@@ -136,6 +139,7 @@ class WriteBack {
  private:
   struct Lane {
     hipStream_t stream = nullptr;
+    std::shared_ptr<gpurt::PinnedBuf> pin;
     uint8_t* host = nullptr;
   };
   struct Piece {
@@ -255,10 +259,10 @@ int run(int argc, char** argv) {
   // thread while this one lists the repository: both are a few hundred ms on a fresh process.
   // ZEST_GPU_PIPES device pipelines pull different files at the same time, so the write-back
   // always has several files (inodes) to write into at once.
-  const int npipes = std::max(1, env_int("ZEST_GPU_PIPES", 2));
+  const int npipes = std::max(1, env_int("ZEST_GPU_PIPES", 4));
   std::vector<std::unique_ptr<gpurt::DeviceXetPull>> dps(static_cast<size_t>(npipes));
   // Write-back: `nwriters` threads, each with its own D2H stream and a pinned piece buffer.
-  const int nwriters = std::max(1, env_int("ZEST_GPU_WRITERS", 4));
+  const int nwriters = std::max(1, env_int("ZEST_GPU_WRITERS", 2 * npipes));
   const size_t piece = size_t(std::max(4, env_int("ZEST_GPU_PIECE_MB", 64))) << 20;
   std::unique_ptr<WriteBack> wb;
   std::string init_err;

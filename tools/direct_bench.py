@@ -154,7 +154,7 @@ def main() -> int:
                 if not cfg:
                     res.update(gpu_cli_pull_s=round(dt, 3), gpu_cli_pull_gbps=round(total / dt / 1e9, 3),
                                gpu_cli_summary=tail[-1] if tail else "", gpu_cli_workers=workers)
-                for ln in workers:
+                for ln in workers + tail[-1:]:
                     print(f"[gpu cli worker {cfg}] {ln}", flush=True)
                 print(f"[gpu cli {cfg}] zest pull --gpus 1 to disk: {total / dt / 1e9:.2f} GB/s ({dt:.1f}s)", flush=True)
                 subprocess.run(["rm", "-rf", str(work / f"gpucli{ci}")])
