@@ -180,7 +180,14 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         if arenas is not None and arenas.get("arena") is not None and arenas["arena"].numel() == world.arena_bytes:
             arena = arenas["arena"]
         else:
-            arena = ops.padded_empty(world.arena_bytes, device)
+            arena = None
+            if want_ipc:  # a HIP VMM arena: the peers map it through dmabuf fds (csrc/bind/hip_vmm.cpp)
+                try:
+                    arena = ops.vmm_empty(world.arena_bytes, device)
+                except Exception as e:  # noqa: BLE001
+                    log(rank, f"VMM arena unavailable ({e}); torch allocation")
+            if arena is None:
+                arena = ops.padded_empty(world.arena_bytes, device)
             if arenas is not None:
                 arenas["arena"] = arena
             if want_ipc:

@@ -11,7 +11,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _rank(rank, port, q, mode):
+def _rank(rank, port, q, mode, alloc="vmm"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
@@ -22,7 +22,7 @@ def _rank(rank, port, q, mode):
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
         w = SyntheticWorld("llama-tiny", seed=11, mode="random", max_xorb_bytes=1 << 20)
-        arena = ops.padded_empty(w.arena_bytes, dev)
+        arena = ops.vmm_empty(w.arena_bytes, dev) if alloc == "vmm" else ops.padded_empty(w.arena_bytes, dev)
         w.generate_on_device(arena)
         w.build_on_device(arena)
         want = arena.clone()
@@ -46,13 +46,15 @@ def _rank(rank, port, q, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["ipc", "xgmi"])
-def test_ipc_exchange_two_ranks_one_gpu(mode):
+@pytest.mark.parametrize("mode,alloc", [("ipc", "vmm"), ("xgmi", "vmm"), ("xgmi", "torch")])
+def test_ipc_exchange_two_ranks_one_gpu(mode, alloc):
+    """vmm: the arena is a HIP VMM mapping shared through dmabuf fds (what bench.py uses); torch: a
+    caching-allocator tensor shared with hipIpcGetMemHandle (small arenas only, see engine.py)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29800 + 50 * (mode == "xgmi") + os.getpid() % 50
-    procs = [ctx.Process(target=_rank, args=(r, port, q, mode)) for r in range(2)]
+    port = 29700 + 50 * (mode == "xgmi") + 100 * (alloc == "torch") + os.getpid() % 50
+    procs = [ctx.Process(target=_rank, args=(r, port, q, mode, alloc)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=180) for _ in procs)
@@ -82,3 +84,48 @@ def test_peer_gather_kernel_segments():
     assert torch.equal(dst, want)
     with pytest.raises(ValueError):
         H.peer_gather([src.data_ptr() + 1], [dst.data_ptr()], [10], 0)
+
+
+def _big_rank(rank, port, q, gib):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from zest_amd import ops
+        from zest_amd.engine import map_peer_arenas
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        n = int(gib * (1 << 30))
+        arena = ops.vmm_empty(n, dev)
+        arena.fill_(rank + 1)  # written by a kernel before the export (that made IPC imports hang)
+        arena[n - 1] = 100 + rank
+        torch.cuda.synchronize()
+        m = map_peer_arenas(arena, rank, 2, deadline_s=60)
+        peer = m.peers[1 - rank] if m is not None else None
+        got = None
+        if peer is not None:
+            got = (peer.numel(), int(peer[0].item()), int(peer[n // 2].item()), int(peer[n - 1].item()))
+        q.put((rank, got))
+        dist.barrier()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_vmm_maps_a_large_written_arena():
+    """A 6 GiB kernel-written arena per rank, mapped by the sibling rank through the VMM path
+    (hipIpcOpenMemHandle of a >= 2 GiB allocation hung on this box)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29950 + os.getpid() % 40
+    gib = 6
+    procs = [ctx.Process(target=_big_rank, args=(r, port, q, gib)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    n = gib << 30
+    assert res == [(0, (n, 2, 2, 101)), (1, (n, 1, 1, 100))], res

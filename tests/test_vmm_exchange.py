@@ -1,0 +1,79 @@
+"""The fd exchange behind the VMM peer mapping (engine._import_vmm_peers), on CPU: 3 gloo ranks,
+each "arena" exported as memfds whose bytes name the owner and the chunk; every rank must import
+every peer's chunks, in order, through the abstract-socket + SCM_RIGHTS protocol.  The HIP side
+(hipMemImportFromShareableHandle + mapping) runs in tests/test_gpu_ipc.py."""
+import os
+
+import torch
+
+
+class _FakeMapping:
+    def __init__(self, rank=None, n_chunks=0, chunk=4096, content=None):
+        self.rank, self.n_chunks, self.chunk, self.content = rank, n_chunks, chunk, content or []
+
+    def export_fds(self):
+        fds = []
+        for k in range(self.n_chunks):
+            fd = os.memfd_create(f"chunk{k}")
+            os.write(fd, f"{self.rank}:{k}".encode())
+            fds.append(fd)
+        return fds
+
+    def dlpack(self, nbytes):
+        return torch.zeros(nbytes, dtype=torch.uint8).__dlpack__()
+
+
+class _FakeHip:
+    def vmm_import(self, fds, chunk, device):
+        return _FakeMapping(content=[os.pread(fd, 32, 0).decode() for fd in fds], chunk=chunk)
+
+
+class _Dev:
+    index = 0
+
+
+class _Arena:
+    device = _Dev()
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    from zest_amd import engine, ops
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ops.hip = lambda: _FakeHip()
+        n_chunks = 3 + rank  # ranks own different chunk counts
+        vm = _FakeMapping(rank, n_chunks)
+        mine = ("vmm", f"tok{port}" if rank == 0 else "ignored", 4096, n_chunks, 100 + rank)
+        objs = [None] * world
+        dist.all_gather_object(objs, mine)
+        hg = dist.new_group(backend="gloo")
+        peers = [None] * world
+        ok = engine._import_vmm_peers(_Arena(), vm, objs, rank, world, hg, peers, 30.0)
+        got = {p: (t.numel(), t._zest_vmm.content) for p, t in enumerate(peers) if t is not None}
+        q.put((rank, ok, got))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_vmm_fd_exchange_three_ranks():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 3, 29900 + os.getpid() % 80
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok, got in res:
+        assert ok is True, (rank, got)
+        assert sorted(got) == [p for p in range(world) if p != rank]
+        for p, (numel, content) in got.items():
+            assert numel == 100 + p
+            assert content == [f"{p}:{k}" for k in range(3 + p)]

@@ -214,15 +214,19 @@ class PeerArenas:
 
 
 def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: float | None = None):
-    """Collective: export this rank's arena with HIP IPC and import every peer's.  Returns a
+    """Collective: share this rank's arena with every peer and map every peer's.  Returns a
     :class:`PeerArenas`, or None unless every rank mapped every peer (MIN-reduced).
 
-    Best called right after the arena is allocated, before any kernel has written it: imports of a
-    16 GB arena that already held a built synthetic model were seen to hang in
-    ``hipIpcOpenMemHandle`` (2 ranks on one GPU, docs/PARITY.md).  ``deadline_s`` (default
-    ``ZEST_IPC_DEADLINE`` = 60 s) bounds each import: a rank whose import does not return in time
+    Arenas from :func:`ops.vmm_empty` (what bench.py allocates when a peer-mapped exchange may be
+    used) go through the HIP VMM path: each rank serves its chunks' dmabuf fds on an abstract Unix
+    socket, and the peers import and map them contiguously (:func:`_import_vmm_peers`).  Other
+    arenas use HIP IPC handles (``reduce_tensor``), imported one rank at a time; on the MI355X box
+    hipIpcOpenMemHandle of a >= 2 GiB allocation hung (64-512 MiB imports took < 2 ms,
+    profiles/ipc_import_sizes_r3.txt), so that path is for small arenas.  ``deadline_s`` (default
+    ``ZEST_IPC_DEADLINE`` = 60 s) bounds the imports: a rank whose imports do not return in time
     reports failure, and the caller falls back to an RCCL exchange."""
     import threading
+    import uuid
 
     import torch.distributed as dist
     from torch.multiprocessing.reductions import reduce_tensor
@@ -230,51 +234,142 @@ def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: floa
         return None
     if deadline_s is None:
         deadline_s = float(os.environ.get("ZEST_IPC_DEADLINE", "60"))
-    try:
-        mine = reduce_tensor(arena)
-    except Exception:
-        mine = None
+    vm = ops.vmm_mapping(arena)
+    if vm is not None:
+        mine = ("vmm", uuid.uuid4().hex, vm.chunk, vm.n_chunks, arena.numel())
+    else:
+        try:
+            mine = ("ipc", reduce_tensor(arena))
+        except Exception:
+            mine = None
     objs = [None] * n_ranks
     dist.all_gather_object(objs, mine, group=group)
     # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
     host_group = dist.new_group(backend="gloo")
     peers = [None] * n_ranks
     ok = 1
-    # One rank imports at a time: two processes opening each other's large dmabuf handles at the
-    # same moment deadlocked inside hipIpcOpenMemHandle (16 GB arenas, 2 ranks on one MI355X); an
-    # exporter that is idle in a barrier answers at once.
-    for turn in range(n_ranks):
-        if turn == rank:
-            res: dict = {}
+    if all(o is not None and o[0] == "vmm" for o in objs):
+        ok = int(_import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadline_s))
+    elif all(o is not None and o[0] == "ipc" for o in objs):
+        # One rank imports at a time: two processes opening each other's large dmabuf handles at
+        # the same moment deadlocked inside hipIpcOpenMemHandle; an exporter idle in a barrier
+        # answers at once.
+        for turn in range(n_ranks):
+            if turn == rank:
+                res: dict = {}
 
-            def imp():
-                try:
-                    H = ops.hip()
-                    for p, o in enumerate(objs):
-                        if p != rank:
-                            if o is None:
-                                raise RuntimeError(f"rank {p} could not export its arena")
-                            fn, args = o
-                            t = fn(*args)
-                            if t.device != arena.device and not H.enable_peer_access(t.device.index):
-                                raise RuntimeError(f"no peer access to {t.device}")
-                            res[p] = t
-                except Exception as e:  # noqa: BLE001
-                    res["error"] = e
-            th = threading.Thread(target=imp, daemon=True)
-            th.start()
-            th.join(deadline_s)
-            if th.is_alive() or "error" in res:
-                ok = 0  # a hung import stays parked in its daemon thread; this rank reports failure
-            else:
-                for p in range(n_ranks):
-                    peers[p] = res.get(p)
-        dist.barrier(group=host_group)
+                def imp():
+                    try:
+                        H = ops.hip()
+                        for p, o in enumerate(objs):
+                            if p != rank:
+                                fn, args = o[1]
+                                t = fn(*args)
+                                if t.device != arena.device and not H.enable_peer_access(t.device.index):
+                                    raise RuntimeError(f"no peer access to {t.device}")
+                                res[p] = t
+                    except Exception as e:  # noqa: BLE001
+                        res["error"] = e
+                th = threading.Thread(target=imp, daemon=True)
+                th.start()
+                th.join(deadline_s)
+                if th.is_alive() or "error" in res:
+                    ok = 0  # a hung import stays parked in its daemon thread; this rank reports failure
+                else:
+                    for p in range(n_ranks):
+                        peers[p] = res.get(p)
+            dist.barrier(group=host_group)
+    else:
+        ok = 0  # some rank could not export (or the ranks disagree on the path)
     flag = torch.tensor([ok], dtype=torch.int32, device=arena.device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
     if not int(flag.item()):
         return None
     return PeerArenas(arena, peers, host_group)
+
+
+def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadline_s) -> bool:
+    """VMM half of :func:`map_peer_arenas`: serve this rank's chunk fds, import every peer's.
+
+    Each rank listens on the abstract Unix socket ``zest-vmm-<token>-<rank>`` (token from rank 0,
+    so concurrent jobs on a node do not collide) and answers every connection with fresh fds of its
+    chunks (SCM_RIGHTS, <= 200 per message); the peer imports them (`_hip.vmm_import`) and wraps the
+    mapping as a tensor.  Every rank serves and imports at the same time: VMM imports do not block
+    on the exporter (16 GiB mapped in 22-43 ms, profiles/vmm_ipc_probe_r3.txt)."""
+    import socket
+    import threading
+
+    import torch.distributed as dist
+    from torch.utils.dlpack import from_dlpack
+
+    token = objs[0][1]
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    srv.bind(f"\0zest-vmm-{token}-{rank}")
+    srv.listen(n_ranks)
+    srv.settimeout(deadline_s)
+    served = {"n": 0, "error": None}
+
+    def serve():
+        try:
+            for _ in range(n_ranks - 1):
+                conn, _ = srv.accept()
+                with conn:
+                    fds = vm.export_fds()
+                    try:
+                        for i in range(0, len(fds), 200):
+                            socket.send_fds(conn, [b"z"], fds[i:i + 200])
+                        conn.recv(1)  # the importer's ack: it holds its own references now
+                    finally:
+                        for fd in fds:
+                            os.close(fd)
+                served["n"] += 1
+        except Exception as e:  # noqa: BLE001
+            served["error"] = e
+
+    res: dict = {}
+
+    def imp():
+        try:
+            H = ops.hip()
+            dev = arena.device.index
+            for k in range(1, n_ranks):
+                p = (rank + k) % n_ranks
+                _, _, chunk, n_chunks, numel = objs[p]
+                with socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET) as c:
+                    c.settimeout(deadline_s)
+                    c.connect(f"\0zest-vmm-{token}-{p}")
+                    fds: list[int] = []
+                    while len(fds) < n_chunks:
+                        _, got, _, _ = socket.recv_fds(c, 1, 200)
+                        if not got:
+                            raise RuntimeError(f"rank {p} closed the fd stream early")
+                        fds += got
+                    try:
+                        m = H.vmm_import(fds, chunk, dev)
+                    finally:
+                        for fd in fds:
+                            os.close(fd)
+                    c.sendall(b"k")
+                t = from_dlpack(m.dlpack(numel))
+                t._zest_vmm = m
+                res[p] = t
+        except Exception as e:  # noqa: BLE001
+            res["error"] = e
+
+    st = threading.Thread(target=serve, daemon=True)
+    st.start()
+    dist.barrier(group=host_group)  # every rank is listening
+    it = threading.Thread(target=imp, daemon=True)
+    it.start()
+    it.join(deadline_s)
+    st.join(deadline_s)
+    srv.close()
+    ok = not it.is_alive() and not st.is_alive() and "error" not in res and served["error"] is None
+    if ok:
+        for p in range(n_ranks):
+            peers[p] = res.get(p)
+    dist.barrier(group=host_group)
+    return ok
 
 
 class DevicePuller:

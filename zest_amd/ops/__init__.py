@@ -60,6 +60,28 @@ def padded_empty(nbytes: int, device, pad: int = PAD) -> torch.Tensor:
     return base[:nbytes]
 
 
+def vmm_empty(nbytes: int, device, pad: int = PAD, chunk: int = 512 << 20) -> torch.Tensor:
+    """Like :func:`padded_empty`, but the storage is a HIP virtual-memory arena built from
+    ``chunk``-sized physical allocations that other processes can map (engine.map_peer_arenas
+    passes the chunks as dmabuf fds).  Imports of torch allocations of >= 2 GiB through
+    hipIpcOpenMemHandle hung on the MI355X box; this path mapped 16 GiB in tens of ms
+    (csrc/bind/hip_vmm.cpp)."""
+    from torch.utils.dlpack import from_dlpack
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError("vmm_empty is for GPU arenas")
+    m = hip().vmm_alloc(nbytes + pad, device.index if device.index is not None else torch.cuda.current_device(),
+                        chunk)
+    t = from_dlpack(m.dlpack(nbytes + pad))[:nbytes]
+    t._zest_vmm = m  # the DLPack deleter keeps the mapping alive for every view; this finds it
+    return t
+
+
+def vmm_mapping(t: torch.Tensor):
+    """The VmmMapping behind a tensor returned by :func:`vmm_empty` (None otherwise)."""
+    return getattr(t, "_zest_vmm", None)
+
+
 def _has_pad(t: torch.Tensor, pad: int = PAD) -> bool:
     st = t.untyped_storage().nbytes()
     end = (t.storage_offset() + t.numel()) * t.element_size()
