@@ -13,8 +13,10 @@
 //
 // Torch sees a mapping through DLPack (kDLROCM): the capsule's deleter holds a reference, so the
 // mapping outlives every tensor view of it.
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <signal.h>
 #include <pybind11/stl.h>
 #include <unistd.h>
 
@@ -121,10 +123,16 @@ std::shared_ptr<VmmMapping> vmm_import(const std::vector<int>& fds, size_t chunk
   m->device = device;
   m->imported = true;
   m->reserve(fds.size());
+  // The HIP 7.0 runtime that PyTorch bundles reads the fd THROUGH `osHandle` (mov (%rsi),%edi before
+  // hsa_amd_vmem_import_shareable_handle); ROCm 7.2's takes the fd as the pointer's value, like CUDA.
+  int ver = 0;
+  vcheck(hipRuntimeGetVersion(&ver), "hipRuntimeGetVersion");
+  const bool by_pointer = ver < 70100000;
   for (size_t k = 0; k < fds.size(); ++k) {
     hipMemGenericAllocationHandle_t h;
-    vcheck(hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>(static_cast<intptr_t>(fds[k])),
-                                           hipMemHandleTypePosixFileDescriptor),
+    int fd = fds[k];
+    void* os_handle = by_pointer ? static_cast<void*>(&fd) : reinterpret_cast<void*>(static_cast<intptr_t>(fd));
+    vcheck(hipMemImportFromShareableHandle(&h, os_handle, hipMemHandleTypePosixFileDescriptor),
            "hipMemImportFromShareableHandle");
     m->h.push_back(h);
     vcheck(hipMemMap(m->va + k * chunk, chunk, 0, h, 0), "hipMemMap");
@@ -185,9 +193,25 @@ py::capsule vmm_dlpack(const std::shared_ptr<VmmMapping>& m, size_t nbytes) {
   });
 }
 
+void on_fatal(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 }  // namespace
 
 void bind_hip_vmm(py::module_& m) {
+  // Diagnostics: print the native stack on SIGSEGV / SIGABRT (install before faulthandler.enable(),
+  // which chains to it after the Python stack).
+  m.def("install_fatal_backtrace", [] {
+    signal(SIGSEGV, on_fatal);
+    signal(SIGABRT, on_fatal);
+  });
   py::class_<VmmMapping, std::shared_ptr<VmmMapping>>(m, "VmmMapping")
       .def_property_readonly("ptr", [](const VmmMapping& v) { return reinterpret_cast<uintptr_t>(v.va); })
       .def_readonly("size", &VmmMapping::size)
@@ -201,6 +225,11 @@ void bind_hip_vmm(py::module_& m) {
       })
       .def("dlpack", &vmm_dlpack, py::arg("nbytes"));
   m.def("vmm_granularity", &granularity, py::arg("device"));
+  m.def("runtime_version", [] {
+    int v = 0;
+    vcheck(hipRuntimeGetVersion(&v), "hipRuntimeGetVersion");
+    return v;
+  });
   m.def(
       "vmm_alloc",
       [](size_t nbytes, int device, size_t chunk) {

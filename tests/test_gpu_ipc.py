@@ -12,7 +12,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _rank(rank, port, q, mode, alloc="vmm"):
+    import faulthandler
+    import sys
+
     import torch.distributed as dist
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.stderr)  # a stack instead of a silent hang
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
@@ -87,7 +91,11 @@ def test_peer_gather_kernel_segments():
 
 
 def _big_rank(rank, port, q, gib):
+    import faulthandler
+    import sys
+
     import torch.distributed as dist
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.stderr)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:

@@ -8,8 +8,12 @@
 // contiguously, checks the first byte of every chunk with a D2H copy, and times the import.
 //
 // Build: hipcc -O2 --offload-arch=gfx950 -o vmm_ipc_probe tools/experiments/vmm_ipc_probe.cpp
-// Run:   vmm_ipc_probe <total GiB> <chunk MiB>     (e.g. 16 512)
+// Run:   vmm_ipc_probe <total GiB> <chunk MiB> [own] [dup]     (e.g. 16 512)
+//   own: the importer first makes (and maps) a VMM arena of its own, as every rank does
+//   dup: the exporter sends dup()s of its fds, as the Python server does
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -82,7 +86,23 @@ static hipMemAllocationProp prop_for(int dev) {
   return p;
 }
 
+static void on_segv(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "SIGSEGV backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int main(int argc, char** argv) {
+  signal(SIGSEGV, on_segv);
+  bool own = false, dup_fds = false;
+  for (int i = 3; i < argc; ++i) {
+    own = own || std::strcmp(argv[i], "own") == 0;
+    dup_fds = dup_fds || std::strcmp(argv[i], "dup") == 0;
+  }
   const size_t total = size_t(std::atof(argc > 1 ? argv[1] : "16") * double(1ull << 30));
   const size_t chunk = size_t(std::atoi(argc > 2 ? argv[2] : "512")) << 20;
   const size_t n = (total + chunk - 1) / chunk;
@@ -122,6 +142,8 @@ int main(int argc, char** argv) {
     std::printf("exporter: %zu x %zu MiB created, mapped, filled, exported (granularity %zu KiB) in %.3f s\n", n,
                 chunk >> 20, gran >> 10, now() - t0);
     std::fflush(stdout);
+    if (dup_fds)
+      for (auto& fd : fds) fd = dup(fd);
     send_fds(sv[0], fds);
     char done = 0;
     if (read(sv[0], &done, 1) != 1) done = 'x';
@@ -132,6 +154,18 @@ int main(int argc, char** argv) {
   }
   // importer
   close(sv[0]);
+  if (own) {  // an arena of the importer's own, mapped in its own range
+    void* ova = nullptr;
+    CK(hipMemAddressReserve(&ova, n * chunk, 0, nullptr, 0));
+    for (size_t k = 0; k < n; ++k) {
+      hipMemGenericAllocationHandle_t h;
+      CK(hipMemCreate(&h, chunk, &prop, 0));
+      CK(hipMemMap(static_cast<uint8_t*>(ova) + k * chunk, chunk, 0, h, 0));
+    }
+    CK(hipMemSetAccess(ova, n * chunk, &acc, 1));
+    std::printf("importer: own arena of %zu chunks mapped\n", n);
+    std::fflush(stdout);
+  }
   const std::vector<int> fds = recv_fds(sv[1], n);
   double t0 = now();
   for (size_t k = 0; k < n; ++k) {

@@ -291,38 +291,47 @@ def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: floa
 def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadline_s) -> bool:
     """VMM half of :func:`map_peer_arenas`: serve this rank's chunk fds, import every peer's.
 
-    Each rank listens on the abstract Unix socket ``zest-vmm-<token>-<rank>`` (token from rank 0,
-    so concurrent jobs on a node do not collide) and answers every connection with fresh fds of its
-    chunks (SCM_RIGHTS, <= 200 per message); the peer imports them (`_hip.vmm_import`) and wraps the
-    mapping as a tensor.  Every rank serves and imports at the same time: VMM imports do not block
-    on the exporter (16 GiB mapped in 22-43 ms, profiles/vmm_ipc_probe_r3.txt)."""
+    Each rank exports its chunks once (fds) and listens on the abstract Unix socket
+    ``zest-vmm-<token>-<rank>`` (token from rank 0, so concurrent jobs on a node do not collide); a
+    thread answers every connection with duplicates of those fds (SCM_RIGHTS, <= 200 per message)
+    and makes no HIP call.  The ranks then import in turns, one rank at a time, as the IPC path
+    does: a process importing while its exporter is itself inside an import is the pattern that
+    deadlocked the IPC path, and an idle exporter costs nothing here (16 GiB of chunks mapped in
+    22-43 ms, profiles/vmm_ipc_probe_r3.txt)."""
     import socket
     import threading
 
     import torch.distributed as dist
     from torch.utils.dlpack import from_dlpack
 
+    debug = os.environ.get("ZEST_IPC_DEBUG") == "1"
+
+    def dbg(msg):
+        if debug:
+            print(f"[vmm rank {rank}] {msg}", flush=True)
+
     token = objs[0][1]
+    fds_mine = vm.export_fds()
+    dbg(f"exported {len(fds_mine)} chunk fds")
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
     srv.bind(f"\0zest-vmm-{token}-{rank}")
     srv.listen(n_ranks)
-    srv.settimeout(deadline_s)
-    served = {"n": 0, "error": None}
+    srv.settimeout(deadline_s * n_ranks)
+    served = {"error": None}
 
     def serve():
         try:
             for _ in range(n_ranks - 1):
                 conn, _ = srv.accept()
                 with conn:
-                    fds = vm.export_fds()
+                    dup = [os.dup(fd) for fd in fds_mine]
                     try:
-                        for i in range(0, len(fds), 200):
-                            socket.send_fds(conn, [b"z"], fds[i:i + 200])
+                        for i in range(0, len(dup), 200):
+                            socket.send_fds(conn, [b"z"], dup[i:i + 200])
                         conn.recv(1)  # the importer's ack: it holds its own references now
                     finally:
-                        for fd in fds:
+                        for fd in dup:
                             os.close(fd)
-                served["n"] += 1
         except Exception as e:  # noqa: BLE001
             served["error"] = e
 
@@ -344,6 +353,7 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
                         if not got:
                             raise RuntimeError(f"rank {p} closed the fd stream early")
                         fds += got
+                    dbg(f"received {len(fds)} fds from rank {p}; importing")
                     try:
                         m = H.vmm_import(fds, chunk, dev)
                     finally:
@@ -353,22 +363,29 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
                 t = from_dlpack(m.dlpack(numel))
                 t._zest_vmm = m
                 res[p] = t
+                dbg(f"mapped rank {p}'s {numel} bytes")
         except Exception as e:  # noqa: BLE001
             res["error"] = e
 
     st = threading.Thread(target=serve, daemon=True)
     st.start()
     dist.barrier(group=host_group)  # every rank is listening
-    it = threading.Thread(target=imp, daemon=True)
-    it.start()
-    it.join(deadline_s)
+    imported = True
+    for turn in range(n_ranks):
+        if turn == rank:
+            it = threading.Thread(target=imp, daemon=True)
+            it.start()
+            it.join(deadline_s)
+            imported = not it.is_alive() and "error" not in res
+        dist.barrier(group=host_group)
     st.join(deadline_s)
     srv.close()
-    ok = not it.is_alive() and not st.is_alive() and "error" not in res and served["error"] is None
+    for fd in fds_mine:
+        os.close(fd)
+    ok = imported and not st.is_alive() and served["error"] is None
     if ok:
         for p in range(n_ranks):
             peers[p] = res.get(p)
-    dist.barrier(group=host_group)
     return ok
 
 
