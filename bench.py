@@ -41,8 +41,10 @@ BASELINE_METRIC = "aggregate pull GB/s + P2P ratio, Llama-3.1-70B at 1/2/4/8 MI3
 MODES = ("bf16", "random")
 
 # Per-phase watchdog limits (seconds) for N > 1; ZEST_BENCH_WATCHDOG=<s> overrides all, =0 disables.
-# "1": --exchange auto also maps the peers' arenas and times the ipc / xgmi exchanges
-IPC_AUTO = "0"
+# "1": --exchange auto also maps the peers' arenas (HIP VMM, dmabuf fds) and times the ipc / xgmi
+# exchanges next to the RCCL ones; a mapping that fails, times out or does not read back falls back
+# to RCCL.  ZEST_EXCHANGE_IPC=0 turns it off.
+IPC_AUTO = "1"
 PHASE_LIMITS = {"init": 180, "setup": 420, "ipc": 90, "autotune": 180, "warmup": 240, "timed": 420,
                 "report": 120}
 

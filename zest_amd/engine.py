@@ -288,6 +288,29 @@ def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: floa
     return PeerArenas(arena, peers, host_group)
 
 
+def _vmm_sentinel(token: str, p: int) -> torch.Tensor:
+    import hashlib
+    return torch.frombuffer(bytearray(hashlib.blake2b(f"{token}:{p}".encode(), digest_size=8).digest()),
+                            dtype=torch.uint8)
+
+
+def _vmm_mark(arena, token: str, rank: int) -> None:
+    """8 bytes in the arena's pad (past its logical end, inside the mapping) that every importer
+    reads back through its new mapping (:func:`_vmm_check`) before trusting it."""
+    st = torch.cuda.current_stream(arena.device)
+    mark = _vmm_sentinel(token, rank)
+    ops.hip().memcpy_async(arena.data_ptr() + arena.numel(), mark.data_ptr(), 8, st.cuda_stream)
+    st.synchronize()
+
+
+def _vmm_check(t, numel: int, token: str, p: int) -> bool:
+    st = torch.cuda.current_stream(t.device)
+    got = torch.zeros(8, dtype=torch.uint8)
+    ops.hip().memcpy_async(got.data_ptr(), t.data_ptr() + numel, 8, st.cuda_stream)
+    st.synchronize()
+    return torch.equal(got, _vmm_sentinel(token, p))
+
+
 def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadline_s) -> bool:
     """VMM half of :func:`map_peer_arenas`: serve this rank's chunk fds, import every peer's.
 
@@ -311,6 +334,7 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
             print(f"[vmm rank {rank}] {msg}", flush=True)
 
     token = objs[0][1]
+    _vmm_mark(arena, token, rank)
     fds_mine = vm.export_fds()
     dbg(f"exported {len(fds_mine)} chunk fds")
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
@@ -362,6 +386,8 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
                     c.sendall(b"k")
                 t = from_dlpack(m.dlpack(numel))
                 t._zest_vmm = m
+                if not _vmm_check(t, numel, token, p):
+                    raise RuntimeError(f"rank {p}'s arena does not read back through the mapping")
                 res[p] = t
                 dbg(f"mapped rank {p}'s {numel} bytes")
         except Exception as e:  # noqa: BLE001
