@@ -334,6 +334,14 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
             print(f"[vmm rank {rank}] {msg}", flush=True)
 
     token = objs[0][1]
+    try:  # a 141 GB arena is 282 chunk fds, held next to a peer's 282 while they are imported
+        import resource
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        want = 4 * max(o[3] for o in objs) + 256
+        if soft != resource.RLIM_INFINITY and soft < want:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (want if hard == resource.RLIM_INFINITY else min(want, hard), hard))
+    except (ImportError, ValueError, OSError):
+        pass
     _vmm_mark(arena, token, rank)
     fds_mine = vm.export_fds()
     dbg(f"exported {len(fds_mine)} chunk fds")
