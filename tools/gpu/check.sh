@@ -1,0 +1,73 @@
+#!/bin/bash
+# GPU-box measurement steps, run through gpurun from this container:
+#
+#   gpurun --timeout 1100 -- 'bash tools/gpu/check.sh OUT_DIR step [step ...]'
+#
+# Every step runs under its own time limit; the first step that fails, times out or faults ends the
+# script (nothing more touches the GPU after it).  Logs land in gpurun_out/OUT_DIR/.
+#
+# steps:
+#   kernels     HIP kernel numerics tests (tests/test_gpu_kernels.py)
+#   tests       full `pytest -m gpu` (one process)
+#   smoke       __graft_entry__.smoke()
+#   bench       default `python bench.py` (N=1, Llama-3.1-70B, bf16 headline + random) ($STEPS/$WARMUP)
+#   rehearsal   self-launched `bench.py --gpus 2` on the one GPU (gloo control, ranks share the
+#               device; --exchange auto incl. the VMM-mapped ipc/xgmi modes), Llama-3.1-8B
+#   ipc         peer-mapped arena tests (tests/test_gpu_ipc.py)
+#   cli         `zest pull --gpus 1` vs host `zest pull` (Llama-3.1-8B from an HBM seeder, sync between)
+#   stripe      host pull from 1 vs 3 loopback seeders
+#   seed        HBM seeding throughput (Mixtral-8x7B, chunks_served/s)
+#   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group)
+#   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
+#   hostbench   `zest bench --synthetic` on the box's CPU
+set -o pipefail
+OUT=gpurun_out/${1:?usage: check.sh OUT_DIR step...}
+shift
+mkdir -p "$OUT"
+export ZEST_SKIP_BUILD=1 TMPDIR=/tmp
+STEPS=${STEPS:-5}
+WARMUP=${WARMUP:-2}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+
+fail() { echo "[check] step $1 failed (rc=$2)"; tail -40 "$3" | grep -v amdgpu.ids; exit 1; }
+
+for step in "$@"; do
+  log=$OUT/$step.log
+  t0=$(date +%s)
+  case $step in
+    kernels) timeout -k 10 400 $PYT tests/test_gpu_kernels.py > $log 2>&1 || fail $step $? $log
+             tail -1 $log ;;
+    tests) timeout -k 10 1000 $PYT -m gpu tests > $log 2>&1 || fail $step $? $log
+           tail -1 $log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 || fail $step $? $log
+           grep -h "smoke" $log ;;
+    bench) timeout -k 10 900 python -u bench.py --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
+           grep -h "aggregate" $log; tail -1 $log | cut -c1-400 ;;
+    rehearsal) ZEST_BENCH_BACKEND=gloo ZEST_BENCH_LOG_ALL=1 timeout -k 10 700 python -u bench.py --gpus 2 \
+                 --model llama-3.1-8b --steps 3 --warmup 1 > $log 2>&1 || fail $step $? $log
+               grep -h "mapped\|autotune\|GB/s aggregate" $log | head -12; tail -1 $log | cut -c1-600 ;;
+    ipc) timeout -k 10 400 $PYT -v tests/test_gpu_ipc.py > $log 2>&1 || fail $step $? $log
+         grep -E "PASSED|FAILED|SKIPPED" $log ;;
+    cli) timeout -k 10 700 python -u tools/direct_bench.py --model llama-3.1-8b --skip-direct --host-after \
+           --out $OUT/cli_vs_host.json > $log 2>&1 || fail $step $? $log
+         grep -h "^\[" $log ;;
+    stripe) timeout -k 10 600 python -u tools/stripe_bench.py --mb 4096 --out $OUT/stripe.json > $log 2>&1 \
+              || fail $step $? $log
+            grep -h "^\[" $log ;;
+    seed) timeout -k 10 600 python -u tools/seed_bench.py > $log 2>&1 || fail $step $? $log
+          tail -5 $log ;;
+    kbench) timeout -k 10 600 python -u tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} > $OUT/kbench.jsonl 2> $log \
+              || fail $step $? $log
+            grep -h kernel $OUT/kbench.jsonl | cut -c1-200 ;;
+    prof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o b70 -- \
+            python3 bench.py --steps 3 --warmup 1 > $log 2>&1 || fail $step $? $log
+          db=$(find $OUT/prof -name "*.db" | head -1)
+          python tools/rocpd_summary.py "$db" --title "70B bench kernels ($(git log -1 --format=%h 2>/dev/null || echo tree))" \
+            > $OUT/kernels.md 2>&1
+          head -30 $OUT/kernels.md; rm -f "$db" ;;
+    hostbench) ./zest_amd/_bin/zest bench --synthetic > $log 2>&1 || fail $step $? $log
+               lscpu | grep -E "Model name|^CPU\(s\)" >> $log; cat $log ;;
+    *) echo "[check] unknown step $step"; exit 2 ;;
+  esac
+  echo "[check] $step ok in $(( $(date +%s) - t0 ))s"
+done
