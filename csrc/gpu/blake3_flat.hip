@@ -7,8 +7,10 @@
 // kernel ran at 1.4 TB/s (profiles/bench70b_n1_kernels_r2.md), about 40 % of the VALU peak for
 // BLAKE3.  Here the work is re-cut so the lanes stay full:
 //
-//   k_hash_plan    one workgroup: exclusive scan of leaves per chunk -> P[c]; WF[t] = the chunk
-//                  that owns leaf 64 t (where wave task t starts); L = total leaves.
+//   k_plan_tiles + k_plan_scan
+//                  exclusive scan of leaves per chunk -> P[c] (per-tile sums, then per-tile scans
+//                  over the whole chip); WF[t] = the chunk that owns leaf 64 t (where wave task t
+//                  starts); L = total leaves.
 //   k_hash_leaves  lane per leaf over the launch's leaves packed back to back (wave task t = leaves
 //                  64t..64t+63, persistent grid, so only the launch's last task has idle lanes);
 //                  next block's loads in flight during each compression; chaining values -> CV[g].
@@ -18,7 +20,7 @@
 //                  CV; the compression with two nodes left carries ROOT and writes the hash.
 //
 // Scratch (caller-owned, one per concurrently running launch): 64 B header | P[n+1] | WF[cap/64+2]
-// | CV[cap][8 words], cap >= total leaves (total_bytes / 1024 + n bounds it).  If the launch has
+// | TS[tiles] | CV[cap][8 words], cap >= total leaves (total_bytes / 1024 + n bounds it).  If the launch has
 // more leaves than cap (caller undersized the scratch) every hash is written as 32 x 0xFF, so the
 // result cannot verify.
 #include <hip/hip_runtime.h>
@@ -32,8 +34,7 @@ namespace {
 constexpr int kWave = 64;
 constexpr uint32_t kMaxChunk = 128u * 1024u;
 constexpr int kTreeG = 8;           // Xet chunks per wave in k_hash_tree
-constexpr int kPlanThreads = 1024;  // k_hash_plan is one workgroup
-constexpr int kPlanRegs = 16;       // plan tiles (x 1024 chunks) whose descriptors are loaded up front
+constexpr int kPlanThreads = 1024;  // chunks per plan tile (one per thread)
 constexpr int kLeafMaxWaves = 8192; // persistent leaf grid cap (32 waves per CU)
 
 struct PlanHdr {
@@ -46,12 +47,15 @@ struct PlanHdr {
 struct Layout {
   uint32_t* P;
   uint32_t* WF;
+  uint32_t* TS;  // per-tile leaf sums (k_plan_tiles -> k_plan_scan)
   uint32_t* CV;
   uint32_t cap;
 };
 
+__host__ __device__ inline uint64_t plan_tiles(int n) { return (uint64_t(n) + kPlanThreads - 1) / kPlanThreads; }
+
 __host__ __device__ inline uint64_t cv_offset(int n, uint64_t cap) {
-  const uint64_t head = 64 + 4 * (uint64_t(n) + 1) + 4 * (cap / 64 + 2);
+  const uint64_t head = 64 + 4 * (uint64_t(n) + 1) + 4 * (cap / 64 + 2) + 4 * plan_tiles(n);
   return (head + 255) & ~uint64_t(255);
 }
 
@@ -59,6 +63,7 @@ __host__ __device__ inline Layout layout(uint8_t* s, int n, uint32_t cap) {
   Layout l;
   l.P = reinterpret_cast<uint32_t*>(s + 64);
   l.WF = l.P + n + 1;
+  l.TS = l.WF + cap / 64 + 2;
   l.CV = reinterpret_cast<uint32_t*>(s + cv_offset(n, cap));
   l.cap = cap;
   return l;
@@ -131,8 +136,7 @@ template <class Src>
 __device__ __forceinline__ uint32_t n_leaves(const Src& s, int c) {
   uint32_t len;
   if constexpr (Src::kPlace) {
-    // the plan needs only the size: one 4-byte load instead of the 32-byte record (the single-
-    // workgroup plan is latency-bound).  A record that later fails its bounds check in get() hashes
+    // the plan needs only the size: one 4-byte load instead of the 32-byte record.  A record that later fails its bounds check in get() hashes
     // as empty leaves, so its chunk hash -- and the file's Merkle check -- fails as it should.
     len = s.chunks[c].ulen;
     if (len > kMaxChunk) len = 0;
@@ -160,56 +164,61 @@ __device__ __forceinline__ const zg::Key8& key_of(int key_mode) {
   return key_mode == 0 ? zg::kDataKeyW : key_mode == 1 ? zg::kNodeKeyW : key_mode == 2 ? zg::kIVW : zg::kZeroW;
 }
 
+// The plan is two chip-wide launches (round 2 ran it as one 1024-thread workgroup on a single CU,
+// 18-21 us per 16k chunks, latency-bound): k_plan_tiles sums the leaves of each 1024-chunk tile,
+// k_plan_scan gives every tile its base (sum of the tile sums before it, at most a few hundred
+// values read by every block) and scans the tile locally.  Neither needs inter-workgroup sync.
 template <class Src>
-__global__ void __launch_bounds__(kPlanThreads) k_hash_plan(Src s, int n, uint8_t* scratch, uint32_t cap) {
-  // Tiles of 1024 chunks, thread t owning chunk 1024 k + t of tile k, so every descriptor load and
-  // P store of a wave is one contiguous run (this kernel runs on a single CU: with one thread per
-  // contiguous chunk range its scattered accesses cost ~30 us per 16k chunks).  The first
-  // kPlanRegs tiles' descriptors are loaded up front, all in flight together.
-  __shared__ uint32_t part[2][kPlanThreads / kWave];
+__global__ void __launch_bounds__(kPlanThreads) k_plan_tiles(Src s, int n, uint8_t* scratch, uint32_t cap) {
+  __shared__ uint32_t red[kPlanThreads / kWave];
   const Layout l = layout(scratch, n, cap);
-  const int t = threadIdx.x, wid = t >> 6;
-  const int tiles = (n + kPlanThreads - 1) / kPlanThreads;
-  uint32_t nbv[kPlanRegs];
-#pragma unroll
-  for (int k = 0; k < kPlanRegs; ++k) nbv[k] = n_leaves(s, min(k * kPlanThreads + t, n - 1));
-  uint32_t carry = 0;
-  // exclusive scan over the tiles: P[c] = first leaf of chunk c; carry = leaves of the tiles so far
-  for (int k = 0; k < tiles; ++k) {
-    uint32_t v = 0;
-    if (k < kPlanRegs) {
-#pragma unroll
-      for (int i = 0; i < kPlanRegs; ++i) v = i == k ? nbv[i] : v;
-    } else {
-      v = n_leaves(s, min(k * kPlanThreads + t, n - 1));
-    }
-    const int c = k * kPlanThreads + t;
-    v = c < n ? v : 0u;
-    const uint32_t incl = zwv::scan_add(v);
-    if ((t & (kWave - 1)) == kWave - 1) part[k & 1][wid] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kPlanThreads / kWave; ++w) {
-      const uint32_t x = part[k & 1][w];
-      before += w < wid ? x : 0u;
-      total += x;
-    }
-    const uint32_t run = carry + before + incl - v;
-    if (c < n) l.P[c] = run;
-    carry += total;
-  }
-  const uint32_t L = carry;
-  const bool overflow = L > cap;
-  __syncthreads();  // P complete (read back below by this block only)
-  if (!overflow) {
-    // WF[task] = chunk owning leaf 64 task: every chunk marks the task starts inside its range
-    for (int c = t; c < n; c += kPlanThreads) {
-      const uint32_t lo = l.P[c], hi = c + 1 < n ? l.P[c + 1] : L;
-      for (uint32_t g = (lo + 63u) & ~63u; g < hi; g += 64) l.WF[g >> 6] = uint32_t(c);
-    }
-  }
+  const int t = threadIdx.x, c = blockIdx.x * kPlanThreads + t;
+  const uint32_t incl = zwv::scan_add(c < n ? n_leaves(s, c) : 0u);
+  if ((t & (kWave - 1)) == kWave - 1) red[t >> 6] = incl;
+  __syncthreads();
   if (t == 0) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int w = 0; w < kPlanThreads / kWave; ++w) sum += red[w];
+    l.TS[blockIdx.x] = sum;
+  }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kPlanThreads) k_plan_scan(Src s, int n, uint8_t* scratch, uint32_t cap) {
+  constexpr int W = kPlanThreads / kWave;
+  __shared__ uint32_t part[W], red_before[W], red_all[W];
+  const Layout l = layout(scratch, n, cap);
+  const int t = threadIdx.x, wid = t >> 6, k = blockIdx.x, tiles = gridDim.x;
+  // this tile's base and the grand total L from the per-tile sums
+  uint32_t before = 0, all = 0;
+  for (int j = t; j < tiles; j += kPlanThreads) {
+    const uint32_t x = l.TS[j];
+    before += j < k ? x : 0u;
+    all += x;
+  }
+  const int c = k * kPlanThreads + t;
+  const uint32_t v = c < n ? n_leaves(s, c) : 0u;
+  const uint32_t incl = zwv::scan_add(v);
+  const uint32_t wb = zwv::scan_add(before), wa = zwv::scan_add(all);
+  if ((t & (kWave - 1)) == kWave - 1) part[wid] = incl, red_before[wid] = wb, red_all[wid] = wa;
+  __syncthreads();
+  uint32_t base = 0, L = 0, wave_off = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    base += red_before[w];
+    L += red_all[w];
+    wave_off += w < wid ? part[w] : 0u;
+  }
+  const bool overflow = L > cap;
+  const uint32_t run = base + wave_off + incl - v;  // P[c] = first leaf of chunk c
+  if (c < n) {
+    l.P[c] = run;
+    // WF[task] = chunk owning leaf 64 task: every chunk marks the task starts inside [run, run + v)
+    if (!overflow)
+      for (uint32_t g = (run + 63u) & ~63u; g < run + v; g += 64) l.WF[g >> 6] = uint32_t(c);
+  }
+  if (k == tiles - 1 && t == 0) {
     l.P[n] = L;
     PlanHdr* h = reinterpret_cast<PlanHdr*>(scratch);
     h->leaves = overflow ? 0u : L;
@@ -360,7 +369,10 @@ hipError_t launch_flat(Src s, int n, int key_mode, uint8_t* out, uint64_t* sizes
                        size_t scratch_bytes, hipStream_t stream) {
   const uint32_t cap = cap_of(n, scratch_bytes);
   if (cap == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_hash_plan<Src>), dim3(1), dim3(kPlanThreads), 0, stream, s, n, scratch, cap);
+  if (n <= 0) return hipSuccess;
+  const uint32_t tiles = uint32_t(plan_tiles(n));
+  hipLaunchKernelGGL((k_plan_tiles<Src>), dim3(tiles), dim3(kPlanThreads), 0, stream, s, n, scratch, cap);
+  hipLaunchKernelGGL((k_plan_scan<Src>), dim3(tiles), dim3(kPlanThreads), 0, stream, s, n, scratch, cap);
   const uint64_t task_bound = (uint64_t(cap) + 63) / 64;
   const uint32_t waves = uint32_t(task_bound < kLeafMaxWaves ? task_bound : kLeafMaxWaves);
   hipLaunchKernelGGL((k_hash_leaves<Src>), dim3((waves + 3) / 4), dim3(256), 0, stream, s, n, key_mode, scratch, cap,

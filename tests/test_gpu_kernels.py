@@ -103,6 +103,27 @@ def test_hash_leaf_flat_vs_wave_kernel_cdc_sizes():
         assert node[i].tobytes() == C.internal_node_hash(data[o:o + int(ln)])
 
 
+def test_hash_leaf_flat_multi_tile_plan():
+    """The leaf plan runs as per-tile sums + per-tile scans over many workgroups (1024 chunks per
+    tile): a launch of 3333 messages spans 4 tiles, the last one partial, with tile sums that differ
+    (tiny messages in one tile, 64-128 KiB ones in another)."""
+    rng = np.random.default_rng(11)
+    lens = ([int(x) for x in rng.integers(0, 2049, 1100)] + [int(x) for x in rng.integers(64 << 10, (128 << 10) + 1, 200)]
+            + [int(x) for x in rng.integers(0, 9000, 2033)])
+    total = sum(lens) + 2 * len(lens) + 64
+    data = rng.integers(0, 256, total, dtype=np.uint8).tobytes()
+    buf = ops.padded_empty(len(data), DEV)
+    buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    offs, pos = [], 1
+    for ln in lens:
+        offs.append(pos)
+        pos += ln + int(rng.integers(0, 2))
+    assert pos <= len(data)
+    flat = _raw_hash_ranges(buf, offs, lens)
+    for i, (o, ln) in enumerate(zip(offs, lens)):
+        assert flat[i].tobytes() == C.chunk_hash(data[o:o + ln]), (i, ln)
+
+
 def test_hash_leaf_flat_oversize_and_undersized_scratch():
     data = bytes(range(256)) * 4096
     buf = ops.padded_empty(len(data), DEV)
@@ -195,6 +216,70 @@ def test_ingest_matches_cpu(policy, fused):
     assert out[:dst_gap] == b"\xab" * dst_gap and out[dst_gap + len(data):] == b"\xab" * dst_gap
     want = b"".join(b.chunk_hashes())
     assert hashes.cpu().numpy().tobytes() == want
+
+
+def _decode_both(body, chunks_data, n):
+    """Index one run, then decode it with the one-kernel batched decoder and with the two-kernel
+    records decoder; returns (output, error word) per decoder."""
+    H = ops.hip()
+    data = b"".join(chunks_data)
+    src = ops.padded_empty(len(body) + 5, DEV)
+    src.zero_()
+    src[5:5 + len(body)].copy_(torch.frombuffer(bytearray(body), dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (5, len(body), 3, 0, n, len(data))
+    dst = ops.padded_empty(len(data) + 3, DEV)
+    ws = ops.IngestWorkspace(DEV, 1, n)
+    hashes = torch.zeros((n, 32), dtype=torch.uint8, device=DEV)
+    ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False)  # leaves the chunk records in ws.chunks
+    st = torch.cuda.current_stream().cuda_stream
+    out = []
+    for rec in (False, True):
+        dst.fill_(0x5A)
+        ws.err.zero_()
+        sp, sb = ws.dec_scratch.get(n, src.numel()) if rec else (0, 0)
+        H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(), ws.chunks.data_ptr(), n,
+                     ws.err.data_ptr(), st, 0, sp, sb)
+        torch.cuda.synchronize()
+        out.append((dst.cpu().numpy().tobytes()[3:3 + len(data)], int(ws.err.item())))
+    return out
+
+
+@pytest.mark.parametrize("policy", ["lz4", "bg4"])
+def test_lz4_records_decoder_matches_batched(policy):
+    """Two-kernel decoder (lane-per-chunk parse into records + record-driven execute) vs the one-
+    kernel batched decoder and the input: literal runs over the 14-bit record field, matches over
+    0x7FFF (split records), tiny chunks whose record region is too small (decode_chunk fallback),
+    BG4 groups of odd sizes; and a corrupted frame gives both decoders the same error word."""
+    rng = np.random.default_rng(21)
+    chunks = [b"a" * 40, b"xyz" * 9 + b"q", rng.bytes(40_000) + bytes(30_001), bytes(100_000),
+              _bf16(32_771, 3)[:65_541], (b"zest " * 30_000)[:131_072], rng.bytes(20_000) * 3, bytes(1),
+              b"ab" * 5000 + rng.bytes(17_000), rng.bytes(9_000)]
+    b = C.XorbBuilder(policy)
+    for ch in chunks:
+        b.add_chunk(ch)
+    body = b.serialize(False)
+    idx = C.index_chunks(body)
+    schemes = [e[2] for e in idx]
+    assert sum(s != 0 for s in schemes) >= 6, schemes
+    data = b"".join(chunks)
+    (ob, eb), (orc, er) = _decode_both(body, chunks, len(chunks))
+    assert eb == 0 and er == 0
+    pos = 0
+    for ch, sc in zip(chunks, schemes):
+        if sc != 0:  # raw chunks are placed by the ingest pass, not by the decoders
+            assert ob[pos:pos + len(ch)] == ch and orc[pos:pos + len(ch)] == ch, (len(ch), sc)
+        pos += len(ch)
+    assert pos == len(data)
+    # corrupt the middle of the longest compressed chunk's stream
+    big = max((e for e in idx if e[2] != 0), key=lambda e: e[1])
+    bad = bytearray(body)
+    mid = big[0] + 8 + big[1] // 2
+    bad[mid:mid + 64] = bytes(rng.integers(0, 256, 64, dtype=np.uint8))
+    (ob, eb), (orc, er) = _decode_both(bytes(bad), chunks, len(chunks))
+    assert eb == er, (hex(eb), hex(er))
+    if eb == 0:
+        assert ob == orc
 
 
 def test_ingest_clip_window():
