@@ -446,20 +446,253 @@ __global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__
   }
 }
 
+// -----------------------------------------------------------------------------------------------
+// Experimental two-kernel decode: SIMT parse (a LANE per chunk) + record-driven execute (a WAVE per
+// chunk).  Not on the ingest path: reachable through zg_lz4_decode_records / hip().lz4_decode(...,
+// rec_scratch=...) for kbench and tests.
+//
+// Why it exists: the wave-per-chunk decoder above parses on the scalar unit (~22 SALU per
+// sequence; a CU has one scalar unit for its 4 SIMDs), and on BG4 bf16 (~6.8k sequences per
+// 64 KiB) 1 GiB took 11.1 ms at 8 waves/SIMD, 14.7 at 4, 21.4 at 2.  Here the parse is vector code
+// with one lane per chunk, every sequence becomes an 8-byte record {literal position | literal
+// length << 18, offset | match length << 16} in a scratch region owned by the chunk (3/8 record
+// per compressed byte: LZ4 needs >= 3 bytes per sequence), and the execute kernel loads 64 records
+// per batch with one vector load and runs exec_batch.  A chunk whose parse fails or does not fit
+// its region gets count kNoRecs and is decoded by decode_chunk, which reports the exact error.
+//
+// Measured on MI355X (profiles/lz4_records_r3.md, 1 GiB of BG4 bf16): the execute kernel alone
+// takes 6.4 ms (1.75x faster than the one-kernel decoder's 11.1), but the parse takes 15 ms: only
+// 16.7k chunks = 261 waves of lanes, each walking ~6.8k sequences through dependent loads, and the
+// compiler's vmcnt(0) waits inside the divergent loop also wait for the record stores.  A parse
+// that stages each lane's stream in LDS in bulk would be the next step.
+constexpr uint32_t kNoRecs = 0xFFFFFFFFu;
+constexpr uint32_t kRecLitMax = 0x3FFFu;  // 14-bit literal field
+constexpr uint32_t kRecMlMax = 0x7FFFu;
+
+__host__ __device__ inline uint64_t rec_index(uint64_t src_off) { return (3 * src_off) >> 3; }
+
+// Per-lane reader over a payload [base, base + clen): 4 bytes at index p as two aligned dword loads
+// (the streams are sequential per lane, so these hit the vector L1 after the first touch) joined
+// by v_alignbyte.  The high dword's address is clamped to the payload's last dword, so nothing
+// past the buffer is touched (its bytes past the payload never decide anything).  Plain values
+// only: a register window selected by lane-varying indices was lowered to scratch memory.
+struct LaneRd {
+  const uint8_t* w;  // payload rounded down to a dword
+  uint32_t k0;       // payload address & 3
+  uint32_t last;     // index (from w) of the payload's last dword
+};
+
+__device__ __forceinline__ uint32_t rd4(const LaneRd& r, uint32_t p) {
+  const uint32_t q = (r.k0 + p) & ~3u;
+  const uint32_t lo = *reinterpret_cast<const uint32_t*>(r.w + q);
+  const uint32_t hi = *reinterpret_cast<const uint32_t*>(r.w + min(q + 4, r.last));
+  return __builtin_amdgcn_alignbyte(hi, lo, (r.k0 + p) & 3);  // byte shift
+}
+
+struct RecOut {
+  uint2* rec;
+  uint32_t n, cap;
+  bool over;
+};
+
+__device__ __forceinline__ void rec_emit(RecOut& o, uint32_t lp, uint32_t lit, uint32_t ml, uint32_t off) {
+  do {
+    const uint32_t l = lit > kRecLitMax ? kRecLitMax : lit;
+    const uint32_t m = lit > kRecLitMax ? 0u : (ml > kRecMlMax ? kRecMlMax : ml);
+    if (o.n < o.cap) o.rec[o.n] = make_uint2(lp | (l << 18), off | (m << 16));
+    else o.over = true;
+    ++o.n;
+    lp += l;
+    lit -= l;
+    ml -= m;
+  } while (lit | ml);
+}
+
+// Parse one chunk's LZ4 frame into records; returns the record count or kNoRecs.
+__device__ uint32_t parse_chunk(const uint8_t* pay, uint32_t clen, uint2* rec, uint32_t cap) {
+  LaneRd r;
+  r.k0 = uint32_t(reinterpret_cast<uintptr_t>(pay) & 3);
+  r.w = pay - r.k0;
+  r.last = (r.k0 + (clen ? clen - 1 : 0)) & ~3u;
+  RecOut o{rec, 0u, cap, false};
+  if (clen < 7 || rd4(r, 0) != 0x184D2204u) return kNoRecs;
+  const uint32_t flg = rd4(r, 4) & 0xFF;
+  if ((flg >> 6) != 1) return kNoRecs;
+  uint32_t ip = 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+  const uint32_t bck = (flg & 0x10) ? 4 : 0;
+  while (true) {
+    if (ip > clen || clen - ip < 4) return kNoRecs;
+    const uint32_t bs = rd4(r, ip);
+    ip += 4;
+    if (bs == 0) break;
+    const uint32_t len = bs & 0x7FFFFFFFu;
+    if (len > clen - ip) return kNoRecs;
+    if (bs >> 31) {  // stored block: literals only
+      if (len) rec_emit(o, ip, len, 0, 0);
+      ip += len;
+    } else {
+      const uint32_t bend = ip + len;
+      while (true) {
+        if (ip >= bend) return kNoRecs;
+        const uint32_t t = rd4(r, ip);  // token + the 3 bytes after it
+        const uint32_t token = t & 0xFF;
+        ++ip;
+        uint32_t lit = token >> 4, ml = token & 15;
+        if (lit == 15) {
+          uint32_t b;
+          do {
+            if (ip >= bend || lit > kMaxChunk) return kNoRecs;
+            b = rd4(r, ip) & 0xFF;
+            ++ip;
+            lit += b;
+          } while (b == 255);
+        }
+        if (lit > bend - ip) return kNoRecs;
+        const uint32_t lp = ip;
+        ip += lit;
+        if (ip == bend) {  // last sequence of the block: literals only
+          if (lit) rec_emit(o, lp, lit, 0, 0);
+          break;
+        }
+        if (bend - ip < 2) return kNoRecs;
+        const uint32_t off = (lit == 0 ? t >> 8 : rd4(r, ip)) & 0xFFFF;  // no literals: already in t
+        ip += 2;
+        if (ml == 15) {
+          uint32_t b;
+          do {
+            if (ip >= bend || ml > kMaxChunk) return kNoRecs;
+            b = rd4(r, ip) & 0xFF;
+            ++ip;
+            ml += b;
+          } while (b == 255);
+        }
+        rec_emit(o, lp, lit, ml + 4, off);
+      }
+    }
+    ip += bck;
+  }
+  return o.over ? kNoRecs : o.n;
+}
+
+__global__ void __launch_bounds__(256) k_lz4_parse(const uint8_t* __restrict__ src, const ZgChunk* __restrict__ chunks,
+                                                   int n_chunks, uint64_t src_n, uint64_t dst_n, uint2* __restrict__ recs,
+                                                   uint32_t* __restrict__ counts) {
+  const int c = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (c >= n_chunks) return;
+  const ZgChunk ch = chunks[c];
+  uint32_t cnt = kNoRecs;
+  if (ch.scheme != 0 && ch.src + ch.clen <= src_n && ch.dst + ch.ulen <= dst_n && ch.ulen <= kMaxChunk) {
+    const uint64_t r0 = rec_index(ch.src), r1 = rec_index(ch.src + ch.clen);
+    cnt = parse_chunk(src + ch.src, ch.clen, recs + r0, uint32_t(r1 - r0));
+  }
+  counts[c] = cnt;
+}
+
+// Execute one chunk's records (64 per batch, the next batch's records loaded while this one runs).
+__device__ uint32_t exec_records(Ctx& X, const uint2* rec, uint32_t cnt, uint32_t lane) {
+  uint2 nx = lane < cnt ? rec[lane] : make_uint2(0u, 0u);
+  for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
+    const uint2 r = nx;
+    const uint32_t i = b0 + kWave + lane;
+    nx = i < cnt ? rec[i] : make_uint2(0u, 0u);
+    Batch B;
+    B.n = uni(min(uint32_t(kWave), cnt - b0));
+    B.rl = X.k0 + (r.x & 0x3FFFFu);
+    B.rh = r.y & 0xFFFFu;
+    B.rx = 0x80000000u | ((r.y >> 16) << 16) | (r.x >> 18);
+    if (!exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+  }
+  return X.obase == X.ulen ? 0u : uint32_t(ZG_ERR_SIZE);
+}
+
+__global__ void __launch_bounds__(256) k_lz4_exec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  const ZgChunk* __restrict__ chunks, int n_chunks,
+                                                  unsigned long long* err, uint64_t src_n, uint64_t dst_n,
+                                                  const uint2* __restrict__ recs, const uint32_t* __restrict__ counts) {
+  __shared__ uint32_t heads[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kWavesPerBlock][kRing];
+  const uint32_t lane = lane_id();
+  const int wave = int(uni(threadIdx.x >> 6));
+  const int stride = int(gridDim.x) * kWavesPerBlock;
+  for (int c = int(uni(blockIdx.x * kWavesPerBlock + uint32_t(wave))); c < n_chunks; c += stride) {
+    ZgChunk ch = chunks[c];
+    ch.src = uni64(ch.src);
+    ch.dst = uni64(ch.dst);
+    ch.clen = uni(ch.clen);
+    ch.ulen = uni(ch.ulen);
+    ch.scheme = uni(ch.scheme);
+    if (ch.scheme == 0) continue;
+    if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
+      if (lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
+      continue;
+    }
+    if (ch.ulen > kMaxChunk) {
+      if (lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      continue;
+    }
+    Ctx X;
+    X.pay = src + ch.src;
+    X.out = dst + ch.dst;
+    X.clen = ch.clen;
+    X.ulen = ch.ulen;
+    X.bg4 = ch.scheme == 2;
+    const uint32_t q = ch.ulen >> 2, r = ch.ulen & 3;
+    X.g1 = q + (r > 0 ? 1u : 0u);
+    X.g2 = X.g1 + q + (r > 1 ? 1u : 0u);
+    X.g3 = X.g2 + q + (r > 2 ? 1u : 0u);
+    X.k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);
+    X.obase = 0;
+    X.heads = heads[wave];
+    X.ring = rings[wave];
+    const uint32_t cnt = uni(counts[c]);
+    const uint32_t code = cnt == kNoRecs ? decode_chunk(X, lane) : exec_records(X, recs + rec_index(ch.src), cnt, lane);
+    if (code && lane == 0) report(err, code, uint32_t(c));
+  }
+}
+
 }  // namespace
 
-extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
-                                            const ZgChunk* chunks, int n_chunks, unsigned long long* err,
-                                            hipStream_t stream) {
+extern "C" hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                                 const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                                 int grid_cap, hipStream_t stream) {
   if (n_chunks <= 0) return hipSuccess;
-  // ZG_LZ4_GRID caps the persistent grid (occupancy experiments).
-  static const int grid_cap = [] {
-    const char* v = getenv("ZG_LZ4_GRID");
-    const int g = v ? atoi(v) : 0;
-    return g > 0 && g < 8192 ? g : 2048;
-  }();
+  if (grid_cap <= 0 || grid_cap >= 8192) grid_cap = 2048;
   const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(k_lz4_batched, dim3(blocks < grid_cap ? blocks : grid_cap), dim3(256), 0, stream, src, dst,
                      chunks, n_chunks, err, src_n, dst_n);
   return hipGetLastError();
 }
+
+extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                            const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                            hipStream_t stream) {
+  // ZG_LZ4_GRID caps the persistent grid (occupancy experiments); default 2048 blocks = 8 waves/SIMD.
+  static const int grid_cap = [] {
+    const char* v = getenv("ZG_LZ4_GRID");
+    return v ? atoi(v) : 0;
+  }();
+  return zg_lz4_batched_decode_grid(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, stream);
+}
+
+extern "C" size_t zg_lz4_rec_scratch_bytes(int n_chunks, uint64_t src_n) {
+  if (n_chunks <= 0) return 0;
+  const uint64_t counts = (4 * uint64_t(n_chunks) + 255) & ~uint64_t(255);
+  return size_t(counts + 8 * (rec_index(src_n) + 2));
+}
+
+extern "C" hipError_t zg_lz4_decode_records(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                            const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                            uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  if (!scratch || scratch_bytes < zg_lz4_rec_scratch_bytes(n_chunks, src_n))
+    return zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
+  uint2* recs = reinterpret_cast<uint2*>(scratch + ((4 * uint64_t(n_chunks) + 255) & ~uint64_t(255)));
+  hipLaunchKernelGGL(k_lz4_parse, dim3((n_chunks + 255) / 256), dim3(256), 0, stream, src, chunks, n_chunks, src_n,
+                     dst_n, recs, counts);
+  const int blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(k_lz4_exec, dim3(blocks < 2048 ? blocks : 2048), dim3(256), 0, stream, src, dst, chunks, n_chunks,
+                     err, src_n, dst_n, recs, counts);
+  return hipGetLastError();
+}
+

@@ -70,6 +70,17 @@ hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uin
                            uint8_t* clip_scratch, unsigned long long* err, hipStream_t stream);
 hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                  const ZgChunk* chunks, int n_chunks, unsigned long long* err, hipStream_t stream);
+// Two-kernel decode (lane-per-chunk parse into records, wave-per-chunk execute) with a caller-owned
+// scratch of zg_lz4_rec_scratch_bytes(n_chunks, src_n) bytes (one per concurrently running
+// launch); a null or short scratch runs zg_lz4_batched_decode instead.
+size_t zg_lz4_rec_scratch_bytes(int n_chunks, uint64_t src_n);
+hipError_t zg_lz4_decode_records(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                 const ZgChunk* chunks, int n_chunks, unsigned long long* err, uint8_t* scratch,
+                                 size_t scratch_bytes, hipStream_t stream);
+// Same with an explicit persistent-grid cap in blocks of 4 waves (0 = default 2048).
+hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                      const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
+                                      hipStream_t stream);
 // K1 keyed BLAKE3 of placed chunks (hashes[hash_index_base + c], sizes likewise when non-null) or of
 // raw (offset, len) messages (key_mode 0 Xet data key, 1 node key, 2 plain, 3 zero key; a message
 // over 128 KiB gets an all-ones hash).  With `scratch` (>= zg_hash_scratch_bytes(n, total message

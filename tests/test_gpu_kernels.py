@@ -233,16 +233,19 @@ def _decode_both(body, chunks_data, n):
     hashes = torch.zeros((n, 32), dtype=torch.uint8, device=DEV)
     ops.ingest_terms(src, dst, terms, hashes, ws=ws, check=False)  # leaves the chunk records in ws.chunks
     st = torch.cuda.current_stream().cuda_stream
+    dec = ops.DecodeScratch(DEV)
     out = []
     for rec in (False, True):
         dst.fill_(0x5A)
         ws.err.zero_()
-        sp, sb = ws.dec_scratch.get(n, src.numel()) if rec else (0, 0)
+        sp, sb = dec.get(n, src.numel()) if rec else (0, 0)
         H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(), ws.chunks.data_ptr(), n,
                      ws.err.data_ptr(), st, 0, sp, sb)
         torch.cuda.synchronize()
         out.append((dst.cpu().numpy().tobytes()[3:3 + len(data)], int(ws.err.item())))
-    return out
+    # per-chunk record counts the parse left at the head of the scratch (-1: decode_chunk fallback)
+    counts = dec.buf[:4 * n].view(torch.int32).cpu().tolist()
+    return out, counts
 
 
 @pytest.mark.parametrize("policy", ["lz4", "bg4"])
@@ -263,8 +266,12 @@ def test_lz4_records_decoder_matches_batched(policy):
     schemes = [e[2] for e in idx]
     assert sum(s != 0 for s in schemes) >= 6, schemes
     data = b"".join(chunks)
-    (ob, eb), (orc, er) = _decode_both(body, chunks, len(chunks))
+    ((ob, eb), (orc, er)), counts = _decode_both(body, chunks, len(chunks))
     assert eb == 0 and er == 0
+    # the records path really ran: every compressed chunk of >= 256 stored bytes parsed into records
+    for e, cnt in zip(idx, counts):
+        if e[2] != 0 and e[1] >= 256:
+            assert cnt > 0, (e, cnt)
     pos = 0
     for ch, sc in zip(chunks, schemes):
         if sc != 0:  # raw chunks are placed by the ingest pass, not by the decoders
@@ -276,7 +283,7 @@ def test_lz4_records_decoder_matches_batched(policy):
     bad = bytearray(body)
     mid = big[0] + 8 + big[1] // 2
     bad[mid:mid + 64] = bytes(rng.integers(0, 256, 64, dtype=np.uint8))
-    (ob, eb), (orc, er) = _decode_both(bytes(bad), chunks, len(chunks))
+    ((ob, eb), (orc, er)), _ = _decode_both(bytes(bad), chunks, len(chunks))
     assert eb == er, (hex(eb), hex(er))
     if eb == 0:
         assert ob == orc

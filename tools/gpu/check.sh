@@ -19,6 +19,7 @@
 #   seed        HBM seeding throughput (Mixtral-8x7B, chunks_served/s)
 #   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group)
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
+#   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
 #   hostbench   `zest bench --synthetic` on the box's CPU
 set -o pipefail
 OUT=gpurun_out/${1:?usage: check.sh OUT_DIR step...}
@@ -65,6 +66,11 @@ for step in "$@"; do
           python tools/rocpd_summary.py "$db" --title "70B bench kernels ($(git log -1 --format=%h 2>/dev/null || echo tree))" \
             > $OUT/kernels.md 2>&1
           head -30 $OUT/kernels.md; rm -f "$db" ;;
+    kprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kprof -o kb -- \
+             python3 tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} > $log 2>&1 || fail $step $? $log
+           db=$(find $OUT/kprof -name "*.db" | head -1)
+           python tools/rocpd_summary.py "$db" --title "kbench ${KBENCH_ONLY:-all} kernels" > $OUT/kernels_kbench.md 2>&1
+           head -24 $OUT/kernels_kbench.md; rm -f "$db" ;;
     hostbench) ./zest_amd/_bin/zest bench --synthetic > $log 2>&1 || fail $step $? $log
                lscpu | grep -E "Model name|^CPU\(s\)" >> $log; cat $log ;;
     *) echo "[check] unknown step $step"; exit 2 ;;

@@ -162,9 +162,10 @@ def main():
         emit(kernel="hash_chunks[flat]", bytes=n, ms=ms, gbps=n / ms / 1e6)
         del body, dst
 
-    def ingest_case(name, raw, policy, iters, fused=None):
+    def ingest_case(name, raw, policy, iters, fused=None, after=None):
         """Pack `raw` into xorb runs with `policy`, then time index+place/decode+hash on the GPU
-        (fused: one place+hash pass; None = the ZEST_FUSED_INGEST default)."""
+        (fused: one place+hash pass; None = the ZEST_FUSED_INGEST default).  `after(src, dst, ws,
+        n_chunks)` runs extra timings on the indexed batch."""
         m = len(raw)
         ends = C.chunk_ends(raw)
         b = C.XorbBuilder(policy)
@@ -208,6 +209,8 @@ def main():
         emit(kernel=f"ingest_{policy}({name}){tag}", bytes=m, ms=ms, gbps=m / ms / 1e6, ratio=len(blob) / m,
              chunks=nck2, schemes={str(k): v for k, v in sorted(schemes.items())}, exact=ok)
         assert ok, name
+        if after is not None:
+            after(src, dst, ws, nck2)
         del src, dst, hashes, ws
 
     if want("lz4"):
@@ -225,6 +228,37 @@ def main():
         raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
         del w
         ingest_case("bf16_1g", raw, "bg4", max(3, a.iters // 4))
+        del raw
+
+    if want("lz4occ"):
+        # K3 alone on a bench-sized BG4 round, persistent grid capped at 8 / 4 / 2 / 1 / 0.5 waves
+        # per SIMD: latency-bound waves speed up with occupancy, an issue-bound decoder does not
+        m = 1 << 30
+        w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
+        raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+        del w
+
+        def occ(src, dst, ws, n):
+            for g in (2048, 1024, 512, 256, 128):
+                ms = timed(lambda: H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(),
+                                                ws.chunks.data_ptr(), n, ws.err.data_ptr(), st, g), 3)
+                ops.raise_on_error(ws.err)
+                emit(kernel=f"lz4_decode(bf16_1g,grid={g})", bytes=m, ms=ms, gbps=m / ms / 1e6,
+                     waves_per_simd=g * 4 / 1024)
+            assert dst[:m].cpu().numpy().tobytes() == raw
+            # the two-kernel decoder: lane-per-chunk parse into records, then record-driven execute
+            dec = ops.DecodeScratch(dev)
+            sp, sb = dec.get(n, src.numel())
+            dst.zero_()
+            ms = timed(lambda: H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(),
+                                            ws.chunks.data_ptr(), n, ws.err.data_ptr(), st, 0, sp, sb), 3)
+            ops.raise_on_error(ws.err)
+            fb = int((dec.buf[:4 * n].view(torch.int32) == -1).sum())
+            emit(kernel="lz4_decode(bf16_1g,records)", bytes=m, ms=ms, gbps=m / ms / 1e6, scratch_mb=sb >> 20,
+                 fallback_chunks=fb)
+            assert dst[:m].cpu().numpy().tobytes() == raw
+
+        ingest_case("bf16_1g", raw, "bg4", 3, after=occ)
         del raw
 
     if want("fuse"):

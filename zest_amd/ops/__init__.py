@@ -160,6 +160,23 @@ class HashScratch:
         return self.buf.data_ptr(), self.buf.numel()
 
 
+class DecodeScratch:
+    """Device scratch of the experimental two-kernel LZ4/BG4 decoder (lz4seq.hip k_lz4_parse +
+    k_lz4_exec: per-chunk sequence records, 3 bytes per compressed byte), grown on demand; one per
+    stream.  Only `hip().lz4_decode(..., rec_scratch=...)` uses it (kbench, tests): the ingest path
+    runs the one-kernel batched decoder, which is faster end to end (profiles/lz4_records_r3.md)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = None
+
+    def get(self, n: int, src_bytes: int) -> tuple[int, int]:
+        need = hip().lz4_rec_scratch_bytes(int(n), int(src_bytes))
+        if self.buf is None or self.buf.numel() < need:
+            self.buf = torch.empty(need + (need >> 3), dtype=torch.uint8, device=self.device)
+        return self.buf.data_ptr(), self.buf.numel()
+
+
 # ----------------------------------------------------------------------------------------------
 # K3 + K4: ingest fetched xorb runs into a destination arena, then K1 chunk hashes
 # ----------------------------------------------------------------------------------------------
