@@ -11,8 +11,8 @@
 #   tests       full `pytest -m gpu` (one process)
 #   smoke       __graft_entry__.smoke()
 #   bench       default `python bench.py` (N=1, Llama-3.1-70B, bf16 headline + random) ($STEPS/$WARMUP)
-#   rehearsal   self-launched `bench.py --gpus 2` on the one GPU (gloo control, ranks share the
-#               device; --exchange auto incl. the VMM-mapped ipc/xgmi modes), Llama-3.1-8B
+#   rehearsal   self-launched `bench.py --gpus $RANKS` (default 2) on the one GPU (gloo control, ranks
+#               share the device; --exchange auto incl. the VMM-mapped ipc/xgmi modes), Llama-3.1-8B
 #   ipc         peer-mapped arena tests (tests/test_gpu_ipc.py)
 #   cli         `zest pull --gpus 1` vs host `zest pull` (Llama-3.1-8B from an HBM seeder, sync between)
 #   stripe      host pull from 1 vs 3 loopback seeders
@@ -44,7 +44,7 @@ for step in "$@"; do
            grep -h "smoke" $log ;;
     bench) timeout -k 10 900 python -u bench.py --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
            grep -h "aggregate" $log; tail -1 $log | cut -c1-400 ;;
-    rehearsal) ZEST_BENCH_BACKEND=gloo ZEST_BENCH_LOG_ALL=1 timeout -k 10 700 python -u bench.py --gpus 2 \
+    rehearsal) ZEST_BENCH_BACKEND=gloo ZEST_BENCH_LOG_ALL=1 timeout -k 10 700 python -u bench.py --gpus ${RANKS:-2} \
                  --model llama-3.1-8b --steps 3 --warmup 1 > $log 2>&1 || fail $step $? $log
                grep -h "mapped\|autotune\|GB/s aggregate" $log | head -12; tail -1 $log | cut -c1-600 ;;
     ipc) timeout -k 10 400 $PYT -v tests/test_gpu_ipc.py > $log 2>&1 || fail $step $? $log
