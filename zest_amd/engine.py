@@ -224,7 +224,8 @@ def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: floa
     hipIpcOpenMemHandle of a >= 2 GiB allocation hung (64-512 MiB imports took < 2 ms,
     profiles/ipc_import_sizes_r3.txt), so that path is for small arenas.  ``deadline_s`` (default
     ``ZEST_IPC_DEADLINE`` = 60 s) bounds the imports: a rank whose imports do not return in time
-    reports failure, and the caller falls back to an RCCL exchange."""
+    reports failure, and the caller falls back to an RCCL exchange.  On the VMM path the deadline
+    covers all the ranks' import turns together."""
     import threading
     import uuid
 
@@ -404,19 +405,33 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
     st = threading.Thread(target=serve, daemon=True)
     st.start()
     dist.barrier(group=host_group)  # every rank is listening
+    # `deadline_s` bounds the whole mapping, not each turn: with 8 ranks and 141 GB arenas a slow
+    # import on every turn would otherwise add up past the caller's watchdog (bench.py's "ipc"
+    # phase) instead of falling back to RCCL.  A rank whose turn starts after the budget is spent
+    # does not import and reports failure; the MIN-reduce in map_peer_arenas then drops the mapping.
+    t_end = time.monotonic() + deadline_s
     imported = True
     for turn in range(n_ranks):
         if turn == rank:
-            it = threading.Thread(target=imp, daemon=True)
-            it.start()
-            it.join(deadline_s)
-            imported = not it.is_alive() and "error" not in res
+            left = t_end - time.monotonic()
+            if left <= 0:
+                imported = False
+                dbg("mapping budget spent before this rank's turn: not importing")
+            else:
+                it = threading.Thread(target=imp, daemon=True)
+                it.start()
+                it.join(left)
+                imported = not it.is_alive() and "error" not in res
         dist.barrier(group=host_group)
-    st.join(deadline_s)
+    # Every turn is over: a peer that imported has been served and acknowledged, so the serving
+    # thread has ended unless some rank skipped its turn; closing the socket ends its accept().
+    st.join(1.0)
+    complete = not st.is_alive() and served["error"] is None
     srv.close()
+    st.join(5.0)
     for fd in fds_mine:
         os.close(fd)
-    ok = imported and not st.is_alive() and served["error"] is None
+    ok = imported and complete
     if ok:
         for p in range(n_ranks):
             peers[p] = res.get(p)
