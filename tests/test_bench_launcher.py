@@ -46,6 +46,16 @@ def test_bench_prints_one_json_line(gpus):
         assert "launching 2 ranks" in p.stderr
 
 
+def test_bench_one_seeder_one_leecher():
+    """BASELINE config 2's shape: rank 0 pulls everything from the origin, rank 1 leeches it all
+    from rank 0 (half of the job's bytes arrive from a peer)."""
+    p, _ = _run(["--gpus", "2", "--seeders", "1", "--steps", "2", "--warmup", "1", "--modes", "random"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = _json_lines(p.stdout)[0]
+    assert out["config"]["parallelism"] == "seed1-leech1"
+    assert abs(out["p2p_ratio"] - 0.5) < 1e-6 and out["value"] > 0
+
+
 def test_bench_hung_rank_fails_fast():
     """Rank 1 stops in the warm-up phase: its watchdog dumps the stack and exits, torchrun tears
     rank 0 down, and the launcher returns non-zero well before any driver timeout."""
