@@ -108,8 +108,8 @@ __device__ __forceinline__ uint32_t bmap(const Ctx& X, uint32_t p) {
 
 // Records of the current batch: lane i holds record i (rl = gap | lit << 16, rh = ml | off << 16).
 // Record formats (per lane), chosen so the common sequence costs the parse almost nothing:
-//   short (fast path): rl = literal stream position | token << 24, rh = the 4 stream bytes after
-//                      the literals (offset in the low 16 bits), rx = 0
+//   short (fast path): rl = the token's stream position, rh = the 4 stream bytes after the
+//                      literals (offset in the low 16 bits), rx = 0; exec_batch loads the token
 //   general:           rl = literal stream position, rh = offset, rx = 1 << 31 | ml << 16 | lit
 //                      (lit <= 0xFFFF, ml <= 0x7FFF after splitting)
 // Stream positions are relative to the dword-aligned payload base (k0 + byte index).
@@ -194,11 +194,14 @@ __device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
 __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   const bool valid = lane < B.n;
   const bool gen = (B.rx >> 31) != 0;
-  const uint32_t tok = B.rl >> 24;
+  // short records carry the token's stream position (the parse spends no scalar work on packing the
+  // token): its byte is loaded here, lane-parallel, once per batch
+  const uint32_t tpos = B.rl - X.k0;
+  const uint32_t tok = valid && !gen ? uint32_t(X.pay[tpos < X.clen ? tpos : 0u]) : 0u;
   const uint32_t lit = !valid ? 0u : gen ? (B.rx & 0xFFFF) : tok >> 4;
   const uint32_t ml = !valid ? 0u : gen ? ((B.rx >> 16) & 0x7FFF) : (tok & 15) + 4;
   const uint32_t off = B.rh & 0xFFFF;
-  const uint32_t lpos = (B.rl & 0xFFFFFF) - X.k0;  // payload offset of this record's literals
+  const uint32_t lpos = gen ? tpos : tpos + 1;  // payload offset of this record's literals
   const uint32_t a2 = scan_add(lit + ml);
   const uint32_t li = scan_add(lit), mi = scan_add(ml);
   const uint32_t opos = X.obase + a2 - lit - ml;  // output offset of the record
@@ -363,7 +366,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
             const uint32_t lit = token >> 4;
             const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
             const bool me = lane == n;
-            rl = me ? (ip + 1) | (token << 24) : rl;  // short record (rx stays 0)
+            rl = me ? ip : rl;  // short record: the token's position (rx stays 0)
             rh = me ? y : rh;
             ip += 3 + lit;
             ++n;
