@@ -356,22 +356,27 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
           // >= 18 bytes before the block end (never the last sequence) and inside the batch:
           // one counter instead of two bounds tests per sequence.
           const uint32_t lim_blk = uni(bend > 18 ? bend - 18 : 0u);
-          uint32_t n = B.n, rl = B.rl, rh = B.rh;
+          uint32_t rl = B.rl, rh = B.rh;
           uint32_t token = uint32_t(sload8(w4, ip)) & 0xFF;
-          uint32_t iters = uni(ip < lim_blk ? min(kWave - n, (lim_blk - ip + 16) / 17) : 0u);
+          const uint32_t iters0 = uni(ip < lim_blk ? min(kWave - B.n, (lim_blk - ip + 16) / 17) : 0u);
+          uint32_t iters = iters0;
+          // the record's lane counts down in a VGPR (lane - n): one VALU op per sequence instead of
+          // a scalar increment on the CU's one scalar unit, which bounds this loop
+          int32_t dn = int32_t(lane) - int32_t(B.n);
           // single-exit loop (a `break` makes the structurizer route the exit flag through VALU)
           // continue while iters > 0 and neither nibble is 15: one integer test (min of the three)
           while (min(min(iters, (token & 15) ^ 15), (token >> 4) ^ 15) != 0) {
             iters = uni(iters - 1);
             const uint32_t lit = token >> 4;
             const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
-            const bool me = lane == n;
+            const bool me = dn == 0;
             rl = me ? ip : rl;  // short record: the token's position (rx stays 0)
             rh = me ? y : rh;
             ip += 3 + lit;
-            ++n;
+            --dn;
             token = (y >> 16) & 0xFF;
           }
+          const uint32_t n = uni(B.n + (iters0 - iters));
           B.n = n;
           B.rl = rl;
           B.rh = rh;
