@@ -108,8 +108,9 @@ __device__ __forceinline__ uint32_t bmap(const Ctx& X, uint32_t p) {
 
 // Records of the current batch: lane i holds record i (rl = gap | lit << 16, rh = ml | off << 16).
 // Record formats (per lane), chosen so the common sequence costs the parse almost nothing:
-//   short (fast path): rl = the token's stream position, rh = the 4 stream bytes after the
-//                      literals (offset in the low 16 bits), rx = 0; exec_batch loads the token
+//   short (fast path): rl = literal stream position, rh = the 4 stream bytes after the literals
+//                      (offset in the low 16 bits), rx = 0; exec_batch loads the token byte
+//                      before the literals
 //   general:           rl = literal stream position, rh = offset, rx = 1 << 31 | ml << 16 | lit
 //                      (lit <= 0xFFFF, ml <= 0x7FFF after splitting)
 // Stream positions are relative to the dword-aligned payload base (k0 + byte index).
@@ -194,14 +195,13 @@ __device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
 __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   const bool valid = lane < B.n;
   const bool gen = (B.rx >> 31) != 0;
-  // short records carry the token's stream position (the parse spends no scalar work on packing the
-  // token): its byte is loaded here, lane-parallel, once per batch
-  const uint32_t tpos = B.rl - X.k0;
-  const uint32_t tok = valid && !gen ? uint32_t(X.pay[tpos < X.clen ? tpos : 0u]) : 0u;
+  // short records carry only the literals' stream position (the parse spends no scalar work on
+  // packing the token): the token byte just before them is loaded here, lane-parallel, per batch
+  const uint32_t lpos = B.rl - X.k0;  // payload offset of this record's literals
+  const uint32_t tok = valid && !gen ? uint32_t(X.pay[lpos - 1 < X.clen ? lpos - 1 : 0u]) : 0u;
   const uint32_t lit = !valid ? 0u : gen ? (B.rx & 0xFFFF) : tok >> 4;
   const uint32_t ml = !valid ? 0u : gen ? ((B.rx >> 16) & 0x7FFF) : (tok & 15) + 4;
   const uint32_t off = B.rh & 0xFFFF;
-  const uint32_t lpos = gen ? tpos : tpos + 1;  // payload offset of this record's literals
   const uint32_t a2 = scan_add(lit + ml);
   const uint32_t li = scan_add(lit), mi = scan_add(ml);
   const uint32_t opos = X.obase + a2 - lit - ml;  // output offset of the record
@@ -364,18 +364,28 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
           // a scalar increment on the CU's one scalar unit, which bounds this loop
           int32_t dn = int32_t(lane) - int32_t(B.n);
           // single-exit loop (a `break` makes the structurizer route the exit flag through VALU)
-          // continue while iters > 0 and neither nibble is 15: one integer test (min of the three)
-          while (min(min(iters, (token & 15) ^ 15), (token >> 4) ^ 15) != 0) {
+          // continue while iters > 0 and neither nibble is 15: one integer test (min of the three),
+          // computed by the vector unit from a VGPR copy of the loaded bytes (the scalar unit, which
+          // bounds this loop, only compares the result)
+          uint32_t go = uni(min(min(iters, (token & 15) ^ 15), (token >> 4) ^ 15));
+          uint32_t lit = token >> 4;
+          uint32_t lp = ip + 1;  // literal position of the current sequence (its token is at lp - 1)
+          while (go != 0) {
             iters = uni(iters - 1);
-            const uint32_t lit = token >> 4;
-            const uint32_t y = uint32_t(sload8(w4, ip + 1 + lit));  // offset lo, offset hi, next token
+            const uint32_t p = lp + lit;
+            const uint32_t y = uint32_t(sload8(w4, p));  // offset lo, offset hi, next token
+            uint32_t yv;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(yv) : "s"(y));
             const bool me = dn == 0;
-            rl = me ? ip : rl;  // short record: the token's position (rx stays 0)
-            rh = me ? y : rh;
-            ip += 3 + lit;
+            rl = me ? lp : rl;  // short record: the literals' position (rx stays 0)
+            rh = me ? yv : rh;
+            lp = p + 3;
             --dn;
-            token = (y >> 16) & 0xFF;
+            lit = (y >> 20) & 15;  // the next token's literal count: all the scalar unit needs of it
+            const uint32_t tv = yv >> 16;
+            go = __builtin_amdgcn_readfirstlane(min(min(iters, (~tv) & 15), ((tv >> 4) & 15) ^ 15));
           }
+          ip = uni(lp - 1);
           const uint32_t n = uni(B.n + (iters0 - iters));
           B.n = n;
           B.rl = rl;
