@@ -99,11 +99,12 @@ struct Ctx {
 // Grouped-stream position -> byte offset in the chunk (identity unless BG4).
 __device__ __forceinline__ uint32_t bmap(const Ctx& X, uint32_t p) {
   if (!X.bg4) return p;
-  const uint32_t a1 = p >= X.g1, a2 = p >= X.g2, a3 = p >= X.g3;
-  uint32_t base = a1 ? X.g1 : 0u;
-  base = a2 ? X.g2 : base;
-  base = a3 ? X.g3 : base;
-  return 4 * (p - base) + a1 + a2 + a3;
+  // grouped position p of group g (start G_g) lands at 4 (p - G_g) + g = 4 p + (g - 4 G_g): one
+  // per-group constant, picked by the three group-start compares
+  uint32_t c = p >= X.g1 ? 1u - 4u * X.g1 : 0u;
+  c = p >= X.g2 ? 2u - 4u * X.g2 : c;
+  c = p >= X.g3 ? 3u - 4u * X.g3 : c;
+  return 4u * p + c;
 }
 
 // Records of the current batch: lane i holds record i (rl = gap | lit << 16, rh = ml | off << 16).
