@@ -24,6 +24,8 @@
 #include "pull.h"
 #include "sha1.h"
 #include "storage.h"
+#include "term_jobs.h"
+#include "term_py.h"
 #include "trace.h"
 #include "tracker.h"
 #include "xet_hash.h"
@@ -164,8 +166,16 @@ class HostXetFetcher {
     for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
     bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
     bridge_->authenticate(repo, repo_type, revision);
-    dl_ = std::make_unique<ParallelDownloader>(*bridge_, concurrency > 0 ? concurrency : int(cfg_.concurrency));
+    threads_ = concurrency > 0 ? concurrency : int(cfg_.concurrency);
+    dl_ = std::make_unique<ParallelDownloader>(*bridge_, threads_);
+    recs_ = std::make_unique<ReconCache>(*bridge_);
   }
+  // Term-range API of the term-sharded swarm pull (csrc/core/term_jobs.h).
+  std::vector<TermShape> shapes(const std::string& hex) { return recs_->shapes(hex); }
+  std::vector<TermJobResult> fetch_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, bool repair) {
+    return fetch_terms_host(*bridge_, *recs_, book_, jobs, hashes, threads_, repair);
+  }
+  size_t settle(const std::string& hex, bool ok) { return book_.settle(*bridge_, hex, ok); }
   std::vector<FileResult> fetch(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
     std::vector<FileResult> out(files.size());
     std::vector<std::string> errs(files.size());
@@ -197,7 +207,11 @@ class HostXetFetcher {
   std::unique_ptr<SwarmDownloader> swarm_;
   std::unique_ptr<XetBridge> bridge_;
   std::unique_ptr<ParallelDownloader> dl_;
+  std::unique_ptr<ReconCache> recs_;
+  SettleBook book_;
+  int threads_ = 16;
 };
+
 
 void bind_extra(py::module_& m) {
   // ---------------- bencode ----------------
@@ -631,6 +645,31 @@ void bind_extra(py::module_& m) {
              return out;
            },
            py::arg("files"), "[(xet_hash, ptr, size), ...] -> one dict per file (chunk_lens: uint32 sizes)")
+      .def("term_shapes", [](HostXetFetcher& self, const std::string& hex) {
+             std::vector<TermShape> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.shapes(hex);
+             }
+             return term_shapes_py(v);
+           }, py::arg("xet_hash"), "[(unpacked_length, n_chunks), ...] of the file's reconstruction terms")
+      .def("fetch_terms",
+           [](HostXetFetcher& self, const std::vector<std::tuple<std::string, uint32_t, uint32_t, uintptr_t, uint64_t>>& v,
+              uintptr_t hashes, bool repair) {
+             const auto jobs = term_jobs_of(v);
+             std::vector<TermJobResult> rs;
+             {
+               py::gil_scoped_release nogil;
+               rs = self.fetch_terms(jobs, reinterpret_cast<uint8_t*>(hashes), repair);
+             }
+             return term_results_py(rs);
+           },
+           py::arg("jobs"), py::arg("hashes_ptr"), py::arg("repair") = false,
+           "[(xet_hash, t0, t1, dst_ptr, chunk0), ...]: fetch + decode + chunk-hash term ranges into host memory")
+      .def("settle", [](HostXetFetcher& self, const std::string& hex, bool ok) {
+             py::gil_scoped_release nogil;
+             return self.settle(hex, ok);
+           }, py::arg("xet_hash"), py::arg("ok"), "publish (ok) or drop the file's quarantined runs")
       .def("stats_json", &HostXetFetcher::stats_json);
 
   // ---------------- pull ----------------

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "../gpurt/device_pull.h"
+#include "term_py.h"
 
 namespace py = pybind11;
 using zest::gpurt::DeviceXetPull;
@@ -71,6 +72,33 @@ void bind_hip_pull(py::module_& m) {
       .def("pull_files", &pull_files_py, py::arg("files"),
            "[(xet_hash, dst_ptr, size), ...] through one pipeline; returns one stats dict per file "
            "(chunk_lens: uint32 chunk sizes in file order)")
+      .def("term_shapes", [](DeviceXetPull& self, const std::string& hex) {
+             std::vector<zest::TermShape> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.term_shapes(hex);
+             }
+             return zest::term_shapes_py(v);
+           }, py::arg("xet_hash"), "[(unpacked_length, n_chunks), ...] of the file's reconstruction terms")
+      .def("pull_terms",
+           [](DeviceXetPull& self, const std::vector<zest::TermJobTuple>& v, uintptr_t hashes, uintptr_t sizes,
+              bool repair) {
+             const auto jobs = zest::term_jobs_of(v);
+             std::vector<zest::TermJobResult> rs;
+             {
+               py::gil_scoped_release nogil;
+               rs = self.pull_terms(jobs, reinterpret_cast<uint8_t*>(hashes), reinterpret_cast<uint64_t*>(sizes),
+                                    repair);
+             }
+             return zest::term_results_py(rs);
+           },
+           py::arg("jobs"), py::arg("hashes_ptr"), py::arg("sizes_ptr") = 0, py::arg("repair") = false,
+           "[(xet_hash, t0, t1, dst_ptr, chunk0), ...]: fetch term ranges, GPU decode + chunk-hash them into "
+           "place (hashes/sizes: device tables indexed by chunk); consecutive chunk indices required")
+      .def("settle", [](DeviceXetPull& self, const std::string& hex, bool ok) {
+             py::gil_scoped_release nogil;
+             return self.settle(hex, ok);
+           }, py::arg("xet_hash"), py::arg("ok"), "publish (ok) or drop the file's quarantined runs")
       .def("stats_json", &DeviceXetPull::stats_json)
       .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

@@ -20,6 +20,7 @@
 #include "config.h"
 #include "storage.h"
 #include "swarm.h"
+#include "term_jobs.h"
 #include "trace.h"
 #include "xet_hash.h"
 #include "xorb.h"
@@ -86,6 +87,7 @@ struct DeviceXetPull::Impl {
       for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
     }
     bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
+    recs_ = std::make_unique<ReconCache>(*bridge_);
     {
       trace::Span sp("device", "init: xet auth");
       bridge_->authenticate(repo, repo_type, revision);
@@ -113,8 +115,7 @@ struct DeviceXetPull::Impl {
 
   // Pull several Xet files (hash, device pointer, size) through ONE pipeline: staging batches
   // cross file boundaries, so there is no per-file drain; every file's Merkle hash is checked in a
-  // single kernel launch at the end.  Term destinations are device addresses relative to the
-  // lowest destination pointer.
+  // single kernel launch at the end.
   //
   // Peer runs are quarantined in the disk cache until their file verified; a file that fails
   // (Merkle mismatch, or any device decode error) has its peer runs dropped and its cache runs
@@ -123,7 +124,7 @@ struct DeviceXetPull::Impl {
   std::vector<PullFileStats> pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
     const auto t0 = std::chrono::steady_clock::now();
     const size_t nf = files.size();
-    std::vector<cas::Reconstruction> recs(nf);
+    std::vector<const cas::Reconstruction*> recs(nf);
     {
       trace::Span sp("device", "reconstructions");
       std::vector<std::string> errs(nf);
@@ -131,7 +132,7 @@ struct DeviceXetPull::Impl {
       auto w = [&]() {
         for (size_t f; (f = k.fetch_add(1)) < nf;) {
           try {
-            recs[f] = bridge_->get_reconstruction(std::get<0>(files[f]));
+            recs[f] = &recs_->get(std::get<0>(files[f]));
           } catch (const std::exception& e) {
             errs[f] = e.what();
           }
@@ -151,8 +152,7 @@ struct DeviceXetPull::Impl {
     for (int attempt = 0; attempt < 2 && !todo.empty(); ++attempt) {
       FetchOptions opt;
       opt.repair = attempt > 0;
-      attempt_ = attempt;
-      Attempt at = run_once(files, recs, todo, opt);
+      Attempt at = run_once(files, recs, todo, opt, attempt);
       fetched += at.fetched;
       if (!at.fetch_err.empty()) {
         settle_all(at, recs, todo, [](size_t) { return false; });
@@ -165,7 +165,7 @@ struct DeviceXetPull::Impl {
       for (size_t j = 0; j < todo.size(); ++j) {
         got[todo[j]] = at.roots[j];
         if (at.roots[j] != std::get<0>(files[todo[j]])) bad.push_back(j);
-        else lens[todo[j]] = std::move(at.chunk_lens[j]);
+        else lens[todo[j]] = std::move(at.seg.chunk_lens[j]);
       }
       settle_all(at, recs, todo, [&](size_t j) { return std::find(bad.begin(), bad.end(), j) == bad.end(); });
       if (bad.empty()) {
@@ -173,9 +173,9 @@ struct DeviceXetPull::Impl {
         break;
       }
       if (attempt == 0) bridge_->stats().verify_failures += bad.size();
-      else if (at.ingest_err)
-        throw Error("IngestError", "code " + std::to_string(at.ingest_err >> 32) + " at " +
-                                       std::to_string(at.ingest_err & 0xFFFFFFFFu));
+      else if (at.seg.ingest_err)
+        throw Error("IngestError", "code " + std::to_string(at.seg.ingest_err >> 32) + " at " +
+                                       std::to_string(at.seg.ingest_err & 0xFFFFFFFFu));
       std::vector<size_t> again;
       for (size_t j : bad) again.push_back(todo[j]);
       if (attempt == 0) bridge_->stats().refetches += again.size();
@@ -188,9 +188,9 @@ struct DeviceXetPull::Impl {
     std::vector<PullFileStats> out(nf);
     for (size_t f = 0; f < nf; ++f) {
       uint64_t nck = 0;
-      for (auto& t : recs[f].terms) nck += t.range.end - t.range.start;
+      for (auto& t : recs[f]->terms) nck += t.range.end - t.range.start;
       out[f].bytes = std::get<2>(files[f]);
-      out[f].terms = recs[f].terms.size();
+      out[f].terms = recs[f]->terms.size();
       out[f].chunks = nck;
       out[f].seconds = secs;
       out[f].fetched_bytes = fetched;  // for the whole call
@@ -199,88 +199,239 @@ struct DeviceXetPull::Impl {
     return out;
   }
 
+  // Term ranges of files into caller memory (the term-sharded swarm pull): every chunk decoded into
+  // place and hashed into the caller's table; no Merkle check here (a range is part of a file), so
+  // the runs behind the terms stay in book_ until settle(file).  A range whose fetched runs do not
+  // match its plan, or any decode error of the call, is refetched once from the CDN.
+  std::vector<TermJobResult> pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
+                                        bool repair) {
+    std::vector<Seg> segs;
+    uint64_t next_chunk = jobs.empty() ? 0 : jobs[0].chunk0;
+    for (const TermJob& j : jobs) {
+      const cas::Reconstruction& rec = recs_->get(j.xet_hash);
+      if (j.t0 > j.t1 || j.t1 > rec.terms.size()) throw Error("RangeOutOfBounds", "term range of " + j.xet_hash);
+      if (j.chunk0 != next_chunk) throw Error("InvalidArgument", "term jobs must cover consecutive chunk indices");
+      for (uint32_t t = j.t0; t < j.t1; ++t) next_chunk += rec.terms[t].range.end - rec.terms[t].range.start;
+      segs.push_back({&rec, j.t0, j.t1, j.dst, j.chunk0});
+    }
+    std::vector<TermJobResult> out(jobs.size());
+    std::vector<size_t> todo(segs.size());
+    for (size_t i = 0; i < todo.size(); ++i) todo[i] = i;
+    for (int attempt = 0; attempt < 2 && !todo.empty(); ++attempt) {
+      FetchOptions opt;
+      opt.repair = repair || attempt > 0;
+      if (attempt > 0) opt.allow_cache = opt.allow_p2p = false;
+      std::vector<Seg> part;
+      for (size_t i : todo) part.push_back(segs[i]);
+      // a retry covers a subset: its chunk indices are no longer consecutive, so run it seg by seg
+      std::vector<std::vector<size_t>> groups;
+      if (attempt == 0) groups.push_back(todo);
+      else
+        for (size_t i : todo) groups.push_back({i});
+      std::vector<size_t> bad;
+      for (const auto& g : groups) {
+        std::vector<Seg> gs;
+        for (size_t i : g) gs.push_back(segs[i]);
+        SegAttempt at = run_segments(gs, hashes, sizes, opt, attempt, {});
+        auto drop = [&](size_t k) {
+          for (size_t t = 0; t < at.sources[k].size(); ++t)
+            bridge_->settle(gs[k].rec->terms[gs[k].t0 + t].hash_hex, at.sources[k][t].src, at.sources[k][t].run_offset,
+                            at.sources[k][t].pending, false);
+        };
+        if (!at.fetch_err.empty()) {
+          for (size_t k = 0; k < gs.size(); ++k) drop(k);
+          for (const auto& j : jobs) book_.settle(*bridge_, j.xet_hash, false);
+          throw Error("DownloadFailed", at.fetch_err);
+        }
+        for (size_t k = 0; k < gs.size(); ++k) {
+          const size_t i = g[k];
+          if (at.ingest_err || !at.planned_ok[k]) {
+            drop(k);
+            bad.push_back(i);
+            continue;
+          }
+          TermJobResult& r = out[i];
+          r.chunk_lens = std::move(at.chunk_lens[k]);
+          r.fetched += at.seg_fetched[k];
+          for (size_t t = 0; t < at.sources[k].size(); ++t) {
+            const TermSource& ts = at.sources[k][t];
+            const cas::Term& term = gs[k].rec->terms[gs[k].t0 + t];
+            book_.add(jobs[i].xet_hash, term.hash_hex, ts.src, ts.run_offset, ts.pending);
+            (ts.src == Source::Peer ? r.from_peer : ts.src == Source::Cache ? r.from_cache : r.from_cdn) +=
+                term.unpacked_length;
+          }
+        }
+        if (at.ingest_err && attempt > 0)
+          throw Error("IngestError", "code " + std::to_string(at.ingest_err >> 32) + " at " +
+                                         std::to_string(at.ingest_err & 0xFFFFFFFFu));
+      }
+      if (!bad.empty() && attempt == 0) bridge_->stats().refetches += bad.size();
+      todo = std::move(bad);
+    }
+    if (!todo.empty()) throw Error("IngestError", "term range of " + jobs[todo[0]].xet_hash + " does not match its plan");
+    return out;
+  }
+
+  size_t settle(const std::string& hex, bool ok) { return book_.settle(*bridge_, hex, ok); }
+  std::vector<TermShape> term_shapes(const std::string& hex) { return recs_->shapes(hex); }
+
   std::string stats_json() const { return bridge_->stats_json(); }
 
   size_t staging_bytes() const { return cap_; }
 
   PullProgressFn progress_;  // set for the duration of one pull_files call
-  int attempt_ = 0;
 
   struct TermSource {
     Source src = Source::Cdn;
     uint32_t run_offset = 0;
     std::string pending;  // quarantine file of a peer run (empty: none)
   };
-  struct Attempt {
-    std::vector<std::string> roots;  // per file of the attempt: Merkle root (Xet hex)
-    std::vector<std::vector<TermSource>> sources;  // per file, per term
-    std::vector<std::vector<uint32_t>> chunk_lens;  // per file: uncompressed chunk sizes
+  // A contiguous term range of one file: outputs from device address `dst`, chunk hashes / sizes
+  // at index chunk0.. of the caller's tables.
+  struct Seg {
+    const cas::Reconstruction* rec;
+    uint32_t t0, t1;
+    uintptr_t dst;
+    uint64_t chunk0;
+  };
+  struct SegAttempt {
+    std::vector<std::vector<TermSource>> sources;   // per seg, per term
+    std::vector<std::vector<uint32_t>> chunk_lens;  // per seg: uncompressed chunk sizes
+    std::vector<uint8_t> planned_ok;                // per seg: every fetched run matched the plan
+    std::vector<uint64_t> seg_fetched;              // per seg: bytes moved
     unsigned long long ingest_err = 0;
     std::string fetch_err;
     uint64_t fetched = 0;
   };
+  struct Attempt {
+    SegAttempt seg;                  // one seg per file of the attempt
+    std::vector<std::string> roots;  // per file of the attempt: Merkle root (Xet hex)
+    uint64_t fetched = 0;
+    std::string fetch_err;
+  };
 
   // Publish (ok) or drop/evict (!ok) the cache runs behind every term of the attempt's files.
   template <typename OkFn>
-  void settle_all(const Attempt& at, const std::vector<cas::Reconstruction>& recs, const std::vector<size_t>& todo,
-                  OkFn ok) {
+  void settle_all(const Attempt& at, const std::vector<const cas::Reconstruction*>& recs,
+                  const std::vector<size_t>& todo, OkFn ok) {
     for (size_t j = 0; j < todo.size(); ++j) {
-      const auto& rec = recs[todo[j]];
+      const auto& rec = *recs[todo[j]];
       const bool good = ok(j);
-      for (size_t i = 0; i < at.sources[j].size() && i < rec.terms.size(); ++i) {
-        const TermSource& ts = at.sources[j][i];
+      for (size_t i = 0; i < at.seg.sources[j].size() && i < rec.terms.size(); ++i) {
+        const TermSource& ts = at.seg.sources[j][i];
         bridge_->settle(rec.terms[i].hash_hex, ts.src, ts.run_offset, ts.pending, good);
       }
     }
   }
 
-  // One pass over files[todo]: fetch (+ chunk records) -> staging -> H2D -> place/hash -> Merkle roots.
+  // Whole files[todo] through run_segments into the internal hash table, then one Merkle launch.
   Attempt run_once(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& all_files,
-                   const std::vector<cas::Reconstruction>& all_recs, const std::vector<size_t>& todo,
-                   const FetchOptions& opt) {
+                   const std::vector<const cas::Reconstruction*>& all_recs, const std::vector<size_t>& todo,
+                   const FetchOptions& opt, int attempt) {
     const size_t nf = todo.size();
     Attempt at;
-    at.sources.resize(nf);
-    // Global term list in file order; chunk indices are global (one hash array for all files).
+    std::vector<Seg> segs;
+    std::vector<uint64_t> file_chunk0(nf + 1, 0);
+    for (size_t f = 0; f < nf; ++f) {
+      const auto& fl = all_files[todo[f]];
+      const cas::Reconstruction& rec = *all_recs[todo[f]];
+      uint64_t off = 0, c = 0;
+      for (const auto& t : rec.terms) {
+        off += t.unpacked_length;
+        c += t.range.end - t.range.start;
+      }
+      if (off != std::get<2>(fl)) throw Error("SizeMismatch", std::get<0>(fl) + " is " + std::to_string(off) + " bytes");
+      segs.push_back({&rec, 0, uint32_t(rec.terms.size()), std::get<1>(fl), file_chunk0[f]});
+      file_chunk0[f + 1] = file_chunk0[f] + c;
+    }
+    const uint64_t nck = file_chunk0[nf];
+    hashes_.ensure(nck ? nck * 32 : 32);
+    sizes_.ensure(nck ? nck : 1);
+    std::function<void(size_t, uint64_t)> prog;
+    if (progress_) prog = [&](size_t seg, uint64_t bytes) { progress_(todo[seg], attempt, bytes); };
+    at.seg = run_segments(segs, hashes_.p, sizes_.p, opt, attempt, prog);
+    at.fetched = at.seg.fetched;
+    at.fetch_err = at.seg.fetch_err;
+    if (!at.fetch_err.empty()) return at;
+    // Merkle roots of every file in one launch
+    trace::Span merkle_span("device", "merkle verify");
+    std::vector<ZgMerkleJob> mjobs(nf);
+    uint64_t max_leaves = 1;
+    for (size_t f = 0; f < nf; ++f) {
+      mjobs[f] = ZgMerkleJob{file_chunk0[f], file_chunk0[f + 1] - file_chunk0[f], 1, 0};
+      max_leaves = std::max<uint64_t>(max_leaves, mjobs[f].n_leaves);
+    }
+    std::vector<uint8_t> roots(32 * std::max<size_t>(nf, 1));
+    if (nf) {
+      merkle_job_.ensure(nf);
+      hip_check(hipMemcpyAsync(merkle_job_.p, mjobs.data(), sizeof(ZgMerkleJob) * nf, hipMemcpyHostToDevice, stream_),
+                "job H2D");
+      const size_t sb = zg_merkle_scratch_bytes(max_leaves, int(nf));
+      merkle_scratch_.ensure(sb);
+      root_.ensure(32 * nf);
+      hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, int(nf), root_.p, merkle_scratch_.p, sb, stream_),
+                "merkle");
+      hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
+      hip_check(hipStreamSynchronize(stream_), "sync");
+    }
+    for (size_t f = 0; f < nf; ++f) {
+      xet::Hash h;
+      std::memcpy(h.data(), roots.data() + 32 * f, 32);
+      at.roots.push_back(xet::to_hex(h));
+    }
+    return at;
+  }
+
+  // One pass over segments: fetch (+ chunk records) -> staging -> H2D -> place/hash.  Segments must
+  // cover consecutive chunk indices (chunk0 of seg k+1 = chunk0 of seg k + its chunks): hashes and
+  // sizes of the pass go to hashes[segs[0].chunk0 ..] in one run.
+  SegAttempt run_segments(const std::vector<Seg>& segs, uint8_t* hash_out, uint64_t* size_out, const FetchOptions& opt,
+                          int attempt, const std::function<void(size_t, uint64_t)>& progress) {
+    (void)attempt;
+    const size_t ns = segs.size();
+    SegAttempt at;
+    at.sources.resize(ns);
+    at.chunk_lens.resize(ns);
+    at.planned_ok.assign(ns, 1);
+    at.seg_fetched.assign(ns, 0);
+    // Global term list in segment order; chunk indices are relative to segs[0].chunk0.
     struct GTerm {
-      size_t file, term;
+      size_t seg, term;
       uint64_t dst;    // device address offset from `base`
-      uint64_t chunk;  // global index of the term's first chunk
+      uint64_t chunk;  // index of the term's first chunk (pass-relative)
       uint32_t nchunks;
       uint64_t ulen;
     };
     std::vector<GTerm> gt;
-    std::vector<uint64_t> file_chunk0(nf + 1, 0), file_dst0(nf, 0);
+    std::vector<uint64_t> seg_chunk0(ns + 1, 0), seg_dst0(ns, 0);
     uintptr_t base = UINTPTR_MAX, top_addr = 0;
-    for (size_t f = 0; f < nf; ++f) {
-      const auto& fl = all_files[todo[f]];
-      base = std::min(base, std::get<1>(fl));
-      top_addr = std::max<uintptr_t>(top_addr, std::get<1>(fl) + std::get<2>(fl));
+    const uint64_t hash_base = ns ? segs[0].chunk0 : 0;
+    for (size_t s = 0; s < ns; ++s) {
+      uint64_t bytes = 0;
+      for (uint32_t t = segs[s].t0; t < segs[s].t1; ++t) bytes += segs[s].rec->terms[t].unpacked_length;
+      base = std::min(base, segs[s].dst);
+      top_addr = std::max<uintptr_t>(top_addr, segs[s].dst + bytes);
     }
-    for (size_t f = 0; f < nf; ++f) {
-      const auto& fl = all_files[todo[f]];
-      const auto& rec = all_recs[todo[f]];
-      if (rec.offset_into_first_range != 0) throw Error("Unsupported", "partial-file reconstruction");
-      at.sources[f].resize(rec.terms.size());
-      file_dst0[f] = std::get<1>(fl) - base;
-      uint64_t off = 0, c = file_chunk0[f];
-      for (size_t i = 0; i < rec.terms.size(); ++i) {
-        const auto& t = rec.terms[i];
+    for (size_t s = 0; s < ns; ++s) {
+      const Seg& sg = segs[s];
+      if (sg.chunk0 != hash_base + seg_chunk0[s]) throw Error("InvalidArgument", "segments must cover consecutive chunks");
+      at.sources[s].resize(sg.t1 - sg.t0);
+      seg_dst0[s] = sg.dst - base;
+      uint64_t off = 0, c = seg_chunk0[s];
+      for (uint32_t i = sg.t0; i < sg.t1; ++i) {
+        const auto& t = sg.rec->terms[i];
         const uint32_t n = uint32_t(t.range.end - t.range.start);
-        gt.push_back({f, i, std::get<1>(fl) - base + off, c, n, t.unpacked_length});
+        gt.push_back({s, i, sg.dst - base + off, c, n, t.unpacked_length});
         off += t.unpacked_length;
         c += n;
       }
-      if (off != std::get<2>(fl)) throw Error("SizeMismatch", std::get<0>(fl) + " is " + std::to_string(off) + " bytes");
-      file_chunk0[f + 1] = c;
+      seg_chunk0[s + 1] = c;
+      at.chunk_lens[s].assign(size_t(c - seg_chunk0[s]), 0);
     }
-    const uint64_t nck = file_chunk0[nf];
+    const uint64_t nck = seg_chunk0[ns];
     const size_t n = gt.size();
-    std::vector<uint32_t> all_lens(nck, 0);
-    hashes_.ensure(nck ? nck * 32 : 32);
-    sizes_.ensure(nck ? nck : 1);
-    uint8_t* dst = reinterpret_cast<uint8_t*>(base);
-    const uint64_t dst_size = nf ? uint64_t(top_addr - base) : 0;
+    uint8_t* dst = ns ? reinterpret_cast<uint8_t*>(base) : nullptr;
+    const uint64_t dst_size = ns ? uint64_t(top_addr - base) : 0;
     hip_check(hipMemsetAsync(err_.p, 0, sizeof(unsigned long long), stream_), "hipMemset");
     std::string& fetch_err = at.fetch_err;
     {
@@ -352,14 +503,14 @@ struct DeviceXetPull::Impl {
           }
           const size_t j = i - bt.begin;
           try {
-            const auto& rec = all_recs[todo[gt[i].file]];
+            const cas::Reconstruction& rec = *segs[gt[i].seg].rec;
             // The run is received straight into this term's region of the pinned buffer when it
             // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
             uint8_t* region = s.host + bt.off[j];
             const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
             auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
             XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
-            at.sources[gt[i].file][gt[i].term] = TermSource{r.source, r.run_offset, r.pending};
+            at.sources[gt[i].seg][gt[i].term - segs[gt[i].seg].t0] = TermSource{r.source, r.run_offset, r.pending};
             auto idx = xet::index_chunks(r.bytes(), r.size());
             if (r.local_end > idx.size() || r.local_start >= r.local_end)
               throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
@@ -379,6 +530,7 @@ struct DeviceXetPull::Impl {
             const uint64_t run0 = bt.src_at[j];
             uint64_t uoff = 0;
             bool ok = r.local_end - r.local_start == gt[i].nchunks;
+            uint32_t* lens = at.chunk_lens[gt[i].seg].data() + (gt[i].chunk - seg_chunk0[gt[i].seg]);
             for (uint32_t c = r.local_start; ok && c < r.local_end; ++c) {
               const xet::ChunkEntry& e = idx[c];
               const uint32_t sc = uint32_t(e.scheme);
@@ -388,10 +540,14 @@ struct DeviceXetPull::Impl {
               }
               cr[c - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
                                                e.clen, e.ulen, sc, uint32_t(j)};
-              all_lens[gt[i].chunk + (c - r.local_start)] = e.ulen;
+              lens[c - r.local_start] = e.ulen;
               uoff += e.ulen;
             }
-            if (!ok || uoff != gt[i].ulen) std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
+            if (!ok || uoff != gt[i].ulen) {
+              std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
+              std::lock_guard<std::mutex> g(mu);
+              at.planned_ok[gt[i].seg] = 0;
+            }
           } catch (const std::exception& e) {
             fail(e.what());
             return;
@@ -416,6 +572,7 @@ struct DeviceXetPull::Impl {
           uint64_t top = 0;
           for (size_t j = 0; j < bt.len.size(); ++j) {
             at.fetched += bt.len[j];
+            at.seg_fetched[gt[bt.begin + j].seg] += bt.len[j];
             top = std::max<uint64_t>(top, bt.src_at[j] + bt.len[j]);
           }
           const uint64_t c0 = chunk_lo(b);
@@ -437,7 +594,8 @@ struct DeviceXetPull::Impl {
           // decode (when the batch has compressed chunks) + one fused pass placing raw chunks and
           // hashing every chunk (csrc/gpu/blake3_flat.hip PlaceSrc)
           hip_check(zg_ingest_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, compressed ? 1 : 0, err_.p,
-                                     hashes_.p + 32 * c0, sizes_.p + c0, 0, hash_scratch_.p, hs_bytes, stream_),
+                                     hash_out + 32 * (hash_base + c0), size_out ? size_out + hash_base + c0 : nullptr, 0,
+                                     hash_scratch_.p, hs_bytes, stream_),
                     "ingest");
           hip_check(hipEventRecord(s.done, stream_), "event");
           // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
@@ -448,12 +606,12 @@ struct DeviceXetPull::Impl {
             ready[b & 1] = b + 2;
             cv.notify_all();
           }
-          if (progress_) {
-            // batches run in term order, and terms are in file order: each touched file's bytes
-            // are complete up to the end of its last term in this batch
+          if (progress) {
+            // batches run in term order, and terms are in segment order: each touched segment's
+            // bytes are complete up to the end of its last term in this batch
             for (size_t i = bt.begin; i < bt.end; ++i)
-              if (i + 1 == bt.end || gt[i + 1].file != gt[i].file)
-                progress_(todo[gt[i].file], attempt_, gt[i].dst + gt[i].ulen - file_dst0[gt[i].file]);
+              if (i + 1 == bt.end || gt[i + 1].seg != gt[i].seg)
+                progress(gt[i].seg, gt[i].dst + gt[i].ulen - seg_dst0[gt[i].seg]);
           }
         }
       } catch (const std::exception& e) {
@@ -467,33 +625,6 @@ struct DeviceXetPull::Impl {
     }
     if (!fetch_err.empty()) return at;
     hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
-    // Merkle roots of every file in one launch
-    trace::Span merkle_span("device", "merkle verify");
-    std::vector<ZgMerkleJob> jobs(nf);
-    uint64_t max_leaves = 1;
-    for (size_t f = 0; f < nf; ++f) {
-      jobs[f] = ZgMerkleJob{file_chunk0[f], file_chunk0[f + 1] - file_chunk0[f], 1, 0};
-      max_leaves = std::max<uint64_t>(max_leaves, jobs[f].n_leaves);
-    }
-    std::vector<uint8_t> roots(32 * std::max<size_t>(nf, 1));
-    if (nf) {
-      merkle_job_.ensure(nf);
-      hip_check(hipMemcpyAsync(merkle_job_.p, jobs.data(), sizeof(ZgMerkleJob) * nf, hipMemcpyHostToDevice, stream_),
-                "job H2D");
-      const size_t sb = zg_merkle_scratch_bytes(max_leaves, int(nf));
-      merkle_scratch_.ensure(sb);
-      root_.ensure(32 * nf);
-      hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, int(nf), root_.p, merkle_scratch_.p, sb, stream_),
-                "merkle");
-      hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
-      hip_check(hipStreamSynchronize(stream_), "sync");
-    }
-    for (size_t f = 0; f < nf; ++f) {
-      xet::Hash h;
-      std::memcpy(h.data(), roots.data() + 32 * f, 32);
-      at.roots.push_back(xet::to_hex(h));
-      at.chunk_lens.emplace_back(all_lens.begin() + long(file_chunk0[f]), all_lens.begin() + long(file_chunk0[f + 1]));
-    }
     return at;
   }
 
@@ -522,6 +653,8 @@ struct DeviceXetPull::Impl {
   std::unique_ptr<storage::XorbCache> cache_;
   std::unique_ptr<SwarmDownloader> swarm_;
   std::unique_ptr<XetBridge> bridge_;
+  std::unique_ptr<ReconCache> recs_;
+  SettleBook book_;
   hipStream_t stream_ = nullptr;
   Slot slots_[2];
   DevBuf<unsigned long long> err_;
@@ -550,6 +683,12 @@ std::vector<PullFileStats> DeviceXetPull::pull_files(const std::vector<PullReque
   return impl_->pull_files(f);
 }
 
+std::vector<TermJobResult> DeviceXetPull::pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
+                                                     bool repair) {
+  return impl_->pull_terms(jobs, hashes, sizes, repair);
+}
+size_t DeviceXetPull::settle(const std::string& xet_hash, bool ok) { return impl_->settle(xet_hash, ok); }
+std::vector<TermShape> DeviceXetPull::term_shapes(const std::string& xet_hash) { return impl_->term_shapes(xet_hash); }
 std::string DeviceXetPull::stats_json() const { return impl_->stats_json(); }
 size_t DeviceXetPull::staging_bytes() const { return impl_->staging_bytes(); }
 

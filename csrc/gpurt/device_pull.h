@@ -15,6 +15,8 @@
 #include <string>
 #include <vector>
 
+#include "term_jobs.h"
+
 namespace zest::gpurt {
 
 struct DevicePullOptions {
@@ -60,6 +62,14 @@ class DeviceXetPull {
   // launch verifies all of them).  Throws zest::Error ("HashMismatch", "DownloadFailed", ...) when a
   // file cannot be verified after its CDN repair pass.
   std::vector<PullFileStats> pull_files(const std::vector<PullRequest>& files, const PullProgressFn& progress = {});
+  // Term ranges of files (the term-sharded swarm pull, csrc/core/term_jobs.h): decoded into place at
+  // each job's device address, chunk hashes / sizes into hashes[32 * i] / sizes[i] (device tables,
+  // i = the job's chunk0 + chunk index).  Jobs must cover consecutive chunk indices.  No Merkle
+  // check: the caller verifies each whole file, then settle(file, ok) publishes or drops the runs.
+  std::vector<TermJobResult> pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
+                                        bool repair = false);
+  size_t settle(const std::string& xet_hash, bool ok);
+  std::vector<TermShape> term_shapes(const std::string& xet_hash);  // (ulen, chunks) per term
   std::string stats_json() const;
   size_t staging_bytes() const;
 

@@ -21,9 +21,13 @@ def pytest_configure(config):
 
 
 def _ensure_built():
-    # Build native extensions in-tree once per session if missing (cheap no-op when up to date).
-    from tools.build import build
+    # Build native extensions in-tree once per session (cheap no-op when up to date).  A tree that
+    # arrives without build/ objects but with built modules (a gpurun snapshot on the GPU box) is
+    # used as is: recompiling there would only relink the same sources.
+    from tools.build import BUILD, EXT, PKG, build
 
+    if not BUILD.exists() and all((PKG / f"{m}{EXT}").exists() for m in ("_core", "_hip")):
+        return
     build(only=None)
 
 

@@ -245,17 +245,20 @@ def test_pull_files_multi_file_pipeline(tmp_path, monkeypatch):
         hub.stop()
 
 
-def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q):
+def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="auto", fault="", round_bytes=None):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if fault:
+        os.environ["ZEST_VMM_FAULT"] = fault
     torch.cuda.set_device(0)
     kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
     dist.init_process_group(backend, rank=rank, world_size=world_size, **kw)
     try:
         from zest_amd.parallel import swarm_pull
         st = {}
-        t = swarm_pull(repo, device="cuda:0", p2p=False, dht=False, stats=st)
+        t = swarm_pull(repo, device="cuda:0", p2p=False, dht=False, stats=st, exchange=exchange,
+                       round_bytes=round_bytes)
         assert all(v.device.type == "cuda" for v in t.values())
         q.put((rank, {k: v.contiguous().view(torch.uint8).cpu().numpy().tobytes() for k, v in t.items()}, st))
     except Exception as e:
@@ -264,11 +267,17 @@ def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world_size,backend", [(1, "nccl"), (2, "gloo")])
-def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend):
-    """Swarm pull into HBM: owners fetch device-direct (GPU decode + Merkle verify), the files are
-    broadcast to the other ranks (here: ranks sharing the one GPU over gloo) and re-verified on the
-    GPU; every rank ends with every tensor."""
+@pytest.mark.parametrize("world_size,backend,exchange,fault", [
+    (1, "nccl", "auto", ""), (2, "gloo", "auto", ""), (2, "gloo", "xgmi", ""), (2, "gloo", "ipc", ""),
+    (2, "gloo", "allgather", ""), (2, "gloo", "auto", "import"), (2, "gloo", "auto", "sentinel"),
+    (2, "gloo", "xgmi", "gather")])
+def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend, exchange, fault):
+    """Term-sharded swarm pull into HBM: each rank fetches its term ranges device-direct (GPU decode
+    + chunk hashes into the arena), the rounds are replicated to the other ranks (here: ranks sharing
+    the one GPU over gloo, arenas peer-mapped through HIP VMM for ipc / xgmi) and every chunk is
+    re-hashed on the receiver; Merkle file hashes on every rank.  Faults (ZEST_VMM_FAULT): a refused
+    import or sentinel falls back to an RCCL exchange; a corrupting gather fails the file hashes and
+    the repair pass refetches + re-sends them over a broadcast."""
     import dataclasses
     import json
     import struct
@@ -295,7 +304,8 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = free_port()
-        procs = [ctx.Process(target=_swarm_pull_gpu_worker, args=(r, world_size, port, world.spec.repo_id, backend, q))
+        procs = [ctx.Process(target=_swarm_pull_gpu_worker,
+                             args=(r, world_size, port, world.spec.repo_id, backend, q, exchange, fault, 512 << 10))
                  for r in range(world_size)]
         for p in procs:
             p.start()
@@ -307,6 +317,19 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend):
             assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
         total = sum(f.size for f in world.xet_files)
         assert sum(r[2]["fetched_bytes"] for r in res) == total
+        modes = {r[2]["exchange"] for r in res}
+        assert len(modes) == 1, modes
+        mode = modes.pop()
+        if world_size == 1:
+            assert mode == "none"
+        elif fault in ("import", "sentinel"):
+            assert mode in ("bcast", "allgather") and not any(r[2]["peer_mapped"] for r in res), res
+        elif exchange != "auto":
+            assert mode == exchange
+        if fault == "gather":
+            assert all(r[2]["repaired_files"] >= 1 for r in res), [r[2] for r in res]
+        print(f"[swarm_pull {world_size}x{backend} {exchange}{'/' + fault if fault else ''}] mode {mode} "
+              f"autotune {res[0][2]['exchange_autotune_s']} phases {res[0][2]['phases']}")
     finally:
         hub.stop()
 

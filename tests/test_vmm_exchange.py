@@ -1,4 +1,4 @@
-"""The fd exchange behind the VMM peer mapping (engine._import_vmm_peers), on CPU: 3 gloo ranks,
+"""The fd exchange behind the VMM peer mapping (zest_amd.parallel.exchange._import_vmm_peers), on CPU: 3 gloo ranks,
 each "arena" exported as memfds whose bytes name the owner and the chunk; every rank must import
 every peer's chunks, in order, through the abstract-socket + SCM_RIGHTS protocol.  The HIP side
 (hipMemImportFromShareableHandle + mapping) runs in tests/test_gpu_ipc.py."""
@@ -48,7 +48,8 @@ class _SlowHip(_FakeHip):
 def _rank(rank, world, port, q, budget=30.0, slow_rank=None):
     import torch.distributed as dist
 
-    from zest_amd import engine, ops
+    from zest_amd import ops
+    from zest_amd.parallel import exchange as engine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:

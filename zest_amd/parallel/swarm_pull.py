@@ -1,36 +1,56 @@
 """Intra-node swarm pull: every GPU of a node ends up with every tensor of a repository in its HBM,
-while each Xet file crosses the network (peers / CDN / local xorb cache) exactly once.
+while each byte crosses the network (peers / CDN / local xorb cache) exactly once.
 
     # one process per GPU (torchrun), backend "nccl" = RCCL over xGMI
     tensors = swarm_pull("meta-llama/Llama-3.1-70B")   # collective; every rank gets all tensors
     tensors = zest_amd.pull("meta-llama/Llama-3.1-70B", device="all")   # the same, public API
 
-Each Xet-backed safetensors file has one owner rank (LPT split by size).  The pull runs in rounds
-of one file per owner:
+This is the bench engine's shape (zest_amd.engine.DevicePuller) fed by the network instead of a
+pinned synthetic origin:
 
-  fetch     the owner pulls its file device-direct (`_hip.DeviceXetPull`: compressed runs -> pinned
-            staging -> GPU decode + BLAKE3 + Merkle check, with the native bridge's peer-quarantine /
-            CDN-repair rules) -- or, on CPU process groups, through the host waterfall into memory
-            (`_core.HostXetFetcher`); no snapshot is written either way
-  agree     one small all_gather of (error, chunk sizes) per round: every rank learns which fetches
-            worked and the chunk boundaries the owner parsed from the xorb headers
-  exchange  the owner seeds the file to the other ranks in pieces of `piece_bytes` (async RCCL
-            broadcasts over xGMI), overlapping the next round's fetch; the GPUs act as BitTorrent
-            peers for each other (BASELINE configs 2 and 3)
-  verify    every receiver hashes each received file on its own device with the owner's chunk
-            boundaries (BLAKE3 per chunk + Merkle) and compares with the published Xet file hash --
-            no CDC pass, and no trust in the owner: wrong boundaries or bytes give another hash
+  plan      rank 0 asks the CAS for every Xet file's reconstruction once; all ranks lay the files out
+            in one HBM arena and split the model's *terms* (not whole files) into byte-balanced
+            contiguous shares, one per rank, each cut into rounds of ~`round_bytes` (tapered head and
+            tail) -- at 8 ranks a 141 GB model is 8 shares of 17.6 GB, whatever the
+            shard sizes are (whole-file ownership left 2 of 8 ranks idle in the last of 4 rounds)
+  fetch     each rank pulls its round's term ranges device-direct (`_hip.DeviceXetPull.pull_terms`:
+            cache -> P2P -> CDN waterfall into pinned staging, GPU LZ4/BG4 decode + BLAKE3 chunk
+            hashes straight into the arena and the shared chunk-hash table); CPU process groups use
+            the host twin (`_core.HostXetFetcher.fetch_terms`)
+  agree     one small all_gather on a gloo control group per round: every rank learns which fetches
+            worked and every fetched range's chunk sizes (parsed from the xorb headers)
+  exchange  the round's regions are replicated over xGMI by the strategy `RoundExchange.autotune`
+            measured fastest at setup (coalesced RCCL broadcasts, slab all-gather, batched p2p, or
+            the peer-mapped HIP VMM `ipc` DMA copies / K8 `xgmi` gather kernel), asynchronously:
+            round k's exchange overlaps round k+1's fetch
+  verify    as each round lands, every receiver BLAKE3-hashes the received chunks itself on a side
+            stream; at the end one Merkle launch per rank checks every file against its published
+            Xet hash -- no rank trusts another's hashes
+  repair    files that fail anywhere are refetched from the CDN by the owners of their terms (their
+            peer / cache runs dropped) and re-exchanged over a plain RCCL broadcast
+  settle    quarantined peer runs are published to the local xorb cache once their file verified
 
 Elastic re-shard: a fetch that fails on its owner is reassigned to a rank that has not
-tried that file yet (least queued bytes); an owner that fails twice is dropped from ownership and
-its queued files move to the others.  Every rank derives the same plan from the all-gathered round
-results, so the collective never diverges.  Only when every owner failed a file do all ranks raise
-SwarmPullError together (no hang).  Reference counterpart: none (the reference stops at files on
-disk; its only failure handling is the per-term waterfall, CONTRIBUTING.md:92-99).
+tried it yet (least queued bytes); an owner that fails twice is dropped from ownership and its queue
+moves to the others.  Every rank derives the same plan from the all-gathered round results, so the
+collective never diverges; only when no owner is left for a range do all ranks raise SwarmPullError
+together.  A rank that *dies* (process exit, hang) is handled by `_Membership`: survivors detect it
+through a failed or timed-out control collective plus stale store heartbeats, agree on the survivor
+set through the rendezvous store, rebuild their control and data groups without it (in-process, no
+exec), and re-shard its unfinished ranges -- ranges some survivor already holds are re-sent from
+there, the rest are refetched.
+
+Reference counterpart: python/zest/__init__.py:49-52 (pull) over parallel_download.zig:91-204 (16
+concurrent term fetches, batch barrier, ordered writes); the reference has no intra-node swarm, and
+its only failure handling is the per-term waterfall (CONTRIBUTING.md:92-99).
 """
 from __future__ import annotations
 
+import json
 import os
+import threading
+import time
+import uuid
 
 import numpy as np
 import torch
@@ -38,33 +58,19 @@ import torch.distributed as dist
 
 from .. import _core, ops
 from .. import device as zdev
-from .swarm_load import assign_owners
+from .exchange import EXCHANGE_MODES, PEER_MAPPED_MODES, RoundExchange, map_peer_arenas, role_stream, tuned_mode
+
+FILE_ALIGN = 4096
+HEAD_TAPER = (0.25, 0.5)
+TAIL_TAPER = (0.5, 0.25, 0.125)
 
 
 class SwarmPullError(RuntimeError):
     pass
 
 
-def _listing(repo, revision, repo_type, group, rank):
-    """Rank 0 asks the hub once; every rank gets the same (commit, files)."""
-    obj = [None]
-    if rank == 0:
-        try:
-            obj[0] = ("ok", _core.list_repo_files(repo, revision, repo_type))
-        except Exception as e:  # every rank must leave the collective the same way
-            obj[0] = ("err", f"{type(e).__name__}: {e}")
-    src = dist.get_global_rank(group, 0) if group is not None else 0
-    dist.broadcast_object_list(obj, src=src, group=group)
-    status, val = obj[0]
-    if status != "ok":
-        raise SwarmPullError(f"listing {repo}@{revision} failed on rank 0: {val}")
-    return val
-
-
-def _all_ok(ok: bool, device, group) -> bool:
-    flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=device)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    return int(flag.item()) == 0
+class _RankLost(RuntimeError):
+    """A collective failed or timed out: some rank is gone (handled by _Membership.rebuild)."""
 
 
 def verify_with_lens(buf: torch.Tensor, lens: bytes, xet_hash: str) -> bool:
@@ -85,175 +91,834 @@ def verify_with_lens(buf: torch.Tensor, lens: bytes, xet_hash: str) -> bool:
     return _core.xet_hex(root[0].cpu().numpy().tobytes()) == xet_hash
 
 
-def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2p: bool = True, peers=None,
-               tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
-               verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
-               piece_bytes: int = 256 << 20, stats: dict | None = None) -> dict[str, torch.Tensor]:
-    """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
-    full set.  `stats`, if given, is filled with this rank's byte counts (fetched / received) and the
-    number of files reassigned after failed fetches."""
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
-    if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
-    device = torch.device(device)
-    commit, files = _listing(repo, revision, repo_type, group, rank)
-    st_files = [f for f in files if f["path"].endswith(".safetensors")]
-    xet = [f for f in st_files if f["xet_hash"]]
-    plain = [f for f in st_files if not f["xet_hash"]]
-    todo = xet + plain
-    bufs = [ops.padded_empty(f["size"], device)[: f["size"]] if device.type == "cuda"
-            else torch.empty(f["size"], dtype=torch.uint8) for f in todo]
-    # Ownership queues (identical on every rank): Xet files by LPT, largest first per owner; the
-    # non-Xet safetensors (host pull) go to rank 0 as one item.
-    owner = assign_owners([f["size"] for f in xet], world)
-    queue: list[list] = [[] for _ in range(world)]
-    for i in sorted(range(len(xet)), key=lambda i: (-xet[i]["size"], i)):
-        queue[owner[i]].append(("xet", i))
-    if plain:
-        queue[0].append(("plain", tuple(range(len(xet), len(todo)))))
-    granks = [dist.get_global_rank(group, r) for r in range(world)] if group is not None else list(range(world))
-    fetcher = _Fetcher(repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
-                       threads)
-    fault = os.environ.get("ZEST_SWARM_FAULT", "")  # "<rank>:<round>[,...]": that fetch raises (tests)
-    faults = {tuple(int(x) for x in item.split(":")) for item in fault.split(",") if item}
-    tried: dict = {}            # item -> ranks that failed it
-    fails = [0] * world
-    alive = [True] * world      # still an owner
-    fetched_by: dict[int, int] = {}   # file index -> owner that fetched it
-    lens_of: dict[int, bytes] = {}
-    works, fetched_bytes, reassigned, j = [], 0, 0, 0
-    while any(queue):
-        this_round = [q.pop(0) if q else None for q in queue]
-        item = this_round[rank]
-        err, lens = "", []
-        if item is not None:
+# ----------------------------------------------------------------------------------------------
+# Planning: byte-balanced contiguous term shares, cut into tapered rounds
+# ----------------------------------------------------------------------------------------------
+def split_bytes(ulen: np.ndarray, a: int, b: int, weights) -> list[tuple[int, int]]:
+    """Cut terms [a, b) into len(weights) contiguous ranges of byte sizes ~ proportional to weights
+    (whole terms; empty ranges allowed)."""
+    n = len(weights)
+    if b <= a:
+        return [(a, a)] * n
+    cu = np.cumsum(ulen[a:b].astype(np.float64))
+    frac = np.cumsum(np.asarray(weights, dtype=np.float64))
+    frac /= frac[-1]
+    cuts = [a] + [a + int(np.searchsorted(cu, cu[-1] * frac[k], side="left")) + 1 for k in range(n - 1)] + [b]
+    cuts = np.maximum.accumulate(np.minimum(np.array(cuts), b))
+    return [(int(cuts[k]), int(cuts[k + 1])) for k in range(n)]
+
+
+def round_weights(share_bytes: int, round_bytes: int, taper: bool = True) -> list[float]:
+    """Relative sizes of a share's rounds: full rounds of `round_bytes`, with geometrically shrinking
+    first and last rounds (nothing overlaps the first fetch or the last exchange)."""
+    n = max(1, -(-int(share_bytes) // int(round_bytes)))
+    if not taper or n < 4:
+        return [1.0] * n
+    mid = max(1, -(-int(share_bytes - (sum(HEAD_TAPER) + sum(TAIL_TAPER)) * round_bytes) // round_bytes))
+    return list(HEAD_TAPER) + [1.0] * mid + list(TAIL_TAPER)
+
+
+class _Plan:
+    """The repository's Xet files laid out in one arena and their terms as one global table."""
+
+    def __init__(self, files: list[dict], shapes: list[list[tuple[int, int]]]):
+        self.files = files
+        self.file_off = []
+        off = 0
+        for f in files:
+            self.file_off.append(off)
+            off = (off + f["size"] + FILE_ALIGN - 1) // FILE_ALIGN * FILE_ALIGN
+        self.arena_bytes = off
+        nt = sum(len(s) for s in shapes)
+        self.t_file = np.zeros(nt, np.int32)
+        self.t_idx = np.zeros(nt, np.int32)       # term index inside its file's reconstruction
+        self.t_ulen = np.zeros(nt, np.int64)
+        self.t_nck = np.zeros(nt, np.int64)
+        self.t_dst = np.zeros(nt, np.int64)       # arena offset of the term's output
+        k = 0
+        for i, (f, sh) in enumerate(zip(files, shapes)):
+            pos = self.file_off[i]
+            if sum(u for u, _ in sh) != f["size"]:
+                raise SwarmPullError(f"{f['path']}: reconstruction covers {sum(u for u, _ in sh)} bytes, "
+                                     f"listing says {f['size']}")
+            for j, (u, c) in enumerate(sh):
+                self.t_file[k], self.t_idx[k], self.t_ulen[k], self.t_nck[k], self.t_dst[k] = i, j, u, c, pos
+                pos += u
+                k += 1
+        self.t_c0 = np.concatenate([[0], np.cumsum(self.t_nck)[:-1]]).astype(np.int64) if nt else np.zeros(0, np.int64)
+        self.n_chunks = int(self.t_nck.sum())
+        self.file_t0 = np.searchsorted(self.t_file, np.arange(len(files)), side="left")
+        self.file_t1 = np.searchsorted(self.t_file, np.arange(len(files)), side="right")
+
+    def region(self, a: int, b: int) -> tuple[int, int]:
+        if b <= a:
+            return (0, 0)
+        return int(self.t_dst[a]), int(self.t_dst[b - 1] + self.t_ulen[b - 1])
+
+    def jobs(self, a: int, b: int, base_ptr: int) -> list:
+        """(xet_hash, t0, t1, dst_ptr, chunk0) per file touched by terms [a, b)."""
+        out = []
+        t = a
+        while t < b:
+            f = int(self.t_file[t])
+            e = min(b, int(self.file_t1[f]))
+            out.append((self.files[f]["xet_hash"], int(self.t_idx[t]), int(self.t_idx[e - 1]) + 1,
+                        base_ptr + int(self.t_dst[t]), int(self.t_c0[t])))
+            t = e
+        return out
+
+    def files_of(self, a: int, b: int) -> list[int]:
+        return sorted(set(int(x) for x in self.t_file[a:b])) if b > a else []
+
+
+# ----------------------------------------------------------------------------------------------
+# Membership: survivors of a lost rank rebuild their groups in-process
+# ----------------------------------------------------------------------------------------------
+class _Membership:
+    """Who is still in the pull, and the groups they talk over.
+
+    ``ctl`` is a gloo group with a bounded timeout (ZEST_SWARM_CTL_TIMEOUT, default 120 s) carrying
+    the per-round agreement; ``data`` carries the piece exchange (RCCL on GPUs).  A heartbeat thread
+    stamps ``hb/<global rank>`` in the rendezvous store every second.  When a collective fails or
+    times out, `rebuild` posts this rank as alive for the next epoch, waits until every other rank
+    has either posted or gone stale (no heartbeat for ZEST_SWARM_HB_STALE s, default 5), lets the first
+    survivor publish the member list with a compare-and-set (so all survivors agree), and builds new
+    groups over the survivors only (use_local_synchronization: the dead rank takes no part)."""
+
+    def __init__(self, group, backend: str, device: torch.device):
+        self.backend = backend
+        self.device = device
+        self.granks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+        self.me = dist.get_rank()
+        self.data = group
+        self.timeout_s = float(os.environ.get("ZEST_SWARM_CTL_TIMEOUT", "120"))
+        self.stale_s = float(os.environ.get("ZEST_SWARM_HB_STALE", "5"))
+        import datetime
+        self._td = datetime.timedelta(seconds=self.timeout_s)
+        if backend == "gloo":
+            self.ctl = group
+        else:
+            self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td)
+        self.epoch = 0
+        self.store = None
+        self._stop = threading.Event()
+        self._hb = None
+        self.enabled = os.environ.get("ZEST_SWARM_ELASTIC", "1") != "0" and "MASTER_ADDR" in os.environ \
+            and "MASTER_PORT" in os.environ and len(self.granks) > 1
+        tok = [uuid.uuid4().hex if self.rank == 0 else None]
+        dist.broadcast_object_list(tok, src=self.granks[0], group=self.ctl)
+        self.prefix = f"zest/swarm/{tok[0]}"
+        if self.enabled:
             try:
-                if (rank, j) in faults:
-                    raise RuntimeError(f"injected fetch failure (round {j})")
-                idx = [item[1]] if item[0] == "xet" else list(item[1])
-                lens = fetcher.fetch([todo[i] for i in idx], [bufs[i] for i in idx])
-            except Exception as e:  # reported through the all-gather: every rank replans the same way
-                err = f"rank {rank}: {type(e).__name__}: {e}"
-        meta = [None] * world
-        dist.all_gather_object(meta, (err, lens), group=group)
-        fatal = []
-        for r, it in enumerate(this_round):
-            if it is None:
-                continue
-            e, ls = meta[r]
-            if e:
-                fails[r] += 1
-                tried.setdefault(it, set()).add(r)
-                if fails[r] >= 2:   # a repeatedly failing owner: hand its queue to the others
-                    alive[r] = False
-                moves = [it] + (queue[r] if not alive[r] else [])
-                if not alive[r]:
-                    queue[r] = []
-                for m in moves:
-                    cands = [q for q in range(world) if alive[q] and q not in tried.get(m, set())]
-                    if not cands:
-                        fatal.append(e if m == it else f"no owner left for {m}")
-                        continue
-                    load = [sum(todo[x[1]]["size"] if x[0] == "xet" else 0 for x in queue[q]) for q in range(world)]
-                    q = min(cands, key=lambda q: (load[q], q))
-                    queue[q].append(m)
-                    reassigned += 1
-                continue
-            idx = [it[1]] if it[0] == "xet" else list(it[1])
-            for k, i in enumerate(idx):
-                fetched_by[i] = r
-                if ls and k < len(ls) and ls[k] is not None:
-                    lens_of[i] = ls[k]
-                if r == rank:
-                    fetched_bytes += todo[i]["size"]
-                # seed the file to every other rank, in pieces (async; overlaps the next round's fetch)
-                n = todo[i]["size"]
-                for off in range(0, n, piece_bytes):
-                    works.append(dist.broadcast(bufs[i][off:off + min(piece_bytes, n - off)], granks[r], group=group,
-                                                async_op=True))
-        if fatal:
-            for w in works:  # leave no collective of an earlier round in flight
-                w.wait()
-            raise SwarmPullError("; ".join(sorted(set(fatal))))
-        j += 1
-    for w in works:
-        w.wait()
-    bad = []
-    if verify_received:
-        for i, f in enumerate(todo):
-            if fetched_by.get(i) == rank or not f["xet_hash"]:
-                continue
-            ok = verify_with_lens(bufs[i], lens_of[i], f["xet_hash"]) if i in lens_of \
-                else zdev.xet_file_hash(bufs[i]) == f["xet_hash"]
-            if not ok:
-                bad.append(f["path"])
-    if not _all_ok(not bad, device, group):
-        raise zdev.VerifyError(f"rank {rank}: received files failed their Xet hash: {bad}" if bad
-                               else f"rank {rank}: a peer rank received corrupt files")
-    if stats is not None:
-        stats.update(files=len(todo), owned=sum(1 for r in fetched_by.values() if r == rank),
-                     fetched_bytes=fetched_bytes,
-                     received_bytes=sum(f["size"] for i, f in enumerate(todo) if fetched_by.get(i) != rank),
-                     reassigned=reassigned, rounds=j)
-    out: dict[str, torch.Tensor] = {}
-    for f, buf in zip(todo, bufs):
-        if f["size"] == 0:
-            continue
-        hlen = int.from_bytes(buf[:8].cpu().numpy().tobytes(), "little")
-        start, meta_ = zdev.parse_safetensors_header(buf[: 8 + hlen].cpu().numpy().tobytes())
-        for k, v in zdev.tensor_views(buf, start, meta_).items():
-            if k in out:
-                raise ValueError(f"duplicate tensor {k} in {f['path']}")
-            out[k] = v
+                # a store client of our own: the heartbeat thread must not share the default store's
+                # socket with the main thread's group creation
+                self.store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                                           timeout=self._td)
+                self._beat()
+                self._hb = threading.Thread(target=self._heartbeat, daemon=True)
+                self._hb.start()
+            except Exception:  # noqa: BLE001 - no store: a lost rank fails the pull (no recovery)
+                self.enabled = False
+
+    @property
+    def rank(self) -> int:
+        return self.granks.index(self.me)
+
+    @property
+    def world(self) -> int:
+        return len(self.granks)
+
+    def _beat(self):
+        self.store.set(f"{self.prefix}/hb/{self.me}", repr(time.time()))
+
+    def _heartbeat(self):
+        while not self._stop.wait(1.0):
+            try:
+                self._beat()
+            except Exception:  # noqa: BLE001
+                return
+
+    def _last_beat(self, g: int) -> float:
+        k = f"{self.prefix}/hb/{g}"
+        try:
+            return float(self.store.get(k)) if self.store.check([k]) else 0.0
+        except Exception:  # noqa: BLE001
+            return 0.0
+
+    def close(self):
+        self._stop.set()
+
+    def rebuild(self) -> list[int]:
+        """Agree on the survivors, rebuild ctl/data groups over them; returns the lost ranks
+        (indices into the previous member list)."""
+        if not self.enabled:
+            raise SwarmPullError("a rank was lost and elastic recovery is off (ZEST_SWARM_ELASTIC=0 or no store)")
+        self.epoch += 1
+        ek = f"{self.prefix}/e{self.epoch}"
+        self.store.set(f"{ek}/alive/{self.me}", "1")
+        t_end = time.monotonic() + self.timeout_s + 2 * self.stale_s
+        while True:
+            now = time.time()
+            alive, pending = [], []
+            for g in self.granks:
+                if self.store.check([f"{ek}/alive/{g}"]):
+                    alive.append(g)
+                elif now - self._last_beat(g) < self.stale_s:
+                    pending.append(g)  # still beating: it is stuck in (or leaving) a collective
+            if not pending or time.monotonic() > t_end:
+                break
+            time.sleep(0.2)
+        got = self.store.compare_set(f"{ek}/members", "", json.dumps(sorted(alive)))
+        members = json.loads(got)
+        if self.me not in members:
+            raise SwarmPullError(f"rank {self.me} was dropped from the swarm (epoch {self.epoch})")
+        lost = [i for i, g in enumerate(self.granks) if g not in members]
+        old_data = self.data
+        self.granks = members
+        self.ctl = dist.new_group(ranks=members, backend="gloo", timeout=self._td, use_local_synchronization=True)
+        if self.backend == "gloo":
+            self.data = self.ctl
+        else:
+            abort = getattr(dist.distributed_c10d, "_abort_process_group", None)
+            if abort is not None and old_data is not None:
+                try:
+                    abort(old_data)
+                except Exception:  # noqa: BLE001
+                    pass
+            self.data = dist.new_group(ranks=members, backend=self.backend, use_local_synchronization=True)
+        return lost
+
+
+# ----------------------------------------------------------------------------------------------
+# Fetchers: device-direct (GPU) or host waterfall (CPU), term ranges into the arena
+# ----------------------------------------------------------------------------------------------
+class _Fetcher:
+    def __init__(self, repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
+                 threads):
+        self.args = (repo, revision, repo_type, p2p, list(peers or []), tracker, dht, list(dht_bootstrap or []))
+        self.device = device
+        self.staging_bytes, self.threads = staging_bytes, threads
+        self._impl = None
+
+    @property
+    def impl(self):
+        if self._impl is None:
+            repo, revision, repo_type, p2p, peers, tracker, dht, boot = self.args
+            if self.device.type == "cuda":
+                self._impl = ops.hip().DeviceXetPull(repo, revision, repo_type, p2p, peers, tracker, dht, boot,
+                                                     self.device.index or 0, self.staging_bytes, self.threads)
+            else:
+                self._impl = _core.HostXetFetcher(repo, revision, repo_type, p2p, peers, tracker, dht, boot,
+                                                  self.threads)
+        return self._impl
+
+    def shapes(self, xet_hash: str):
+        return self.impl.term_shapes(xet_hash)
+
+    def fetch(self, jobs, hashes: torch.Tensor, sizes: torch.Tensor | None, repair: bool = False):
+        if self.device.type == "cuda":
+            return self.impl.pull_terms(jobs, hashes.data_ptr(), sizes.data_ptr() if sizes is not None else 0, repair)
+        return self.impl.fetch_terms(jobs, hashes.data_ptr(), repair)
+
+    def settle(self, xet_hash: str, ok: bool):
+        if self._impl is not None:
+            self._impl.settle(xet_hash, ok)
+
+    def stats(self) -> dict:
+        return json.loads(self._impl.stats_json()) if self._impl is not None else {}
+
+
+# ----------------------------------------------------------------------------------------------
+# The pull
+# ----------------------------------------------------------------------------------------------
+def _fault_spec() -> dict:
+    """ZEST_SWARM_FAULT items: "<rank>:<round>" (that fetch raises), "exit:<rank>:<round>" (that
+    rank's process exits at that round)."""
+    out = {"fail": set(), "exit": set()}
+    for item in os.environ.get("ZEST_SWARM_FAULT", "").split(","):
+        p = item.split(":")
+        if len(p) == 2:
+            out["fail"].add((int(p[0]), int(p[1])))
+        elif len(p) == 3 and p[0] == "exit":
+            out["exit"].add((int(p[1]), int(p[2])))
     return out
 
 
-class _Fetcher:
-    """Fetches this rank's owned files into their buffers, one round at a time, and returns each
-    file's chunk sizes (uint32 bytes; None for non-Xet files).  On a GPU the Xet files go
-    device-direct through one DeviceXetPull; on CPU through one HostXetFetcher (in memory, no
-    snapshot).  Both are built on first use and kept, so the hub session and the peer connections
-    carry over between rounds.  Non-Xet safetensors come through the host pull."""
+class _Swarm:
+    def __init__(self, repo, revision, group, device, *, p2p, peers, tracker, dht, dht_bootstrap, repo_type,
+                 verify_received, staging_bytes, threads, round_bytes, exchange):
+        self.t0 = time.perf_counter()
+        self.times: dict = {}
+        self.repo, self.revision, self.repo_type = repo, revision, repo_type
+        backend = str(dist.get_backend(group)).lower()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.backend = backend
+        self.m = _Membership(group, backend, self.device)
+        self.verify = verify_received
+        self.round_bytes = int(round_bytes)
+        self.exchange_req = exchange
+        self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
+                                staging_bytes, threads)
+        self.fault = _fault_spec()
+        self.stats = {"reassigned": 0, "recovered_ranks": 0, "resent_bytes": 0, "repaired_files": 0,
+                      "from_peer": 0, "from_cdn": 0, "from_cache": 0, "fetched_wire_bytes": 0}
 
-    def __init__(self, repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
-                 threads):
-        self.repo, self.revision, self.repo_type, self.device = repo, revision, repo_type, device
-        self.p2p, self.peers, self.tracker, self.dht = p2p, list(peers or []), tracker, dht
-        self.dht_bootstrap, self.staging_bytes, self.threads = list(dht_bootstrap or []), staging_bytes, threads
-        self._dp = None
-        self._hf = None
+    def _mark(self, name, t):
+        self.times[name] = round(self.times.get(name, 0.0) + time.perf_counter() - t, 4)
 
-    def fetch(self, files, bufs) -> list:
-        lens: list = [None] * len(files)
-        xet = [k for k, f in enumerate(files) if f["xet_hash"]]
-        host = [k for k, f in enumerate(files) if not f["xet_hash"]]
-        req = [(files[k]["xet_hash"], bufs[k].data_ptr(), files[k]["size"]) for k in xet]
-        if xet and self.device.type == "cuda":
-            if self._dp is None:
-                self._dp = ops.hip().DeviceXetPull(self.repo, self.revision, self.repo_type, self.p2p, self.peers,
-                                                   self.tracker, self.dht, self.dht_bootstrap,
-                                                   self.device.index or 0, self.staging_bytes, self.threads)
-            # the buffers exist (allocated on the current stream) before the pull's private stream
-            # writes them; a device-wide sync would also wait for the previous rounds' RCCL broadcasts
-            torch.cuda.current_stream(self.device).synchronize()
-            res = self._dp.pull_files(req)
-        elif xet:
-            if self._hf is None:
-                self._hf = _core.HostXetFetcher(self.repo, self.revision, self.repo_type, self.p2p, self.peers,
-                                                self.tracker, self.dht, self.dht_bootstrap, self.threads)
-            res = self._hf.fetch_files(req)
-        else:
-            res = []
-        for k, r in zip(xet, res):
-            lens[k] = r["chunk_lens"]
-        if host:
-            r = _core.pull(self.repo, self.revision, self.p2p, self.peers, self.tracker, self.dht,
-                           self.dht_bootstrap, [files[k]["path"] for k in host], True, 0, self.repo_type)
-            if r["failed_files"]:
-                raise SwarmPullError(f"host pull failed for {r['failed_files']} file(s)")
-            for k in host:
-                bufs[k].copy_(zdev.load_file(os.path.join(r["snapshot_dir"], files[k]["path"]),
-                                             self.device).view(torch.uint8))
-        return lens
+    # -- control plane ------------------------------------------------------------------------
+    def _gather(self, obj):
+        out = [None] * self.m.world
+        try:
+            dist.all_gather_object(out, obj, group=self.m.ctl)
+        except Exception as e:  # noqa: BLE001 - gloo reports a dead or stuck peer as a RuntimeError
+            raise _RankLost(str(e)) from e
+        return out
+
+    def _bcast_from0(self, obj):
+        box = [obj]
+        try:
+            dist.broadcast_object_list(box, src=self.m.granks[0], group=self.m.ctl)
+        except Exception as e:  # noqa: BLE001
+            raise _RankLost(str(e)) from e
+        return box[0]
+
+    # -- setup --------------------------------------------------------------------------------
+    def listing_and_plan(self):
+        t = time.perf_counter()
+        obj = None
+        if self.m.rank == 0:
+            try:
+                commit, files = _core.list_repo_files(self.repo, self.revision, self.repo_type)
+                st = [f for f in files if f["path"].endswith(".safetensors")]
+                xet = [f for f in st if f["xet_hash"]]
+                shapes = _parallel_map(lambda f: [tuple(x) for x in self.fetcher.shapes(f["xet_hash"])], xet, 8)
+                obj = ("ok", commit, st, shapes)
+            except Exception as e:  # noqa: BLE001 - every rank leaves the same way
+                obj = ("err", f"{type(e).__name__}: {e}")
+        obj = self._bcast_from0(obj)
+        if obj[0] != "ok":
+            raise SwarmPullError(f"listing/planning {self.repo}@{self.revision} failed on rank 0: {obj[1]}")
+        _, self.commit, st_files, shapes = obj
+        self.xet_files = [f for f in st_files if f["xet_hash"]]
+        self.plain_files = [f for f in st_files if not f["xet_hash"]]
+        self.plan = _Plan(self.xet_files, shapes)
+        self._mark("plan_s", t)
+
+    def allocate(self):
+        t = time.perf_counter()
+        P = self.plan
+        n = max(1, P.arena_bytes)
+        want_map = (self.cuda and self.m.world > 1 and os.environ.get("ZEST_EXCHANGE_IPC", "1") != "0"
+                    and self.exchange_req in ("auto", "ipc", "xgmi"))
+        self.arena = None
+        if want_map:
+            try:
+                self.arena = ops.vmm_empty(n, self.device)
+            except Exception:  # noqa: BLE001 - torch allocation, RCCL exchanges only
+                self.arena = None
+        if self.arena is None:
+            self.arena = ops.padded_empty(n, self.device) if self.cuda else torch.empty(n + ops.PAD, dtype=torch.uint8)[:n]
+        nck = max(1, P.n_chunks)
+        self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
+        self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
+        self.lens = np.zeros(nck, dtype=np.uint32)   # every chunk's size, filled as rounds are agreed
+        self.mapped = None
+        if want_map and self.exchange_req != "p2p":
+            t_map = time.perf_counter()
+            self.mapped = map_peer_arenas(self.arena, self.m.rank, self.m.world, self.m.data)
+            self._mark("map_s", t_map)
+        self._mark("alloc_s", t)
+
+    def shard(self):
+        """Per-rank queues of items (term ranges), identical on every rank."""
+        P = self.plan
+        nt = len(P.t_ulen)
+        W = self.m.world
+        cu = np.cumsum(P.t_ulen.astype(np.float64))
+        total = cu[-1] if nt else 0.0
+        bounds = [0] + [int(np.searchsorted(cu, total * r / W, side="left")) + 1 for r in range(1, W)] + [nt]
+        bounds = np.maximum.accumulate(np.minimum(np.array(bounds), nt))
+        shares = [(int(bounds[r]), int(bounds[r + 1])) for r in range(W)]
+        max_share = max((int(P.t_ulen[a:b].sum()) for a, b in shares), default=0)
+        taper = os.environ.get("ZEST_ROUND_TAPER", "1") != "0"
+        weights = round_weights(max_share, self.round_bytes, taper) if max_share else [1.0]
+        self.items: list[tuple[int, int]] = []
+        self.queue: list[list[int]] = [[] for _ in range(W)]
+        for r, (a, b) in enumerate(shares):
+            for ra, rb in split_bytes(P.t_ulen, a, b, weights):
+                if rb > ra:
+                    self.items.append((ra, rb))
+                    self.queue[r].append(len(self.items) - 1)
+        self.n_rounds_planned = len(weights)
+        self.tried: dict = {}        # item -> members (global ranks) that failed it
+        self.fails: dict = {}        # global rank -> failed fetches
+        self.owner_of: dict = {}     # item -> global rank that fetched it
+        self.have: set = set()       # items this rank holds (fetched, or received and hashed)
+        self.item_lens: dict = {}    # item -> uint32 chunk sizes (bytes), known to every rank
+        self.fetched_bytes = 0       # unpacked bytes this rank fetched from the network
+
+    # -- exchange -----------------------------------------------------------------------------
+    def setup_exchange(self):
+        t = time.perf_counter()
+        W = self.m.world
+        self.xchg = RoundExchange(self.arena, self.m.rank, W, self.m.data, "p2p")
+        if self.mapped is not None:
+            self.xchg.enable_ipc(self.mapped)
+        self.verify_stream = role_stream(self.device, "verify") if self.cuda else None
+        self._hash_scratch = ops.HashScratch(self.device) if self.cuda else None
+        if W == 1:
+            self.xchg.mode = "none"
+            return
+        req = self.exchange_req
+        if req != "auto":
+            if req in PEER_MAPPED_MODES and not self.xchg.mapped:
+                raise SwarmPullError(f"exchange={req}: mapping the peers' arenas failed")
+            self.xchg.mode = req
+            return
+        cached = tuned_mode(W, self.backend, self.xchg.mapped)
+        if cached is not None:
+            self.xchg.mode = cached
+            return
+        if not self.cuda:
+            self.xchg.mode = "bcast"  # CPU groups: nothing to tune over xGMI
+            return
+        # time the strategies on the first rounds' planned regions (the arena holds nothing yet)
+        regs = []
+        for k in range(min(3, max(len(q) for q in self.queue))):
+            regs.append([self.plan.region(*self.items[q[k]]) if k < len(q) else (0, 0) for q in self.queue])
+        try:
+            self.xchg.autotune(regs, EXCHANGE_MODES)
+        except Exception as e:  # noqa: BLE001
+            raise _RankLost(str(e)) from e
+        self._mark("autotune_s", t)
+
+    def _hash_received(self, recv_items, works):
+        """Hash the chunks of `recv_items` (owned by peers) once `works` landed; returns an event
+        (GPU) marking completion, or None (CPU: done on return)."""
+        P = self.plan
+        if not self.cuda:
+            for w in works:
+                w.wait()
+            if self.verify:
+                for it in recv_items:
+                    offs, lens, c0 = self._chunk_layout(it)
+                    self.hashes[c0:c0 + len(lens)] = ops.hash_ranges(self.arena, offs, lens)
+            self.have.update(recv_items)
+            return None
+        H = ops.hip()
+        with torch.cuda.stream(self.verify_stream):
+            for w in works:
+                w.wait()
+            if self.verify:
+                for it in recv_items:
+                    offs, lens, c0 = self._chunk_layout(it)
+                    if not len(lens):
+                        continue
+                    od = torch.from_numpy(offs.view(np.int64)).to(self.device, non_blocking=False)
+                    ld = torch.from_numpy(lens.view(np.int32)).to(self.device, non_blocking=False)
+                    sp, sb = self._hash_scratch.get(len(lens), int(lens.sum(dtype=np.uint64)))
+                    H.hash_ranges(self.arena.data_ptr(), od.data_ptr(), ld.data_ptr(), len(lens),
+                                  self.hashes.data_ptr() + 32 * c0, ops.KEY_DATA, self.verify_stream.cuda_stream, sp, sb)
+                    od.record_stream(self.verify_stream)
+                    ld.record_stream(self.verify_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.verify_stream)
+        del P
+        return ev
+
+    def _chunk_layout(self, it: int):
+        """Arena offsets (uint64), sizes (uint32) and first global chunk of item it's chunks."""
+        P = self.plan
+        a, b = self.items[it]
+        lens = np.frombuffer(self.item_lens[it], dtype=np.uint32)
+        nck = P.t_nck[a:b]
+        term_of = np.repeat(np.arange(a, b), nck)
+        cs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))])
+        first = np.concatenate([[0], np.cumsum(nck)[:-1]]).astype(np.int64)  # chunk position of each term
+        start_in_term = cs[:-1] - cs[first][np.repeat(np.arange(b - a), nck)]
+        offs = (P.t_dst[term_of].astype(np.uint64) + start_in_term).astype(np.uint64)
+        return offs, lens, int(P.t_c0[a])
+
+    # -- main loop ----------------------------------------------------------------------------
+    def run(self):
+        self.round_no = 0
+        self.pending_events: list = []   # (event, items) of received rounds not yet known to be hashed
+        while True:
+            try:
+                self._rounds()
+                self._settle_received()
+                return
+            except _RankLost as e:
+                self._recover(str(e))
+
+    def _settle_received(self):
+        for ev, items in self.pending_events:
+            if ev is not None:
+                ev.synchronize()
+            self.have.update(items)
+        self.pending_events = []
+
+    def _rounds(self):
+        P = self.plan
+        while any(self.queue):
+            me = self.m.rank
+            this = [q.pop(0) if q else None for q in self.queue]
+            self.inflight = list(this)   # popped but not yet agreed (re-queued by _recover)
+            it = this[me]
+            if (self.m.me, self.round_no) in self.fault["exit"]:
+                os._exit(1)  # fault injection: this rank dies mid-pull (tests)
+            err, lens, info = "", b"", {}
+            t = time.perf_counter()
+            if it is not None and it in self.have:  # a re-send after recovery: the bytes are here
+                lens = self.item_lens[it]
+            elif it is not None:
+                try:
+                    if (self.m.me, self.round_no) in self.fault["fail"]:
+                        raise RuntimeError(f"injected fetch failure (round {self.round_no})")
+                    a, b = self.items[it]
+                    res = self.fetcher.fetch(P.jobs(a, b, self.arena.data_ptr()), self.hashes, self.sizes)
+                    lens = b"".join(r["chunk_lens"] for r in res)
+                    info = {k: sum(r[k] for r in res) for k in ("fetched", "from_peer", "from_cdn", "from_cache")}
+                except Exception as e:  # noqa: BLE001 - reported through the all-gather
+                    err = f"rank {self.m.me}: {type(e).__name__}: {e}"
+            self._mark("fetch_s", t)
+            t = time.perf_counter()
+            meta = self._gather((it, err, lens))
+            self._mark("agree_s", t)
+            fatal, regions, recv = [], [], []
+            for r, (item, e, ls) in enumerate(meta):
+                if item is None:
+                    regions.append((0, 0))
+                    continue
+                g = self.m.granks[r]
+                if e:
+                    self.fails[g] = self.fails.get(g, 0) + 1
+                    self.tried.setdefault(item, set()).add(g)
+                    moves = [item]
+                    if self.fails[g] >= 2:   # a repeatedly failing owner: hand its queue to the others
+                        moves += self.queue[r]
+                        self.queue[r] = []
+                    for mv in moves:
+                        cands = [q for q in range(self.m.world)
+                                 if self.fails.get(self.m.granks[q], 0) < 2 and self.m.granks[q] not in self.tried.get(mv, set())]
+                        if not cands:
+                            fatal.append(e if mv == item else f"no owner left for terms {self.items[mv]} "
+                                                              f"(rank {g} dropped)")
+                            continue
+                        load = [sum(int(P.t_ulen[self.items[x][0]:self.items[x][1]].sum()) for x in self.queue[q])
+                                for q in range(self.m.world)]
+                        q = min(cands, key=lambda q: (load[q], q))
+                        self.queue[q].append(mv)
+                        self.stats["reassigned"] += 1
+                    regions.append((0, 0))
+                    continue
+                self.item_lens[item] = ls
+                first_time = item not in self.owner_of
+                self.owner_of.setdefault(item, g)
+                regions.append(P.region(*self.items[item]))
+                if r == me:
+                    if first_time and info:
+                        a, b = self.items[item]
+                        self.fetched_bytes += int(P.t_ulen[a:b].sum())
+                        self.stats["fetched_wire_bytes"] += info["fetched"]
+                        for k in ("from_peer", "from_cdn", "from_cache"):
+                            self.stats[k] += info[k]
+                    self.have.add(item)
+                elif item not in self.have:  # (a re-send also reaches ranks holding it: same bytes)
+                    recv.append(item)
+                if not first_time and r == me:
+                    a, b = self.items[item]
+                    self.stats["resent_bytes"] += int(P.t_ulen[a:b].sum())
+            self.inflight = []
+            if fatal:
+                self._settle_received()
+                raise SwarmPullError("; ".join(sorted(set(fatal))))
+            if self.m.world > 1 and any(hi > lo for lo, hi in regions):
+                t = time.perf_counter()
+                try:
+                    works = self.xchg.exchange(regions, synced=True)
+                    ev = self._hash_received(recv, works)
+                except Exception as e:  # noqa: BLE001
+                    raise _RankLost(str(e)) from e
+                if ev is not None:
+                    self.pending_events.append((ev, recv))
+                self._mark("exchange_issue_s", t)
+            self.round_no += 1
+
+    def _recover(self, why: str):
+        """A rank was lost: rebuild the groups over the survivors and re-shard (see _Membership)."""
+        t = time.perf_counter()
+        old_world, old_granks = self.m.world, list(self.m.granks)
+        # whatever the dead peer's exchanges left in flight is abandoned; only finished hashing counts
+        done = []
+        for ev, items in self.pending_events:
+            if ev is None or ev.query():
+                done += items
+        self.have.update(done)
+        self.pending_events = []
+        lost = self.m.rebuild()
+        if not lost:
+            raise SwarmPullError(f"collective failed but every rank is alive: {why}")
+        self.stats["recovered_ranks"] += len(lost)
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+        # queues of the survivors, in their new order; everything of the lost ranks is re-planned
+        keep = {g: self.queue[old_granks.index(g)] for g in self.m.granks}
+        orphan = [x for i in lost for x in self.queue[i]]
+        # ranges popped in the failed round but never agreed: back to their owner, or orphaned
+        for i, x in enumerate(getattr(self, "inflight", [])):
+            if x is not None and x not in self.owner_of:
+                if old_granks[i] in keep:
+                    keep[old_granks[i]].insert(0, x)
+                else:
+                    orphan.append(x)
+        self.inflight = []
+        self.queue = [keep[g] for g in self.m.granks]
+        # which items does every survivor hold?  (fetched ones, and received ones already hashed)
+        fetched = sorted(self.owner_of)
+        holds = self._gather(sorted(i for i in fetched if i in self.have))
+        holders = {i: [r for r, h in enumerate(holds) if i in set(h)] for i in fetched}
+        resend, refetch = [], list(orphan)
+        for i in fetched:
+            hs = holders[i]
+            if len(hs) == self.m.world:
+                continue
+            if hs:
+                resend.append((i, hs[0]))
+            else:
+                refetch.append(i)
+                self.owner_of.pop(i, None)
+        for i, r in resend:
+            self.queue[r].insert(0, i)   # the holder sends it first (no fetch: its bytes are there)
+        P = self.plan
+        for i in sorted(set(refetch)):
+            load = [sum(int(P.t_ulen[self.items[x][0]:self.items[x][1]].sum()) for x in q) for q in self.queue]
+            q = min(range(self.m.world), key=lambda q: (load[q], q))
+            self.queue[q].append(i)
+        self.xchg = RoundExchange(self.arena, self.m.rank, self.m.world, self.m.data,
+                                  "bcast" if self.m.world > 1 else "none")
+        self._mark("recover_s", t)
+        if self.m.rank == 0:
+            print(f"[zest swarm] lost rank(s) {[old_granks[i] for i in lost]} of {old_world}: continuing on "
+                  f"{self.m.world}; {len(resend)} range(s) re-sent, {len(set(refetch))} refetched", flush=True)
+
+    # -- verification, repair, settle ---------------------------------------------------------
+    def verify_files(self) -> list[int]:
+        """Merkle file hashes on this rank; returns the indices of files failing on ANY rank."""
+        P = self.plan
+        nf = len(self.xet_files)
+        if nf == 0:
+            return []
+        t = time.perf_counter()
+        for it, ls in self.item_lens.items():
+            a, _ = self.items[it]
+            c0 = int(P.t_c0[a])
+            arr = np.frombuffer(ls, dtype=np.uint32)
+            self.lens[c0:c0 + len(arr)] = arr
+        bad_local = np.zeros(nf, dtype=np.int32)
+        if self.verify:
+            empty = _core.xet_hex(_core.file_hash([]))
+            idx = [i for i in range(nf) if P.file_t1[i] > P.file_t0[i]]
+            for i in range(nf):
+                if i not in idx and self.xet_files[i]["xet_hash"] != empty:
+                    bad_local[i] = 1
+            jobs = [(int(P.t_c0[P.file_t0[i]]), int(P.t_nck[P.file_t0[i]:P.file_t1[i]].sum())) for i in idx]
+            sizes = torch.from_numpy(self.lens.astype(np.int64))
+            sizes = sizes.to(self.device) if self.cuda else sizes
+            if self.cuda:
+                torch.cuda.current_stream(self.device).wait_stream(self.verify_stream)
+            roots = ops.merkle_roots(self.hashes, sizes, jobs, file_hash=True).cpu().numpy()
+            for j, i in enumerate(idx):
+                if _core.xet_hex(roots[j].tobytes()) != self.xet_files[i]["xet_hash"]:
+                    bad_local[i] = 1
+        flags = torch.from_numpy(bad_local)
+        try:
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.m.ctl)
+        except Exception as e:  # noqa: BLE001
+            raise _RankLost(str(e)) from e
+        self._mark("verify_s", t)
+        return [i for i in range(nf) if flags[i]]
+
+    def repair(self, bad: list[int]) -> None:
+        """Owners refetch the failed files' terms from the CDN; the ranges are re-sent to every rank
+        over a plain RCCL broadcast (a broken peer mapping cannot corrupt them twice)."""
+        t = time.perf_counter()
+        P = self.plan
+        badset = set(bad)
+        for i in bad:
+            self.fetcher.settle(self.xet_files[i]["xet_hash"], False)
+        # split each fetched item into its pieces inside bad files; the item's owner refetches them
+        pieces = []   # (owner rank, a, b)
+        for it, g in sorted(self.owner_of.items()):
+            a, b = self.items[it]
+            t_ = a
+            while t_ < b:
+                f = int(P.t_file[t_])
+                e = min(b, int(P.file_t1[f]))
+                if f in badset:
+                    pieces.append((self.m.granks.index(g) if g in self.m.granks else 0, t_, e))
+                t_ = e
+        self.xchg.mode = "bcast" if self.m.world > 1 else self.xchg.mode
+        per_rank = [[(a, b) for r, a, b in pieces if r == q] for q in range(self.m.world)]
+        for k in range(max((len(p) for p in per_rank), default=0)):
+            mine = per_rank[self.m.rank][k] if k < len(per_rank[self.m.rank]) else None
+            err = ""
+            if mine is not None:
+                try:
+                    self.fetcher.fetch(P.jobs(mine[0], mine[1], self.arena.data_ptr()), self.hashes, self.sizes,
+                                       repair=True)
+                except Exception as e:  # noqa: BLE001
+                    err = f"rank {self.m.me}: {type(e).__name__}: {e}"
+            errs = self._gather(err)
+            if any(errs):
+                raise zdev.VerifyError("repair fetch failed: " + "; ".join(e for e in errs if e))
+            if self.m.world > 1:
+                regions = [P.region(*per_rank[q][k]) if k < len(per_rank[q]) else (0, 0) for q in range(self.m.world)]
+                works = self.xchg.exchange(regions)
+                self.stats["resent_bytes"] += sum(hi - lo for q, (lo, hi) in enumerate(regions) if q != self.m.rank)
+                recv = []
+                for q in range(self.m.world):
+                    if q != self.m.rank and k < len(per_rank[q]):
+                        self.items.append(per_rank[q][k])
+                        idx = len(self.items) - 1
+                        a, b = per_rank[q][k]
+                        self.item_lens[idx] = self._lens_of(a, b)
+                        recv.append(idx)
+                ev = self._hash_received(recv, works)
+                if ev is not None:
+                    ev.synchronize()
+        self.stats["repaired_files"] += len(bad)
+        self._mark("repair_s", t)
+
+    def _lens_of(self, a: int, b: int) -> bytes:
+        P = self.plan
+        c0, c1 = int(P.t_c0[a]), int(P.t_c0[b - 1] + P.t_nck[b - 1])
+        return self.lens[c0:c1].tobytes()
+
+    def settle(self, ok_files: set[int]):
+        mine = set()
+        for it, g in self.owner_of.items():
+            if g == self.m.me:
+                mine.update(self.plan.files_of(*self.items[it]))
+        for i in mine:
+            self.fetcher.settle(self.xet_files[i]["xet_hash"], i in ok_files)
+
+    def plain(self) -> list[torch.Tensor]:
+        """Non-Xet safetensors: rank 0 pulls them through the host path; broadcast to the others."""
+        files = self.plain_files
+        if not files:
+            return []
+        bufs = [ops.padded_empty(f["size"], self.device)[: f["size"]] if self.cuda
+                else torch.empty(f["size"], dtype=torch.uint8) for f in files]
+        err = ""
+        if self.m.rank == 0:
+            try:
+                r = _core.pull(self.repo, self.revision, *self.fetcher.args[3:8], [f["path"] for f in files], True, 0,
+                               self.repo_type)
+                if r["failed_files"]:
+                    raise SwarmPullError(f"host pull failed for {r['failed_files']} file(s)")
+                for f, b in zip(files, bufs):
+                    b.copy_(zdev.load_file(os.path.join(r["snapshot_dir"], f["path"]), self.device).view(torch.uint8))
+                self.fetched_bytes += sum(f["size"] for f in files)
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+        err = self._bcast_from0(err)
+        if err:
+            raise SwarmPullError(f"non-Xet safetensors: {err}")
+        for b in bufs:
+            if b.numel() and self.m.world > 1:
+                dist.broadcast(b, src=self.m.granks[0], group=self.m.data)
+        return bufs
+
+    def tensors(self, plain_bufs) -> dict[str, torch.Tensor]:
+        out: dict[str, torch.Tensor] = {}
+        views = [(f, self.arena[o:o + f["size"]]) for f, o in zip(self.xet_files, self.plan.file_off)]
+        views += list(zip(self.plain_files, plain_bufs))
+        for f, buf in views:
+            if f["size"] == 0:
+                continue
+            hlen = int.from_bytes(buf[:8].cpu().numpy().tobytes(), "little")
+            start, meta_ = zdev.parse_safetensors_header(buf[: 8 + hlen].cpu().numpy().tobytes())
+            for k, v in zdev.tensor_views(buf, start, meta_).items():
+                if k in out:
+                    raise ValueError(f"duplicate tensor {k} in {f['path']}")
+                out[k] = v
+        return out
+
+
+def _parallel_map(fn, items, threads: int):
+    if not items:
+        return []
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(threads, len(items))) as ex:
+        return list(ex.map(fn, items))
+
+
+def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2p: bool = True, peers=None,
+               tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
+               verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
+               round_bytes: int | None = None, exchange: str = "auto",
+               stats: dict | None = None) -> dict[str, torch.Tensor]:
+    """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
+    full set (views into one arena per rank).  `exchange`: "auto" (measured at setup, cached per
+    process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
+    ZEST_SWARM_ROUND_MB, 1024 MiB): per-rank bytes per pipeline round.  `stats`, if given, is filled
+    with this rank's numbers: bytes fetched / received, the exchange mode and its autotune times,
+    per-phase seconds, re-shards and recovered ranks."""
+    if round_bytes is None:
+        round_bytes = int(os.environ.get("ZEST_SWARM_ROUND_MB", "1024")) << 20
+    if exchange not in ("auto",) + EXCHANGE_MODES:
+        raise ValueError(f"exchange={exchange!r}")
+    sw = _Swarm(repo, revision, group, device, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
+                dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify_received,
+                staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange)
+    try:
+        while True:
+            try:
+                sw.listing_and_plan()
+                break
+            except _RankLost as e:
+                sw.m.rebuild()
+                del e
+        sw.allocate()
+        sw.shard()
+        sw.setup_exchange()
+        t_pull = time.perf_counter()
+        sw.run()
+        if sw.cuda:
+            torch.cuda.synchronize(sw.device)
+        sw._mark("pull_s", t_pull)
+        bad = sw.verify_files()
+        for _ in range(2):
+            if not bad:
+                break
+            sw.repair(bad)
+            bad = sw.verify_files()
+        nf = len(sw.xet_files)
+        sw.settle(set(range(nf)) - set(bad))
+        if bad:
+            raise zdev.VerifyError(f"rank {sw.m.me}: files failed their Xet hash after repair: "
+                                   f"{[sw.xet_files[i]['path'] for i in bad]}")
+        plain = sw.plain()
+        out = sw.tensors(plain)
+        if sw.cuda:
+            torch.cuda.synchronize(sw.device)
+        if stats is not None:
+            total = sum(f["size"] for f in sw.xet_files) + sum(f["size"] for f in sw.plain_files)
+            wall = time.perf_counter() - sw.t0
+            stats.update(
+                files=len(sw.xet_files) + len(sw.plain_files), fetched_bytes=sw.fetched_bytes,
+                received_bytes=total - sw.fetched_bytes, total_bytes=total,
+                p2p_ratio=(total - sw.fetched_bytes) / total if total else 0.0,
+                rounds=sw.round_no, planned_rounds=sw.n_rounds_planned, items=len(sw.items),
+                exchange=sw.xchg.mode, exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
+                peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
+                GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
+                fetch_stats=sw.fetcher.stats(), **sw.stats)
+        return out
+    finally:
+        sw.m.close()
