@@ -169,6 +169,7 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     mapped = arenas.get("peers") if arenas is not None else None
     wd.arm("setup")
     t_setup = time.time()
+    phase: dict = {}
     # bf16 mode stores chunks the way Xet stores real checkpoints: BG4-LZ4 frames (compressed on the
     # GPU) when smaller than the chunk, so the pull decodes them on the GPU.
     comp = "bg4" if (mode == "bf16" and cuda) else "none"
@@ -197,17 +198,21 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
                 # them (imports of a built arena were seen to hang, docs/PARITY.md)
                 from zest_amd.engine import map_peer_arenas
                 wd.arm("ipc")
+                t_map = time.time()
                 mapped = map_peer_arenas(arena, rank, world_size)
+                phase["map_s"] = round(time.time() - t_map, 3)
                 wd.arm("setup")
                 if arenas is not None:
                     arenas["peers"] = mapped
                 log(rank, f"peer arenas mapped over HIP IPC before the build: {mapped is not None}")
         world.generate_on_device(arena)
-        world.build_on_device(arena)
+        # N > 1: each rank chunks / hashes / compresses only its files, then the plan is all-gathered
+        world.build_on_device(arena, shard=(rank, world_size, None) if dist is not None else None)
         torch.cuda.synchronize()
     else:
         contents = world.build_on_host()
         arena = torch.zeros(world.arena_bytes + 4096, dtype=torch.uint8)[: world.arena_bytes]
+    phase["world_s"] = round(time.time() - t_setup - phase.get("map_s", 0.0), 3)
     log(rank, f"[{mode}] xet plan: {world.n_chunks} chunks, {world.n_xorbs} xorbs, {len(world.terms)} terms "
               f"({time.time() - t_setup:.1f}s)")
     if cuda:  # host oracle spot check of the GPU chunk hashes (8 chunks spread over the model)
@@ -233,11 +238,13 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         ipc = mapped is not None and puller.enable_ipc(mapped)
         if a.exchange in ("ipc", "xgmi") and not ipc:
             raise SystemExit(f"--exchange {a.exchange}: mapping the peers' arenas failed")
+    t_origin = time.time()
     if cuda:
         puller.build_origin()
         torch.cuda.synchronize()
     else:
         puller.build_origin_host(contents)
+    phase["origin_s"] = round(time.time() - t_origin, 3)
     # ZEST_GRAPH=1 (one GPU): a step is one HIP graph launch.  Opt-in: the graph's H2D copies ran at
     # 51.2 GB/s against 56.2 for the eager copy-stream pipeline (profiles/hip_graph_r2.md).
     graph = puller.capture_graph() if world_size == 1 and os.environ.get("ZEST_GRAPH") == "1" else False
@@ -245,6 +252,8 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         log(rank, "step captured in a HIP graph")
     log(rank, f"[{mode}] origin {puller.origin.n / 1e9:.2f} GB pinned on rank {rank}; rounds {puller.n_rounds}; "
               f"setup {time.time() - t_setup:.1f}s")
+    phase["setup_s"] = round(time.time() - t_setup, 3)
+    t_tune = time.time()
     if world_size > 1:
         wd.arm("autotune")
         if exchange_pick is not None and (exchange_pick not in ("ipc", "xgmi") or ipc):
@@ -274,7 +283,9 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
             sync()
             puller.check()
 
+    phase["autotune_s"] = round(time.time() - t_tune, 3)
     wd.arm("warmup")
+    t_warm = time.time()
     try:
         warmup()
     except ops.IngestError as e:  # the error word is all-reduced: every rank takes this branch
@@ -283,6 +294,7 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         log(rank, f"exchange {puller.exchange} failed verification ({e}); falling back to p2p")
         puller.exchange = "p2p"
         warmup()
+    phase["warmup_s"] = round(time.time() - t_warm, 3)
     puller.err.zero_()
     wd.arm("timed")
     barrier()
@@ -303,6 +315,13 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         dist.all_reduce(recv)
         dist.all_reduce(ing)
     step_s = float(elapsed.item()) / max(1, a.steps)
+    phase["timed_s"] = round(float(elapsed.item()), 3)
+    # what each rank received from its peers per step, over the measured step time (GB/s)
+    rx = [float(puller.bytes_received) / step_s / 1e9]
+    if dist is not None:
+        rx_all = [None] * world_size
+        dist.all_gather_object(rx_all, rx[0])
+        rx = rx_all
     res = {
         "mode": mode, "step_s": step_s, "model_bytes": world.model_bytes,
         "value": world_size * world.model_bytes / step_s / 1e9,
@@ -314,6 +333,7 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         "exchange": puller.exchange if world_size > 1 else "none",
         "exchange_autotune_s": {m: round(v, 4) for m, v in puller.exchange_times.items()},
         "hip_graph": bool(graph), "pipeline": getattr(puller, "pipeline", "cpu"), "seeders": seeders,
+        "phase_s": phase, "exchange_rx_GBps": [round(x, 6) for x in rx],
     }
     puller.close()
     del puller, arena
@@ -328,6 +348,30 @@ def _data_note(r: dict) -> str:
         stored = "chunks stored raw"
     return (f"synthetic ({what} of the real tensor shapes; real Xet CDC/xorbs/hashes; {stored}; "
             "origin = pinned host memory standing in for the CDN)")
+
+
+def device_id(device) -> str:
+    """PCI address of a GPU ("cpu" for host rehearsals)."""
+    import torch
+    if device.type != "cuda":
+        return "cpu"
+    p = torch.cuda.get_device_properties(device)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+
+
+def topology(dist, device, world_size: int):
+    """(ranks the collective backend counted, every rank's device PCI address, all distinct?).  The
+    count is an all_reduce of ones on the job's default group (RCCL on GPUs): proof of how many
+    ranks the measured collectives really spanned."""
+    import torch
+    me = device_id(device)
+    if dist is None:
+        return 1, [me], me != "cpu"
+    one = torch.ones(1, dtype=torch.int32, device=device)
+    dist.all_reduce(one)
+    ids = [None] * world_size
+    dist.all_gather_object(ids, me)
+    return int(one.item()), ids, len(set(ids)) == world_size and "cpu" not in ids
 
 
 def rank_main(a) -> None:
@@ -368,6 +412,11 @@ def rank_main(a) -> None:
         else:
             from zest_amd.parallel import nccl_options
             dist.init_process_group("nccl", device_id=device, pg_options=nccl_options(), timeout=timeout)
+    rccl_ranks, devices, distinct = topology(dist, device, world_size)
+    log(rank, f"collective ranks {rccl_ranks} ({backend if dist is not None else 'none'}), devices {devices}")
+    if backend == "nccl" and dist is not None and (not distinct or rccl_ranks != world_size):
+        # an RCCL number only counts when every rank drove its own GPU
+        raise SystemExit(f"refusing an nccl run over {devices} ({rccl_ranks} ranks counted by the collective)")
     spec = models.get(a.model)
     results, pick, arenas = [], None, {}
     for mode in a.modes:
@@ -408,7 +457,9 @@ def rank_main(a) -> None:
                    "verify": "blake3 of every chunk on every rank + merkle file hashes",
                    "numa_bound_cpus": len(numa_cpus), "hip_graph": head["hip_graph"],
                    "pipeline": head["pipeline"], "device": a.device,
-                   "backend": backend if world_size > 1 else "none"},
+                   "backend": backend if world_size > 1 else "none",
+                   "rccl_ranks": rccl_ranks, "devices": devices, "distinct_devices": distinct,
+                   "phase_s": head["phase_s"], "exchange_rx_GBps": head["exchange_rx_GBps"]},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -41,9 +41,15 @@ def test_bench_prints_one_json_line(gpus):
     # both data modes measured; the first (bf16) is the headline
     assert out["config"]["modes"] == ["bf16", "random"]
     assert out["extra"]["bf16_GBps"] == out["value"] and out["extra"]["random_GBps"] > 0
+    # self-validation: ranks the collective counted, the devices behind them, per-phase seconds
+    cfg = out["config"]
+    assert cfg["rccl_ranks"] == gpus and cfg["devices"] == ["cpu"] * gpus and cfg["distinct_devices"] is False
+    assert set(cfg["phase_s"]) >= {"world_s", "origin_s", "setup_s", "autotune_s", "warmup_s", "timed_s"}
+    assert len(cfg["exchange_rx_GBps"]) == gpus
     if gpus > 1:
         assert out["config"]["backend"] == "gloo" and 0 < out["p2p_ratio"] < 1
         assert "launching 2 ranks" in p.stderr
+        assert sum(cfg["exchange_rx_GBps"]) > 0
 
 
 def test_bench_one_seeder_one_leecher():

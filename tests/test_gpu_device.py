@@ -326,8 +326,11 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend, ex
             assert mode in ("bcast", "allgather") and not any(r[2]["peer_mapped"] for r in res), res
         elif exchange != "auto":
             assert mode == exchange
-        if fault == "gather":
-            assert all(r[2]["repaired_files"] >= 1 for r in res), [r[2] for r in res]
+        if fault == "gather":  # the corrupted receive failed the file hashes: repaired over a broadcast
+            assert all(r[2]["repaired_files"] >= 1 and r[2]["repair_exchange"] == "bcast" for r in res), \
+                [r[2] for r in res]
+        else:
+            assert all(r[2]["repaired_files"] == 0 for r in res)
         print(f"[swarm_pull {world_size}x{backend} {exchange}{'/' + fault if fault else ''}] mode {mode} "
               f"autotune {res[0][2]['exchange_autotune_s']} phases {res[0][2]['phases']}")
     finally:

@@ -892,6 +892,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         if sw.cuda:
             torch.cuda.synchronize(sw.device)
         sw._mark("pull_s", t_pull)
+        round_mode = sw.xchg.mode
         bad = sw.verify_files()
         for _ in range(2):
             if not bad:
@@ -915,7 +916,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 received_bytes=total - sw.fetched_bytes, total_bytes=total,
                 p2p_ratio=(total - sw.fetched_bytes) / total if total else 0.0,
                 rounds=sw.round_no, planned_rounds=sw.n_rounds_planned, items=len(sw.items),
-                exchange=sw.xchg.mode, exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
+                exchange=round_mode, repair_exchange=sw.xchg.mode if sw.stats["repaired_files"] else None,
+                exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
                 peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
                 GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
                 fetch_stats=sw.fetcher.stats(), **sw.stats)

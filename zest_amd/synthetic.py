@@ -113,43 +113,69 @@ class SyntheticWorld:
             data = arena[f.arena_off + len(f.header):f.arena_off + f.size]
             ops.fill_synthetic(data, f.data_seed, 0, MODES[self.mode])
 
-    def build_on_device(self, arena: torch.Tensor, hash_batch: int = 1 << 20) -> None:
-        """CDC + chunk hashes + file hashes + xorb/term plan, from content already in `arena`."""
-        offs, lens, fidx = [], [], []
-        for i, f in enumerate(self.xet_files):
-            region = arena[f.arena_off:f.arena_off + f.size]
-            cand = ops.cdc_candidates(region)
-            ends = ops.select_chunks(cand, f.size)
-            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
-            offs.append(starts + np.uint64(f.arena_off))
-            lens.append((ends - starts).astype(np.uint32))
-            fidx.append(np.full(len(ends), i, dtype=np.int32))
-        self._set_chunks(np.concatenate(offs), np.concatenate(lens), np.concatenate(fidx))
-        dev = arena.device
-        hashes = torch.empty((self.n_chunks, 32), dtype=torch.uint8, device=dev)
-        for a in range(0, self.n_chunks, hash_batch):
-            b = min(self.n_chunks, a + hash_batch)
-            hashes[a:b] = ops.hash_ranges(arena, self.chunk_off[a:b], self.chunk_len[a:b])
-        sizes = torch.from_numpy(self.chunk_len.astype(np.int64)).to(dev)
-        fh = ops.merkle_roots(hashes, sizes, self.merkle_jobs(), file_hash=True)
-        self.chunk_hashes = hashes.cpu().numpy()
-        self.file_hashes = fh.cpu().numpy()
+    def build_on_device(self, arena: torch.Tensor, hash_batch: int = 1 << 20, shard=None) -> None:
+        """CDC + chunk hashes + file hashes (+ BG4-LZ4 stored sizes) + xorb/term plan, from content
+        already in `arena`.
+
+        shard = (rank, n_ranks, group): each rank chunks, hashes and compresses only the files it
+        owns (byte-balanced LPT over the file sizes), then the per-file results (~49 B per chunk:
+        offsets, sizes, hashes, stored sizes) are all-gathered, so every rank ends with the same plan
+        at ~1/n of the GPU work (bench.py at N > 1; the content itself is regenerated on every rank,
+        which is cheap)."""
+        nf = len(self.xet_files)
+        if shard is None:
+            own = list(range(nf))
+        else:
+            from .parallel.swarm_load import assign_owners
+            rank, n_ranks, group = shard
+            owner = assign_owners([f.size for f in self.xet_files], n_ranks)
+            own = [i for i in range(nf) if owner[i] == rank]
+        per_file = {i: self._build_file(arena, i, hash_batch) for i in own}
+        if shard is not None and shard[1] > 1:
+            import torch.distributed as dist
+            objs = [None] * shard[1]
+            dist.all_gather_object(objs, per_file, group=shard[2])
+            for o in objs:
+                per_file.update(o)
+        parts = [per_file[i] for i in range(nf)]
+        self._set_chunks(np.concatenate([p["offs"] for p in parts]), np.concatenate([p["lens"] for p in parts]),
+                         np.concatenate([np.full(len(p["lens"]), i, dtype=np.int32) for i, p in enumerate(parts)]))
+        self.chunk_hashes = np.concatenate([p["hashes"] for p in parts])
+        self.file_hashes = np.stack([p["file_hash"] for p in parts])
         if self.compression == "bg4":
-            self._compress_sizes(arena)
+            self.chunk_clen = np.concatenate([p["clen"] for p in parts])
+            self.chunk_scheme = np.concatenate([p["scheme"] for p in parts])
         self._plan_xorbs()
 
-    def _compress_sizes(self, arena: torch.Tensor, batch: int = 8192) -> None:
-        """Stored size and scheme of every chunk under BG4-LZ4 (GPU compression, frames discarded:
-        the origin build compresses its own share again)."""
-        clen = self.chunk_len.astype(np.uint32).copy()
-        scheme = np.zeros(self.n_chunks, dtype=np.uint8)
-        for a in range(0, self.n_chunks, batch):
-            b = min(self.n_chunks, a + batch)
-            _, flen = ops.compress_chunks(arena, self.chunk_off[a:b], self.chunk_len[a:b], bg4=True)
-            keep = flen > 0
-            clen[a:b][keep] = flen[keep]
-            scheme[a:b][keep] = 2
-        self.chunk_clen, self.chunk_scheme = clen, scheme
+    def _build_file(self, arena: torch.Tensor, i: int, hash_batch: int) -> dict:
+        """One Xet file on the GPU: CDC boundaries (K5), chunk hashes (K1), file hash (K2) and, for
+        compressed worlds, every chunk's BG4-LZ4 stored size and scheme (frames discarded: the
+        origin build compresses its own share again)."""
+        f = self.xet_files[i]
+        region = arena[f.arena_off:f.arena_off + f.size]
+        ends = ops.select_chunks(ops.cdc_candidates(region), f.size)
+        starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+        offs = starts + np.uint64(f.arena_off)
+        lens = (ends - starts).astype(np.uint32)
+        dev = arena.device
+        hashes = torch.empty((len(lens), 32), dtype=torch.uint8, device=dev)
+        for a in range(0, len(lens), hash_batch):
+            b = min(len(lens), a + hash_batch)
+            hashes[a:b] = ops.hash_ranges(arena, offs[a:b], lens[a:b])
+        sizes = torch.from_numpy(lens.astype(np.int64)).to(dev)
+        fh = ops.merkle_roots(hashes, sizes, [(0, len(lens))], file_hash=True)
+        out = {"offs": offs, "lens": lens, "hashes": hashes.cpu().numpy(), "file_hash": fh[0].cpu().numpy()}
+        if self.compression == "bg4":
+            clen = lens.astype(np.uint32).copy()
+            scheme = np.zeros(len(lens), dtype=np.uint8)
+            for a in range(0, len(lens), 8192):
+                b = min(len(lens), a + 8192)
+                _, flen = ops.compress_chunks(arena, offs[a:b], lens[a:b], bg4=True)
+                keep = flen > 0
+                clen[a:b][keep] = flen[keep]
+                scheme[a:b][keep] = 2
+            out["clen"], out["scheme"] = clen, scheme
+        return out
 
     def pack_serialized(self, arena: torch.Tensor, a: int, b: int, out: torch.Tensor, out_off: np.ndarray) -> None:
         """Serialize chunks [a, b) ([8-byte header | stored payload], what the CAS serves) into `out`
