@@ -107,12 +107,20 @@ struct RangeSrc {  // raw (offset, len) messages (k_hash_ranges semantics: > 128
 // LZ4 kernel before this launch and are hashed from there.  The arena is written once and never
 // read back, where place-then-hash read it again (round 2: k_place_raw 28 % + k_hash_leaves 22 % of
 // the pull's kernel time, profiles/bench70b_n1_kernels_r2c.md).
+//
+// A raw chunk's hash therefore covers the staging bytes the same wave just stored into the arena
+// (the copy is exercised against the source bytes, misaligned both sides, by
+// tests/test_gpu_kernels.py::test_fused_ingest_places_exact_bytes), and receivers of the swarm
+// exchange re-hash what landed in their own arena.  A descriptor that fails its bounds check is not
+// placed, hashes as empty (so its file's Merkle check fails) and is reported in the error word as
+// ZG_ERR_RANGE at its chunk index, like the unfused k_place_raw did.
 struct PlaceSrc {
   const ZgChunk* chunks;
   const uint8_t* src;
   uint64_t src_n;
   uint8_t* dst;
   uint64_t dst_n;
+  unsigned long long* err;
   static constexpr bool kBadIsFF = false;
   static constexpr bool kPlace = true;
   __device__ __forceinline__ bool raw_ok(const ZgChunk& ch) const {
@@ -120,15 +128,19 @@ struct PlaceSrc {
   }
   __device__ __forceinline__ void get(int c, const uint8_t*& p, uint32_t& len, bool& bad) const {
     const ZgChunk ch = chunks[c];
-    bad = false;
     len = ch.ulen;
     if (ch.scheme == 0) {
-      if (!raw_ok(ch)) len = 0;
+      bad = !raw_ok(ch);
+      if (bad) len = 0;
       p = src + (len ? ch.src : 0);
     } else {
-      if (ch.dst + len > dst_n || len > kMaxChunk) len = 0;
+      bad = ch.dst + len > dst_n || len > kMaxChunk;
+      if (bad) len = 0;
       p = dst + (len ? ch.dst : 0);
     }
+  }
+  __device__ __forceinline__ void report(int c) const {
+    if (err) atomicCAS(err, 0ull, (static_cast<unsigned long long>(ZG_ERR_RANGE) << 32) | uint32_t(c));
   }
 };
 
@@ -276,6 +288,9 @@ __global__ void __launch_bounds__(256) k_hash_leaves(Src s, int n, int key_mode,
     s.get(c, p, len, bad);
     const uint32_t seg = len > (b << 10) ? min(len - (b << 10), 1024u) : 0u;
     uint32_t cv[8];
+    if constexpr (Src::kPlace) {
+      if (bad && b == 0) s.report(c);  // one report per bad descriptor (its first leaf's lane)
+    }
     zg::hash_leaf(p + (uint64_t(b) << 10), seg, b, key, mode, nb == 1, cv);
     if (nb == 1) {
       if (Src::kBadIsFF && bad) {
@@ -399,9 +414,9 @@ hipError_t zg_hash_chunks_flat(const uint8_t* dst, uint64_t dst_n, const ZgChunk
 }
 
 hipError_t zg_place_hash_flat(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
-                              int n_chunks, uint8_t* hashes, uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes,
-                              hipStream_t stream) {
-  return launch_flat(PlaceSrc{chunks, src, src_n, dst, dst_n}, n_chunks, 0, hashes, sizes, scratch, scratch_bytes,
+                              int n_chunks, unsigned long long* err, uint8_t* hashes, uint64_t* sizes, uint8_t* scratch,
+                              size_t scratch_bytes, hipStream_t stream) {
+  return launch_flat(PlaceSrc{chunks, src, src_n, dst, dst_n, err}, n_chunks, 0, hashes, sizes, scratch, scratch_bytes,
                      stream);
 }
 

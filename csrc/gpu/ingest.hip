@@ -707,7 +707,7 @@ hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, ui
     const hipError_t e = zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
     if (e != hipSuccess) return e;
   }
-  return zg_place_hash_flat(src, src_n, dst, dst_n, chunks, n_chunks, hashes + 32 * uint64_t(hash_index_base),
+  return zg_place_hash_flat(src, src_n, dst, dst_n, chunks, n_chunks, err, hashes + 32 * uint64_t(hash_index_base),
                             sizes ? sizes + hash_index_base : nullptr, scratch, scratch_bytes, stream);
 }
 

@@ -218,6 +218,51 @@ def test_ingest_matches_cpu(policy, fused):
     assert hashes.cpu().numpy().tobytes() == want
 
 
+def test_fused_ingest_places_exact_bytes():
+    """The fused place+hash pass (zg_ingest_chunks, raw chunks copied by the hashing waves) at
+    misaligned src/dst offsets: every in-bounds raw chunk lands byte-exact and hashes like the host
+    oracle of its arena bytes; a descriptor past the arena is not placed, hashes as empty and is
+    reported as ZG_ERR_RANGE at its index (the fused path used to drop it silently)."""
+    rng = np.random.default_rng(31)
+    sizes = [40_001, 65_536, 8_191, 131_072, 77_777, 1]
+    data = [rng.bytes(n) for n in sizes]
+    src_host = bytearray(3)
+    rec = np.zeros(len(sizes), dtype=ops.CHUNK_DTYPE)
+    dpos = 5
+    for i, d in enumerate(data):
+        src_host += b"\0" * 8  # the chunk header slot (payload follows it)
+        rec[i] = (len(src_host), dpos, len(d), len(d), 0, 0)
+        src_host += d + b"\x11" * (i % 3)
+        dpos += len(d) + 7
+    dst_n = dpos
+    bad = 3
+    rec[bad]["dst"] = dst_n - 3  # in the last gap, running past the arena end
+    src = ops.padded_empty(len(src_host), DEV)
+    src.copy_(torch.frombuffer(src_host, dtype=torch.uint8))
+    dst = ops.padded_empty(dst_n, DEV)
+    dst.fill_(0xCD)
+    chunks = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
+    hashes = torch.zeros((len(sizes), 32), dtype=torch.uint8, device=DEV)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    H = ops.hip()
+    scr = ops.HashScratch(DEV)
+    sp, sb = scr.get(len(sizes), sum(sizes))
+    H.ingest_chunks(src.data_ptr(), src.numel(), dst.data_ptr(), dst_n, chunks.data_ptr(), len(sizes), False,
+                    err.data_ptr(), hashes.data_ptr(), 0, 0, torch.cuda.current_stream().cuda_stream, sp, sb)
+    torch.cuda.synchronize()
+    assert int(err.item()) == (2 << 32) | bad, hex(int(err.item()))
+    out = dst.cpu().numpy().tobytes()
+    got = hashes.cpu().numpy()
+    for i, d in enumerate(data):
+        o = int(rec[i]["dst"])
+        if i == bad:
+            assert out[o:dst_n] == b"\xcd" * (dst_n - o)  # not placed
+            assert got[i].tobytes() == C.chunk_hash(b"")
+            continue
+        assert out[o:o + len(d)] == d, i
+        assert got[i].tobytes() == C.chunk_hash(out[o:o + len(d)]), i
+
+
 def _decode_both(body, chunks_data, n):
     """Index one run, then decode it with the one-kernel batched decoder and with the two-kernel
     records decoder; returns (output, error word) per decoder."""
