@@ -254,8 +254,28 @@ std::shared_ptr<Mapping> map_file(const std::string& path) {
 }
 }  // namespace
 
-// A quarantine file `{run}.p{pid}-{seq}.unverified` is stale when its writer is gone (no process
-// with that pid) or it is older than `max_age_s` (pid reuse; a pull never holds a run that long).
+// Identity of this process's pid namespace on this boot: a pid is only meaningful to kill() inside
+// the namespace it came from.  Hash of the kernel boot id and the pid-namespace inode, 12 hex digits.
+const std::string& pid_namespace_token() {
+  static const std::string tok = [] {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    auto mix = [&](const std::string& s) {
+      for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    };
+    if (auto b = read_file("/proc/sys/kernel/random/boot_id")) mix(std::string(b->begin(), b->end()));
+    struct stat st;
+    if (::stat("/proc/self/ns/pid", &st) == 0) mix(std::to_string(uint64_t(st.st_ino)) + ":" + std::to_string(st.st_dev));
+    char buf[17];
+    std::snprintf(buf, sizeof buf, "%012llx", static_cast<unsigned long long>(h & 0xFFFFFFFFFFFFull));
+    return std::string(buf);
+  }();
+  return tok;
+}
+
+// A quarantine file `{run}.p{pid}-{seq}-n{ns}.unverified` is stale when it is older than `max_age_s`
+// (a pull never holds a run that long), or when its writer ran in this pid namespace and is gone (no
+// process with that pid).  A writer in another namespace -- another container sharing the cache --
+// is invisible to kill(), so only the age limit applies to its files.
 bool stale_pending(const std::string& path, int64_t max_age_s) {
   const std::string suffix = XorbCache::kPendingSuffix;
   if (path.size() < suffix.size() || path.compare(path.size() - suffix.size(), suffix.size(), suffix) != 0)
@@ -265,6 +285,11 @@ bool stale_pending(const std::string& path, int64_t max_age_s) {
   if (max_age_s >= 0 && ::time(nullptr) - st.st_mtim.tv_sec > max_age_s) return true;
   const size_t p = path.rfind(".p");
   if (p == std::string::npos) return true;  // pre-round-3 name without a pid: nobody owns it
+  const size_t ns = path.rfind("-n");
+  if (ns != std::string::npos && ns > p) {
+    const std::string tok = path.substr(ns + 2, path.size() - suffix.size() - (ns + 2));
+    if (tok != pid_namespace_token()) return false;  // another namespace: age limit only
+  }
   const long pid = std::strtol(path.c_str() + p + 2, nullptr, 10);
   if (pid <= 0) return true;
   return ::kill(pid_t(pid), 0) != 0 && errno == ESRCH;
@@ -329,7 +354,7 @@ std::string XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset
   // promote() publishes exactly the bytes that belonged to the file that verified.
   static std::atomic<uint64_t> seq{0};
   const std::string path = run_path(hex, chunk_offset) + ".p" + std::to_string(::getpid()) + "-" +
-                           std::to_string(seq.fetch_add(1)) + kPendingSuffix;
+                           std::to_string(seq.fetch_add(1)) + "-n" + pid_namespace_token() + kPendingSuffix;
   write_file_atomic(path, data, n, /*durable=*/false);
   return path;
 }

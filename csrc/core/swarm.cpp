@@ -164,6 +164,10 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
       auto sc = score_.find(key);
       if (sc != score_.end() && sc->second >= 3) continue;  // banned / repeatedly failing
       const PeerLoad& l = load_[key];
+      // a discovered peer that answered NOT_FOUND far more often than it served holds little of
+      // this repo: skip it (direct peers, named by the user, are always tried)
+      if (l.misses >= 8 && l.misses > 4 * (l.hits + 1) && std::find(direct_.begin(), direct_.end(), a) == direct_.end())
+        continue;
       const std::pair<int, int> k{l.misses > l.hits + 2 ? 1 : 0, l.inflight};
       if (!best || k < best_key) {
         best = (rot + j) % n;
@@ -183,6 +187,27 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
       bool hit = false, miss = false;
       uint64_t got = 0;
       std::optional<bt::ChunkResult> out;
+      // the request counted by pick() is released on every path, exceptions of any type included
+      struct Release {
+        SwarmDownloader* self;
+        const std::string& key;
+        bool& hit;
+        bool& miss;
+        uint64_t& got;
+        const net::Addr& a;
+        ~Release() {
+          std::lock_guard<std::mutex> g(self->mu_);
+          PeerLoad& l = self->load_[key];
+          l.inflight--;
+          l.bytes += got;
+          l.hits += hit;
+          l.misses += miss;
+          if (hit) {
+            if (self->served_by_.insert(key).second) self->stats_.peers_connected++;
+            self->remember(a);
+          }
+        }
+      } release{this, key, hit, miss, got, a};
       try {
         auto s = pool_->get_or_connect(a, ih);
         if (s->supports_xet()) {
@@ -217,18 +242,12 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
           std::lock_guard<std::mutex> g(mu_);
           score_[key]++;
         }
-      }
-      {
+      } catch (const std::exception& e) {  // system_error / bad_alloc from connect or request
+        stats_.peer_failures++;
+        ZTRACE("swarm", "peer " << key << " failed " << xet::to_hex(hash) << ": " << e.what());
+        pool_->remove(a);
         std::lock_guard<std::mutex> g(mu_);
-        PeerLoad& l = load_[key];
-        l.inflight--;
-        l.bytes += got;
-        l.hits += hit;
-        l.misses += miss;
-        if (hit) {
-          if (served_by_.insert(key).second) stats_.peers_connected++;
-          remember(a);
-        }
+        score_[key]++;
       }
       if (out) return out;
     }

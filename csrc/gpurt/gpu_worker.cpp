@@ -434,6 +434,17 @@ int run(int argc, char** argv) {
         if (out[k].repaired && file_err[k].empty()) wb->post(k, 0, out[k].size);  // the repair pass replaced its bytes
       wb->drain();
       wb->stop();
+      // Durable before visible: the verified marker trusts size + mtime only, so a renamed file whose
+      // pages never reached the disk (crash, power loss) must not carry one.  Like the host path
+      // (downloader.cpp) the data is synced before the rename; the group's files sync concurrently.
+      {
+        std::vector<std::thread> syncs;
+        for (size_t k = 0; k < out.size(); ++k)
+          if (file_err[k].empty() && out[k].err.empty()) syncs.emplace_back([&out, k] {
+              if (::fdatasync(out[k].fd) != 0) out[k].err = std::string("fdatasync: ") + std::strerror(errno);
+            });
+        for (auto& t : syncs) t.join();
+      }
       t_last_write = now_s();
       for (size_t k = 0; k < out.size(); ++k) {
         WriteBack::File& f = out[k];

@@ -2,6 +2,8 @@
 // Built by `python tools/build.py --only tests` (and `--asan` for an ASan/UBSan build) or CMake
 // (`ctest`), run by tests/test_cpp_core.py.  Vectors are independent of the reference's Zig tests
 // (port the assertions, not the code).
+#include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -350,6 +352,19 @@ TEST(xorb_cache_quarantine_per_fetch) {
   CHECK(cache.sweep_pending(3600) == 1);
   CHECK(storage::exists(live) && !storage::exists(dead));
   CHECK(storage::stale_pending(live, -1) == false && storage::stale_pending(live, 0) == false);
+  // a dead pid of THIS pid namespace is stale; the same dead pid written from another namespace
+  // (another container sharing the cache: invisible to kill) only ages out
+  const std::string ns = live.substr(live.rfind("-n") + 2, 12);
+  const std::string dead_here = live.substr(0, live.rfind(".p")) + ".p999999999-1-n" + ns + ".unverified";
+  const std::string foreign = live.substr(0, live.rfind(".p")) + ".p999999999-2-nforeign00000.unverified";
+  storage::write_file_atomic(dead_here, good.data(), good.size(), false);
+  storage::write_file_atomic(foreign, good.data(), good.size(), false);
+  CHECK(storage::stale_pending(dead_here, 3600) && !storage::stale_pending(foreign, 3600));
+  struct timespec old_t[2] = {{0, 0}, {::time(nullptr) - 7200, 0}};
+  old_t[0] = old_t[1];
+  CHECK(::utimensat(AT_FDCWD, foreign.c_str(), old_t, 0) == 0);
+  CHECK(storage::stale_pending(foreign, 3600));
+  CHECK(cache.sweep_pending(3600) == 2 && storage::exists(live));
 }
 
 TEST(peer_pool_leases) {
