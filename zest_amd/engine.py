@@ -52,6 +52,8 @@ class RoundWork:
     terms_host: np.ndarray | None = None   # the same records on the host (host header walk)
     table_off: int = 0                     # byte offset of the round's chunk records in a host table
     compressed: bool = True                # any chunk of the round stored LZ4/BG4 (decoder launch needed)
+    rec_rel: int = 0                       # ride-along records: their offset from the span start (0 = none)
+    copy_len: int = 0                      # bytes of the round's H2D copy (span [+ gap + records])
 
 
 # Pinned allocations kept for reuse by the next OriginStore of this process (capacity, pointer).
@@ -203,22 +205,45 @@ class DevicePuller:
         # rounds[k][r] = (a, b) term range for rank r in round k
         per_rank = [split_rounds(world, a, b, self.round_weights) for a, b in self.rank_terms]
         self.rounds_all = [[per_rank[r][k] for r in range(n_ranks)] for k in range(self.n_rounds)]
-        # this rank's origin layout: its terms' serialized bytes back to back, in order
+        # Pipeline shape (see the streams below): "copy" when any chunk is stored compressed.
+        compressed = bool(world.chunk_clen is not None and np.any(world.chunk_clen < world.chunk_len))
+        pipeline = os.environ.get("ZEST_PIPELINE", "copy" if compressed else "lanes")
+        # Ride-along chunk records (copy pipeline): the host walks each round's chunk headers in the
+        # pinned origin right before the round's H2D copy is issued and writes the ZgChunk records
+        # just behind the round's bytes, so ONE copy brings bytes and records and the lane launches
+        # decode + place/hash directly -- no device header walk (k_index_terms: a one-thread-per-term
+        # HBM pointer chase, ~1 ms in front of every 1 GiB round's decode) and no separate record
+        # upload between the large transfers.  This is what the device-direct pull does with the
+        # records its fetch workers build (csrc/gpurt/device_pull.cpp).  ZEST_RIDE_RECORDS=0: device walk.
+        self.ride_records = (self.is_cuda and pipeline == "copy" and os.environ.get("ZEST_RIDE_RECORDS", "1") != "0")
+        # this rank's origin layout: its terms' serialized bytes back to back, in order (with ride-along
+        # records: round by round, each round's span followed by its record area)
         a_r, b_r = self.rank_terms[rank]
         ser_len = T["ser_len"][a_r:b_r].astype(np.int64)
         self.term_origin_off = np.concatenate([[0], np.cumsum(ser_len)]).astype(np.int64)  # relative to a_r
-        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device, origin_reserve)
+        round_base, pos = [], 0
+        for k in range(self.n_rounds):
+            a, b = self.rounds_all[k][rank]
+            span_len = int(self.term_origin_off[b - a_r] - self.term_origin_off[a - a_r])
+            if self.ride_records:
+                nck = int(T["c1"][b - 1] - T["c0"][a]) if b > a else 0
+                round_base.append(pos)
+                pos += -(-(-(-span_len // 256) * 256 + nck * ops.CHUNK_DTYPE.itemsize) // 4096) * 4096
+            else:
+                round_base.append(int(self.term_origin_off[a - a_r]))
+        origin_bytes = pos if self.ride_records else int(self.term_origin_off[-1])
+        self.origin = OriginStore(origin_bytes, self.device, origin_reserve)
         self.rounds: list[RoundWork] = []
         max_span, max_terms, max_chunks = 0, 1, 1
         for k in range(self.n_rounds):
             a, b = self.rounds_all[k][rank]
-            span_off = int(self.term_origin_off[a - a_r])
+            span_off = round_base[k]
             span_len = int(self.term_origin_off[b - a_r] - self.term_origin_off[a - a_r])
             if b > a:
                 c0 = int(T["c0"][a])
                 nck = int(T["c1"][b - 1] - c0)
                 rec = np.zeros(b - a, dtype=ops.TERM_DTYPE)
-                rec["src"] = self.term_origin_off[a - a_r:b - a_r] - span_off
+                rec["src"] = self.term_origin_off[a - a_r:b - a_r] - self.term_origin_off[a - a_r]
                 rec["src_len"] = T["ser_len"][a:b]
                 rec["dst"] = T["dst"][a:b]
                 rec["chunk_base"] = T["c0"][a:b] - c0
@@ -229,9 +254,12 @@ class DevicePuller:
             else:
                 c0, nck, rec, region, terms_dev = 0, 0, None, (0, 0), None
             comp = bool(world.chunk_scheme is not None and b > a and world.chunk_scheme[c0:c0 + nck].any())
+            rec_rel = -(-span_len // 256) * 256 if self.ride_records and b > a else 0
+            copy_len = rec_rel + nck * ops.CHUNK_DTYPE.itemsize if rec_rel else span_len
             self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev, rec,
-                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize, comp))
-            max_span = max(max_span, span_len)
+                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize, comp,
+                                         rec_rel, copy_len))
+            max_span = max(max_span, copy_len)
             max_terms = max(max_terms, b - a)
             max_chunks = max(max_chunks, nck)
         self.regions = [[self._region(k, r) for r in range(n_ranks)] for k in range(self.n_rounds)]
@@ -280,14 +308,16 @@ class DevicePuller:
             # bf16 round decodes in ~13 ms against ~16 ms of H2D; in "lanes" the two lanes drift
             # into copying together and decoding together, leaving PCIe idle: 54.3 vs 64.3 GB/s).
             # Default: "copy" when any chunk is stored compressed; ZEST_PIPELINE overrides.
-            compressed = bool(np.any(world.chunk_clen < world.chunk_len))
-            self.pipeline = os.environ.get("ZEST_PIPELINE", "copy" if compressed else "lanes")
+            self.pipeline = pipeline
             if self.pipeline not in ("lanes", "copy"):
                 raise ValueError(f"ZEST_PIPELINE={self.pipeline!r}: expected 'lanes' or 'copy'")
             if self.pipeline == "copy":
                 self.copy_stream = copy_stream
                 self.h2d_done = [torch.cuda.Event() for _ in self.staging]
                 self.slot_free = [torch.cuda.Event() for _ in self.staging]
+                # per round: its copy of the previous step has finished reading the origin, so the
+                # host may rewrite the round's ride-along records (None until first recorded)
+                self._rec_copied = [None] * self.n_rounds
         # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
         # and returns, so a caller looping over step() without syncing queues thousands of commands
         # over many steps, and past ~10 steps queued the HIP runtime fed the device measurably slower
@@ -355,29 +385,33 @@ class DevicePuller:
         H = ops.hip()
         st = torch.cuda.current_stream(self.device).cuda_stream
         tmp = ops.padded_empty(min(pack_batch_bytes, self.origin.n) + (64 << 20), self.device)
-        t = a_r
-        while t < b_r:
-            base = int(self.term_origin_off[t - a_r])
-            u = t
-            while u < b_r and self.term_origin_off[u + 1 - a_r] - base <= tmp.numel():
-                u += 1
-            if u == t:
-                raise RuntimeError("term larger than pack batch")
-            c0, c1 = int(T["c0"][t]), int(T["c1"][u - 1])
-            ser = w.chunk_clen[c0:c1].astype(np.uint64) + np.uint64(8)
-            out_off = (np.cumsum(ser) - ser).astype(np.uint64)
-            w.pack_serialized(self.arena, c0, c1, tmp, out_off)
-            n = int(self.term_origin_off[u - a_r] - base)
-            H.memcpy_async(self.origin.ptr + base, tmp.data_ptr(), n, st)
-            torch.cuda.synchronize(self.device)
-            t = u
+        for rw in self.rounds:  # a round's span is contiguous in the origin (records may follow it)
+            t = rw.term_a
+            while t < rw.term_b:
+                base = int(self.term_origin_off[t - a_r])
+                u = t
+                while u < rw.term_b and self.term_origin_off[u + 1 - a_r] - base <= tmp.numel():
+                    u += 1
+                if u == t:
+                    raise RuntimeError("term larger than pack batch")
+                c0, c1 = int(T["c0"][t]), int(T["c1"][u - 1])
+                ser = w.chunk_clen[c0:c1].astype(np.uint64) + np.uint64(8)
+                out_off = (np.cumsum(ser) - ser).astype(np.uint64)
+                w.pack_serialized(self.arena, c0, c1, tmp, out_off)
+                n = int(self.term_origin_off[u - a_r] - base)
+                at = rw.span_off + base - int(self.term_origin_off[rw.term_a - a_r])
+                H.memcpy_async(self.origin.ptr + at, tmp.data_ptr(), n, st)
+                torch.cuda.synchronize(self.device)
+                t = u
 
     def build_origin_host(self, contents: dict[str, bytes]) -> None:
         w = self.world
         T = w.terms
         a_r, b_r = self.rank_terms[self.rank]
+        start = {rw.term_a: rw.span_off for rw in self.rounds if rw.term_b > rw.term_a}
         pos = 0
         for t in range(a_r, b_r):
+            pos = start.get(t, pos)  # each round's span starts at its own origin offset
             f = w.xet_files[int(T["file"][t])]
             data = contents[f.path]
             for c in range(int(T["c0"][t]), int(T["c1"][t])):
@@ -435,30 +469,44 @@ class DevicePuller:
             self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
         return rec_ptr
 
-    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int, chunks=None) -> None:
+    def _ride_records(self, rw: RoundWork, k: int) -> None:
+        """Host header walk of round k's runs in the pinned origin, into the round's record area
+        right behind its bytes (one H2D copy then carries both).  The area is rewritten only after
+        the previous step's copy of this round has read it (its event), so the host runs at most one
+        step ahead of the copy engine, as step()'s run-ahead bound allows anyway."""
+        ev = self._rec_copied[k]
+        if ev is not None:
+            ev.synchronize()
+        e = _core.index_runs(self.origin.ptr + rw.span_off, rw.span_len, rw.terms_host.ctypes.data,
+                             rw.term_b - rw.term_a, self.origin.ptr + rw.span_off + rw.rec_rel, rw.n_chunks)
+        if e:
+            self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
+
+    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int, chunks_ptr: int | None = None) -> None:
         """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes.
-        `chunks`: device chunk records already uploaded for this round (copy pipeline)."""
+        `chunks_ptr`: device address of the round's chunk records already in staging (ride-along)."""
         if rw.term_b <= rw.term_a:
             return
         nbytes = rw.n_chunks * ops.CHUNK_DTYPE.itemsize
-        if chunks is None:
+        if chunks_ptr is None:
             chunks = ws.chunks
+            chunks_ptr = chunks.data_ptr()
             if self.host_index and not self._capturing:
-                H.memcpy_async(chunks.data_ptr(), self._host_records(rw), nbytes, st)
+                H.memcpy_async(chunks_ptr, self._host_records(rw), nbytes, st)
             else:
                 chunks[:nbytes].zero_()
-                H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, chunks.data_ptr(),
+                H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, chunks_ptr,
                               self.err.data_ptr(), st)
         sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
         if ops.FUSED_INGEST:
             # decode (compressed rounds only) + ONE pass that places raw chunks and hashes every chunk
-            H.ingest_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(),
+            H.ingest_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks_ptr,
                             rw.n_chunks, rw.compressed, self.err.data_ptr(), self.hashes.data_ptr() + 32 * rw.c0, 0, 0,
                             st, sp, sb)
             return
-        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(),
+        H.place_chunks(src.data_ptr(), rw.span_len, self.arena.data_ptr(), self.arena.numel(), chunks_ptr,
                        rw.n_chunks, 0, self.arena.numel(), self.err.data_ptr(), st)
-        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), chunks.data_ptr(), rw.n_chunks,
+        H.hash_chunks(self.arena.data_ptr(), self.arena.numel(), chunks_ptr, rw.n_chunks,
                       self.hashes.data_ptr() + 32 * rw.c0, 0, 0, st, sp, sb)
 
     def capture_graph(self) -> bool:
@@ -520,20 +568,27 @@ class DevicePuller:
                 if self._rx:
                     _core.trace.roctx_push(f"engine: round {k}")
                 copy_mode = self.pipeline == "copy" and not self._capturing
+                chunks_ptr = None
                 if copy_mode:
                     slot = k % len(self.staging)
+                    if rw.rec_rel:
+                        self._ride_records(rw, k)
+                        chunks_ptr = src.data_ptr() + rw.rec_rel
                     with torch.cuda.stream(self.copy_stream):
                         self.copy_stream.wait_event(self.slot_free[slot])  # no-op before first use
-                        if rw.span_len:
-                            H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
+                        if rw.copy_len:
+                            H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.copy_len,
                                            self.copy_stream.cuda_stream)
                         self.h2d_done[slot].record(self.copy_stream)
+                        if rw.rec_rel:
+                            ev = self._rec_copied[k] = self._rec_copied[k] or torch.cuda.Event()
+                            ev.record(self.copy_stream)
                 with torch.cuda.stream(comp):
                     if copy_mode:
                         comp.wait_event(self.h2d_done[slot])
                     elif rw.span_len:
                         H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, st)
-                    self._ingest_round(H, rw, src, ws, st)
+                    self._ingest_round(H, rw, src, ws, st, chunks_ptr)
                     if copy_mode:
                         self.slot_free[slot].record(comp)
                     if self.n_ranks > 1:
