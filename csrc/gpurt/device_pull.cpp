@@ -92,16 +92,33 @@ struct DeviceXetPull::Impl {
       trace::Span sp("device", "init: xet auth");
       bridge_->authenticate(repo, repo_type, revision);
     }
+    if (!o.defer_device) init_device();
+  }
+
+  // Device half of the set-up (stream, pinned + device staging): separate from the host half above
+  // so a caller can run the Xet auth / cache scan while the HIP runtime is still coming up
+  // (gpu_worker.cpp).  The two pinned slots are page-locked concurrently.  Idempotent.
+  void init_device() {
+    std::lock_guard<std::mutex> g(init_mu_);
+    if (device_ready_) return;
     trace::Span sp("device", "init: staging alloc");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    std::string errs[2];
+    std::thread pin1([&] {
+      if (!slots_[1].pin.alloc(cap_ + 4096)) errs[1] = "pinning the staging buffer failed";
+    });
+    if (!slots_[0].pin.alloc(cap_ + 4096)) errs[0] = "pinning the staging buffer failed";
+    pin1.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw Error("HipError", e);
     for (auto& s : slots_) {
-      if (!s.pin.alloc(cap_ + 4096)) throw Error("HipError", "pinning the staging buffer failed");
       s.host = s.pin.data();
       s.dev.ensure(cap_);
       hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
     }
     err_.ensure(1);
+    device_ready_ = true;
   }
 
   ~Impl() {
@@ -122,6 +139,7 @@ struct DeviceXetPull::Impl {
   // evicted, then is pulled once more straight from the CDN with the refetched runs replacing the
   // cached ones — so one corrupt copy costs one refetch, not a permanently failing pull.
   std::vector<PullFileStats> pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
+    init_device();
     const auto t0 = std::chrono::steady_clock::now();
     const size_t nf = files.size();
     std::vector<const cas::Reconstruction*> recs(nf);
@@ -205,6 +223,7 @@ struct DeviceXetPull::Impl {
   // match its plan, or any decode error of the call, is refetched once from the CDN.
   std::vector<TermJobResult> pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
                                         bool repair) {
+    init_device();
     std::vector<Seg> segs;
     uint64_t next_chunk = jobs.empty() ? 0 : jobs[0].chunk0;
     for (const TermJob& j : jobs) {
@@ -656,6 +675,8 @@ struct DeviceXetPull::Impl {
   std::unique_ptr<ReconCache> recs_;
   SettleBook book_;
   hipStream_t stream_ = nullptr;
+  std::mutex init_mu_;
+  bool device_ready_ = false;
   Slot slots_[2];
   DevBuf<unsigned long long> err_;
   DevBuf<uint8_t> hashes_;
@@ -689,6 +710,7 @@ std::vector<TermJobResult> DeviceXetPull::pull_terms(const std::vector<TermJob>&
 }
 size_t DeviceXetPull::settle(const std::string& xet_hash, bool ok) { return impl_->settle(xet_hash, ok); }
 std::vector<TermShape> DeviceXetPull::term_shapes(const std::string& xet_hash) { return impl_->term_shapes(xet_hash); }
+void DeviceXetPull::init_device() { impl_->init_device(); }
 std::string DeviceXetPull::stats_json() const { return impl_->stats_json(); }
 size_t DeviceXetPull::staging_bytes() const { return impl_->staging_bytes(); }
 

@@ -31,6 +31,7 @@ struct DevicePullOptions {
   int device = 0;
   size_t staging_bytes = size_t(1) << 30;  // per pinned slot (two slots)
   int threads = 16;                        // fetch workers
+  bool defer_device = false;  // construct the host side only; init_device() (or the first pull) does the rest
 };
 
 struct PullRequest {
@@ -72,6 +73,8 @@ class DeviceXetPull {
   std::vector<TermShape> term_shapes(const std::string& xet_hash);  // (ulen, chunks) per term
   std::string stats_json() const;
   size_t staging_bytes() const;
+  // Device set-up (HIP stream, pinned + device staging) when the options deferred it.  Idempotent.
+  void init_device();
 
  private:
   struct Impl;

@@ -269,12 +269,28 @@ int run(int argc, char** argv) {
   double t_init = 0, t_hip = 0, t_dp = 0;
   std::thread init([&] {
     try {
-      int dev_count = 0;
-      hip_ok(hipGetDeviceCount(&dev_count), "hipGetDeviceCount");
-      if (dev_count < 1) throw Error("NoDevice", "no GPU visible to this worker");
-      hip_ok(hipSetDevice(0), "hipSetDevice");  // the CLI pinned this worker with HIP_VISIBLE_DEVICES
-      hip_ok(hipFree(nullptr), "hipFree");      // runtime + device context up
-      t_hip = now_s();
+      // The HIP runtime + device context (~160 ms on a fresh process) come up on their own thread
+      // while the pipelines' host halves (xorb cache scan, swarm, Xet auth over HTTP) are built;
+      // then every pipeline's pinned staging and the write-back buffers are allocated concurrently.
+      std::string hip_err;
+      std::thread hip_up([&] {
+        try {
+          int dev_count = 0;
+          hip_ok(hipGetDeviceCount(&dev_count), "hipGetDeviceCount");
+          if (dev_count < 1) throw Error("NoDevice", "no GPU visible to this worker");
+          hip_ok(hipSetDevice(0), "hipSetDevice");  // the CLI pinned this worker with HIP_VISIBLE_DEVICES
+          hip_ok(hipFree(nullptr), "hipFree");      // runtime + device context up
+        } catch (const std::exception& e) {
+          hip_err = e.what();
+        }
+        t_hip = now_s();
+      });
+      struct JoinHip {
+        std::thread& t;
+        ~JoinHip() {
+          if (t.joinable()) t.join();
+        }
+      } join_hip{hip_up};
       gpurt::DevicePullOptions o;
       o.repo = a.repo;
       o.revision = a.revision;
@@ -287,6 +303,7 @@ int run(int argc, char** argv) {
       o.device = 0;
       o.staging_bytes = a.staging_mb << 20;
       o.threads = a.threads;
+      o.defer_device = true;
       std::vector<std::string> errs(dps.size());
       std::vector<std::thread> mk;
       for (size_t k = 0; k < dps.size(); ++k)
@@ -300,8 +317,29 @@ int run(int argc, char** argv) {
       for (auto& t : mk) t.join();
       for (auto& e : errs)
         if (!e.empty()) throw Error("DeviceInit", e);
+      hip_up.join();
+      if (!hip_err.empty()) throw Error("DeviceInit", hip_err);
+      mk.clear();
+      for (size_t k = 0; k < dps.size(); ++k)
+        mk.emplace_back([&, k] {
+          try {
+            hip_ok(hipSetDevice(0), "hipSetDevice");
+            dps[k]->init_device();
+          } catch (const std::exception& e) {
+            errs[k] = e.what();
+          }
+        });
+      std::string wb_err;
+      try {
+        wb = std::make_unique<WriteBack>(nwriters, piece);
+      } catch (const std::exception& e) {
+        wb_err = e.what();
+      }
+      for (auto& t : mk) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) throw Error("DeviceInit", e);
+      if (!wb_err.empty()) throw Error("DeviceInit", wb_err);
       t_dp = now_s();
-      wb = std::make_unique<WriteBack>(nwriters, piece);
     } catch (const std::exception& e) {
       init_err = e.what();
     }
