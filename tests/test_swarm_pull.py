@@ -154,10 +154,10 @@ def _api_worker(rank, world_size, port, repo, q, fault):
         from zest_amd.parallel import swarm_pull
         st = {}
         try:
-            if fault:  # the stats of the re-shard are only visible through swarm_pull itself
+            if fault:  # swarm_pull itself (the same call the public API makes)
                 t = swarm_pull(repo, p2p=False, dht=False, stats=st)
             else:
-                t = zest_amd.pull(repo, device="all", p2p=False, dht=False)
+                t = zest_amd.pull(repo, device="all", p2p=False, dht=False, stats=st)
             q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
         except Exception as e:
             q.put((rank, type(e).__name__, str(e), st))
@@ -186,8 +186,9 @@ def test_pull_device_all_is_a_swarm_pull_without_snapshot(hub_env, tmp_path):
     want = _expected(world)
     res = _run_api(3, world.spec.repo_id)
     assert [r[1] for r in res] == ["ok"] * 3, res
-    for _, _, got, _ in res:
+    for _, _, got, st in res:
         assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert st["exchange"] in ("bcast", "allgather", "p2p") and st["world"] == 3  # the mode it used
     snaps = list((tmp_path / "hf").rglob("snapshots/*/*")) if (tmp_path / "hf").exists() else []
     assert not snaps, snaps
 

@@ -56,16 +56,21 @@ def disable() -> None:
 def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = False, verify: bool = True,
          p2p: bool = True, peers=None, tracker=None, dht: bool = True, dht_bootstrap=None, include=None,
          group=None, repo_type: str = "model", verbose: bool = False, direct: bool = False,
-         save_snapshot: bool = False, threads: int = 16, staging_bytes: int = 1 << 30):
+         save_snapshot: bool = False, threads: int = 16, staging_bytes: int = 1 << 30, stats: dict | None = None,
+         exchange: str = "auto", round_bytes: int | None = None):
     """Download `repo@revision` via zest.
 
     * default: returns the HF-cache snapshot directory (reference behaviour).
     * device="cuda:N" (or as_tensors=True): also loads every *.safetensors file into that GPU's HBM,
       verifies each against its Xet file hash on the GPU, and returns {tensor_name: tensor}.
     * device="all": collective over `group` (default WORLD) — every rank gets all tensors on its
-      own GPU (CPU process groups: host memory).  Each Xet file is fetched once, device-direct, by
-      one owner rank and seeded to the others over xGMI (RCCL broadcasts), re-verified on every
-      receiver; no snapshot is written (zest_amd.parallel.swarm_pull).
+      own GPU (CPU process groups: host memory).  The model's reconstruction terms are split into
+      byte-balanced per-rank shares; each rank fetches its share device-direct, round by round,
+      and the rounds are replicated over xGMI with the exchange strategy measured fastest at setup
+      (`exchange`, default "auto"), every received chunk re-hashed on the receiver, every file
+      Merkle-checked on every rank; no snapshot is written (zest_amd.parallel.swarm_pull).
+      `stats` (a dict) receives the exchange mode used, bytes fetched / received, per-phase
+      seconds, re-shards and recovered ranks.
     * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
       cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct);
       `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.  With
@@ -81,7 +86,8 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
 
         return swarm_pull(repo, revision, group=group, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
                           dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify,
-                          staging_bytes=staging_bytes, threads=threads)
+                          staging_bytes=staging_bytes, threads=threads, stats=stats, exchange=exchange,
+                          round_bytes=round_bytes)
     if direct:
         from .direct import pull_to_device
 
