@@ -115,7 +115,7 @@ def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: floa
     dist.all_gather_object(objs, mine, group=group)
     # host-only barrier (gloo): does not wait on this rank's GPU streams like an RCCL barrier
     host_group = dist.new_group(backend="gloo") if group is None else \
-        dist.new_group(ranks=dist.get_process_group_ranks(group), backend="gloo")
+        dist.new_group(ranks=dist.get_process_group_ranks(group), backend="gloo", use_local_synchronization=True)
     peers = [None] * n_ranks
     ok = 1
     if all(o is not None and o[0] == "vmm" for o in objs):

@@ -198,7 +198,9 @@ class _Membership:
         if backend == "gloo":
             self.ctl = group
         else:
-            self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td)
+            # a subgroup's members create it alone (the other ranks of the job are not in this call)
+            self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td,
+                                      use_local_synchronization=group is not None)
         self.epoch = 0
         self.store = None
         self._stop = threading.Event()
