@@ -279,3 +279,18 @@ def test_swarm_pull_survives_a_lost_rank(hub_env):
         assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
         assert st["recovered_ranks"] == 1 and st["world"] == 2
     assert dt < 150, dt
+
+
+def test_swarm_pull_eight_ranks_lose_two(hub_env):
+    """N = 8 rehearsal on gloo: term shares over 8 ranks, then ranks 3 and 6 die in the same round;
+    the six survivors agree on the member list once, re-shard both ranks' ranges and all finish
+    with every tensor verified."""
+    world, hub = hub_env
+    want = _expected(world)
+    res, codes, dt = _run_elastic(8, world.spec.repo_id, "exit:3:1,exit:6:1", 96 << 10, expect_dead=(3, 6))
+    assert codes[3] == 1 and codes[6] == 1, codes
+    assert [r[0] for r in res] == [0, 1, 2, 4, 5, 7] and all(r[1] == "ok" for r in res), res
+    for _, _, got, st in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert st["recovered_ranks"] == 2 and st["world"] == 6
+    assert dt < 170, dt

@@ -21,6 +21,9 @@
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
 #   hostbench   `zest bench --synthetic` on the box's CPU
+#   swarm       term-sharded swarm_pull GPU tests (modes, VMM fault hooks) (tests/test_gpu_device.py -k swarm_pull)
+#   swarmbench  public pull(device="all") end to end from a loopback HBM seeder, $SWARM_RANKS (1,2,3) ranks,
+#               $SWARM_MODEL (llama-3.1-8b) -> swarm_pull.json
 set -o pipefail
 OUT=gpurun_out/${1:?usage: check.sh OUT_DIR step...}
 shift
@@ -71,6 +74,11 @@ for step in "$@"; do
            db=$(find $OUT/kprof -name "*.db" | head -1)
            python tools/rocpd_summary.py "$db" --title "kbench ${KBENCH_ONLY:-all} kernels" > $OUT/kernels_kbench.md 2>&1
            head -24 $OUT/kernels_kbench.md; rm -f "$db" ;;
+    swarm) timeout -k 10 500 $PYT -v -s tests/test_gpu_device.py -k swarm_pull > $log 2>&1 || fail $step $? $log
+           grep -E "PASSED|FAILED|^\[swarm_pull" $log ;;
+    swarmbench) timeout -k 10 700 python -u tools/swarm_bench.py --model ${SWARM_MODEL:-llama-3.1-8b} \
+                  --ranks ${SWARM_RANKS:-1,2,3} ${SWARM_ARGS:-} --out $OUT/swarm_pull.json > $log 2>&1 || fail $step $? $log
+                grep -h "^\[" $log ;;
     hostbench) ./zest_amd/_bin/zest bench --synthetic > $log 2>&1 || fail $step $? $log
                lscpu | grep -E "Model name|^CPU\(s\)" >> $log; cat $log ;;
     *) echo "[check] unknown step $step"; exit 2 ;;

@@ -195,12 +195,14 @@ class _Membership:
         self.stale_s = float(os.environ.get("ZEST_SWARM_HB_STALE", "5"))
         import datetime
         self._td = datetime.timedelta(seconds=self.timeout_s)
+        # A control group of our own with a bounded timeout, even over a gloo job: a collective whose
+        # peer died must fail in bounded time on EVERY survivor (ranks that wait on a live neighbour
+        # that already left the collective would otherwise sit out the job group's 30-minute default).
+        # A subgroup's members create it alone (the other ranks of the job are not in this call).
+        self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td,
+                                  use_local_synchronization=group is not None)
         if backend == "gloo":
-            self.ctl = group
-        else:
-            # a subgroup's members create it alone (the other ranks of the job are not in this call)
-            self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td,
-                                      use_local_synchronization=group is not None)
+            self.data = self.ctl  # CPU (or one-GPU gloo) exchanges: the same bounded timeout
         self.epoch = 0
         self.store = None
         self._stop = threading.Event()
@@ -212,10 +214,13 @@ class _Membership:
         self.prefix = f"zest/swarm/{tok[0]}"
         if self.enabled:
             try:
-                # a store client of our own: the heartbeat thread must not share the default store's
-                # socket with the main thread's group creation
-                self.store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
-                                           timeout=self._td)
+                # store clients of our own, one per thread (a client is not safe to share between
+                # threads): the heartbeat thread's, and the main thread's for the membership votes
+                def client():
+                    return dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                                         timeout=self._td)
+                self.store = client()
+                self._hb_store = client()
                 self._beat()
                 self._hb = threading.Thread(target=self._heartbeat, daemon=True)
                 self._hb.start()
@@ -231,7 +236,7 @@ class _Membership:
         return len(self.granks)
 
     def _beat(self):
-        self.store.set(f"{self.prefix}/hb/{self.me}", repr(time.time()))
+        self._hb_store.set(f"{self.prefix}/hb/{self.me}", repr(time.time()))
 
     def _heartbeat(self):
         while not self._stop.wait(1.0):
