@@ -517,21 +517,29 @@ class _Swarm:
             self.have.update(recv_items)
             return None
         H = ops.hip()
+        # The chunk tables go up first, from pinned memory on the (idle) current stream: a pageable
+        # copy issued on the verify stream would block the host until that stream -- which waits for
+        # this round's exchange -- got there, serializing the next round's fetch behind the exchange.
+        jobs = []
+        if self.verify:
+            up = torch.cuda.current_stream(self.device)
+            for it in recv_items:
+                offs, lens, c0 = self._chunk_layout(it)
+                if not len(lens):
+                    continue
+                od = torch.from_numpy(offs.view(np.int64)).pin_memory().to(self.device, non_blocking=True)
+                ld = torch.from_numpy(lens.view(np.int32)).pin_memory().to(self.device, non_blocking=True)
+                jobs.append((od, ld, lens, c0))
+            self.verify_stream.wait_stream(up)
         with torch.cuda.stream(self.verify_stream):
             for w in works:
                 w.wait()
-            if self.verify:
-                for it in recv_items:
-                    offs, lens, c0 = self._chunk_layout(it)
-                    if not len(lens):
-                        continue
-                    od = torch.from_numpy(offs.view(np.int64)).to(self.device, non_blocking=False)
-                    ld = torch.from_numpy(lens.view(np.int32)).to(self.device, non_blocking=False)
-                    sp, sb = self._hash_scratch.get(len(lens), int(lens.sum(dtype=np.uint64)))
-                    H.hash_ranges(self.arena.data_ptr(), od.data_ptr(), ld.data_ptr(), len(lens),
-                                  self.hashes.data_ptr() + 32 * c0, ops.KEY_DATA, self.verify_stream.cuda_stream, sp, sb)
-                    od.record_stream(self.verify_stream)
-                    ld.record_stream(self.verify_stream)
+            for od, ld, lens, c0 in jobs:
+                sp, sb = self._hash_scratch.get(len(lens), int(lens.sum(dtype=np.uint64)))
+                H.hash_ranges(self.arena.data_ptr(), od.data_ptr(), ld.data_ptr(), len(lens),
+                              self.hashes.data_ptr() + 32 * c0, ops.KEY_DATA, self.verify_stream.cuda_stream, sp, sb)
+                od.record_stream(self.verify_stream)
+                ld.record_stream(self.verify_stream)
             ev = torch.cuda.Event()
             ev.record(self.verify_stream)
         del P
