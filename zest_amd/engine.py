@@ -80,6 +80,9 @@ def _staging_take(nbytes: int, device: torch.device) -> torch.Tensor:
 
 _role_stream = role_stream
 
+# Ride-along chunk records in the copy pipeline (DevicePuller.ride_records); ZEST_RIDE_RECORDS overrides.
+RIDE_RECORDS_DEFAULT = "0"
+
 
 def release_pinned_pool() -> None:
     """Free the pinned buffers kept by closed OriginStores."""
@@ -215,7 +218,7 @@ class DevicePuller:
         # HBM pointer chase, ~1 ms in front of every 1 GiB round's decode) and no separate record
         # upload between the large transfers.  This is what the device-direct pull does with the
         # records its fetch workers build (csrc/gpurt/device_pull.cpp).  ZEST_RIDE_RECORDS=0: device walk.
-        self.ride_records = (self.is_cuda and pipeline == "copy" and os.environ.get("ZEST_RIDE_RECORDS", "1") != "0")
+        self.ride_records = (self.is_cuda and pipeline == "copy" and os.environ.get("ZEST_RIDE_RECORDS", RIDE_RECORDS_DEFAULT) != "0")
         # this rank's origin layout: its terms' serialized bytes back to back, in order (with ride-along
         # records: round by round, each round's span followed by its record area)
         a_r, b_r = self.rank_terms[rank]
