@@ -498,8 +498,8 @@ class DevicePuller:
                 H.memcpy_async(chunks_ptr, self._host_records(rw), nbytes, st)
             else:
                 chunks[:nbytes].zero_()
-                H.index_terms(src.data_ptr(), rw.terms_dev.data_ptr(), rw.term_b - rw.term_a, chunks_ptr,
-                              self.err.data_ptr(), st)
+                ops.index_terms(H, src.data_ptr(), rw.span_len, rw.terms_dev.data_ptr(), rw.term_b - rw.term_a,
+                                chunks_ptr, self.err.data_ptr(), st, None if self._capturing else ws)
         sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
         if ops.FUSED_INGEST:
             # decode (compressed rounds only) + ONE pass that places raw chunks and hashes every chunk
