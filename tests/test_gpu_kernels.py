@@ -290,11 +290,14 @@ def test_index_scan_matches_serial_walk(case):
         run = body[r0:bounds[c1 - 1]]
         terms[t] = (len(src_host), len(run), 11 + uoffs[c0], c0, c1 - c0, uoffs[c1] - uoffs[c0])
         src_host += run + b"\0" * (t + 2)
+    def hdr_at(t, j):  # src offset of chunk j's header (j inside term t)
+        c0 = cuts[t]
+        return int(terms[t]["src"]) + (bounds[j - 1] if j else 0) - (bounds[c0 - 1] if c0 else 0)
+
     if case == "bad_version":
-        src_host[int(terms[1]["src"]) + (bounds[cuts[1] + 2] - bounds[cuts[1]])] = 9  # a header mid-term 1
+        src_host[hdr_at(1, cuts[1] + 2)] = 9  # version byte of a header mid-term 1
     elif case == "bad_length":
-        h = int(terms[2]["src"]) + (bounds[cuts[2] + 1] - bounds[cuts[2]])
-        src_host[h + 1] ^= 0x40  # clen of a chunk in term 2
+        src_host[hdr_at(2, cuts[2] + 1) + 3] ^= 0x40  # clen's top byte of a chunk in term 2
     elif case == "short_run":
         terms[0]["src_len"] -= 100
     elif case == "zeros":
