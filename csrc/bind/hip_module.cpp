@@ -158,8 +158,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("scratch"), py::arg("scratch_bytes"),
      "fused ingest: LZ4/BG4 decode of compressed chunks, then one pass that places raw chunks and hashes all");
   m.def("lz4_decode", [](uintptr_t src, uint64_t src_n, uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n,
-                         uintptr_t err, uintptr_t st, int grid_cap, uintptr_t rec_scratch, size_t rec_scratch_bytes) {
-    if (rec_scratch)
+                         uintptr_t err, uintptr_t st, int grid_cap, uintptr_t rec_scratch, size_t rec_scratch_bytes,
+                         bool pair) {
+    if (pair)
+      check(zg_lz4_pair_decode(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n,
+                               P<unsigned long long>(err), grid_cap, S(st)),
+            "zg_lz4_pair_decode");
+    else if (rec_scratch)
       check(zg_lz4_decode_records(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n,
                                   P<unsigned long long>(err), P<uint8_t>(rec_scratch), rec_scratch_bytes, S(st)),
             "zg_lz4_decode_records");
@@ -169,9 +174,10 @@ PYBIND11_MODULE(_hip, m) {
             "zg_lz4_batched_decode");
   }, py::arg("src"), py::arg("src_n"), py::arg("dst"), py::arg("dst_n"), py::arg("chunks"), py::arg("n"),
      py::arg("err"), py::arg("stream"), py::arg("grid_cap") = 0, py::arg("rec_scratch") = 0,
-     py::arg("rec_scratch_bytes") = 0,
-     "K3 alone on the compressed chunks of `chunks` (raw ones are skipped): the two-kernel records decoder "
-     "with rec_scratch (>= lz4_rec_scratch_bytes), else the one-kernel batched decoder");
+     py::arg("rec_scratch_bytes") = 0, py::arg("pair") = false,
+     "K3 alone on the compressed chunks of `chunks` (raw ones are skipped): `pair` = producer/consumer wave "
+     "pairs (grid_cap in pairs), else the two-kernel records decoder with rec_scratch (>= "
+     "lz4_rec_scratch_bytes), else the one-kernel batched decoder");
   m.def("lz4_rec_scratch_bytes", [](int n, uint64_t src_n) { return zg_lz4_rec_scratch_bytes(n, src_n); });
   m.def("hash_ranges", [](uintptr_t buf, uintptr_t offs, uintptr_t lens, int n, uintptr_t out, int key_mode,
                           uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "lz4win.h"
 #include "wave64.h"
@@ -316,8 +317,11 @@ __device__ __forceinline__ uint64_t sload8(const uint32_t* w4, uint32_t p) {
   return v >> (8 * (p & 3));
 }
 
-// Decode one LZ4 frame chunk; returns 0 or an error code.
-__device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
+// Parse one LZ4 frame chunk into batches of records, handing each full batch to `flush` (which
+// executes it here, or passes it to a consumer wave in k_lz4_pair); returns 0 or an error code.
+// The caller checks the decoded size.
+template <class Flush>
+__device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& flush) {
   const uint32_t k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);  // stream pos = k0 + byte index
   const uint32_t* w4 = reinterpret_cast<const uint32_t*>(X.pay - k0);
   const uint32_t end = k0 + X.clen;
@@ -329,7 +333,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
   const uint32_t bck = (flg & 0x10) ? 4 : 0;
   Batch B{0, 0, 0, 0};
   while (true) {
-    if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+    if (B.n > kFlushAbove && !flush(B)) return ZG_ERR_LZ4;
     if (ip > end || end - ip < 4) return ZG_ERR_LZ4;
     const uint32_t bs = uint32_t(sload8(w4, ip));
     ip += 4;
@@ -347,7 +351,7 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
         // v_readfirstlane each) and keep every compare and branch of the parse on the scalar unit
         ip = uni(ip);
         B.n = uni(B.n);
-        if (B.n > kFlushAbove && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+        if (B.n > kFlushAbove && !flush(B)) return ZG_ERR_LZ4;
         if (ip >= bend) return ZG_ERR_LZ4;
         // Fast loop over the common short sequence (literals < 15, match < 19: no length bytes):
         // one 8-byte read at the end of its literals gives the offset and the NEXT token, so the
@@ -432,7 +436,14 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
     }
     ip += bck;
   }
-  if (B.n && !exec_batch(B, X, lane)) return ZG_ERR_LZ4;
+  if (B.n && !flush(B)) return ZG_ERR_LZ4;
+  return 0u;
+}
+
+// Decode one LZ4 frame chunk with this wave alone; returns 0 or an error code.
+__device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
+  const uint32_t code = parse_frame(X, lane, [&](Batch& B) { return exec_batch(B, X, lane); });
+  if (code) return code;
   return X.obase == X.ulen ? 0u : uint32_t(ZG_ERR_SIZE);
 }
 
@@ -478,6 +489,155 @@ __global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__
     X.ring = rings[wave];
     const uint32_t code = decode_chunk(X, lane);
     if (code && lane == 0) report(err, code, uint32_t(c));
+  }
+}
+
+// -----------------------------------------------------------------------------------------------
+// Producer/consumer pairs (k_lz4_pair): two waves per chunk.  The one-wave decoder alternates its
+// scalar parse of 64 sequences with their lane-parallel execution, so a chunk's latency is the SUM of
+// the two halves; a launch with fewer chunks than resident waves (a 256 MiB batch is ~4 k chunks
+// against 8 k wave slots, the tail rounds of a pull fewer still) leaves that latency exposed.  Here
+// wave 0 of a block parses (parse_frame, unchanged) and publishes each full batch into an LDS ring
+// of kPairSlots slots; wave 1 takes the batches in order and runs exec_batch (its own heads / history
+// ring / output position), so parse and execute of a chunk overlap on two SIMDs and the chip holds
+// twice the waves for the same chunk count.  Slot hand-off: a batch number q uses slot q % R; the
+// producer waits until the slot was consumed q / R times, writes the records, then (release) marks
+// it full; the consumer waits for full (acquire), copies the records out, marks it consumed.  Every
+// chunk ends with an end marker carrying the parse status; a consumer whose exec_batch fails sets
+// the chunk's abort mark (the producer stops at its next publish) and drains to the end marker.
+// Every wait is bounded (kPairSpinMax sleeps): a protocol bug cannot hang the GPU -- the block
+// reports ZG_ERR_LZ4 and leaves.
+constexpr uint32_t kPairSlots = 4;
+constexpr uint32_t kPairEnd = 0x80000000u;   // n field of an end marker (| status code)
+constexpr uint32_t kPairSpinMax = 1u << 22;  // ~0.1 s of s_sleep 1
+
+struct PairLds {
+  uint32_t rl[kPairSlots][kWave], rh[kPairSlots][kWave], rx[kPairSlots][kWave];
+  uint32_t n[kPairSlots];
+  uint32_t full[kPairSlots];  // times the producer filled the slot
+  uint32_t done[kPairSlots];  // times the consumer emptied it
+  uint32_t abort;             // chunk index + 1 whose execution failed
+  uint32_t dead;              // a wait ran out: both waves leave
+  uint32_t heads[kWave];
+  __attribute__((aligned(16))) uint8_t ring[kRing];
+};
+
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
+  return uni(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Wait until *p == want; false (and the block marked dead) when the wait runs out.
+__device__ __forceinline__ bool lds_wait(PairLds& L, const uint32_t* p, uint32_t want, uint32_t lane) {
+  for (uint32_t k = 0; lds_acquire(p) != want; ++k) {
+    if (k > kPairSpinMax || lds_acquire(&L.dead)) {
+      lds_release(&L.dead, 1u, lane);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(128) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  const ZgChunk* __restrict__ chunks, int n_chunks,
+                                                  unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
+  __shared__ PairLds L;
+  const uint32_t lane = lane_id();
+  const bool producer = uni(threadIdx.x >> 6) == 0;
+  if (threadIdx.x < kPairSlots) L.full[threadIdx.x] = L.done[threadIdx.x] = 0;
+  if (threadIdx.x == 0) L.abort = L.dead = 0;
+  __syncthreads();
+  uint32_t q = 0;  // batch sequence number, counted identically by both waves
+  for (int c = int(uni(blockIdx.x)); c < n_chunks; c += int(gridDim.x)) {
+    ZgChunk ch = chunks[c];
+    ch.src = uni64(ch.src);
+    ch.dst = uni64(ch.dst);
+    ch.clen = uni(ch.clen);
+    ch.ulen = uni(ch.ulen);
+    ch.scheme = uni(ch.scheme);
+    if (ch.scheme == 0) continue;
+    if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
+      if (!producer && lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
+      continue;
+    }
+    if (ch.ulen > kMaxChunk) {
+      if (!producer && lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      continue;
+    }
+    Ctx X;
+    X.pay = src + ch.src;
+    X.out = dst + ch.dst;
+    X.clen = ch.clen;
+    X.ulen = ch.ulen;
+    X.bg4 = ch.scheme == 2;
+    const uint32_t qq = ch.ulen >> 2, r = ch.ulen & 3;
+    X.g1 = qq + (r > 0 ? 1u : 0u);
+    X.g2 = X.g1 + qq + (r > 1 ? 1u : 0u);
+    X.g3 = X.g2 + qq + (r > 2 ? 1u : 0u);
+    X.k0 = uint32_t(reinterpret_cast<uintptr_t>(X.pay) & 3);
+    X.obase = 0;
+    X.heads = L.heads;
+    X.ring = L.ring;
+    const uint32_t cmark = uint32_t(c) + 1u;
+    if (producer) {
+      bool alive = true;
+      auto publish = [&](uint32_t n, uint32_t rl, uint32_t rh, uint32_t rx) -> bool {
+        const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
+        if (!lds_wait(L, &L.done[slot], uses, lane)) return alive = false;
+        L.rl[slot][lane] = rl;
+        L.rh[slot][lane] = rh;
+        L.rx[slot][lane] = rx;
+        if (lane == 0) L.n[slot] = n;
+        lds_release(&L.full[slot], uses + 1u, lane);
+        ++q;
+        return true;
+      };
+      const uint32_t code = parse_frame(X, lane, [&](Batch& B) {
+        if (lds_acquire(&L.abort) == cmark) return false;  // the consumer failed this chunk: stop
+        const bool ok = publish(B.n, B.rl, B.rh, B.rx);
+        B.n = 0;
+        B.rl = B.rh = B.rx = 0;
+        return ok;
+      });
+      if (!alive || !publish(kPairEnd | code, 0u, 0u, 0u)) return;
+    } else {
+      bool failed = false;
+      while (true) {
+        const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
+        if (!lds_wait(L, &L.full[slot], uses + 1u, lane)) {
+          if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
+          return;
+        }
+        Batch B;
+        B.n = uni(L.n[slot]);
+        B.rl = L.rl[slot][lane];
+        B.rh = L.rh[slot][lane];
+        B.rx = L.rx[slot][lane];
+        lds_release(&L.done[slot], uses + 1u, lane);
+        ++q;
+        if (B.n & kPairEnd) {
+          const uint32_t code = B.n & ~kPairEnd;
+          if (!failed) {
+            if (code) {
+              if (lane == 0) report(err, code, uint32_t(c));
+            } else if (X.obase != X.ulen) {
+              if (lane == 0) report(err, ZG_ERR_SIZE, uint32_t(c));
+            }
+          }
+          break;
+        }
+        if (!failed && !exec_batch(B, X, lane)) {
+          failed = true;
+          if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
+          lds_release(&L.abort, cmark, lane);
+        }
+      }
+    }
   }
 }
 
@@ -698,6 +858,16 @@ extern "C" hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t sr
   return hipGetLastError();
 }
 
+extern "C" hipError_t zg_lz4_pair_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                         const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
+                                         hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  if (grid_cap <= 0 || grid_cap > 8192) grid_cap = 4096;  // 4096 pairs = 8 waves / SIMD
+  hipLaunchKernelGGL(k_lz4_pair, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream, src, dst,
+                     chunks, n_chunks, err, src_n, dst_n);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                             const ZgChunk* chunks, int n_chunks, unsigned long long* err,
                                             hipStream_t stream) {
@@ -706,6 +876,15 @@ extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, 
     const char* v = getenv("ZG_LZ4_GRID");
     return v ? atoi(v) : 0;
   }();
+  // ZG_LZ4_PAIR: 1 = producer/consumer pairs for every launch, auto = for launches with fewer chunks
+  // than the one-wave grid holds (2 x 8192 here), 0 / unset = the one-wave decoder.
+  static const int pair = [] {
+    const char* v = getenv("ZG_LZ4_PAIR");
+    if (!v) return 0;
+    return std::string(v) == "auto" ? 2 : atoi(v) ? 1 : 0;
+  }();
+  if (pair == 1 || (pair == 2 && n_chunks < 16384))
+    return zg_lz4_pair_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, stream);
   return zg_lz4_batched_decode_grid(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, stream);
 }
 

@@ -84,6 +84,10 @@ size_t zg_lz4_rec_scratch_bytes(int n_chunks, uint64_t src_n);
 hipError_t zg_lz4_decode_records(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                  const ZgChunk* chunks, int n_chunks, unsigned long long* err, uint8_t* scratch,
                                  size_t scratch_bytes, hipStream_t stream);
+// Producer/consumer decode: two waves per chunk (scalar parse -> LDS batch ring -> lane-parallel
+// execute), for launches with fewer chunks than resident waves.  grid_cap: pairs (0 = 4096).
+hipError_t zg_lz4_pair_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                              int n_chunks, unsigned long long* err, int grid_cap, hipStream_t stream);
 // Same with an explicit persistent-grid cap in blocks of 4 waves (0 = default 2048).
 hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                       const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,

@@ -342,14 +342,15 @@ def _decode_both(body, chunks_data, n):
     st = torch.cuda.current_stream().cuda_stream
     dec = ops.DecodeScratch(DEV)
     out = []
-    for rec in (False, True):
+    for rec in (False, True, "pair"):
         dst.fill_(0x5A)
         ws.err.zero_()
-        sp, sb = dec.get(n, src.numel()) if rec else (0, 0)
+        sp, sb = dec.get(n, src.numel()) if rec is True else (0, 0)
         H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(), ws.chunks.data_ptr(), n,
-                     ws.err.data_ptr(), st, 0, sp, sb)
+                     ws.err.data_ptr(), st, 0, sp, sb, rec == "pair")
         torch.cuda.synchronize()
         out.append((dst.cpu().numpy().tobytes()[3:3 + len(data)], int(ws.err.item())))
+    # the records decoder left per-chunk record counts at the head of its scratch (read below)
     # per-chunk record counts the parse left at the head of the scratch (-1: decode_chunk fallback)
     counts = dec.buf[:4 * n].view(torch.int32).cpu().tolist()
     return out, counts
@@ -373,8 +374,8 @@ def test_lz4_records_decoder_matches_batched(policy):
     schemes = [e[2] for e in idx]
     assert sum(s != 0 for s in schemes) >= 6, schemes
     data = b"".join(chunks)
-    ((ob, eb), (orc, er)), counts = _decode_both(body, chunks, len(chunks))
-    assert eb == 0 and er == 0
+    ((ob, eb), (orc, er), (opr, epr)), counts = _decode_both(body, chunks, len(chunks))
+    assert eb == 0 and er == 0 and epr == 0
     # the records path really ran: every compressed chunk of >= 256 stored bytes parsed into records
     for e, cnt in zip(idx, counts):
         if e[2] != 0 and e[1] >= 256:
@@ -383,6 +384,7 @@ def test_lz4_records_decoder_matches_batched(policy):
     for ch, sc in zip(chunks, schemes):
         if sc != 0:  # raw chunks are placed by the ingest pass, not by the decoders
             assert ob[pos:pos + len(ch)] == ch and orc[pos:pos + len(ch)] == ch, (len(ch), sc)
+            assert opr[pos:pos + len(ch)] == ch, ("pair", len(ch), sc)
         pos += len(ch)
     assert pos == len(data)
     # corrupt the middle of the longest compressed chunk's stream
@@ -390,10 +392,10 @@ def test_lz4_records_decoder_matches_batched(policy):
     bad = bytearray(body)
     mid = big[0] + 8 + big[1] // 2
     bad[mid:mid + 64] = bytes(rng.integers(0, 256, 64, dtype=np.uint8))
-    ((ob, eb), (orc, er)), _ = _decode_both(bytes(bad), chunks, len(chunks))
-    assert eb == er, (hex(eb), hex(er))
+    ((ob, eb), (orc, er), (opr, epr)), _ = _decode_both(bytes(bad), chunks, len(chunks))
+    assert eb == er == epr, (hex(eb), hex(er), hex(epr))
     if eb == 0:
-        assert ob == orc
+        assert ob == orc == opr
 
 
 def test_ingest_clip_window():

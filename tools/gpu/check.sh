@@ -17,7 +17,7 @@
 #   cli         `zest pull --gpus 1` vs host `zest pull` (Llama-3.1-8B from an HBM seeder, sync between)
 #   stripe      host pull from 1 vs 3 loopback seeders
 #   seed        HBM seeding throughput (Mixtral-8x7B, chunks_served/s)
-#   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group)
+#   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group, e.g. k3pair)
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
 #   hostbench   `zest bench --synthetic` on the box's CPU

@@ -261,6 +261,42 @@ def main():
         ingest_case("bf16_1g", raw, "bg4", 3, after=occ)
         del raw
 
+    if want("k3pair"):
+        # round 4: producer/consumer wave pairs (k_lz4_pair) vs the one-wave decoder, and the scan-based
+        # header walk (k_index_scan + k_index_chain) vs the serial k_index_terms, at a small launch
+        # (256 MiB, ~4 k chunks: fewer chunks than wave slots) and a bench round (1 GiB)
+        for m, tag in ((256 << 20, "bf16_256m"), (1 << 30, "bf16_1g")):
+            w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
+            raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+            del w
+
+            def pair(src, dst, ws, n, m=m, tag=tag, raw=raw):
+                for label, kw in (("one-wave", {}), ("pair", {"pair": True})):
+                    dst.zero_()
+                    ms = timed(lambda: H.lz4_decode(src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(),
+                                                    ws.chunks.data_ptr(), n, ws.err.data_ptr(), st, 0, **kw), 5)
+                    ops.raise_on_error(ws.err)
+                    emit(kernel=f"lz4_decode({tag},{label})", bytes=m, ms=ms, gbps=m / ms / 1e6, chunks=n)
+                    assert dst[:m].cpu().numpy().tobytes() == raw, label
+                nt = ws.max_terms
+                chunks0 = ws.chunks.clone()
+                for label in ("serial", "scan"):
+                    ws.err.zero_()
+                    if label == "serial":
+                        fn = lambda: H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(),
+                                                   ws.err.data_ptr(), st)
+                    else:
+                        sp, sb = ws.index_scratch()
+                        fn = lambda: H.index_terms_scan(src.data_ptr(), src.numel(), ws.terms.data_ptr(), nt,
+                                                        ws.chunks.data_ptr(), ws.err.data_ptr(), sp, sb, st)
+                    ms = timed(fn, 5)
+                    ops.raise_on_error(ws.err)
+                    emit(kernel=f"index_terms({tag},{label})", bytes=src.numel(), ms=ms, gbps=src.numel() / ms / 1e6,
+                         terms=nt, chunks=n, same_records=bool(torch.equal(ws.chunks, chunks0)))
+
+            ingest_case(tag, raw, "bg4", 3, after=pair)
+            del raw
+
     if want("fuse"):
         # a bench round of raw chunks (1 GiB random bytes): place then hash vs the fused one pass,
         # and the same for a BG4 bf16 round (decode + place/hash)
