@@ -1,10 +1,14 @@
 """Intra-node parallelism: one process per GPU, RCCL over xGMI via torch.distributed ("nccl").
 
-* `DevicePuller` (zest_amd.engine): owner-sharded term ingest + peer-to-peer round exchange of the
-  HBM arena — the swarm pull used by bench.py.
+* `exchange.RoundExchange`: per-round replication of arena regions over xGMI (RCCL p2p / coalesced
+  broadcasts / slab all-gather, or peer-mapped HIP VMM arenas read by DMA copies or the K8 kernel),
+  autotuned per machine; `map_peer_arenas` builds the peer mappings.
+* `DevicePuller` (zest_amd.engine): owner-sharded term ingest from a pinned origin + that exchange —
+  the swarm pull bench.py measures.
+* `swarm_pull`: the same machinery fed by the network (public `pull(device="all")`): byte-balanced
+  term shares fetched device-direct, rounds exchanged over xGMI, every chunk re-hashed on every GPU,
+  Merkle-checked per file; survives a lost rank.
 * `swarm_load`: replicate a pulled snapshot into every GPU's HBM, each file read by one owner rank.
-* `swarm_pull`: the same straight from the network: each Xet file pulled device-direct by one owner
-  rank, broadcast over xGMI to the others, re-verified on every GPU.
 * `init_from_env`: torchrun-style rendezvous (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
 * `bind_local_numa`: pin a rank to the CPUs of its GPU's NUMA node, so its pinned host staging and
   origin pages are first-touched next to the GPU's PCIe root (8 ranks x ~57 GB/s of H2D must not

@@ -73,24 +73,6 @@ class _RankLost(RuntimeError):
     """A collective failed or timed out: some rank is gone (handled by _Membership.rebuild)."""
 
 
-def verify_with_lens(buf: torch.Tensor, lens: bytes, xet_hash: str) -> bool:
-    """Xet file hash of `buf` with the given uint32 chunk sizes (BLAKE3 + Merkle on buf's device)."""
-    n = buf.numel()
-    if n == 0:
-        return _core.xet_hex(_core.file_hash([])) == xet_hash
-    if buf.device.type != "cuda":
-        h = _core.xet_file_hash_lens(buf.numpy(), lens)
-        return bool(h) and _core.xet_hex(h) == xet_hash
-    sizes = np.frombuffer(lens, dtype=np.uint32)
-    if int(sizes.sum(dtype=np.uint64)) != n or (len(sizes) and int(sizes.max()) > 128 * 1024):
-        return False
-    starts = np.concatenate([[0], np.cumsum(sizes, dtype=np.uint64)[:-1]]).astype(np.uint64)
-    hashes = ops.hash_ranges(buf, starts, sizes)
-    sz = torch.from_numpy(sizes.astype(np.int64)).to(buf.device)
-    root = ops.merkle_roots(hashes, sz, [(0, len(sizes))], file_hash=True)
-    return _core.xet_hex(root[0].cpu().numpy().tobytes()) == xet_hash
-
-
 # ----------------------------------------------------------------------------------------------
 # Planning: byte-balanced contiguous term shares, cut into tapered rounds
 # ----------------------------------------------------------------------------------------------
