@@ -294,3 +294,31 @@ def test_swarm_pull_eight_ranks_lose_two(hub_env):
         assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
         assert st["recovered_ranks"] == 2 and st["world"] == 6
     assert dt < 170, dt
+
+
+def test_swarm_plan_term_shares_and_jobs():
+    """The plan behind swarm_pull: files laid out 4 KiB aligned in one arena, byte-balanced contiguous
+    term shares per rank, rounds cut by bytes with the head/tail taper, and a round item spanning two
+    files turned into one fetch job per file with consecutive chunk indices."""
+    import numpy as np
+
+    from zest_amd.parallel.swarm_pull import _Plan, round_weights, split_bytes
+    files = [{"path": "a.safetensors", "size": 10_000, "xet_hash": "a" * 64},
+             {"path": "b.safetensors", "size": 7_000, "xet_hash": "b" * 64}]
+    shapes = [[(4000, 2), (6000, 3)], [(3000, 1), (4000, 4)]]
+    P = _Plan(files, shapes)
+    assert P.file_off == [0, 12288] and P.arena_bytes == 12288 + 8192
+    assert P.t_dst.tolist() == [0, 4000, 12288, 15288] and P.t_c0.tolist() == [0, 2, 5, 6] and P.n_chunks == 10
+    assert P.region(1, 3) == (4000, 15288)
+    jobs = P.jobs(1, 4, 1 << 40)
+    assert jobs == [("a" * 64, 1, 2, (1 << 40) + 4000, 2), ("b" * 64, 0, 2, (1 << 40) + 12288, 5)]
+    assert P.files_of(1, 3) == [0, 1]
+    # shares and rounds
+    ulen = np.array([100] * 40, dtype=np.int64)
+    assert split_bytes(ulen, 0, 40, [1.0, 1.0]) == [(0, 20), (20, 40)]
+    assert split_bytes(ulen, 5, 5, [1.0, 1.0]) == [(5, 5), (5, 5)]
+    w = round_weights(10 << 30, 1 << 30)
+    assert w[:2] == [0.25, 0.5] and w[-3:] == [0.5, 0.25, 0.125] and abs(sum(w) - 10) < 1.0
+    assert round_weights(3 << 30, 1 << 30) == [1.0, 1.0, 1.0]
+    cuts = split_bytes(ulen, 0, 40, w)
+    assert cuts[0][0] == 0 and cuts[-1][1] == 40 and all(a <= b for a, b in cuts)
