@@ -183,8 +183,14 @@ class _Membership:
         # A subgroup's members create it alone (the other ranks of the job are not in this call).
         self.ctl = dist.new_group(ranks=self.granks, backend="gloo", timeout=self._td,
                                   use_local_synchronization=group is not None)
+        self._own_data = False
         if backend == "gloo":
             self.data = self.ctl  # CPU (or one-GPU gloo) exchanges: the same bounded timeout
+        elif os.environ.get("ZEST_SWARM_ELASTIC", "1") != "0" and len(self.granks) > 1:
+            # a data group of our own, so a lost rank's recovery can abort it without touching the
+            # caller's group (aborting the default group would leave nothing to rebuild from)
+            self.data = dist.new_group(ranks=self.granks, backend=backend, use_local_synchronization=group is not None)
+            self._own_data = True
         self.epoch = 0
         self.store = None
         self._stop = threading.Event()
@@ -269,11 +275,12 @@ class _Membership:
             self.data = self.ctl
         else:
             abort = getattr(dist.distributed_c10d, "_abort_process_group", None)
-            if abort is not None and old_data is not None:
+            if abort is not None and old_data is not None and self._own_data:
                 try:
-                    abort(old_data)
+                    abort(old_data)  # in-flight RCCL kernels waiting on the dead rank exit
                 except Exception:  # noqa: BLE001
                     pass
+            self._own_data = True
             self.data = dist.new_group(ranks=members, backend=self.backend, use_local_synchronization=True)
         return lost
 
