@@ -112,8 +112,9 @@ struct RangeSrc {  // raw (offset, len) messages (k_hash_ranges semantics: > 128
 // (the copy is exercised against the source bytes, misaligned both sides, by
 // tests/test_gpu_kernels.py::test_fused_ingest_places_exact_bytes), and receivers of the swarm
 // exchange re-hash what landed in their own arena.  A descriptor that fails its bounds check is not
-// placed, hashes as empty (so its file's Merkle check fails) and is reported in the error word as
-// ZG_ERR_RANGE at its chunk index, like the unfused k_place_raw did.
+// placed, is hashed over its planned leaves with no bytes in them (never its real hash, so its file's
+// Merkle check fails) and is reported in the error word as ZG_ERR_RANGE at its chunk index, like the
+// unfused k_place_raw did.
 struct PlaceSrc {
   const ZgChunk* chunks;
   const uint8_t* src;
