@@ -251,7 +251,10 @@ FileResult ParallelDownloader::reconstruct(const std::string& hex, const std::st
       }
     } else {
       trace::Span sp("download", "pwrite");
+      uint64_t n = 0;
+      for (const iovec& v : iov) n += v.iov_len;
       pwritev_all(fd, iov, off - skip);
+      storage::start_writeback(fd, off - skip, n);
     }
     hashes[i] = std::move(hs);
     if (on_term) on_term(total, f.source);

@@ -120,6 +120,10 @@ bool read_range(const std::string& path, uint64_t off, uint64_t n, uint8_t* out)
 
 void remove_file(const std::string& path) { ::unlink(path.c_str()); }
 
+void start_writeback(int fd, uint64_t off, uint64_t len) {
+  if (fd >= 0 && len) (void)::sync_file_range(fd, off64_t(off), off64_t(len), SYNC_FILE_RANGE_WRITE);
+}
+
 void write_ref(const Config& cfg, const std::string& repo_id, const std::string& ref, const std::string& commit) {
   write_file_atomic(cfg.repo_dir(repo_id) + "/refs/" + ref, commit);
 }

@@ -34,6 +34,10 @@ std::optional<Bytes> read_file(const std::string& path);
 // Read [off, off+n) of a file into out (false if short/missing).
 bool read_range(const std::string& path, uint64_t off, uint64_t n, uint8_t* out);
 void remove_file(const std::string& path);
+// Start the disk write-back of [off, off + len) of fd now (sync_file_range WRITE, no wait): the
+// final fdatasync before a file's rename then only waits for what is still in flight, instead of
+// flushing the whole file in the pull's tail.  Best effort (filesystems without it ignore it).
+void start_writeback(int fd, uint64_t off, uint64_t len);
 
 // HF cache: models--org--name/refs/{ref} = commit
 void write_ref(const Config& cfg, const std::string& repo_id, const std::string& ref, const std::string& commit);

@@ -178,6 +178,7 @@ class WriteBack {
         if (w <= 0) e = std::string("pwrite: ") + std::strerror(errno);
         else done += uint64_t(w);
       }
+      if (e.empty()) storage::start_writeback(fl.fd, p.off, p.len);  // the disk works behind the pull
       std::lock_guard<std::mutex> g(mu_);
       if (!e.empty() && fl.err.empty()) fl.err = e;
       if (--pending_ == 0) idle_.notify_all();

@@ -23,6 +23,7 @@
 #   hostbench   `zest bench --synthetic` on the box's CPU
 #   benchnew    bench.py --modes bf16 with the round-4 opt-ins on (ZEST_RIDE_RECORDS=1 ZEST_INDEX_SCAN=1
 #               ZG_LZ4_PAIR=auto) -> A/B against `bench`
+#   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
 #   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=auto ZEST_INDEX_SCAN=1")
 #   swarm       term-sharded swarm_pull GPU tests (modes, VMM fault hooks) (tests/test_gpu_device.py -k swarm_pull)
 #   swarmbench  public pull(device="all") end to end from a loopback HBM seeder, $SWARM_RANKS (1,2,3) ranks,
@@ -80,6 +81,9 @@ for step in "$@"; do
     benchnew) ZEST_RIDE_RECORDS=1 ZEST_INDEX_SCAN=1 ZG_LZ4_PAIR=auto timeout -k 10 700 python -u bench.py --modes bf16 \
                 --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
               grep -h "aggregate" $log; tail -1 $log | cut -c1-400 ;;
+    benchA|benchB) v=BENCH_ENV_${step#bench}; env ${!v:-} timeout -k 10 700 python -u bench.py --modes ${BENCH_MODES:-bf16} \
+                --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
+              echo "env: ${!v:-}"; grep -h "aggregate" $log ;;
     gpubench) env ${GPUBENCH_ENV:-} timeout -k 10 500 python -u -m zest_amd.gpubench --json > $OUT/gpubench.json 2> $log \
                 || fail $step $? $log
               python -c "import json,sys; [print(r['name'], round(r['throughput_mbps']/1e3,1), 'GB/s') for r in json.load(open(sys.argv[1]))['results']]" $OUT/gpubench.json ;;

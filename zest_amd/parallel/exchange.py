@@ -537,6 +537,11 @@ class RoundExchange:
             # gloo moves device tensors only through its collectives; a batched isend/irecv of
             # device tensors never completed (2-rank rehearsal on one GPU)
             modes = tuple(m for m in modes if m != "p2p")
+        # Time on a prefix of every region: bandwidth over xGMI is flat well below a 1 GiB round, and
+        # a sweep of full rounds (modes x passes x rounds) cost seconds of setup in the one-GPU
+        # rehearsal, where gloo stages device tensors through the host (profiles/r4/swarm_pull_r4b.json).
+        cap = int(os.environ.get("ZEST_AUTOTUNE_MB", "256" if self.backend() == "nccl" else "32")) << 20
+        region_lists = [[(lo, min(hi, lo + cap)) if hi > lo else (lo, hi) for lo, hi in regs] for regs in region_lists]
         times = {}
         moved = self.bytes_moved
         for mode in modes:
