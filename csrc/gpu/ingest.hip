@@ -110,111 +110,6 @@ __global__ void k_index_terms(const uint8_t* __restrict__ src, const ZgTerm* __r
   walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
 }
 
-// K4b: the same walk without its HBM pointer chase.  Each hop of the serial walk waits ~1 us for a
-// header 8-128 KiB past the previous one (one dependent miss per chunk: ~1 ms per 1000-chunk term).
-// Here the headers come to the walker in bulk first:
-//   k_index_scan   every byte position of the buffer (16 per lane, 24 bytes loaded) is tested for a
-//                  plausible chunk header -- version 0, scheme <= 2, 1 <= ulen <= 128 KiB, clen
-//                  bounded, raw => clen == ulen, and the chunk ends inside the buffer -- and the
-//                  positions that pass are appended to a candidate list (~1 per chunk: the test
-//                  passes ~6e-9 of random positions).  One read of the buffer at HBM speed.
-//   k_index_chain  one wave per term: the term's candidates go into an LDS hash table (position ->
-//                  header), then lane 0 runs the exact walk of k_index_terms, fetching each header
-//                  from the table -- an LDS probe instead of an HBM round trip -- or from memory when
-//                  it is missing (table full, list overflow, a header the plausibility test
-//                  rejects).  The table only caches the bytes the walk reads, so the records and
-//                  the error codes are those of the serial walk for any input.
-constexpr int kScanPerLane = 16;
-constexpr uint32_t kHashSlots = 8192;  // per term (LDS: 12 B a slot); a xorb holds <= 8192 chunks
-constexpr uint32_t kMaxProbes = 32;    // linear probing bound (load factor ~0.12 for a 1000-chunk term)
-
-struct ScanHdr {
-  unsigned long long count;  // candidates found (may exceed the list's capacity)
-  unsigned long long pad[7];
-};
-
-__global__ void __launch_bounds__(256) k_index_scan(const uint8_t* __restrict__ src, uint64_t src_n,
-                                                    ScanHdr* __restrict__ hdr, uint64_t* __restrict__ cand, uint64_t cap) {
-  const uint64_t base = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) * kScanPerLane;
-  if (base >= src_n) return;
-  // 24 bytes from a 16-aligned position (src is 16-aligned; buffers carry >= 4 KiB of padding)
-  const uint4 a = *reinterpret_cast<const uint4*>(src + base);
-  const uint2 b = *reinterpret_cast<const uint2*>(src + base + 16);
-  const uint32_t d[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
-#pragma unroll
-  for (int i = 0; i < kScanPerLane; ++i) {
-    const int k = i >> 2, sh = i & 3;
-    const uint32_t lo = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-    if ((lo & 0xFF) != 0) continue;  // version byte: rejects ~255 of 256 positions
-    const uint32_t hi = __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], sh);
-    const uint32_t clen = lo >> 8, scheme = hi & 0xFF, ulen = hi >> 8;
-    const uint64_t p = base + uint64_t(i);
-    if (scheme > 2 || ulen == 0 || ulen > kMaxChunk || clen == 0 || clen > kMaxChunk + 4096 ||
-        (scheme == 0 && clen != ulen) || p + 8 + clen > src_n)
-      continue;
-    const unsigned long long j = atomicAdd(&hdr->count, 1ull);
-    if (j < cap) cand[j] = p;
-  }
-}
-
-__device__ __forceinline__ uint32_t hslot(uint32_t key) { return (key * 2654435761u) >> (32 - 13); }
-
-struct TableHdr {
-  const uint8_t* p;
-  const uint32_t* keys;
-  const uint2* vals;
-  __device__ __forceinline__ void operator()(uint64_t off, uint32_t& lo, uint32_t& hi) const {
-    if (off < 0xFFFFFFFFull) {
-      const uint32_t key = uint32_t(off) + 1u;
-      uint32_t s = hslot(key);
-      for (uint32_t n = 0; n < kMaxProbes; ++n, s = (s + 1) & (kHashSlots - 1)) {
-        const uint32_t k = keys[s];
-        if (k == key) {
-          const uint2 v = vals[s];
-          lo = v.x;
-          hi = v.y;
-          return;
-        }
-        if (k == 0) break;
-      }
-    }
-    load8(p + off, lo, hi);  // not in the table: read it
-  }
-};
-
-__global__ void __launch_bounds__(64) k_index_chain(const uint8_t* __restrict__ src, const ZgTerm* __restrict__ terms,
-                                                    ZgChunk* __restrict__ chunks, unsigned long long* err,
-                                                    const ScanHdr* __restrict__ hdr, const uint64_t* __restrict__ cand,
-                                                    uint64_t cap) {
-  __shared__ uint32_t keys[kHashSlots];
-  __shared__ uint2 vals[kHashSlots];
-  const int t = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const ZgTerm tm = terms[t];
-  for (uint32_t s = lane; s < kHashSlots; s += kWave) keys[s] = 0;
-  __syncthreads();
-  const uint64_t n = min(hdr->count, (unsigned long long)cap);
-  for (uint64_t i = lane; i < n; i += kWave) {
-    const uint64_t p = cand[i];
-    if (p < tm.src || p - tm.src >= tm.src_len || p - tm.src >= 0xFFFFFFFFull) continue;
-    const uint32_t key = uint32_t(p - tm.src) + 1u;
-    uint32_t lo, hi;
-    load8(src + p, lo, hi);
-    uint32_t s = hslot(key);
-    for (uint32_t k = 0; k < kMaxProbes; ++k, s = (s + 1) & (kHashSlots - 1)) {
-      const uint32_t old = atomicCAS(&keys[s], 0u, key);
-      if (old == 0u) {
-        vals[s] = make_uint2(lo, hi);
-        break;
-      }
-      if (old == key) break;
-    }
-  }
-  __syncthreads();
-  if (lane != 0) return;
-  walk_term(tm, t, chunks, err, TableHdr{src + tm.src, keys, vals});
-}
-
 using zwv::wave_copy;  // wave64.h
 
 // K3a: place uncompressed chunks (scheme 0): one wave per chunk, clipped to [clip_lo, clip_hi).
@@ -729,28 +624,6 @@ hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, 
                           unsigned long long* err, hipStream_t stream) {
   if (n_terms <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_index_terms, dim3((n_terms + 63) / 64), dim3(64), 0, stream, src, terms, n_terms, chunks, err);
-  return hipGetLastError();
-}
-
-size_t zg_index_scan_scratch_bytes(int n_chunks) {
-  return sizeof(ScanHdr) + 8 * (2 * uint64_t(n_chunks > 0 ? n_chunks : 0) + 1024);
-}
-
-hipError_t zg_index_terms_scan(const uint8_t* src, uint64_t src_n, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
-                               unsigned long long* err, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
-  if (n_terms <= 0) return hipSuccess;
-  // unaligned source or no scratch: the serial walk (same records, same errors)
-  if (!scratch || scratch_bytes < zg_index_scan_scratch_bytes(0) || (reinterpret_cast<uintptr_t>(src) & 15) ||
-      src_n == 0)
-    return zg_index_terms(src, terms, n_terms, chunks, err, stream);
-  ScanHdr* hdr = reinterpret_cast<ScanHdr*>(scratch);
-  uint64_t* cand = reinterpret_cast<uint64_t*>(scratch + sizeof(ScanHdr));
-  const uint64_t cap = (scratch_bytes - sizeof(ScanHdr)) / 8;
-  hipError_t e = hipMemsetAsync(hdr, 0, sizeof(ScanHdr), stream);
-  if (e != hipSuccess) return e;
-  const uint64_t lanes = (src_n + kScanPerLane - 1) / kScanPerLane;
-  hipLaunchKernelGGL(k_index_scan, dim3(uint32_t((lanes + 255) / 256)), dim3(256), 0, stream, src, src_n, hdr, cand, cap);
-  hipLaunchKernelGGL(k_index_chain, dim3(n_terms), dim3(kWave), 0, stream, src, terms, chunks, err, hdr, cand, cap);
   return hipGetLastError();
 }
 

@@ -58,13 +58,6 @@ enum {
 // All launchers return hipError_t of the launch and never synchronize.
 hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
                           unsigned long long* err, hipStream_t stream);
-// Same records and errors, without the per-chunk HBM pointer chase: one scan of src[0, src_n) for
-// plausible headers (k_index_scan), then each term's walk reads its headers from an LDS table
-// (k_index_chain).  `scratch`: >= zg_index_scan_scratch_bytes(total chunks) of device memory (one per
-// concurrently running launch); without it, or with a src not 16-byte aligned, the serial walk runs.
-size_t zg_index_scan_scratch_bytes(int n_chunks);
-hipError_t zg_index_terms_scan(const uint8_t* src, uint64_t src_n, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
-                               unsigned long long* err, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream);
 // Descriptors are bounds-checked in-kernel against src_n / dst_n (bytes).  A clip window narrower
 // than [0, dst_n) needs `clip_scratch` (ZG_CLIP_SCRATCH_BYTES of device memory owned by the caller,
 // one per concurrently running launch): compressed chunks that straddle the window decode there

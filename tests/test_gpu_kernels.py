@@ -265,68 +265,6 @@ def test_fused_ingest_places_exact_bytes():
         assert got[i].tobytes() == C.chunk_hash(out[o:o + len(d)]), i
 
 
-@pytest.mark.parametrize("case", ["valid", "bad_version", "bad_length", "short_run", "zeros"])
-def test_index_scan_matches_serial_walk(case):
-    """zg_index_terms_scan (one scan for header candidates + per-term walks over an LDS table) writes
-    the same chunk records and the same error word as the serial walk k_index_terms: on valid runs
-    at odd offsets (raw + LZ4 + BG4 chunks, header-like zero runs in the data) and on corrupt ones."""
-    rng = random.Random(41)
-    parts = [rng.randbytes(300_000), bytes(200_000), _bf16(150_000, 2), b"\0\x10\0\0\0\x10\0\0" * 9000]
-    data = b"".join(parts)
-    ends = C.chunk_ends(data)
-    b = C.XorbBuilder("auto")
-    prev = 0
-    for e in ends:
-        b.add_chunk(data[prev:e])
-        prev = e
-    body = bytearray(b.serialize(False))
-    bounds = b.chunk_boundaries()
-    nck = len(ends)
-    cuts = [0, nck // 3, 2 * nck // 3, nck]
-    uoffs = [0] + list(ends)
-    src_host = bytearray(5)
-    terms = np.zeros(3, dtype=ops.TERM_DTYPE)
-    for t in range(3):
-        c0, c1 = cuts[t], cuts[t + 1]
-        r0 = 0 if c0 == 0 else bounds[c0 - 1]
-        run = body[r0:bounds[c1 - 1]]
-        terms[t] = (len(src_host), len(run), 11 + uoffs[c0], c0, c1 - c0, uoffs[c1] - uoffs[c0])
-        src_host += run + b"\0" * (t + 2)
-    def hdr_at(t, j):  # src offset of chunk j's header (j inside term t)
-        c0 = cuts[t]
-        return int(terms[t]["src"]) + (bounds[j - 1] if j else 0) - (bounds[c0 - 1] if c0 else 0)
-
-    if case == "bad_version":
-        src_host[hdr_at(1, cuts[1] + 2)] = 9  # version byte of a header mid-term 1
-    elif case == "bad_length":
-        src_host[hdr_at(2, cuts[2] + 1) + 3] ^= 0x40  # clen's top byte of a chunk in term 2
-    elif case == "short_run":
-        terms[0]["src_len"] -= 100
-    elif case == "zeros":
-        src_host += bytes(64 << 10)  # trailing header-like zeros past the last term
-    src = ops.padded_empty(len(src_host), DEV)
-    src.copy_(torch.frombuffer(src_host, dtype=torch.uint8))
-    H = ops.hip()
-    st = torch.cuda.current_stream().cuda_stream
-    tdev = torch.from_numpy(terms.view(np.uint8).copy()).to(DEV)
-    outs = []
-    for scan in (False, True):
-        chunks = torch.full((nck * ops.CHUNK_DTYPE.itemsize,), 0x77, dtype=torch.uint8, device=DEV)
-        err = torch.zeros(1, dtype=torch.int64, device=DEV)
-        if scan:
-            sb = H.index_scan_scratch_bytes(nck)
-            scratch = torch.empty(sb, dtype=torch.uint8, device=DEV)
-            H.index_terms_scan(src.data_ptr(), src.numel(), tdev.data_ptr(), 3, chunks.data_ptr(), err.data_ptr(),
-                               scratch.data_ptr(), sb, st)
-        else:
-            H.index_terms(src.data_ptr(), tdev.data_ptr(), 3, chunks.data_ptr(), err.data_ptr(), st)
-        torch.cuda.synchronize()
-        outs.append((chunks.cpu().numpy().tobytes(), int(err.item())))
-    assert outs[0][1] == outs[1][1], (hex(outs[0][1]), hex(outs[1][1]))
-    assert outs[0][0] == outs[1][0]
-    assert (outs[0][1] == 0) == (case in ("valid", "zeros"))
-
-
 def _decode_both(body, chunks_data, n):
     """Index one run, then decode it with the one-kernel batched decoder and with the two-kernel
     records decoder; returns (output, error word) per decoder."""

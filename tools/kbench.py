@@ -262,9 +262,10 @@ def main():
         del raw
 
     if want("k3pair"):
-        # round 4: producer/consumer wave pairs (k_lz4_pair) vs the one-wave decoder, and the scan-based
-        # header walk (k_index_scan + k_index_chain) vs the serial k_index_terms, at a small launch
-        # (256 MiB, ~4 k chunks: fewer chunks than wave slots) and a bench round (1 GiB)
+        # round 4: producer/consumer wave pairs (k_lz4_pair) vs the one-wave decoder, and the serial
+        # header walk k_index_terms, at a small launch (256 MiB, ~4 k chunks: fewer chunks than wave
+        # slots) and a bench round (1 GiB).  (A scan-based header walk measured here at 5.4 / 12.3 ms
+        # against 0.51 / 0.61 ms serial was removed: profiles/r4/kbench_k3pair_r4b.jsonl.)
         for m, tag in ((256 << 20, "bf16_256m"), (1 << 30, "bf16_1g")):
             w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
             raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
@@ -280,19 +281,12 @@ def main():
                     assert dst[:m].cpu().numpy().tobytes() == raw, label
                 nt = ws.max_terms
                 chunks0 = ws.chunks.clone()
-                for label in ("serial", "scan"):
-                    ws.err.zero_()
-                    if label == "serial":
-                        fn = lambda: H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(),
-                                                   ws.err.data_ptr(), st)
-                    else:
-                        sp, sb = ws.index_scratch()
-                        fn = lambda: H.index_terms_scan(src.data_ptr(), src.numel(), ws.terms.data_ptr(), nt,
-                                                        ws.chunks.data_ptr(), ws.err.data_ptr(), sp, sb, st)
-                    ms = timed(fn, 5)
-                    ops.raise_on_error(ws.err)
-                    emit(kernel=f"index_terms({tag},{label})", bytes=src.numel(), ms=ms, gbps=src.numel() / ms / 1e6,
-                         terms=nt, chunks=n, same_records=bool(torch.equal(ws.chunks, chunks0)))
+                ws.err.zero_()
+                ms = timed(lambda: H.index_terms(src.data_ptr(), ws.terms.data_ptr(), nt, ws.chunks.data_ptr(),
+                                                 ws.err.data_ptr(), st), 5)
+                ops.raise_on_error(ws.err)
+                emit(kernel=f"index_terms({tag},serial)", bytes=src.numel(), ms=ms, gbps=src.numel() / ms / 1e6,
+                     terms=nt, chunks=n, same_records=bool(torch.equal(ws.chunks, chunks0)))
 
             ingest_case(tag, raw, "bg4", 3, after=pair)
             del raw

@@ -210,15 +210,6 @@ class IngestWorkspace:
             if self.device.type == "cuda" else None
         self._clip_scratch = None
         self.hash_scratch = HashScratch(self.device) if self.device.type == "cuda" else None
-        self._index_scratch = None
-
-    def index_scratch(self) -> tuple[int, int]:
-        """Device scratch of the scan-based header walk (zg_index_terms_scan), private to this
-        workspace (so to its stream): (pointer, bytes)."""
-        if self._index_scratch is None:
-            self._index_scratch = torch.empty(hip().index_scan_scratch_bytes(self.max_chunks), dtype=torch.uint8,
-                                              device=self.device)
-        return self._index_scratch.data_ptr(), self._index_scratch.numel()
 
     def clip_scratch(self) -> int:
         """Device scratch for clipped decodes, private to this workspace (so to its stream)."""
@@ -228,19 +219,14 @@ class IngestWorkspace:
 
 
 FUSED_INGEST = os.environ.get("ZEST_FUSED_INGEST", "1") != "0"
-# Header walk of device-resident runs: one scan for header candidates + per-term walks over an LDS
-# table (zg_index_terms_scan) instead of one HBM round trip per chunk.  ZEST_INDEX_SCAN=0: serial walk.
-INDEX_SCAN = os.environ.get("ZEST_INDEX_SCAN", "0") != "0"  # opt-in until measured on the GPU
 
 
 def index_terms(H, src_ptr: int, src_n: int, terms_ptr: int, n_terms: int, chunks_ptr: int, err_ptr: int, stream: int,
                 ws: "IngestWorkspace | None" = None) -> None:
-    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4)."""
-    if INDEX_SCAN and ws is not None:
-        sp, sb = ws.index_scratch()
-        H.index_terms_scan(src_ptr, src_n, terms_ptr, n_terms, chunks_ptr, err_ptr, sp, sb, stream)
-    else:
-        H.index_terms(src_ptr, terms_ptr, n_terms, chunks_ptr, err_ptr, stream)
+    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4).  One thread per
+    term chases its headers (~0.6 ms per 1 GiB round, profiles/r4/kbench_k3pair_r4b.jsonl); a
+    candidate-scan + LDS-table walk tried in round 4 measured 10-20x slower and was removed."""
+    H.index_terms(src_ptr, terms_ptr, n_terms, chunks_ptr, err_ptr, stream)
 
 
 def ingest_terms(src: torch.Tensor, dst: torch.Tensor, terms: np.ndarray, hashes: torch.Tensor,
