@@ -441,7 +441,10 @@ class _Swarm:
         shares = [(int(bounds[r]), int(bounds[r + 1])) for r in range(W)]
         max_share = max((int(P.t_ulen[a:b].sum()) for a, b in shares), default=0)
         taper = os.environ.get("ZEST_ROUND_TAPER", "1") != "0"
-        weights = round_weights(max_share, self.round_bytes, taper) if max_share else [1.0]
+        # One rank: nothing to overlap a fetch with, so the whole share is one pull_terms call (every
+        # round boundary drains the fetch pipeline: 16 rounds of 1 GiB cost ~25 ms each on
+        # Llama-3.1-8B, profiles/r4/swarm_pull_r4b.json).
+        weights = round_weights(max_share, self.round_bytes, taper) if max_share and W > 1 else [1.0]
         self.items: list[tuple[int, int]] = []
         self.queue: list[list[int]] = [[] for _ in range(W)]
         for r, (a, b) in enumerate(shares):
