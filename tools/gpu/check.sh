@@ -21,8 +21,6 @@
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
 #   hostbench   `zest bench --synthetic` on the box's CPU
-#   benchnew    bench.py --modes bf16 with the round-4 opt-ins on (ZEST_RIDE_RECORDS=1
-#               ZG_LZ4_PAIR=auto) -> A/B against `bench`
 #   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
 #   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=auto")
 #   swarm       term-sharded swarm_pull GPU tests (modes, VMM fault hooks) (tests/test_gpu_device.py -k swarm_pull)
@@ -78,9 +76,6 @@ for step in "$@"; do
            db=$(find $OUT/kprof -name "*.db" | head -1)
            python tools/rocpd_summary.py "$db" --title "kbench ${KBENCH_ONLY:-all} kernels" > $OUT/kernels_kbench.md 2>&1
            head -24 $OUT/kernels_kbench.md; rm -f "$db" ;;
-    benchnew) ZEST_RIDE_RECORDS=1 ZG_LZ4_PAIR=auto timeout -k 10 700 python -u bench.py --modes bf16 \
-                --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
-              grep -h "aggregate" $log; tail -1 $log | cut -c1-400 ;;
     benchA|benchB) v=BENCH_ENV_${step#bench}; env ${!v:-} timeout -k 10 700 python -u bench.py --modes ${BENCH_MODES:-bf16} \
                 --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
               echo "env: ${!v:-}"; grep -h "aggregate" $log ;;

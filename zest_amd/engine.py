@@ -52,8 +52,6 @@ class RoundWork:
     terms_host: np.ndarray | None = None   # the same records on the host (host header walk)
     table_off: int = 0                     # byte offset of the round's chunk records in a host table
     compressed: bool = True                # any chunk of the round stored LZ4/BG4 (decoder launch needed)
-    rec_rel: int = 0                       # ride-along records: their offset from the span start (0 = none)
-    copy_len: int = 0                      # bytes of the round's H2D copy (span [+ gap + records])
 
 
 # Pinned allocations kept for reuse by the next OriginStore of this process (capacity, pointer).
@@ -79,10 +77,6 @@ def _staging_take(nbytes: int, device: torch.device) -> torch.Tensor:
 
 
 _role_stream = role_stream
-
-# Ride-along chunk records in the copy pipeline (DevicePuller.ride_records); ZEST_RIDE_RECORDS overrides.
-RIDE_RECORDS_DEFAULT = "0"
-
 
 def release_pinned_pool() -> None:
     """Free the pinned buffers kept by closed OriginStores."""
@@ -211,36 +205,20 @@ class DevicePuller:
         # Pipeline shape (see the streams below): "copy" when any chunk is stored compressed.
         compressed = bool(world.chunk_clen is not None and np.any(world.chunk_clen < world.chunk_len))
         pipeline = os.environ.get("ZEST_PIPELINE", "copy" if compressed else "lanes")
-        # Ride-along chunk records (copy pipeline): the host walks each round's chunk headers in the
-        # pinned origin right before the round's H2D copy is issued and writes the ZgChunk records
-        # just behind the round's bytes, so ONE copy brings bytes and records and the lane launches
-        # decode + place/hash directly -- no device header walk (k_index_terms: a one-thread-per-term
-        # HBM pointer chase, ~1 ms in front of every 1 GiB round's decode) and no separate record
-        # upload between the large transfers.  This is what the device-direct pull does with the
-        # records its fetch workers build (csrc/gpurt/device_pull.cpp).  ZEST_RIDE_RECORDS=0: device walk.
-        self.ride_records = (self.is_cuda and pipeline == "copy" and os.environ.get("ZEST_RIDE_RECORDS", RIDE_RECORDS_DEFAULT) != "0")
-        # this rank's origin layout: its terms' serialized bytes back to back, in order (with ride-along
-        # records: round by round, each round's span followed by its record area)
+        # The bf16 (copy) pipeline walks each round's chunk headers on the device (k_index_terms,
+        # ~0.6 ms per 1 GiB round on its lane, under the round's ~18 ms H2D copy).  Round 4 tried a
+        # host walk whose records rode the round's H2D copy: 58.4 vs 64.3 GB/s on the 70B bench
+        # (profiles/r4/bench_ride_records_r4c.log), so it was removed.
+        # this rank's origin layout: its terms' serialized bytes back to back, in order
         a_r, b_r = self.rank_terms[rank]
         ser_len = T["ser_len"][a_r:b_r].astype(np.int64)
         self.term_origin_off = np.concatenate([[0], np.cumsum(ser_len)]).astype(np.int64)  # relative to a_r
-        round_base, pos = [], 0
-        for k in range(self.n_rounds):
-            a, b = self.rounds_all[k][rank]
-            span_len = int(self.term_origin_off[b - a_r] - self.term_origin_off[a - a_r])
-            if self.ride_records:
-                nck = int(T["c1"][b - 1] - T["c0"][a]) if b > a else 0
-                round_base.append(pos)
-                pos += -(-(-(-span_len // 256) * 256 + nck * ops.CHUNK_DTYPE.itemsize) // 4096) * 4096
-            else:
-                round_base.append(int(self.term_origin_off[a - a_r]))
-        origin_bytes = pos if self.ride_records else int(self.term_origin_off[-1])
-        self.origin = OriginStore(origin_bytes, self.device, origin_reserve)
+        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device, origin_reserve)
         self.rounds: list[RoundWork] = []
         max_span, max_terms, max_chunks = 0, 1, 1
         for k in range(self.n_rounds):
             a, b = self.rounds_all[k][rank]
-            span_off = round_base[k]
+            span_off = int(self.term_origin_off[a - a_r])
             span_len = int(self.term_origin_off[b - a_r] - self.term_origin_off[a - a_r])
             if b > a:
                 c0 = int(T["c0"][a])
@@ -257,12 +235,9 @@ class DevicePuller:
             else:
                 c0, nck, rec, region, terms_dev = 0, 0, None, (0, 0), None
             comp = bool(world.chunk_scheme is not None and b > a and world.chunk_scheme[c0:c0 + nck].any())
-            rec_rel = -(-span_len // 256) * 256 if self.ride_records and b > a else 0
-            copy_len = rec_rel + nck * ops.CHUNK_DTYPE.itemsize if rec_rel else span_len
             self.rounds.append(RoundWork(a, b, c0, nck, span_off, span_len, region, terms_dev, rec,
-                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize, comp,
-                                         rec_rel, copy_len))
-            max_span = max(max_span, copy_len)
+                                         sum(r.n_chunks for r in self.rounds) * ops.CHUNK_DTYPE.itemsize, comp))
+            max_span = max(max_span, span_len)
             max_terms = max(max_terms, b - a)
             max_chunks = max(max_chunks, nck)
         self.regions = [[self._region(k, r) for r in range(n_ranks)] for k in range(self.n_rounds)]
@@ -318,9 +293,6 @@ class DevicePuller:
                 self.copy_stream = copy_stream
                 self.h2d_done = [torch.cuda.Event() for _ in self.staging]
                 self.slot_free = [torch.cuda.Event() for _ in self.staging]
-                # per round: its copy of the previous step has finished reading the origin, so the
-                # host may rewrite the round's ride-along records (None until first recorded)
-                self._rec_copied = [None] * self.n_rounds
         # Host run-ahead bound: step() issues ~10 HIP commands per round (~1300 per 70B step) in ~10 ms
         # and returns, so a caller looping over step() without syncing queues thousands of commands
         # over many steps, and past ~10 steps queued the HIP runtime fed the device measurably slower
@@ -388,7 +360,7 @@ class DevicePuller:
         H = ops.hip()
         st = torch.cuda.current_stream(self.device).cuda_stream
         tmp = ops.padded_empty(min(pack_batch_bytes, self.origin.n) + (64 << 20), self.device)
-        for rw in self.rounds:  # a round's span is contiguous in the origin (records may follow it)
+        for rw in self.rounds:  # a round's span is contiguous in the origin
             t = rw.term_a
             while t < rw.term_b:
                 base = int(self.term_origin_off[t - a_r])
@@ -472,34 +444,19 @@ class DevicePuller:
             self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
         return rec_ptr
 
-    def _ride_records(self, rw: RoundWork, k: int) -> None:
-        """Host header walk of round k's runs in the pinned origin, into the round's record area
-        right behind its bytes (one H2D copy then carries both).  The area is rewritten only after
-        the previous step's copy of this round has read it (its event), so the host runs at most one
-        step ahead of the copy engine, as step()'s run-ahead bound allows anyway."""
-        ev = self._rec_copied[k]
-        if ev is not None:
-            ev.synchronize()
-        e = _core.index_runs(self.origin.ptr + rw.span_off, rw.span_len, rw.terms_host.ctypes.data,
-                             rw.term_b - rw.term_a, self.origin.ptr + rw.span_off + rw.rec_rel, rw.n_chunks)
-        if e:
-            self.err.fill_(e)  # (stream-ordered, like the device walk's error word)
-
-    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int, chunks_ptr: int | None = None) -> None:
-        """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes.
-        `chunks_ptr`: device address of the round's chunk records already in staging (ride-along)."""
+    def _ingest_round(self, H, rw: RoundWork, src: torch.Tensor, ws, st: int) -> None:
+        """Round rw on stream st: header walk (host or device), place/decode, BLAKE3 chunk hashes."""
         if rw.term_b <= rw.term_a:
             return
         nbytes = rw.n_chunks * ops.CHUNK_DTYPE.itemsize
-        if chunks_ptr is None:
-            chunks = ws.chunks
-            chunks_ptr = chunks.data_ptr()
-            if self.host_index and not self._capturing:
-                H.memcpy_async(chunks_ptr, self._host_records(rw), nbytes, st)
-            else:
-                chunks[:nbytes].zero_()
-                ops.index_terms(H, src.data_ptr(), rw.span_len, rw.terms_dev.data_ptr(), rw.term_b - rw.term_a,
-                                chunks_ptr, self.err.data_ptr(), st, None if self._capturing else ws)
+        chunks = ws.chunks
+        chunks_ptr = chunks.data_ptr()
+        if self.host_index and not self._capturing:
+            H.memcpy_async(chunks_ptr, self._host_records(rw), nbytes, st)
+        else:
+            chunks[:nbytes].zero_()
+            ops.index_terms(H, src.data_ptr(), rw.span_len, rw.terms_dev.data_ptr(), rw.term_b - rw.term_a,
+                            chunks_ptr, self.err.data_ptr(), st, None if self._capturing else ws)
         sp, sb = ws.hash_scratch.get(rw.n_chunks, rw.region[1] - rw.region[0])
         if ops.FUSED_INGEST:
             # decode (compressed rounds only) + ONE pass that places raw chunks and hashes every chunk
@@ -571,27 +528,20 @@ class DevicePuller:
                 if self._rx:
                     _core.trace.roctx_push(f"engine: round {k}")
                 copy_mode = self.pipeline == "copy" and not self._capturing
-                chunks_ptr = None
                 if copy_mode:
                     slot = k % len(self.staging)
-                    if rw.rec_rel:
-                        self._ride_records(rw, k)
-                        chunks_ptr = src.data_ptr() + rw.rec_rel
                     with torch.cuda.stream(self.copy_stream):
                         self.copy_stream.wait_event(self.slot_free[slot])  # no-op before first use
-                        if rw.copy_len:
-                            H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.copy_len,
+                        if rw.span_len:
+                            H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len,
                                            self.copy_stream.cuda_stream)
                         self.h2d_done[slot].record(self.copy_stream)
-                        if rw.rec_rel:
-                            ev = self._rec_copied[k] = self._rec_copied[k] or torch.cuda.Event()
-                            ev.record(self.copy_stream)
                 with torch.cuda.stream(comp):
                     if copy_mode:
                         comp.wait_event(self.h2d_done[slot])
                     elif rw.span_len:
                         H.memcpy_async(src.data_ptr(), self.origin.ptr + rw.span_off, rw.span_len, st)
-                    self._ingest_round(H, rw, src, ws, st, chunks_ptr)
+                    self._ingest_round(H, rw, src, ws, st)
                     if copy_mode:
                         self.slot_free[slot].record(comp)
                     if self.n_ranks > 1:

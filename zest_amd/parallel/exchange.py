@@ -537,10 +537,12 @@ class RoundExchange:
             # gloo moves device tensors only through its collectives; a batched isend/irecv of
             # device tensors never completed (2-rank rehearsal on one GPU)
             modes = tuple(m for m in modes if m != "p2p")
-        # Time on a prefix of every region: bandwidth over xGMI is flat well below a 1 GiB round, and
-        # a sweep of full rounds (modes x passes x rounds) cost seconds of setup in the one-GPU
-        # rehearsal, where gloo stages device tensors through the host (profiles/r4/swarm_pull_r4b.json).
-        cap = int(os.environ.get("ZEST_AUTOTUNE_MB", "256" if self.backend() == "nccl" else "32")) << 20
+        # Time on a 256 MiB prefix of every region: bandwidth over xGMI is flat well below a 1 GiB
+        # round, and a sweep of full rounds (modes x passes x rounds) cost seconds of setup in the
+        # one-GPU rehearsal, where gloo stages device tensors through the host
+        # (profiles/r4/swarm_pull_r4b.json).  Much smaller prefixes drown the modes' differences in
+        # fixed costs (32 MiB: every mode 0.080 s in a 4-rank rehearsal, profiles/r4/rehearsal_n4_r4c.log).
+        cap = int(os.environ.get("ZEST_AUTOTUNE_MB", "256")) << 20
         region_lists = [[(lo, min(hi, lo + cap)) if hi > lo else (lo, hi) for lo, hi in regs] for regs in region_lists]
         times = {}
         moved = self.bytes_moved
