@@ -266,7 +266,8 @@ def main():
         # header walk k_index_terms, at a small launch (256 MiB, ~4 k chunks: fewer chunks than wave
         # slots) and a bench round (1 GiB).  (A scan-based header walk measured here at 5.4 / 12.3 ms
         # against 0.51 / 0.61 ms serial was removed: profiles/r4/kbench_k3pair_r4b.jsonl.)
-        for m, tag in ((256 << 20, "bf16_256m"), (1 << 30, "bf16_1g")):
+        for m, tag in ((128 << 20, "bf16_128m"), (256 << 20, "bf16_256m"), (512 << 20, "bf16_512m"),
+                       (768 << 20, "bf16_768m"), (1 << 30, "bf16_1g")):
             w = (np.random.default_rng(0).standard_normal(m // 2).astype(np.float32) * 0.02)
             raw = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
             del w
