@@ -876,14 +876,18 @@ extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, 
     const char* v = getenv("ZG_LZ4_GRID");
     return v ? atoi(v) : 0;
   }();
-  // ZG_LZ4_PAIR: 1 = producer/consumer pairs for every launch, auto = for launches with fewer chunks
-  // than the one-wave grid holds (2 x 8192 here), 0 / unset = the one-wave decoder.
+  // ZG_LZ4_PAIR: 1 = producer/consumer pairs for every launch, 0 = the one-wave decoder, auto
+  // (default) = pairs for launches of fewer than kPairBelow chunks.  Measured on BG4 bf16 (kbench
+  // k3pair, profiles/r4/kbench_k3pair_sizes_r4e.jsonl), one-wave -> pair: 128 MiB (2.1 k chunks)
+  // 46 -> 70 GB/s, 256 MiB 79 -> 83, 512 MiB (8.4 k) 93 -> 106, but 768 MiB (12.6 k) 117 -> 108 and
+  // 1 GiB 120 -> 112: pairs pay off while the chunks do not fill the one-wave grid's 8192 waves.
+  constexpr int kPairBelow = 10240;
   static const int pair = [] {
     const char* v = getenv("ZG_LZ4_PAIR");
-    if (!v) return 0;
-    return std::string(v) == "auto" ? 2 : atoi(v) ? 1 : 0;
+    if (!v || std::string(v) == "auto") return 2;
+    return atoi(v) ? 1 : 0;
   }();
-  if (pair == 1 || (pair == 2 && n_chunks < 16384))
+  if (pair == 1 || (pair == 2 && n_chunks < kPairBelow))
     return zg_lz4_pair_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, stream);
   return zg_lz4_batched_decode_grid(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, stream);
 }

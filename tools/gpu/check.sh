@@ -22,7 +22,7 @@
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
 #   hostbench   `zest bench --synthetic` on the box's CPU
 #   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
-#   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=auto")
+#   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=0")
 #   swarm       term-sharded swarm_pull GPU tests (modes, VMM fault hooks) (tests/test_gpu_device.py -k swarm_pull)
 #   swarmbench  public pull(device="all") end to end from a loopback HBM seeder, $SWARM_RANKS (1,2,3) ranks,
 #               $SWARM_MODEL (llama-3.1-8b) -> swarm_pull.json
