@@ -11,6 +11,8 @@
 // (src/bt_peer.zig); this is the intra-node replacement (SURVEY §5.8 "direct P2P all-to-all").
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "zgpu.h"
 
 namespace {
@@ -65,10 +67,19 @@ extern "C" hipError_t zg_peer_gather(const ZgPeerSegs* segs, hipStream_t stream)
     if (segs->n[i] > max_n) max_n = segs->n[i];
   }
   if (max_n == 0) return hipSuccess;
-  // ~8 blocks per CU over the whole launch (256 CUs), at least one per segment.
+  // At most ~2 blocks per CU (512 over 256 CUs; ZG_PEER_GATHER_BLOCKS overrides), at least one per
+  // segment.  The gather runs next to the round's decode and hash kernels, and the decoder is
+  // occupancy-bound (profiles/lz4_records_r3.md): a grid of 8 blocks per CU would take every wave
+  // slot for the whole transfer.  512 blocks keep 512 x 256 lanes x 128 B = 16 MiB of remote reads
+  // in flight, far above the bandwidth-delay product of 7 links (~350 GB/s x a few us).
+  static const uint64_t total = [] {
+    const char* v = getenv("ZG_PEER_GATHER_BLOCKS");
+    const long b = v ? atol(v) : 512;
+    return uint64_t(b < 1 ? 1 : b > 8192 ? 8192 : b);
+  }();
   const uint64_t per_block = uint64_t(kThreads) * kUnroll * 16;
   uint64_t bps = (max_n + per_block - 1) / per_block;
-  const uint64_t cap = 2048 / uint64_t(segs->nseg);
+  const uint64_t cap = total / uint64_t(segs->nseg);
   if (bps > cap) bps = cap;
   if (bps < 1) bps = 1;
   hipLaunchKernelGGL(k_peer_gather, dim3(uint32_t(bps) * uint32_t(segs->nseg)), dim3(kThreads), 0, stream, *segs,
