@@ -391,7 +391,8 @@ class _Swarm:
                 commit, files = _core.list_repo_files(self.repo, self.revision, self.repo_type)
                 st = [f for f in files if f["path"].endswith(".safetensors")]
                 xet = [f for f in st if f["xet_hash"]]
-                shapes = _parallel_map(lambda f: [tuple(x) for x in self.fetcher.shapes(f["xet_hash"])], xet, 8)
+                shapes = _parallel_map(lambda f: [tuple(x) for x in self.fetcher.shapes(f["xet_hash"])], xet,
+                                        max(8, self.fetcher.threads))
                 obj = ("ok", commit, st, shapes)
             except Exception as e:  # noqa: BLE001 - every rank leaves the same way
                 obj = ("err", f"{type(e).__name__}: {e}")
