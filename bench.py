@@ -374,7 +374,17 @@ def topology(dist, device, world_size: int):
     return int(one.item()), ids, len(set(ids)) == world_size and "cpu" not in ids
 
 
+# HIP hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default, and the box's setting, is 4).
+# A rank drives up to ~9 streams (copy, two compute lanes, verify, up to four peer-copy streams or
+# the all-gather unpack, the caller's) and HIP maps streams onto the hardware queues round-robin, so
+# with 4 queues independent streams share in-order queues.  8 measured neutral at N = 1 (70B:
+# 64.44 / 56.85 GB/s vs 64.23 / 56.83 with 4, profiles/r4/bench_hwq8_r4g.log).  Set before HIP starts.
+HW_QUEUES = "8"
+
+
 def rank_main(a) -> None:
+    if a.device == "cuda" and os.environ.get("ZEST_BENCH_HW_QUEUES", HW_QUEUES) != "0":
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZEST_BENCH_HW_QUEUES", HW_QUEUES)
     import torch
 
     from zest_amd import models, ops
