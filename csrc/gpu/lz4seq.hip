@@ -184,6 +184,48 @@ __device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
   X.out[bmap(X, p)] = uint8_t(v);
 }
 
+// Literal runs of at least kWideLit bytes in a long batch (BG4 bf16: the two mantissa planes of a
+// chunk are ~16 KiB literal runs each, ~half of every chunk's output) are copied 16 bytes per lane,
+// 1 KiB per wave pass: five aligned dword loads + v_alignbyte, then 16 byte stores at one address
+// with immediate offsets (stride 4 inside one BG4 group, 1 otherwise).  The lane-per-byte literal
+// passes spend ~35 wave instructions per 64 bytes (lane -> record map, shuffles, a byte load and a
+// byte store per lane); this is ~2-3 per 64 bytes.  Only long batches take it: their match sources
+// come back from HBM and their LDS ring is rebuilt from HBM afterwards, so these bytes need not
+// enter the ring.
+constexpr uint32_t kWideLit = 512;
+
+__device__ __forceinline__ void wide_literals(const Ctx& X, uint32_t src, uint32_t dst, uint32_t n, uint32_t lane) {
+  for (uint32_t off = lane * 16u; off < n; off += 16u * kWave) {
+    const uint32_t cnt = n - off < 16u ? n - off : 16u;
+    const uint32_t p0 = dst + off;  // grouped-stream position of the lane's first byte
+    const uint8_t* a = X.pay + src + off;
+    if (cnt == 16u) {
+      const uintptr_t ai = reinterpret_cast<uintptr_t>(a);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(ai & ~uintptr_t(3));
+      const uint32_t sh = uint32_t(ai & 3);
+      uint32_t d[5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = w[i];
+      d[4] = sh ? w[4] : 0u;  // (the literals are followed by >= 4 frame bytes: end mark / next token)
+      uint32_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);  // shift in bytes
+      const uint32_t q0 = bmap(X, p0), q1 = bmap(X, p0 + 15u);
+      const uint32_t step = X.bg4 ? 4u : 1u;
+      if (q1 == q0 + 15u * step) {  // one BG4 group (or no BG4): fixed stride
+        uint8_t* o = X.out + q0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[j * step] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) X.out[bmap(X, p0 + uint32_t(j))] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
+      }
+    } else {
+      for (uint32_t j = 0; j < cnt; ++j) X.out[bmap(X, p0 + j)] = a[j];
+    }
+  }
+}
+
 // Execute the batch's records.  Returns false (nothing written for the bad records) when any
 // record is out of range.
 //
@@ -205,7 +247,12 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   const uint32_t ml = !valid ? 0u : gen ? ((B.rx >> 16) & 0x7FFF) : (tok & 15) + 4;
   const uint32_t off = B.rh & 0xFFFF;
   const uint32_t a2 = scan_add(lit + ml);
-  const uint32_t li = scan_add(lit), mi = scan_add(ml);
+  const uint32_t span = __builtin_amdgcn_readlane(a2, 63);
+  const bool long_batch = span + 4 * kWave >= kRing;
+  // long literal runs of a long batch go through wide_literals, the rest one byte per lane
+  const bool wide = long_batch && lit >= kWideLit;
+  const uint32_t litp = wide ? 0u : lit;
+  const uint32_t li = scan_add(litp), mi = scan_add(ml);
   const uint32_t opos = X.obase + a2 - lit - ml;  // output offset of the record
   const uint32_t mstart = opos + lit;          // output offset of its match
   const bool bad = valid && (lpos + lit > X.clen || mstart + ml > X.ulen || (ml && (off == 0 || off > mstart)));
@@ -213,14 +260,18 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
   B.rl = B.rh = B.rx = 0;
   if (__builtin_amdgcn_ballot_w64(bad)) return false;
   const uint32_t ltot = __builtin_amdgcn_readlane(li, 63), mtot = __builtin_amdgcn_readlane(mi, 63);
-  const uint32_t span = __builtin_amdgcn_readlane(a2, 63);
   X.obase += span;
   const uint32_t oend = X.obase;  // one past the batch's last output byte
   // Far match sources (kRing or more behind the batch end) are read back from HBM, so every earlier
   // store must be acknowledged first; a short batch whose sources all lie in the LDS ring skips
   // that wait (BG4 exponent-plane matches are short-range).
-  if (span + 4 * kWave >= kRing || __builtin_amdgcn_ballot_w64(ml != 0 && oend - (mstart - off) >= kRing))
+  if (long_batch || __builtin_amdgcn_ballot_w64(ml != 0 && oend - (mstart - off) >= kRing))
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // earlier batches' stores are in L2
+  for (uint64_t wm = __builtin_amdgcn_ballot_w64(wide); wm; wm &= wm - 1) {
+    const uint32_t r = uint32_t(__builtin_ctzll(wm));
+    wide_literals(X, __builtin_amdgcn_readlane(lpos, r), __builtin_amdgcn_readlane(opos, r),
+                  __builtin_amdgcn_readlane(lit, r), lane);
+  }
   // literal bytes, one per lane; four passes' loads in flight at once
   for (uint32_t g0 = 0; g0 < ltot; g0 += 4 * kWave) {
     uint32_t to[4], v[4];
@@ -231,8 +282,8 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
       v[j] = 0;
       if (t0 < ltot) {
         const uint32_t t = t0 + lane;
-        const uint32_t s = owner(X, li - lit, li, t0, lane);
-        const uint32_t k = t - shfl(li - lit, s);
+        const uint32_t s = owner(X, li - litp, li, t0, lane);
+        const uint32_t k = t - shfl(li - litp, s);
         const uint32_t from = shfl(lpos, s) + k, dst = shfl(opos, s) + k;  // all lanes shuffle
         if (t < ltot) {
           to[j] = dst;
@@ -245,7 +296,7 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
     for (int j = 0; j < 4; ++j)
       if (to[j] != 0xFFFFFFFFu) put_byte(X, to[j], v[j]);
   }
-  if (span + 4 * kWave < kRing) {
+  if (!long_batch) {
     // short batch: far sources all precede it (already visible); group four passes
     for (uint32_t g0 = 0; g0 < mtot; g0 += 4 * kWave) {
       MatchLane m[4];
@@ -279,8 +330,22 @@ __device__ bool exec_batch(Batch& B, Ctx& X, uint32_t lane) {
       if (m.on) X.out[bmap(X, m.d)] = uint8_t(load_u8_coherent(X.out + bmap(X, m.q)));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ring rebuild: eight loads per lane in flight before their LDS stores (one L2 round trip per
+    // 512 bytes instead of one per 64)
     const uint32_t lo = oend > kRing ? oend - kRing : 0u;
-    for (uint32_t p = lo + lane; p < oend; p += kWave) X.ring[p & (kRing - 1)] = uint8_t(load_u8_coherent(X.out + bmap(X, p)));
+    for (uint32_t p0 = lo; p0 < oend; p0 += 8 * kWave) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t p = p0 + uint32_t(j) * kWave + lane;
+        v[j] = p < oend ? load_u8_coherent(X.out + bmap(X, p)) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t p = p0 + uint32_t(j) * kWave + lane;
+        if (p < oend) X.ring[p & (kRing - 1)] = uint8_t(v[j]);
+      }
+    }
   }
   return true;
 }

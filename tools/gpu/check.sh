@@ -20,6 +20,7 @@
 #   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group, e.g. k3pair)
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
+#   kpmc        rocprofv3 --pmc SQ counters (per launch) of kbench ($KBENCH_ONLY), kernels matching $PMC_KERNEL
 #   hostbench   `zest bench --synthetic` on the box's CPU
 #   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
 #   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=0")
@@ -87,6 +88,13 @@ for step in "$@"; do
     swarmbench) timeout -k 10 700 python -u tools/swarm_bench.py --model ${SWARM_MODEL:-llama-3.1-8b} \
                   --ranks ${SWARM_RANKS:-1,2,3} ${SWARM_ARGS:-} --out $OUT/swarm_pull.json > $log 2>&1 || fail $step $? $log
                 grep -h "^\[" $log ;;
+    kpmc) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
+            SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAVES --kernel-trace -d $OUT/pmc -o p \
+            --output-format csv -- python3 tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} > $log 2>&1 \
+            || fail $step $? $log
+          f=$(find $OUT/pmc -name "*counter_collection.csv" | head -1)
+          python tools/gpu/pmc_summary.py "$f" "${PMC_KERNEL:-lz4}" > $OUT/pmc_summary.txt 2>&1; cat $OUT/pmc_summary.txt
+          rm -rf $OUT/pmc ;;
     hostbench) ./zest_amd/_bin/zest bench --synthetic > $log 2>&1 || fail $step $? $log
                lscpu | grep -E "Model name|^CPU\(s\)" >> $log; cat $log ;;
     *) echo "[check] unknown step $step"; exit 2 ;;
