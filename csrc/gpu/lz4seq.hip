@@ -185,45 +185,41 @@ __device__ __forceinline__ void put_byte(const Ctx& X, uint32_t p, uint32_t v) {
 }
 
 // Literal runs of at least kWideLit bytes in a long batch (BG4 bf16: the two mantissa planes of a
-// chunk are ~16 KiB literal runs each, ~half of every chunk's output) are copied 16 bytes per lane,
-// 1 KiB per wave pass: five aligned dword loads + v_alignbyte, then 16 byte stores at one address
-// with immediate offsets (stride 4 inside one BG4 group, 1 otherwise).  The lane-per-byte literal
-// passes spend ~35 wave instructions per 64 bytes (lane -> record map, shuffles, a byte load and a
-// byte store per lane); this is ~2-3 per 64 bytes.  Only long batches take it: their match sources
-// come back from HBM and their LDS ring is rebuilt from HBM afterwards, so these bytes need not
-// enter the ring.
+// chunk are ~16 KiB literal runs each, ~half of every chunk's output) are copied 1 KiB per wave
+// step: lane i moves stream bytes i, i + 64, ..., i + 960, sixteen byte loads then sixteen byte
+// stores from one address each with immediate offsets (64 B apart in the payload; 256 B apart in a
+// BG4 group's output, 64 B otherwise).  Every load and store instruction stays coalesced (64
+// consecutive payload bytes; 64 output bytes 4 apart = 4 lines), and the lane -> record map,
+// shuffles and BG4 address math of the lane-per-byte literal passes (~35 wave instructions per 64
+// bytes) drop to ~2.  (A 16-bytes-per-lane variant -- one dwordx4-sized read per lane -- scattered
+// each byte store over 64 lines and made the one-wave decoder 10 % slower.)  Only long batches take
+// it: their match sources come back from HBM and their LDS ring is rebuilt from HBM afterwards, so
+// these bytes need not enter the ring.
 constexpr uint32_t kWideLit = 512;
 
 __device__ __forceinline__ void wide_literals(const Ctx& X, uint32_t src, uint32_t dst, uint32_t n, uint32_t lane) {
-  for (uint32_t off = lane * 16u; off < n; off += 16u * kWave) {
-    const uint32_t cnt = n - off < 16u ? n - off : 16u;
-    const uint32_t p0 = dst + off;  // grouped-stream position of the lane's first byte
-    const uint8_t* a = X.pay + src + off;
-    if (cnt == 16u) {
-      const uintptr_t ai = reinterpret_cast<uintptr_t>(a);
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(ai & ~uintptr_t(3));
-      const uint32_t sh = uint32_t(ai & 3);
-      uint32_t d[5];
+  constexpr uint32_t kStep = 16 * kWave;
+  uint32_t base = 0;
+  for (; base + kStep <= n; base += kStep) {
+    const uint8_t* a = X.pay + src + base + lane;
+    uint32_t v[16];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) d[i] = w[i];
-      d[4] = sh ? w[4] : 0u;  // (the literals are followed by >= 4 frame bytes: end mark / next token)
-      uint32_t v[4];
+    for (int j = 0; j < 16; ++j) v[j] = a[j * kWave];
+    const uint32_t q0 = bmap(X, dst + base), q1 = bmap(X, dst + base + kStep - 1);
+    if (!X.bg4) {
+      uint8_t* o = X.out + q0 + lane;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);  // shift in bytes
-      const uint32_t q0 = bmap(X, p0), q1 = bmap(X, p0 + 15u);
-      const uint32_t step = X.bg4 ? 4u : 1u;
-      if (q1 == q0 + 15u * step) {  // one BG4 group (or no BG4): fixed stride
-        uint8_t* o = X.out + q0;
+      for (int j = 0; j < 16; ++j) o[j * kWave] = uint8_t(v[j]);
+    } else if (q1 - q0 == 4 * (kStep - 1)) {  // one BG4 group: byte p goes to 4 p + c
+      uint8_t* o = X.out + q0 + 4 * lane;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) o[j * step] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
-      } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) X.out[bmap(X, p0 + uint32_t(j))] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
-      }
+      for (int j = 0; j < 16; ++j) o[j * 4 * kWave] = uint8_t(v[j]);
     } else {
-      for (uint32_t j = 0; j < cnt; ++j) X.out[bmap(X, p0 + j)] = a[j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) X.out[bmap(X, dst + base + uint32_t(j) * kWave + lane)] = uint8_t(v[j]);
     }
   }
+  for (uint32_t p = base + lane; p < n; p += kWave) X.out[bmap(X, dst + p)] = X.pay[src + p];
 }
 
 // Execute the batch's records.  Returns false (nothing written for the bad records) when any
