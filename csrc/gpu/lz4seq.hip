@@ -508,7 +508,10 @@ __device__ uint32_t decode_chunk(Ctx& X, uint32_t lane) {
   return X.obase == X.ulen ? 0u : uint32_t(ZG_ERR_SIZE);
 }
 
-__global__ void __launch_bounds__(256) k_lz4_batched(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+// amdgpu_waves_per_eu(8): keep 8 waves per SIMD (<= 64 VGPRs).  The decoder is occupancy-bound
+// (profiles/lz4_records_r3.md), and with the wide literal copy inlined the register allocator
+// otherwise settled on 127 VGPRs = 4 waves per SIMD (hipcc -Rpass-analysis=kernel-resource-usage).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_batched(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                      const ZgChunk* __restrict__ chunks, int n_chunks,
                                                      unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
   __shared__ uint32_t heads[kWavesPerBlock][kWave];
@@ -604,7 +607,8 @@ __device__ __forceinline__ bool lds_wait(PairLds& L, const uint32_t* p, uint32_t
   return true;
 }
 
-__global__ void __launch_bounds__(128) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+// (8 waves per SIMD: see k_lz4_batched)
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   const ZgChunk* __restrict__ chunks, int n_chunks,
                                                   unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
   __shared__ PairLds L;
@@ -937,15 +941,17 @@ extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, 
     const char* v = getenv("ZG_LZ4_GRID");
     return v ? atoi(v) : 0;
   }();
-  // ZG_LZ4_PAIR: 1 = producer/consumer pairs for every launch, 0 = the one-wave decoder, auto
-  // (default) = pairs for launches of fewer than kPairBelow chunks.  Measured on BG4 bf16 (kbench
-  // k3pair, profiles/r4/kbench_k3pair_sizes_r4e.jsonl), one-wave -> pair: 128 MiB (2.1 k chunks)
-  // 46 -> 70 GB/s, 256 MiB 79 -> 83, 512 MiB (8.4 k) 93 -> 106, but 768 MiB (12.6 k) 117 -> 108 and
-  // 1 GiB 120 -> 112: pairs pay off while the chunks do not fill the one-wave grid's 8192 waves.
+  // ZG_LZ4_PAIR: 1 (default) = producer/consumer pairs, 0 = the one-wave decoder, auto = pairs for
+  // launches of fewer than kPairBelow chunks.  With the wide literal copies and both kernels held at
+  // 8 waves per SIMD, pairs win at every size (BG4 bf16, kbench k3pair, one-wave -> pair: 128 MiB
+  // 48 -> 78 GB/s, 256 MiB 82 -> 95, 512 MiB 95 -> 124, 1 GiB 123 -> 136;
+  // profiles/r4/kbench_k3_wide_r4j.jsonl).  Before them the one-wave decoder won from ~10 k chunks
+  // up (profiles/r4/kbench_k3pair_sizes_r4e.jsonl), which is what `auto` keeps.
   constexpr int kPairBelow = 10240;
   static const int pair = [] {
     const char* v = getenv("ZG_LZ4_PAIR");
-    if (!v || std::string(v) == "auto") return 2;
+    if (!v) return 1;
+    if (std::string(v) == "auto") return 2;
     return atoi(v) ? 1 : 0;
   }();
   if (pair == 1 || (pair == 2 && n_chunks < kPairBelow))

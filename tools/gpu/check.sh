@@ -20,6 +20,8 @@
 #   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group, e.g. k3pair)
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
 #   kprof       rocprofv3 --kernel-trace --stats of kbench ($KBENCH_ONLY) -> per-kernel summary
+#   kvar        kbench ($KBENCH_ONLY) once per kernel-build variant in $VARIANTS (dirs under variants/, each a
+#               zest_amd package copy with its own _hip .so) -> kbench_<variant>.jsonl
 #   kpmc        rocprofv3 --pmc SQ counters (per launch) of kbench ($KBENCH_ONLY), kernels matching $PMC_KERNEL
 #   hostbench   `zest bench --synthetic` on the box's CPU
 #   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
@@ -88,6 +90,11 @@ for step in "$@"; do
     swarmbench) timeout -k 10 700 python -u tools/swarm_bench.py --model ${SWARM_MODEL:-llama-3.1-8b} \
                   --ranks ${SWARM_RANKS:-1,2,3} ${SWARM_ARGS:-} --out $OUT/swarm_pull.json > $log 2>&1 || fail $step $? $log
                 grep -h "^\[" $log ;;
+    kvar) for v in ${VARIANTS:?}; do
+            ZEST_PKG_ROOT=variants/$v timeout -k 10 300 python -u tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} \
+              > $OUT/kbench_$v.jsonl 2>> $log || fail $step $? $log
+            echo "variant $v"; grep -h '"kernel"' $OUT/kbench_$v.jsonl | cut -c1-110
+          done ;;
     kpmc) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
             SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAVES --kernel-trace -d $OUT/pmc -o p \
             --output-format csv -- python3 tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} > $log 2>&1 \

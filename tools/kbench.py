@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import time
 
 import sys
@@ -17,6 +18,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+if os.environ.get("ZEST_PKG_ROOT"):  # A/B of kernel builds: a package copy with another _hip .so
+    sys.path.insert(0, os.environ["ZEST_PKG_ROOT"])
 
 from zest_amd import _core as C
 from zest_amd import ops
