@@ -296,6 +296,57 @@ def test_swarm_pull_eight_ranks_lose_two(hub_env):
     assert dt < 170, dt
 
 
+def _store_worker(rank, world_size, port, repo, q, fault):
+    """Like _elastic_worker, with the rendezvous store hosted by the test process (as torchrun's
+    agent hosts it), so that rank 0 may die too."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZEST_SWARM_FAULT=fault,
+                      ZEST_SWARM_CTL_TIMEOUT="20", ZEST_SWARM_HB_STALE="3")
+    store = dist.TCPStore("127.0.0.1", port, world_size, is_master=False)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world_size)
+    from zest_amd.parallel import swarm_pull
+    st = {}
+    try:
+        t = swarm_pull(repo, p2p=False, dht=False, stats=st, round_bytes=256 << 10)
+        q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
+    except Exception as e:
+        q.put((rank, type(e).__name__, str(e), st))
+
+
+def test_swarm_pull_survives_losing_the_planning_rank(hub_env):
+    """Rank 0 lists the repository and makes the plan; here it dies doing so.  The others wait for
+    the plan only while rank 0's heartbeat is fresh, then rebuild their groups without it, and the
+    next survivor plans: ranks 1 and 2 end with every tensor."""
+    import queue as _q
+    world, hub = hub_env
+    want = _expected(world)
+    port = free_port()
+    store = torch.distributed.TCPStore("127.0.0.1", port, 3, is_master=True, wait_for_workers=False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_store_worker, args=(r, 3, port, world.spec.repo_id, q, "exit:0:-1")) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = []
+    for _ in range(2):
+        try:
+            res.append(q.get(timeout=180))
+        except _q.Empty:
+            break
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    del store
+    res.sort(key=lambda r: r[0])
+    assert procs[0].exitcode == 1
+    assert [r[0] for r in res] == [1, 2] and [r[1] for r in res] == ["ok", "ok"], res
+    for _, _, got, st in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert st["world"] == 2
+
+
 def test_swarm_plan_term_shares_and_jobs():
     """The plan behind swarm_pull: files laid out 4 KiB aligned in one arena, byte-balanced contiguous
     term shares per rank, rounds cut by bytes with the head/tail taper, and a round item spanning two

@@ -329,7 +329,7 @@ class _Fetcher:
 # ----------------------------------------------------------------------------------------------
 def _fault_spec() -> dict:
     """ZEST_SWARM_FAULT items: "<rank>:<round>" (that fetch raises), "exit:<rank>:<round>" (that
-    rank's process exits at that round)."""
+    rank's process exits at that round; round -1: while the listing / plan is made)."""
     out = {"fail": set(), "exit": set()}
     for item in os.environ.get("ZEST_SWARM_FAULT", "").split(","):
         p = item.split(":")
@@ -382,10 +382,33 @@ class _Swarm:
             raise _RankLost(str(e)) from e
         return box[0]
 
+    def _plan_from0(self, obj):
+        """Rank 0's listing/plan to every rank.  Through the rendezvous store when there is one: the
+        listing (a CAS reconstruction per file) may take longer than the control group's bounded
+        timeout on a slow network, so the other ranks wait for as long as rank 0's heartbeat stays
+        fresh instead of failing a timed-out collective and rebuilding groups around a rank that is
+        only slow.  Without a store: a broadcast on the control group."""
+        m = self.m
+        if not m.enabled:
+            return self._bcast_from0(obj)
+        key = f"{m.prefix}/e{m.epoch}/plan"
+        if m.rank == 0:
+            m.store.set(key, json.dumps(obj))
+            return obj
+        root, t0 = m.granks[0], time.time()
+        while not m.store.check([key]):
+            # (a root that has not stamped its first heartbeat yet counts from when this wait began)
+            if time.time() - max(m._last_beat(root), t0) > m.stale_s:
+                raise _RankLost(f"rank {root} stopped while listing {self.repo}")  # survivors re-plan
+            time.sleep(0.05)
+        return json.loads(m.store.get(key))
+
     # -- setup --------------------------------------------------------------------------------
     def listing_and_plan(self):
         t = time.perf_counter()
         obj = None
+        if (self.m.me, -1) in self.fault["exit"]:
+            os._exit(1)  # fault injection (tests): this rank dies while the plan is being made
         if self.m.rank == 0:
             try:
                 commit, files = _core.list_repo_files(self.repo, self.revision, self.repo_type)
@@ -396,7 +419,7 @@ class _Swarm:
                 obj = ("ok", commit, st, shapes)
             except Exception as e:  # noqa: BLE001 - every rank leaves the same way
                 obj = ("err", f"{type(e).__name__}: {e}")
-        obj = self._bcast_from0(obj)
+        obj = self._plan_from0(obj)
         if obj[0] != "ok":
             raise SwarmPullError(f"listing/planning {self.repo}@{self.revision} failed on rank 0: {obj[1]}")
         _, self.commit, st_files, shapes = obj
