@@ -241,7 +241,11 @@ class _Membership:
             return 0.0
 
     def close(self):
+        # stop the heartbeat thread before the caller tears the process down: a daemon thread caught
+        # inside a store call at interpreter exit aborted the process (SIGABRT) now and then
         self._stop.set()
+        if self._hb is not None:
+            self._hb.join(timeout=10)
 
     def rebuild(self) -> list[int]:
         """Agree on the survivors, rebuild ctl/data groups over them; returns the lost ranks
