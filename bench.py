@@ -383,7 +383,11 @@ HW_QUEUES = "8"
 
 
 def rank_main(a) -> None:
-    if a.device == "cuda" and os.environ.get("ZEST_BENCH_HW_QUEUES", HW_QUEUES) != "0":
+    # Only when every rank has a GPU of its own: ranks sharing one GPU (the gloo rehearsal) would
+    # stack 4 x 8 queues on one device, and the 4-rank rehearsal ran 133-150 GB/s with 8 queues per
+    # rank against 186 with 4 (profiles/r4/rehearsal_r4d.log, rehearsal_n4_hwq8_r4l.log).
+    if (a.device == "cuda" and os.environ.get("ZEST_BENCH_BACKEND", "nccl") == "nccl"
+            and os.environ.get("ZEST_BENCH_HW_QUEUES", HW_QUEUES) != "0"):
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZEST_BENCH_HW_QUEUES", HW_QUEUES)
     import torch
 
