@@ -46,6 +46,9 @@ void init_locked(State& s, const char* v) {
     return;
   }
   s.path = v;
+  // "%p" in the path: this process's pid (several processes tracing at once, e.g. a swarm's ranks
+  // and the seeder they pull from)
+  if (const size_t k = s.path.find("%p"); k != std::string::npos) s.path.replace(k, 2, std::to_string(::getpid()));
   s.mode.store(kFile);
   if (!s.atexit_registered) {
     std::atexit(at_exit);

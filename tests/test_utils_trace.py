@@ -87,3 +87,22 @@ def test_roctx_ranges_optional():
         assert r.returncode == 0, r.stderr
         if want:
             assert r.stdout.strip() == f"roctx {want}"
+
+
+def test_trace_path_pid_substitution(tmp_path):
+    """ZEST_TRACE=...%p...: each process writes its own trace (a swarm's ranks and their seeder)."""
+    code = """
+from zest_amd.utils import Span
+with Span("test", "one"):
+    pass
+"""
+    env = dict(os.environ, ZEST_TRACE=str(tmp_path / "t.%p.json"))
+    root = str(__import__("pathlib").Path(__file__).resolve().parents[1])
+    pids = []
+    for _ in range(2):
+        p = subprocess.Popen([sys.executable, "-c", code], env=env, cwd=root)
+        assert p.wait() == 0
+        pids.append(p.pid)
+    for pid in pids:
+        ev = json.loads((tmp_path / f"t.{pid}.json").read_text())["traceEvents"]
+        assert any(e.get("name") == "one" for e in ev)

@@ -23,6 +23,8 @@
 #   kvar        kbench ($KBENCH_ONLY) once per kernel-build variant in $VARIANTS (dirs under variants/, each a
 #               zest_amd package copy with its own _hip .so) -> kbench_<variant>.jsonl
 #   kpmc        rocprofv3 --pmc SQ counters (per launch) of kbench ($KBENCH_ONLY), kernels matching $PMC_KERNEL
+#   swarmtrace  public pull(device="all") at N = 1 under ZEST_TRACE (Chrome trace of the device pipeline:
+#               fetch waits, H2D + decode/hash submits, settle) -> trace summary
 #   hostbench   `zest bench --synthetic` on the box's CPU
 #   benchA/benchB  bench.py --modes $BENCH_MODES (bf16) with extra env $BENCH_ENV_A / $BENCH_ENV_B (A/B of opt-ins)
 #   gpubench    `zest bench --gpu --json` rows ($GPUBENCH_ENV: extra env, e.g. "ZG_LZ4_PAIR=0")
@@ -102,6 +104,13 @@ for step in "$@"; do
           f=$(find $OUT/pmc -name "*counter_collection.csv" | head -1)
           python tools/gpu/pmc_summary.py "$f" "${PMC_KERNEL:-lz4}" > $OUT/pmc_summary.txt 2>&1; cat $OUT/pmc_summary.txt
           rm -rf $OUT/pmc ;;
+    swarmtrace) ZEST_TRACE=$PWD/$OUT/swarm_trace.%p.json timeout -k 10 400 python -u tools/swarm_bench.py \
+                  --model ${SWARM_MODEL:-llama-3.1-8b} --ranks 1 --out $OUT/swarm_trace_run.json > $log 2>&1 \
+                  || fail $step $? $log
+                grep -h "^\[N=" $log | cut -c1-200
+                for t in $OUT/swarm_trace.*.json; do echo "== $t"; python tools/trace_summary.py $t --top 20; done \
+                  > $OUT/swarm_trace_summary.txt 2>&1
+                cat $OUT/swarm_trace_summary.txt; rm -f $OUT/swarm_trace.*.json ;;
     hostbench) ./zest_amd/_bin/zest bench --synthetic > $log 2>&1 || fail $step $? $log
                lscpu | grep -E "Model name|^CPU\(s\)" >> $log; cat $log ;;
     *) echo "[check] unknown step $step"; exit 2 ;;
