@@ -299,9 +299,37 @@ class _Fetcher:
         self.device = device
         self.staging_bytes, self.threads = staging_bytes, threads
         self._impl = None
+        self._warm = None
+        self._warm_err = None
+
+    def prewarm(self) -> None:
+        """Build the pipeline (Xet auth, pinned staging, cache scan, swarm) on a side thread, so it
+        comes up while rank 0 lists the repository instead of in front of this rank's first fetch
+        (the constructor releases the GIL)."""
+        if self._impl is not None or self._warm is not None:
+            return
+
+        def build():
+            try:
+                self._make()
+            except Exception as e:  # noqa: BLE001 - raised again by `impl`
+                self._warm_err = e
+        self._warm = threading.Thread(target=build, daemon=True)
+        self._warm.start()
 
     @property
     def impl(self):
+        if self._warm is not None:
+            self._warm.join()
+            self._warm = None
+            if self._warm_err is not None:
+                e, self._warm_err = self._warm_err, None
+                raise e
+        if self._impl is None:
+            self._make()
+        return self._impl
+
+    def _make(self):
         if self._impl is None:
             repo, revision, repo_type, p2p, peers, tracker, dht, boot = self.args
             if self.device.type == "cuda":
@@ -310,7 +338,6 @@ class _Fetcher:
             else:
                 self._impl = _core.HostXetFetcher(repo, revision, repo_type, p2p, peers, tracker, dht, boot,
                                                   self.threads)
-        return self._impl
 
     def shapes(self, xet_hash: str):
         return self.impl.term_shapes(xet_hash)
@@ -319,6 +346,11 @@ class _Fetcher:
         if self.device.type == "cuda":
             return self.impl.pull_terms(jobs, hashes.data_ptr(), sizes.data_ptr() if sizes is not None else 0, repair)
         return self.impl.fetch_terms(jobs, hashes.data_ptr(), repair)
+
+    def join(self) -> None:
+        """Wait for a prewarm still running (a rank that never fetched)."""
+        if self._warm is not None:
+            self._warm.join()
 
     def settle(self, xet_hash: str, ok: bool):
         if self._impl is not None:
@@ -362,6 +394,7 @@ class _Swarm:
         self.exchange_req = exchange
         self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
                                 staging_bytes, threads)
+        self.fetcher.prewarm()
         self.fault = _fault_spec()
         self.stats = {"reassigned": 0, "recovered_ranks": 0, "resent_bytes": 0, "repaired_files": 0,
                       "from_peer": 0, "from_cdn": 0, "from_cache": 0, "fetched_wire_bytes": 0}
@@ -958,4 +991,5 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 fetch_stats=sw.fetcher.stats(), **sw.stats)
         return out
     finally:
+        sw.fetcher.join()
         sw.m.close()
