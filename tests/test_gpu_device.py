@@ -245,12 +245,15 @@ def test_pull_files_multi_file_pipeline(tmp_path, monkeypatch):
         hub.stop()
 
 
-def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="auto", fault="", round_bytes=None):
+def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="auto", fault="", round_bytes=None,
+                           swarm_fault=""):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if fault:
         os.environ["ZEST_VMM_FAULT"] = fault
+    if swarm_fault:
+        os.environ.update(ZEST_SWARM_FAULT=swarm_fault, ZEST_SWARM_CTL_TIMEOUT="20", ZEST_SWARM_HB_STALE="3")
     torch.cuda.set_device(0)
     kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
     dist.init_process_group(backend, rank=rank, world_size=world_size, **kw)
@@ -264,7 +267,8 @@ def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="a
     except Exception as e:
         q.put((rank, f"{type(e).__name__}: {e}", {}))
     finally:
-        dist.destroy_process_group()
+        if not swarm_fault:  # (the default group still counts a dead rank)
+            dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world_size,backend,exchange,fault", [
@@ -333,6 +337,65 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend, ex
             assert all(r[2]["repaired_files"] == 0 for r in res)
         print(f"[swarm_pull {world_size}x{backend} {exchange}{'/' + fault if fault else ''}] mode {mode} "
               f"autotune {res[0][2]['exchange_autotune_s']} phases {res[0][2]['phases']}")
+    finally:
+        hub.stop()
+
+
+def test_swarm_pull_device_survives_a_lost_rank(tmp_path, monkeypatch):
+    """SURVEY §5.3 on the GPU: 3 ranks share the device (gloo control, peer-mapped arenas, autotuned
+    exchange); rank 2 exits at its second round.  Ranks 0 and 1 detect it through the control group
+    and the store heartbeats, rebuild their groups in-process, re-shard rank 2's ranges (re-sent by a
+    holder or refetched) and end with every tensor verified in HBM."""
+    import dataclasses
+    import json
+    import queue as _q
+    import struct
+
+    import torch.multiprocessing as mp
+
+    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
+    world = SyntheticWorld(spec, seed=23, mode="bf16")
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+        want = {}
+        for f in world.xet_files:
+            data = world.file_bytes_host(f)
+            (hlen,) = struct.unpack("<Q", data[:8])
+            for name, ent in json.loads(data[8:8 + hlen]).items():
+                if name != "__metadata__":
+                    a, b = ent["data_offsets"]
+                    want[name] = data[8 + hlen + a:8 + hlen + b]
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = free_port()
+        procs = [ctx.Process(target=_swarm_pull_gpu_worker,
+                             args=(r, 3, port, world.spec.repo_id, "gloo", q, "auto", "", 256 << 10, "exit:2:1"))
+                 for r in range(3)]
+        for p in procs:
+            p.start()
+        res = []
+        for _ in range(2):
+            try:
+                res.append(q.get(timeout=150))
+            except _q.Empty:
+                break
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+        res.sort(key=lambda r: r[0])
+        assert procs[2].exitcode == 1
+        assert [r[0] for r in res] == [0, 1], res
+        for rank, got, st in res:
+            assert isinstance(got, dict), got
+            assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+            assert st["recovered_ranks"] == 1 and st["world"] == 2, st
+        print(f"[swarm_pull lost rank] exchange {res[0][2]['exchange']} phases {res[0][2]['phases']}")
     finally:
         hub.stop()
 
