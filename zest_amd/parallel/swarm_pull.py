@@ -301,6 +301,7 @@ class _Fetcher:
         self._impl = None
         self._warm = None
         self._warm_err = None
+        self._lock = threading.Lock()  # `impl` is reached from the reconstruction warm-up thread too
 
     def prewarm(self) -> None:
         """Build the pipeline (Xet auth, pinned staging, cache scan, swarm) on a side thread, so it
@@ -319,15 +320,16 @@ class _Fetcher:
 
     @property
     def impl(self):
-        if self._warm is not None:
-            self._warm.join()
-            self._warm = None
-            if self._warm_err is not None:
-                e, self._warm_err = self._warm_err, None
-                raise e
-        if self._impl is None:
-            self._make()
-        return self._impl
+        with self._lock:
+            if self._warm is not None:
+                self._warm.join()
+                self._warm = None
+                if self._warm_err is not None:
+                    e, self._warm_err = self._warm_err, None
+                    raise e
+            if self._impl is None:
+                self._make()
+            return self._impl
 
     def _make(self):
         if self._impl is None:
@@ -349,8 +351,9 @@ class _Fetcher:
 
     def join(self) -> None:
         """Wait for a prewarm still running (a rank that never fetched)."""
-        if self._warm is not None:
-            self._warm.join()
+        w = self._warm
+        if w is not None:
+            w.join()
 
     def settle(self, xet_hash: str, ok: bool):
         if self._impl is not None:
@@ -514,6 +517,21 @@ class _Swarm:
                     self.items.append((ra, rb))
                     self.queue[r].append(len(self.items) - 1)
         self.n_rounds_planned = len(weights)
+        # Rank 0 holds every reconstruction from planning; the others fetch theirs now, on a side
+        # thread, while the arena is mapped and the exchange autotuned, instead of in front of
+        # their first fetch.
+        self._recon_warm = None
+        if self.m.rank != 0 and self.queue[self.m.rank]:
+            mine = sorted({f for it in self.queue[self.m.rank] for f in P.files_of(*self.items[it])})
+            hexes = [self.xet_files[f]["xet_hash"] for f in mine]
+
+            def warm():
+                try:
+                    _parallel_map(self.fetcher.shapes, hexes, max(8, self.fetcher.threads))
+                except Exception:  # noqa: BLE001 - the fetch itself reports any real failure
+                    pass
+            self._recon_warm = threading.Thread(target=warm, daemon=True)
+            self._recon_warm.start()
         self.tried: dict = {}        # item -> members (global ranks) that failed it
         self.fails: dict = {}        # global rank -> failed fetches
         self.owner_of: dict = {}     # item -> global rank that fetched it
@@ -991,5 +1009,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 fetch_stats=sw.fetcher.stats(), **sw.stats)
         return out
     finally:
+        if getattr(sw, "_recon_warm", None) is not None:
+            sw._recon_warm.join()
         sw.fetcher.join()
         sw.m.close()
