@@ -537,6 +537,12 @@ class RoundExchange:
             # gloo moves device tensors only through its collectives; a batched isend/irecv of
             # device tensors never completed (2-rank rehearsal on one GPU)
             modes = tuple(m for m in modes if m != "p2p")
+            if self._peer_arenas is not None:
+                # ...and stages them through host memory (device -> host -> TCP -> host -> device):
+                # with the arenas peer-mapped, only the modes that move device memory directly are
+                # worth timing (the gloo sweep alone took 1.9-4.1 s of a 2-3-rank rehearsal's setup,
+                # profiles/r4/swarm_pull_r4r.json, and never won)
+                modes = tuple(m for m in modes if m in PEER_MAPPED_MODES)
         # Time on a 256 MiB prefix of every region: bandwidth over xGMI is flat well below a 1 GiB
         # round, and a sweep of full rounds (modes x passes x rounds) cost seconds of setup in the
         # one-GPU rehearsal, where gloo stages device tensors through the host
