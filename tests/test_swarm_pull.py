@@ -260,6 +260,7 @@ def test_swarm_pull_term_shards_and_stats(hub_env):
         assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
         assert st["exchange"] in ("bcast", "allgather", "p2p") and st["world"] == 3
         assert st["rounds"] >= 2 and st["items"] >= 6
+        assert st["pipelined"]  # round k + 1 fetched on the second pipeline while round k is agreed
         assert st["fetched_bytes"] + st["received_bytes"] == total
         assert abs(st["fetched_bytes"] - total / 3) < 0.2 * total, st["fetched_bytes"]
         assert set(st["phases"]) >= {"plan_s", "fetch_s", "agree_s", "verify_s", "pull_s"}

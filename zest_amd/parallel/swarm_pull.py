@@ -398,6 +398,18 @@ class _Swarm:
         self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
                                 staging_bytes, threads)
         self.fetcher.prewarm()
+        # Cross-round fetch pipelining (ZEST_SWARM_PIPELINE, default on at N > 1): round k + 1's
+        # ranges are fetched on a second pipeline while round k's fetch drains and is agreed, so the
+        # connections never sit idle at a round boundary.  (The second pipeline joins no DHT: one
+        # node per process is enough, and two would contend for the DHT port.)
+        self.pipelined = os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
+        self.fetchers = [self.fetcher]
+        if self.pipelined:
+            f2 = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, False, dht_bootstrap,
+                          staging_bytes, threads)
+            f2.prewarm()
+            self.fetchers.append(f2)
+        self._fut = None
         self.fault = _fault_spec()
         self.stats = {"reassigned": 0, "recovered_ranks": 0, "resent_bytes": 0, "repaired_files": 0,
                       "from_peer": 0, "from_cdn": 0, "from_cache": 0, "fetched_wire_bytes": 0}
@@ -648,29 +660,73 @@ class _Swarm:
             self.have.update(items)
         self.pending_events = []
 
+    def _fetch_one(self, fetcher, it, round_no: int):
+        """Fetch item `it` (term ranges) into the arena: (error text, chunk sizes, source counters)."""
+        P = self.plan
+        if it is None:
+            return "", b"", {}
+        if it in self.have:  # a re-send after recovery: the bytes are here
+            return "", self.item_lens[it], {}
+        try:
+            if (self.m.me, round_no) in self.fault["fail"]:
+                raise RuntimeError(f"injected fetch failure (round {round_no})")
+            a, b = self.items[it]
+            res = fetcher.fetch(P.jobs(a, b, self.arena.data_ptr()), self.hashes, self.sizes)
+            lens = b"".join(r["chunk_lens"] for r in res)
+            info = {k: sum(r[k] for r in res) for k in ("fetched", "from_peer", "from_cdn", "from_cache")}
+            return "", lens, info
+        except Exception as e:  # noqa: BLE001 - reported through the all-gather
+            return f"rank {self.m.me}: {type(e).__name__}: {e}", b"", {}
+
+    def _pop_round(self) -> list:
+        """Next round's item per rank: every rank pops the same queues at the same point."""
+        return [q.pop(0) if q else None for q in self.queue]
+
+    def _submit(self, nxt: list, round_no: int):
+        from concurrent.futures import ThreadPoolExecutor
+        if not hasattr(self, "_pool"):
+            self._pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="zest-swarm-fetch")
+        f = self.fetchers[round_no % len(self.fetchers)]
+        return self._pool.submit(self._fetch_one, f, nxt[self.m.rank], round_no)
+
+    def _join_fetch(self):
+        """Wait for a fetch still in flight (its result is dropped: its item is re-queued)."""
+        if self._fut is not None:
+            try:
+                self._fut.result()
+            except Exception:  # noqa: BLE001
+                pass
+            self._fut = None
+
     def _rounds(self):
         P = self.plan
-        while any(self.queue):
-            me = self.m.rank
-            this = [q.pop(0) if q else None for q in self.queue]
+        me = self.m.rank
+        nxt = self._pop_round()
+        self.inflight_next = []
+        if self.pipelined:
+            self._fut = self._submit(nxt, self.round_no)
+        while any(x is not None for x in nxt) or any(self.queue):
+            this = nxt
             self.inflight = list(this)   # popped but not yet agreed (re-queued by _recover)
             it = this[me]
             if (self.m.me, self.round_no) in self.fault["exit"]:
                 os._exit(1)  # fault injection: this rank dies mid-pull (tests)
-            err, lens, info = "", b"", {}
             t = time.perf_counter()
-            if it is not None and it in self.have:  # a re-send after recovery: the bytes are here
-                lens = self.item_lens[it]
-            elif it is not None:
-                try:
-                    if (self.m.me, self.round_no) in self.fault["fail"]:
-                        raise RuntimeError(f"injected fetch failure (round {self.round_no})")
-                    a, b = self.items[it]
-                    res = self.fetcher.fetch(P.jobs(a, b, self.arena.data_ptr()), self.hashes, self.sizes)
-                    lens = b"".join(r["chunk_lens"] for r in res)
-                    info = {k: sum(r[k] for r in res) for k in ("fetched", "from_peer", "from_cdn", "from_cache")}
-                except Exception as e:  # noqa: BLE001 - reported through the all-gather
-                    err = f"rank {self.m.me}: {type(e).__name__}: {e}"
+            if self.pipelined:
+                # the next round's items are assigned now, before this round is agreed (a range
+                # re-queued by this round's failures is taken up one round later), and fetched on the
+                # other pipeline while this round's fetch finishes
+                nxt = self._pop_round()
+                self.inflight_next = list(nxt)
+                fut, self._fut = self._fut, None
+                # (nothing is in flight only when the previous pop found every queue empty, i.e.
+                # `it` is None; a synchronous fetch covers anything else)
+                err, lens, info = fut.result() if fut is not None else \
+                    self._fetch_one(self.fetchers[self.round_no % len(self.fetchers)], it, self.round_no)
+                if any(x is not None for x in nxt):
+                    self._fut = self._submit(nxt, self.round_no + 1)
+            else:
+                err, lens, info = self._fetch_one(self.fetcher, it, self.round_no)
             self._mark("fetch_s", t)
             t = time.perf_counter()
             meta = self._gather((it, err, lens))
@@ -721,6 +777,7 @@ class _Swarm:
                     self.stats["resent_bytes"] += int(P.t_ulen[a:b].sum())
             self.inflight = []
             if fatal:
+                self._join_fetch()
                 self._settle_received()
                 raise SwarmPullError("; ".join(sorted(set(fatal))))
             if self.m.world > 1 and any(hi > lo for lo, hi in regions):
@@ -734,6 +791,9 @@ class _Swarm:
                     self.pending_events.append((ev, recv))
                 self._mark("exchange_issue_s", t)
             self.round_no += 1
+            if not self.pipelined:
+                nxt = self._pop_round()
+        self.inflight_next = []
 
     def _recover(self, why: str):
         """A rank was lost: rebuild the groups over the survivors and re-shard (see _Membership)."""
@@ -746,6 +806,7 @@ class _Swarm:
                 done += items
         self.have.update(done)
         self.pending_events = []
+        self._join_fetch()  # (its range is re-queued below with the other unagreed ones)
         lost = self.m.rebuild()
         if not lost:
             raise SwarmPullError(f"collective failed but every rank is alive: {why}")
@@ -755,14 +816,18 @@ class _Swarm:
         # queues of the survivors, in their new order; everything of the lost ranks is re-planned
         keep = {g: self.queue[old_granks.index(g)] for g in self.m.granks}
         orphan = [x for i in lost for x in self.queue[i]]
-        # ranges popped in the failed round but never agreed: back to their owner, or orphaned
-        for i, x in enumerate(getattr(self, "inflight", [])):
-            if x is not None and x not in self.owner_of:
-                if old_granks[i] in keep:
-                    keep[old_granks[i]].insert(0, x)
-                else:
-                    orphan.append(x)
+        # ranges popped but never agreed (the failed round's, and the next round's already handed to
+        # the other pipeline): back to their owner, in order, or orphaned
+        for popped in (getattr(self, "inflight_next", []), getattr(self, "inflight", [])):
+            for i, x in enumerate(popped):
+                if x is not None and x not in self.owner_of:
+                    if old_granks[i] in keep:
+                        if x not in keep[old_granks[i]]:
+                            keep[old_granks[i]].insert(0, x)
+                    else:
+                        orphan.append(x)
         self.inflight = []
+        self.inflight_next = []
         self.queue = [keep[g] for g in self.m.granks]
         # which items does every survivor hold?  (fetched ones, and received ones already hashed)
         fetched = sorted(self.owner_of)
@@ -836,7 +901,8 @@ class _Swarm:
         P = self.plan
         badset = set(bad)
         for i in bad:
-            self.fetcher.settle(self.xet_files[i]["xet_hash"], False)
+            for f in self.fetchers:
+                f.settle(self.xet_files[i]["xet_hash"], False)
         # split each fetched item into its pieces inside bad files; the item's owner refetches them
         pieces = []   # (owner rank, a, b)
         for it, g in sorted(self.owner_of.items()):
@@ -891,7 +957,8 @@ class _Swarm:
             if g == self.m.me:
                 mine.update(self.plan.files_of(*self.items[it]))
         for i in mine:
-            self.fetcher.settle(self.xet_files[i]["xet_hash"], i in ok_files)
+            for f in self.fetchers:
+                f.settle(self.xet_files[i]["xet_hash"], i in ok_files)
 
     def plain(self) -> list[torch.Tensor]:
         """Non-Xet safetensors: rank 0 pulls them through the host path; broadcast to the others."""
@@ -934,6 +1001,18 @@ class _Swarm:
                     raise ValueError(f"duplicate tensor {k} in {f['path']}")
                 out[k] = v
         return out
+
+
+def _merged_stats(parts: list) -> dict:
+    """The pipelines' stats dicts summed (numbers) / first seen (other values)."""
+    out: dict = {}
+    for d in parts:
+        for k, v in d.items():
+            if isinstance(v, (int, float)) and not isinstance(v, bool) and isinstance(out.get(k, 0), (int, float)):
+                out[k] = out.get(k, 0) + v
+            else:
+                out.setdefault(k, v)
+    return out
 
 
 def _parallel_map(fn, items, threads: int):
@@ -1006,10 +1085,18 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
                 peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
                 GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
-                fetch_stats=sw.fetcher.stats(), **sw.stats)
+                fetch_stats=_merged_stats([f.stats() for f in sw.fetchers]), pipelined=sw.pipelined, **sw.stats)
         return out
     finally:
         if getattr(sw, "_recon_warm", None) is not None:
             sw._recon_warm.join()
-        sw.fetcher.join()
+        if getattr(sw, "_fut", None) is not None:
+            try:
+                sw._fut.result()
+            except Exception:  # noqa: BLE001 - the pull already failed
+                pass
+        if getattr(sw, "_pool", None) is not None:
+            sw._pool.shutdown(wait=True)
+        for f in getattr(sw, "fetchers", [sw.fetcher]):
+            f.join()
         sw.m.close()
