@@ -719,12 +719,12 @@ class _Swarm:
                 nxt = self._pop_round()
                 self.inflight_next = list(nxt)
                 fut, self._fut = self._fut, None
+                if any(x is not None for x in nxt):  # submitted BEFORE waiting: the two overlap
+                    self._fut = self._submit(nxt, self.round_no + 1)
                 # (nothing is in flight only when the previous pop found every queue empty, i.e.
                 # `it` is None; a synchronous fetch covers anything else)
                 err, lens, info = fut.result() if fut is not None else \
                     self._fetch_one(self.fetchers[self.round_no % len(self.fetchers)], it, self.round_no)
-                if any(x is not None for x in nxt):
-                    self._fut = self._submit(nxt, self.round_no + 1)
             else:
                 err, lens, info = self._fetch_one(self.fetcher, it, self.round_no)
             self._mark("fetch_s", t)
