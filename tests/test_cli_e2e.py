@@ -429,7 +429,9 @@ def test_http_pull_sse_progress(hub, nodes):
     files = {"model.safetensors": sample_files(big=12_000_000)["model.safetensors"],
              "config.json": b'{"model_type": "llama"}'}
     commit = hub.add_repo(REPO_ID, files, xet_min_size=1000)
-    hub.xorb_delay_s = 0.15
+    # staggered: the ~12 terms finish at distinct times (0.15-0.9 s), so some poll of the stream
+    # sees a partial byte count (all at once, they could land between two polls)
+    hub.xorb_delay_s, hub.xorb_delay_stagger = 0.15, 6
     a = nodes("a")
     a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
     a.wait_healthy()

@@ -108,6 +108,9 @@ class FakeHub:
         self.corrupt_xorbs: set[str] = set()   # xorb hex -> flipped byte in the body
         self.ignore_range = False
         self.xorb_delay_s = 0.0                # slow CDN: sleep before each xorb response
+        self.xorb_delay_stagger = 0            # k > 0: the n-th xorb response waits (1 + n % k) x the delay
+        self._xorb_gets = 0
+        self._delay_lock = threading.Lock()
         self.tracker_peers: dict[bytes, dict[str, float]] = {}
         self._srv: ThreadingHTTPServer | None = None
         self._thr: threading.Thread | None = None
@@ -542,7 +545,10 @@ class FakeHub:
             self._count("xorb_fail")
             return self._json(h, {"error": "injected failure"}, 500)
         if self.xorb_delay_s:
-            time.sleep(self.xorb_delay_s)
+            with self._delay_lock:
+                n = self._xorb_gets
+                self._xorb_gets += 1
+            time.sleep(self.xorb_delay_s * (1 + (n % self.xorb_delay_stagger if self.xorb_delay_stagger else 0)))
         data = self.xorbs[idx].data
         if data is None:  # metadata-only world: the bytes live with the peers
             self._count("xorb_missing")
