@@ -1033,7 +1033,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
     ZEST_SWARM_ROUND_MB, 1024 MiB): per-rank bytes per pipeline round.  `stats`, if given, is filled
     with this rank's numbers: bytes fetched / received, the exchange mode and its autotune times,
-    per-phase seconds, re-shards and recovered ranks."""
+    per-phase seconds (with cross-round pipelining, `fetch_s` is the time spent waiting for a round's
+    fetch to finish, not the fetches' own duration), re-shards and recovered ranks."""
     if round_bytes is None:
         round_bytes = int(os.environ.get("ZEST_SWARM_ROUND_MB", "1024")) << 20
     if exchange not in ("auto",) + EXCHANGE_MODES:
