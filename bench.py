@@ -38,6 +38,15 @@ import sys
 import time
 
 BASELINE_METRIC = "aggregate pull GB/s + P2P ratio, Llama-3.1-70B at 1/2/4/8 MI355X peers"
+HEADLINE_REPO = "meta-llama/Llama-3.1-70B"
+
+
+def metric_name(spec) -> str:
+    """BASELINE.json's metric for the headline model; any other model is named as what it is."""
+    if spec.repo_id == HEADLINE_REPO:
+        return BASELINE_METRIC
+    return (f"aggregate pull GB/s + P2P ratio, {spec.repo_id.split('/')[-1]} at 1/2/4/8 MI355X peers "
+            f"(not the headline config: {HEADLINE_REPO.split('/')[-1]})")
 MODES = ("bf16", "random")
 
 # Per-phase watchdog limits (seconds) for N > 1; ZEST_BENCH_WATCHDOG=<s> overrides all, =0 disables.
@@ -73,6 +82,13 @@ def parse_args(argv=None):
                     help="intra-node replication strategy; auto = time each on this machine during setup")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo rehearsal of the whole bench on host memory (tests; not a GPU number)")
+    ap.add_argument("--swarm-row", default="auto", choices=["auto", "on", "off"],
+                    help="also time the PUBLIC path, zest_amd.parallel.swarm_pull (= pull(device='all')), on the "
+                         "last data mode's world, its CDN served from the same pinned origin through an "
+                         "in-process memory CAS (mem:// fetch_info URLs, no sockets); reported under "
+                         "extra.swarm_pull_*.  auto: on for one GPU")
+    ap.add_argument("--swarm-steps", type=int, default=2)
+    ap.add_argument("--swarm-warmup", type=int, default=1)
     a = ap.parse_args(argv)
     a.modes = [a.mode] if a.mode else [m for m in a.modes.split(",") if m]
     bad = [m for m in a.modes if m not in MODES]
@@ -151,7 +167,7 @@ class Watchdog:
 # ------------------------------------------------------------------------------------------------
 # One rank
 # ------------------------------------------------------------------------------------------------
-def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=None, arenas=None) -> dict:
+def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=None, arenas=None, keep=None) -> dict:
     """Build the synthetic world of one data mode, pull it a.warmup + a.steps times; returns the
     measured numbers (every rank) plus the puller's exchange choice."""
     import numpy as np
@@ -335,9 +351,113 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         "hip_graph": bool(graph), "pipeline": getattr(puller, "pipeline", "cpu"), "seeders": seeders,
         "phase_s": phase, "exchange_rx_GBps": [round(x, 6) for x in rx],
     }
+    if keep is not None:  # the swarm row serves its CDN from this world's pinned origin
+        keep["world"], keep["puller"] = world, puller
+        return res
     puller.close()
     del puller, arena
     return res
+
+
+def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
+    """Time the public path on the world the engine just pulled: zest_amd.parallel.swarm_pull (what
+    zest_amd.pull(repo, device="all") runs), listing + reconstructions from an in-process fake hub,
+    every term's CDN fetch served from this rank's pinned origin through a mem:// memory CAS (the
+    same cache -> P2P -> CDN waterfall, the bytes copied into the pinned staging like a NIC's DMA),
+    then DeviceXetPull's pipeline (copy stream H2D || GPU decode + BLAKE3), the exchange at N > 1 and
+    the Merkle check of every file.  A step is one whole swarm_pull call; the fetch pipelines are
+    kept between calls (reuse_pipeline), reconstructions are asked for anew every call.  The xorb
+    cache is empty and cache writes are off (a device pull into HBM; nothing is read from disk)."""
+    import tempfile
+
+    import numpy as np
+    import torch
+
+    from zest_amd import ops
+    from zest_amd.parallel import swarm_pull as sp
+    from zest_amd.testing import FakeHub
+
+    world, puller = keep["world"], keep["puller"]
+    cuda = device.type == "cuda"
+    wd.arm("setup")
+    t_setup = time.time()
+    # the engine's device buffers go first: the swarm pull allocates its own 141 GB arena
+    puller.release_device()
+    keep.pop("arena", None)
+    if cuda:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    hub = FakeHub()
+    hub.xorb_url = "mem://origin"
+    hub.start()
+    hub.add_world(world, exact=True, payload=False)
+    T = world.terms
+    a_r, b_r = puller.rank_terms[rank]
+    ts = range(a_r, b_r)
+    ops.mem_origin_clear()
+    ops.mem_origin_add([world.xorb_hash_hex(int(T["xorb"][t])) for t in ts], [int(T["ser0"][t]) for t in ts],
+                       [puller.origin.ptr + int(puller.term_origin_off[t - a_r]) for t in ts],
+                       [int(T["ser_len"][t]) for t in ts])
+    cache = tempfile.mkdtemp(prefix="zest-bench-cache-")
+    for k, v in hub.env(cache).items():
+        os.environ[k] = v
+    os.environ["ZEST_CACHE_WRITES"] = "0"
+    own_pg = False
+    if dist is None:  # one rank: swarm_pull is a collective over a group of one
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+        own_pg = True
+    import torch.distributed as tdist
+    setup_s = time.time() - t_setup
+
+    def one(st):
+        out = sp.swarm_pull(world.spec.repo_id, device=device if cuda else None, p2p=False, dht=False,
+                            round_bytes=a.round_mb << 20, stats=st, reuse_pipeline=True)
+        n = len(out)
+        del out
+        return n
+
+    wd.arm("warmup")
+    t_w = time.time()
+    for _ in range(a.swarm_warmup):
+        one({})
+    warm_s = time.time() - t_w
+    wd.arm("timed")
+    times, st = [], {}
+    for _ in range(a.swarm_steps):
+        st = {}
+        tdist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_t = one(st)
+        if cuda:
+            torch.cuda.synchronize()
+        tdist.barrier()
+        times.append(time.perf_counter() - t0)
+    el = torch.tensor(times, dtype=torch.float64, device=device if (cuda and not own_pg) else "cpu")
+    if world_size > 1:
+        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)  # every step at its slowest rank
+    wd.arm("report")
+    times = el.cpu().tolist()
+    step_s = float(sum(times) / len(times))
+    sp.release_pipelines()
+    ops.mem_origin_clear()
+    hub.stop()
+    if own_pg:
+        tdist.destroy_process_group()
+    total = st.get("total_bytes", world.model_bytes)
+    return {"swarm_pull_GBps": round(world_size * total / step_s / 1e9, 3),
+            "swarm_pull_ms_per_step": round(step_s * 1e3, 3),
+            "swarm_pull_step_s": [round(x, 4) for x in times],
+            "swarm_pull_mode": keep.get("mode"), "swarm_pull_tensors": n_t,
+            "swarm_pull_p2p_ratio": round(float(st.get("p2p_ratio", 0.0)), 4),
+            "swarm_pull_exchange": st.get("exchange"), "swarm_pull_phases": st.get("phases"),
+            "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
+                                                                                  "bytes_from_peer")},
+            "swarm_pull_setup_s": round(setup_s, 3), "swarm_pull_warmup_s": round(warm_s, 3),
+            "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
+            "swarm_pull_verify": "merkle file hashes of every file on every rank"}
 
 
 def _data_note(r: dict) -> str:
@@ -433,16 +553,31 @@ def rank_main(a) -> None:
         raise SystemExit(f"refusing an nccl run over {devices} ({rccl_ranks} ranks counted by the collective)")
     spec = models.get(a.model)
     results, pick, arenas = [], None, {}
-    for mode in a.modes:
-        r = run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=pick, arenas=arenas)
+    swarm_row = (a.swarm_row == "on" or (a.swarm_row == "auto" and world_size == 1)) and cuda and a.seeders in (0, world_size)
+    keep = {} if swarm_row else None
+    for i, mode in enumerate(a.modes):
+        last = i == len(a.modes) - 1
+        r = run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=pick, arenas=arenas,
+                     keep=keep if last else None)
         pick = r["exchange"] if world_size > 1 else None
         log(rank, f"[{mode}] {r['value']:.3f} GB/s aggregate, {r['step_s'] * 1e3:.1f} ms/step, "
                   f"exchange {r['exchange']}")
         results.append(r)
+    swarm = {}
+    if keep:
+        keep["mode"] = results[-1]["mode"]
+        keep["arena"] = arenas.pop("arena", None)
+        arenas.clear()
+        keep.pop("arena", None)
+        swarm = run_swarm_row(a, keep, device, rank, world_size, dist, wd)
+        log(rank, f"[swarm_pull {keep['mode']}] {swarm['swarm_pull_GBps']:.3f} GB/s aggregate, "
+                  f"{swarm['swarm_pull_ms_per_step']:.1f} ms/step (public path, memory CAS)")
+        keep["puller"].close()
+        keep.clear()
     head = results[0]
     seeders = head["seeders"]
     out = {
-        "metric": BASELINE_METRIC,
+        "metric": metric_name(spec),
         "value": round(head["value"], 3),
         "unit": "GB/s",
         "n_gpus": world_size,
@@ -459,7 +594,7 @@ def rank_main(a) -> None:
         "extra": {f"{r['mode']}_GBps": round(r["value"], 3) for r in results}
         | {f"{r['mode']}_ms_per_step": round(r["step_s"] * 1e3, 3) for r in results}
         | {f"{r['mode']}_p2p_ratio": round(r["p2p_ratio"], 4) for r in results}
-        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results},
+        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results} | swarm,
         "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,
                    "parallelism": (f"swarm{world_size}" if seeders == world_size
                                    else f"seed{seeders}-leech{world_size - seeders}"),

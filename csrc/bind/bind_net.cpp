@@ -172,6 +172,12 @@ class HostXetFetcher {
   }
   // Term-range API of the term-sharded swarm pull (csrc/core/term_jobs.h).
   std::vector<TermShape> shapes(const std::string& hex) { return recs_->shapes(hex); }
+  std::vector<TermKey> term_keys(const std::string& hex) { return recs_->keys(hex); }
+  std::vector<uint8_t> cached_terms(const std::vector<std::string>& hexes, const std::vector<uint32_t>& starts,
+                                    const std::vector<uint32_t>& ends) {
+    return zest::cached_terms(*cache_, hexes, starts, ends, threads_);
+  }
+  void reset_reconstructions() { recs_->clear(); }
   std::vector<TermJobResult> fetch_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, bool repair) {
     return fetch_terms_host(*bridge_, *recs_, book_, jobs, hashes, threads_, repair);
   }
@@ -653,6 +659,25 @@ void bind_extra(py::module_& m) {
              }
              return term_shapes_py(v);
            }, py::arg("xet_hash"), "[(unpacked_length, n_chunks), ...] of the file's reconstruction terms")
+      .def("term_keys", [](HostXetFetcher& self, const std::string& hex) {
+             std::vector<zest::TermKey> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.term_keys(hex);
+             }
+             return zest::term_keys_py(v);
+           }, py::arg("xet_hash"), "[(xorb_hex, chunk_start, chunk_end), ...] of the file's reconstruction terms")
+      .def("cached_terms", [](HostXetFetcher& self, std::vector<std::string> hexes, std::vector<uint32_t> starts,
+                              std::vector<uint32_t> ends) {
+             std::vector<uint8_t> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.cached_terms(hexes, starts, ends);
+             }
+             return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+           }, py::arg("hexes"), py::arg("starts"), py::arg("ends"),
+           "one byte per term: 1 when the local xorb cache covers its chunk range (planner possession check)")
+      .def("reset_reconstructions", &HostXetFetcher::reset_reconstructions, "forget cached reconstructions (between pulls)")
       .def("fetch_terms",
            [](HostXetFetcher& self, const std::vector<std::tuple<std::string, uint32_t, uint32_t, uintptr_t, uint64_t>>& v,
               uintptr_t hashes, bool repair) {
@@ -738,6 +763,19 @@ void bind_extra(py::module_& m) {
     py::gil_scoped_release nogil;
     return storage::xet_hash_of_file(file, threads);
   }, py::arg("file"), py::arg("threads") = 0, "Xet file hash of a file on disk (CDC + BLAKE3 + Merkle)");
+  // ---------------- in-process memory origin (mem:// fetch_info URLs; hub.h) ----------------
+  m.def("mem_origin_add", [](std::vector<std::string> hexes, std::vector<uint64_t> starts, std::vector<uintptr_t> ptrs,
+                             std::vector<uint64_t> lens) {
+    if (starts.size() != hexes.size() || ptrs.size() != hexes.size() || lens.size() != hexes.size())
+      throw std::invalid_argument("mem_origin_add: lists of different lengths");
+    for (size_t i = 0; i < hexes.size(); ++i)
+      cas::mem_origin_add(hexes[i], starts[i], reinterpret_cast<const uint8_t*>(ptrs[i]), lens[i]);
+    return cas::mem_origin_size();
+  }, py::arg("xorb_hexes"), py::arg("url_starts"), py::arg("ptrs"), py::arg("lens"),
+     "serve fetch_info url_range [start, start + len) of each xorb from host memory at ptr (caller keeps it alive)");
+  m.def("mem_origin_clear", &cas::mem_origin_clear);
+  m.def("mem_origin_size", &cas::mem_origin_size);
+
   m.def("list_repo_files", [](std::string repo, std::string revision, std::string repo_type) {
     Config cfg = Config::from_env();
     std::vector<hub::RepoFile> files;

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "../gpurt/device_pull.h"
+#include "hub.h"
 #include "term_py.h"
 
 namespace py = pybind11;
@@ -40,10 +41,23 @@ py::list pull_files_py(DeviceXetPull& self, const std::vector<std::tuple<std::st
 }  // namespace
 
 void bind_hip_pull(py::module_& m) {
+  // This module links its own copy of the host core: the memory origin that DeviceXetPull's fetches
+  // read must be registered here (zest_amd.ops.mem_origin_add registers in _core and _hip).
+  m.def("mem_origin_add", [](std::vector<std::string> hexes, std::vector<uint64_t> starts, std::vector<uintptr_t> ptrs,
+                             std::vector<uint64_t> lens) {
+    if (starts.size() != hexes.size() || ptrs.size() != hexes.size() || lens.size() != hexes.size())
+      throw std::invalid_argument("mem_origin_add: lists of different lengths");
+    for (size_t i = 0; i < hexes.size(); ++i)
+      zest::cas::mem_origin_add(hexes[i], starts[i], reinterpret_cast<const uint8_t*>(ptrs[i]), lens[i]);
+    return zest::cas::mem_origin_size();
+  }, py::arg("xorb_hexes"), py::arg("url_starts"), py::arg("ptrs"), py::arg("lens"));
+  m.def("mem_origin_clear", &zest::cas::mem_origin_clear);
+  m.def("mem_origin_size", &zest::cas::mem_origin_size);
+
   py::class_<DeviceXetPull>(m, "DeviceXetPull", "Xet pull with GPU ingest + verification into HBM")
       .def(py::init([](const std::string& repo, const std::string& revision, const std::string& repo_type, bool p2p,
                        std::vector<std::string> peers, std::optional<std::string> tracker, bool dht,
-                       std::vector<std::string> boot, int device, size_t staging, int threads) {
+                       std::vector<std::string> boot, int device, size_t staging, int threads, int slots) {
              DevicePullOptions o;
              o.repo = repo;
              o.revision = revision;
@@ -56,6 +70,7 @@ void bind_hip_pull(py::module_& m) {
              o.device = device;
              o.staging_bytes = staging;
              o.threads = threads;
+             o.slots = slots;
              // Authentication talks HTTP: release the GIL (the hub may be served from this process).
              py::gil_scoped_release nogil;
              return new DeviceXetPull(o);
@@ -63,7 +78,7 @@ void bind_hip_pull(py::module_& m) {
            py::arg("repo"), py::arg("revision") = "main", py::arg("repo_type") = "model", py::arg("p2p") = true,
            py::arg("peers") = std::vector<std::string>{}, py::arg("tracker") = std::nullopt, py::arg("dht") = true,
            py::arg("dht_bootstrap") = std::vector<std::string>{}, py::arg("device") = 0,
-           py::arg("staging_bytes") = size_t(1) << 30, py::arg("threads") = 16)
+           py::arg("staging_bytes") = size_t(1) << 30, py::arg("threads") = 16, py::arg("slots") = 0)
       .def("pull_file",
            [](DeviceXetPull& self, const std::string& hex, uintptr_t dst, uint64_t size) {
              return pull_files_py(self, {std::make_tuple(hex, dst, size)})[0].cast<py::dict>();
@@ -80,6 +95,25 @@ void bind_hip_pull(py::module_& m) {
              }
              return zest::term_shapes_py(v);
            }, py::arg("xet_hash"), "[(unpacked_length, n_chunks), ...] of the file's reconstruction terms")
+      .def("term_keys", [](DeviceXetPull& self, const std::string& hex) {
+             std::vector<zest::TermKey> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.term_keys(hex);
+             }
+             return zest::term_keys_py(v);
+           }, py::arg("xet_hash"), "[(xorb_hex, chunk_start, chunk_end), ...] of the file's reconstruction terms")
+      .def("cached_terms", [](DeviceXetPull& self, std::vector<std::string> hexes, std::vector<uint32_t> starts,
+                              std::vector<uint32_t> ends) {
+             std::vector<uint8_t> v;
+             {
+               py::gil_scoped_release nogil;
+               v = self.cached_terms(hexes, starts, ends);
+             }
+             return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+           }, py::arg("hexes"), py::arg("starts"), py::arg("ends"),
+           "one byte per term: 1 when the local xorb cache covers its chunk range (planner possession check)")
+      .def("reset_reconstructions", &DeviceXetPull::reset_reconstructions, "forget cached reconstructions (between pulls)")
       .def("pull_terms",
            [](DeviceXetPull& self, const std::vector<zest::TermJobTuple>& v, uintptr_t hashes, uintptr_t sizes,
               bool repair) {
@@ -99,6 +133,14 @@ void bind_hip_pull(py::module_& m) {
              py::gil_scoped_release nogil;
              return self.settle(hex, ok);
            }, py::arg("xet_hash"), py::arg("ok"), "publish (ok) or drop the file's quarantined runs")
+      .def("sibling", [](const DeviceXetPull& self, size_t staging, int slots) { return self.sibling(staging, slots); },
+           py::arg("staging_bytes") = 0, py::arg("slots") = 0,
+           "a second pipeline (own streams + staging) sharing this one's Xet session, caches and settle book")
+      .def("flush_cache_writes", [](DeviceXetPull& self) {
+             py::gil_scoped_release nogil;
+             self.flush_cache_writes();
+           }, "wait for the write-behind xorb cache queue")
+      .def("cache_writer_json", &DeviceXetPull::cache_writer_json)
       .def("stats_json", &DeviceXetPull::stats_json)
       .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

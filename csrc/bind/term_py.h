@@ -44,4 +44,10 @@ inline pybind11::list term_shapes_py(const std::vector<TermShape>& v) {
   return out;
 }
 
+inline pybind11::list term_keys_py(const std::vector<TermKey>& v) {
+  pybind11::list out;
+  for (const auto& t : v) out.append(pybind11::make_tuple(t.hex, t.start, t.end));
+  return out;
+}
+
 }  // namespace zest

@@ -82,7 +82,8 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         if (cache_ && cfg_.cache_writes) {
           try {
             trace::Span sp("cache", "put_pending");
-            out.pending = cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
+            out.pending = writer_ ? writer_->put_pending(hex, r->chunk_offset, r->bytes(), r->size())
+                                  : cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
             out.run_offset = r->chunk_offset;
           } catch (const Error&) {
           }
@@ -104,25 +105,42 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
       swarm_->report_bad_peer(r->peer);  // served a run that does not even parse
     }
   }
-  // 3. CDN
+  // 3. CDN: straight into the sink's memory when it has room (no intermediate buffer)
   if (!cas_) throw Error("NotAuthenticated");
   trace::Span span("cdn", "fetch " + hex.substr(0, 12));
-  Bytes body = cas_->fetch(*fi);
-  span.arg("\"bytes\":" + std::to_string(body.size()));
+  const size_t want = size_t(fi->url_range.end - fi->url_range.start + 1);
+  Bytes body;
+  const uint8_t* run = nullptr;
+  size_t run_len = 0;
+  if (uint8_t* d = sink ? sink(want) : nullptr) {
+    if (size_t n = cas_->fetch_into(*fi, d, want)) {
+      run = d;
+      run_len = n;
+      out.ext = d;
+      out.ext_len = n;
+    }
+  }
+  if (!run) {
+    body = cas_->fetch(*fi);
+    run = body.data();
+    run_len = body.size();
+  }
+  span.arg("\"bytes\":" + std::to_string(run_len));
   stats_.xorbs_from_cdn++;
-  stats_.bytes_from_cdn += body.size();
+  stats_.bytes_from_cdn += run_len;
   if (swarm_) {
     swarm_->stats().cdn_xorbs++;
     swarm_->stats().total_xorbs++;
-    swarm_->stats().total_bytes += body.size();
+    swarm_->stats().total_bytes += run_len;
   }
   if (cache_ && cfg_.cache_writes) {
     try {
-      cache_->put_run(hex, uint32_t(fi->range.start), body.data(), body.size(), opt.repair);
+      if (writer_) writer_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
+      else cache_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
     } catch (const Error&) {
     }
   }
-  land(out, body.data(), body.size(), &body);
+  if (!out.ext) land(out, body.data(), body.size(), &body);
   out.local_start = uint32_t(term.range.start - fi->range.start);
   out.local_end = uint32_t(term.range.end - fi->range.start);
   out.source = Source::Cdn;
@@ -133,6 +151,15 @@ void XetBridge::settle(const std::string& xorb_hex, Source src, uint32_t run_off
                        bool ok) {
   if (!cache_) return;
   try {
+    if (writer_) {  // queued behind the run's own write (same xorb, same writer, FIFO)
+      if (src == Source::Peer && !pending.empty()) {
+        if (ok) writer_->promote(xorb_hex, run_offset, pending);
+        else writer_->discard_pending(pending);
+      } else if (src == Source::Cache && !ok) {
+        writer_->evict(xorb_hex, run_offset);
+      }
+      return;
+    }
     if (src == Source::Peer && !pending.empty()) {
       if (ok) cache_->promote(xorb_hex, run_offset, pending);
       else cache_->discard_pending(pending);

@@ -76,11 +76,16 @@ class XetBridge {
   void print_stats(std::ostream& w) const;
   std::string stats_json() const;
   SwarmDownloader* swarm() { return swarm_; }
+  // Route cache writes (CDN runs, quarantined peer runs, and the settle operations behind them)
+  // through a write-behind queue instead of the fetch thread (device pulls; see storage::CacheWriter).
+  void set_writer(storage::CacheWriter* w) { writer_ = w; }
+  storage::CacheWriter* writer() const { return writer_; }
 
  private:
   const Config& cfg_;
   storage::XorbCache* cache_;
   SwarmDownloader* swarm_;
+  storage::CacheWriter* writer_ = nullptr;
   std::unique_ptr<cas::CasClient> cas_;
   FetchStats stats_;
 };

@@ -8,6 +8,8 @@
 #include <cctype>
 #include <cerrno>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "json.h"
 #include "storage.h"
@@ -230,10 +232,16 @@ Reconstruction CasClient::get_reconstruction(const std::string& file_hash_hex) c
 }
 
 Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
+  const uint64_t want = fi.url_range.end - fi.url_range.start + 1;
+  if (is_mem_url(fi.url)) {
+    const uint8_t* p = mem_origin_find(fi.url, fi.url_range.start, fi.url_range.end);
+    if (!p) throw Error("HttpError", "xorb fetch status 404 (memory origin has no run at " + fi.url + ")");
+    return Bytes(p, p + want);
+  }
   http::RequestOptions opt;
   opt.timeout_ms = timeout_ms;
   Bytes out;
-  out.reserve(size_t(fi.url_range.end - fi.url_range.start + 1));
+  out.reserve(size_t(want));
   opt.sink = [&](const uint8_t* p, size_t n) {
     out.insert(out.end(), p, p + n);
     return true;
@@ -243,7 +251,6 @@ Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
   if (fi.url.rfind(url_, 0) == 0) h.emplace_back("Authorization", "Bearer " + token_);
   http::Response r = http::get_range(fi.url, fi.url_range.start, fi.url_range.end, h, opt);
   if (r.status != 200 && r.status != 206) throw Error("HttpError", "xorb fetch status " + std::to_string(r.status));
-  const uint64_t want = fi.url_range.end - fi.url_range.start + 1;
   if (r.status == 200 && out.size() > want) {
     // Server ignored Range: slice it ourselves.
     Bytes s(out.begin() + long(fi.url_range.start), out.begin() + long(fi.url_range.start + want));
@@ -251,6 +258,80 @@ Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
   }
   if (out.size() != want) throw Error("ShortRead", "xorb range length mismatch");
   return out;
+}
+
+size_t CasClient::fetch_into(const FetchInfo& fi, uint8_t* dst, size_t room, int timeout_ms) const {
+  const uint64_t want = fi.url_range.end - fi.url_range.start + 1;
+  if (!dst || want > room) return 0;
+  if (is_mem_url(fi.url)) {
+    const uint8_t* p = mem_origin_find(fi.url, fi.url_range.start, fi.url_range.end);
+    if (!p) throw Error("HttpError", "xorb fetch status 404 (memory origin has no run at " + fi.url + ")");
+    std::memcpy(dst, p, want);
+    return size_t(want);
+  }
+  http::RequestOptions opt;
+  opt.timeout_ms = timeout_ms;
+  uint64_t pos = 0;
+  bool overflow = false;
+  opt.sink = [&](const uint8_t* p, size_t n) {
+    if (pos + n > want) {  // a server that ignored Range: stop reading, fall back to fetch()
+      overflow = true;
+      return false;
+    }
+    std::memcpy(dst + pos, p, n);
+    pos += n;
+    return true;
+  };
+  http::Headers h;
+  if (fi.url.rfind(url_, 0) == 0) h.emplace_back("Authorization", "Bearer " + token_);
+  http::Response r;
+  try {
+    r = http::get_range(fi.url, fi.url_range.start, fi.url_range.end, h, opt);
+  } catch (const Error& e) {
+    if (overflow) return 0;
+    throw;
+  }
+  if (overflow) return 0;
+  if (r.status == 200) return fi.url_range.start == 0 && pos == want ? size_t(pos) : 0;  // whole body = range
+  if (r.status != 206) throw Error("HttpError", "xorb fetch status " + std::to_string(r.status));
+  if (pos != want) throw Error("ShortRead", "xorb range length mismatch");
+  return size_t(pos);
+}
+
+namespace {
+struct MemRun {
+  const uint8_t* data;
+  uint64_t len;
+};
+std::mutex g_mem_mu;
+std::map<std::pair<std::string, uint64_t>, MemRun> g_mem;  // (xorb hex, url_range.start) -> run
+}  // namespace
+
+void mem_origin_add(const std::string& xorb_hex, uint64_t url_start, const uint8_t* data, uint64_t len) {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  g_mem[{xorb_hex, url_start}] = MemRun{data, len};
+}
+
+void mem_origin_clear() {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  g_mem.clear();
+}
+
+size_t mem_origin_size() {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  return g_mem.size();
+}
+
+const uint8_t* mem_origin_find(const std::string& url, uint64_t start, uint64_t end_inclusive) {
+  // mem://<name>/<xorb hex>[?query]
+  std::string hex = url.substr(url.rfind('/') + 1);
+  hex = hex.substr(0, hex.find('?'));
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  auto it = g_mem.upper_bound({hex, start});
+  if (it == g_mem.begin()) return nullptr;
+  --it;  // the run starting at or before `start`
+  if (it->first.first != hex || end_inclusive + 1 > it->first.second + it->second.len) return nullptr;
+  return it->second.data + (start - it->first.second);
 }
 
 }  // namespace zest::cas

@@ -82,10 +82,26 @@ class CasClient {
   CasClient(std::string cas_url, std::string token) : url_(std::move(cas_url)), token_(std::move(token)) {}
   Reconstruction get_reconstruction(const std::string& file_hash_hex) const;
   Bytes fetch(const FetchInfo& fi, int timeout_ms = 120000) const;
+  // The url_range straight into caller memory of `room` bytes (a pinned staging region): no
+  // intermediate heap buffer.  Returns the bytes written, or 0 when the range does not fit `room`
+  // or the server ignored the Range header (the caller falls back to fetch()).
+  size_t fetch_into(const FetchInfo& fi, uint8_t* dst, size_t room, int timeout_ms = 120000) const;
   const std::string& url() const { return url_; }
 
  private:
   std::string url_, token_;
 };
+
+// In-process memory origin: fetch_info URLs `mem://<name>/<xorb hex>` are served from host memory
+// registered here instead of over HTTP (the bench's CDN stand-in for the public swarm_pull path: the
+// same fetch_term waterfall, the bytes copied from pinned host memory like a NIC's DMA into the
+// staging buffer, no sockets).  A run is keyed by (xorb hex, url_range.start); a fetch must ask for
+// exactly a registered run or a prefix of one.  Registration is process-global and thread-safe.
+void mem_origin_add(const std::string& xorb_hex, uint64_t url_start, const uint8_t* data, uint64_t len);
+void mem_origin_clear();
+size_t mem_origin_size();
+// (data, len) of the registered run covering [start, end_inclusive] of `url`'s xorb, or nullptr.
+const uint8_t* mem_origin_find(const std::string& url, uint64_t start, uint64_t end_inclusive);
+inline bool is_mem_url(const std::string& url) { return url.rfind("mem://", 0) == 0; }
 
 }  // namespace zest::cas

@@ -334,6 +334,41 @@ std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, 
   return std::nullopt;
 }
 
+bool XorbCache::covers(const std::string& hex, uint32_t start, uint32_t end) const {
+  if (end <= start) return false;
+  if (registry_ && !registry_->has(hex) && run_offsets(hex).empty()) return false;
+  for (uint32_t off : run_offsets(hex)) {
+    if (off > start) continue;
+    const std::string path = cfg_.xorb_cache_path(off == 0 ? hex : hex + "." + std::to_string(off));
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;
+    struct stat st;
+    const uint64_t size = ::fstat(fd, &st) == 0 ? uint64_t(st.st_size) : 0;
+    (void)::posix_fadvise(fd, 0, 0, POSIX_FADV_RANDOM);
+    uint64_t p = 0;
+    uint32_t k = 0;
+    const uint32_t need = end - off;
+    bool ok = true;
+    while (k < need) {
+      uint8_t h[xet::kChunkHeaderLen];
+      if (p + xet::kChunkHeaderLen > size || ::pread(fd, h, sizeof h, off_t(p)) != ssize_t(sizeof h)) {
+        ok = false;
+        break;
+      }
+      const uint64_t clen = uint64_t(h[1]) | uint64_t(h[2]) << 8 | uint64_t(h[3]) << 16;
+      if (h[0] != 0 || h[4] > 2 || p + xet::kChunkHeaderLen + clen > size) {
+        ok = false;
+        break;
+      }
+      p += xet::kChunkHeaderLen + clen;
+      ++k;
+    }
+    ::close(fd);
+    if (ok) return true;
+  }
+  return false;
+}
+
 std::optional<CacheHit> XorbCache::get_with_range(const std::string& hex, uint32_t range_start) const {
   if (auto full = read_file(cfg_.xorb_cache_path(hex))) return CacheHit{std::move(*full), 0};
   if (auto part = read_file(cfg_.xorb_cache_path(hex + "." + std::to_string(range_start))))
@@ -352,14 +387,22 @@ void XorbCache::put_run(const std::string& hex, uint32_t chunk_offset, const uin
   if (registry_) registry_->add(hex);
 }
 
-std::string XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+std::string XorbCache::pending_path(const std::string& hex, uint32_t chunk_offset) const {
   // One quarantine file per fetch: `{run}.p{pid}-{seq}.unverified`.  Files are reconstructed
   // concurrently, so two fetches of the same run (from different peers) must not share a name:
   // promote() publishes exactly the bytes that belonged to the file that verified.
   static std::atomic<uint64_t> seq{0};
-  const std::string path = run_path(hex, chunk_offset) + ".p" + std::to_string(::getpid()) + "-" +
-                           std::to_string(seq.fetch_add(1)) + "-n" + pid_namespace_token() + kPendingSuffix;
+  return run_path(hex, chunk_offset) + ".p" + std::to_string(::getpid()) + "-" + std::to_string(seq.fetch_add(1)) +
+         "-n" + pid_namespace_token() + kPendingSuffix;
+}
+
+void XorbCache::write_pending(const std::string& path, const uint8_t* data, size_t n) {
   write_file_atomic(path, data, n, /*durable=*/false);
+}
+
+std::string XorbCache::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+  const std::string path = pending_path(hex, chunk_offset);
+  write_pending(path, data, n);
   return path;
 }
 
@@ -536,6 +579,145 @@ std::string xet_hash_of_file(const std::string& file, int threads) {
   for (auto& t : ts) t.join();
   if (m != MAP_FAILED) ::munmap(m, n);
   return xet::to_hex(xet::file_hash(leaves));
+}
+
+}  // namespace zest::storage
+
+namespace zest::storage {
+
+CacheWriter::CacheWriter(XorbCache* cache, size_t max_bytes, int threads)
+    : cache_(cache), max_bytes_(max_bytes), queues_(size_t(std::max(1, threads))) {
+  for (int q = 0; q < int(queues_.size()); ++q) threads_.emplace_back([this, q] { worker(q); });
+}
+
+CacheWriter::~CacheWriter() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();  // workers drain their queues before leaving
+}
+
+bool CacheWriter::reserve(size_t n) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (in_flight_ + n > max_bytes_) {
+    st_.dropped_bytes += n;
+    return false;
+  }
+  in_flight_ += n;
+  st_.queued_bytes += n;
+  return true;
+}
+
+Bytes CacheWriter::take_buffer(size_t n) {
+  std::lock_guard<std::mutex> g(mu_);
+  // smallest pooled buffer that fits: its pages are already faulted in
+  size_t best = pool_.size();
+  for (size_t i = 0; i < pool_.size(); ++i)
+    if (pool_[i].capacity() >= n && (best == pool_.size() || pool_[i].capacity() < pool_[best].capacity())) best = i;
+  if (best == pool_.size()) return Bytes();
+  Bytes b = std::move(pool_[best]);
+  pool_bytes_ -= b.capacity();
+  pool_[best] = std::move(pool_.back());
+  pool_.pop_back();
+  return b;
+}
+
+void CacheWriter::push(Op op) {
+  // per-xorb order: every operation on one xorb goes to the same writer
+  const size_t q = op.hex.empty() ? 0 : std::hash<std::string>{}(op.hex) % queues_.size();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    queues_[q].push_back(std::move(op));
+    st_.ops++;
+  }
+  cv_.notify_all();
+}
+
+bool CacheWriter::put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace) {
+  if (!reserve(n)) return false;
+  Op op{Op::Run, hex, "", chunk_offset, replace, take_buffer(n)};
+  op.data.assign(data, data + n);
+  push(std::move(op));
+  return true;
+}
+
+std::string CacheWriter::put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n) {
+  if (!reserve(n)) return "";
+  Op op{Op::Pending, hex, cache_->pending_path(hex, chunk_offset), chunk_offset, false, take_buffer(n)};
+  op.data.assign(data, data + n);
+  std::string path = op.path;
+  push(std::move(op));
+  return path;
+}
+
+void CacheWriter::promote(const std::string& hex, uint32_t chunk_offset, const std::string& pending) {
+  push(Op{Op::Promote, hex, pending, chunk_offset, false, {}});
+}
+void CacheWriter::discard_pending(const std::string& pending) {
+  // a quarantine path embeds its xorb's hex: same writer as the write it discards
+  const size_t slash = pending.rfind('/');
+  std::string hex = pending.substr(slash == std::string::npos ? 0 : slash + 1, 64);
+  push(Op{Op::Discard, hex, pending, 0, false, {}});
+}
+void CacheWriter::evict(const std::string& hex, uint32_t chunk_offset) {
+  push(Op{Op::Evict, hex, "", chunk_offset, false, {}});
+}
+
+void CacheWriter::flush() {
+  std::unique_lock<std::mutex> g(mu_);
+  idle_cv_.wait(g, [&] {
+    if (busy_) return false;
+    for (auto& q : queues_)
+      if (!q.empty()) return false;
+    return true;
+  });
+}
+
+CacheWriter::Stats CacheWriter::stats() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return st_;
+}
+
+void CacheWriter::worker(int q) {
+  while (true) {
+    Op op;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [&] { return stop_ || !queues_[size_t(q)].empty(); });
+      if (queues_[size_t(q)].empty()) return;  // stop_ and drained
+      op = std::move(queues_[size_t(q)].front());
+      queues_[size_t(q)].pop_front();
+      ++busy_;
+    }
+    const size_t n = op.data.size();
+    try {
+      switch (op.kind) {
+        case Op::Run: cache_->put_run(op.hex, op.offset, op.data.data(), n, op.replace); break;
+        case Op::Pending: cache_->write_pending(op.path, op.data.data(), n); break;
+        case Op::Promote: cache_->promote(op.hex, op.offset, op.path); break;
+        case Op::Discard: cache_->discard_pending(op.path); break;
+        case Op::Evict: cache_->evict(op.hex, op.offset); break;
+      }
+    } catch (const std::exception&) {
+      // best effort, like the synchronous path (a failed cache write only costs a refetch)
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (n) {
+        in_flight_ -= n;
+        st_.written_bytes += n;
+        op.data.clear();
+        if (pool_bytes_ + op.data.capacity() <= max_bytes_) {  // pooled buffers stay within the bound
+          pool_bytes_ += op.data.capacity();
+          pool_.push_back(std::move(op.data));
+        }
+      }
+      --busy_;
+    }
+    idle_cv_.notify_all();
+  }
 }
 
 }  // namespace zest::storage

@@ -7,12 +7,15 @@
 // the registry is updated on every put (seed-while-downloading) and thread-safe.
 #pragma once
 
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <optional>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -110,6 +113,10 @@ class XorbCache {
   // `range.start == 0 && one fetch entry` rule produces, xet_bridge.zig:189-217 — the source of
   // its P2P RangeOutOfBounds failures) is never served for chunks it does not hold.
   std::optional<CacheHit> find(const std::string& hex, uint32_t start, uint32_t end) const;
+  // Does a cached run cover chunks [start, end)?  The planner's possession check (swarm_pull): only
+  // the chunk headers up to `end` are read (pread, no readahead of the payload), and nothing is
+  // mapped or touched.  A true answer is re-validated by find() when the term is fetched.
+  bool covers(const std::string& hex, uint32_t start, uint32_t end) const;
   // Legacy lookup kept for callers that want the raw run at an exact offset.
   std::optional<CacheHit> get_with_range(const std::string& hex, uint32_t range_start) const;
   // Store a run of serialized chunks starting at chunk `chunk_offset`: offset 0 goes to `{hex}`,
@@ -145,10 +152,67 @@ class XorbCache {
   // pull, so runs orphaned by a killed pull do not pile up outside the cache bound.
   size_t sweep_pending(int64_t max_age_s = 24 * 3600);
 
+  // Quarantine file name for a new pending run (what put_pending writes to).
+  std::string pending_path(const std::string& hex, uint32_t chunk_offset) const;
+  void write_pending(const std::string& path, const uint8_t* data, size_t n);
+
  private:
   std::string run_path(const std::string& hex, uint32_t chunk_offset) const;
   const Config& cfg_;
   XorbRegistry* registry_;
+};
+
+// Write-behind for the xorb cache.  A device pull moves tens of GB/s; writing every fetched run to
+// disk on the fetch threads (8.3 ms per 64 MiB peer run in round 4's trace) put the disk in front of
+// the H2D copy.  Here a fetch thread copies the run into a pooled buffer and returns; `threads`
+// writers drain the queue in per-xorb FIFO order (a promote/discard/evict queued after a write of
+// the same xorb runs after it).  The queue is bounded by `max_bytes`: when it is full a run is not
+// cached at all (counted in `dropped_bytes`) -- the cache is best effort, the pull never waits on
+// the disk.  The reference writes synchronously on the fetch task (swarm.zig:416-420,
+// xet_bridge.zig:203-208).  The destructor drains the queue.
+class CacheWriter {
+ public:
+  CacheWriter(XorbCache* cache, size_t max_bytes, int threads = 2);
+  ~CacheWriter();
+  CacheWriter(const CacheWriter&) = delete;
+  CacheWriter& operator=(const CacheWriter&) = delete;
+  // false: dropped (queue full)
+  bool put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace);
+  // The quarantine path the run will be written to, or "" when dropped.
+  std::string put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  void promote(const std::string& hex, uint32_t chunk_offset, const std::string& pending);
+  void discard_pending(const std::string& pending);
+  void evict(const std::string& hex, uint32_t chunk_offset);
+  void flush();  // wait until every queued operation ran
+  struct Stats {
+    uint64_t queued_bytes = 0, written_bytes = 0, dropped_bytes = 0, ops = 0;
+  };
+  Stats stats() const;
+
+ private:
+  struct Op {
+    enum Kind { Run, Pending, Promote, Discard, Evict } kind;
+    std::string hex, path;
+    uint32_t offset = 0;
+    bool replace = false;
+    Bytes data;
+  };
+  bool reserve(size_t n);
+  Bytes take_buffer(size_t n);
+  void push(Op op);
+  void worker(int q);
+  XorbCache* cache_;
+  size_t max_bytes_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::vector<std::deque<Op>> queues_;
+  std::vector<Bytes> pool_;  // buffers of written runs, reused (no page faults on the fetch path)
+  size_t pool_bytes_ = 0;
+  size_t in_flight_ = 0;     // queued + being written (bytes)
+  size_t busy_ = 0;          // operations popped and not finished
+  bool stop_ = false;
+  Stats st_;
+  std::vector<std::thread> threads_;
 };
 
 }  // namespace zest::storage

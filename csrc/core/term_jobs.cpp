@@ -34,6 +34,41 @@ std::vector<TermShape> ReconCache::shapes(const std::string& hex) {
   return out;
 }
 
+std::vector<TermKey> ReconCache::keys(const std::string& hex) {
+  const cas::Reconstruction& r = get(hex);
+  std::vector<TermKey> out;
+  out.reserve(r.terms.size());
+  for (const auto& t : r.terms) out.push_back({t.hash_hex, uint32_t(t.range.start), uint32_t(t.range.end)});
+  return out;
+}
+
+void ReconCache::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  recs_.clear();
+}
+
+std::vector<uint8_t> cached_terms(const storage::XorbCache& cache, const std::vector<std::string>& hexes,
+                                  const std::vector<uint32_t>& starts, const std::vector<uint32_t>& ends, int threads) {
+  const size_t n = hexes.size();
+  if (starts.size() != n || ends.size() != n) throw Error("InvalidArgument", "cached_terms: lists of different lengths");
+  std::vector<uint8_t> out(n, 0);
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < n;) {
+      try {
+        out[i] = cache.covers(hexes[i], starts[i], ends[i]) ? 1 : 0;
+      } catch (const std::exception&) {
+        out[i] = 0;
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < std::max(1, std::min<int>(threads, int(n))); ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  return out;
+}
+
 void SettleBook::add(const std::string& file_hex, const std::string& xorb_hex, Source src, uint32_t run_offset,
                      const std::string& pending) {
   // Only runs with something to settle: a quarantined peer run, or a cache hit (evicted on failure).
@@ -53,6 +88,26 @@ size_t SettleBook::settle(XetBridge& bridge, const std::string& file_hex, bool o
   }
   for (const Run& r : runs) bridge.settle(r.xorb_hex, r.src, r.run_offset, r.pending, ok);
   return runs.size();
+}
+
+size_t SettleBook::discard(XetBridge& bridge, const std::vector<std::pair<std::string, std::string>>& runs) {
+  std::vector<Run> gone;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& [file, pending] : runs) {
+      auto it = runs_.find(file);
+      if (it == runs_.end()) continue;
+      auto& v = it->second;
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].pending == pending) {
+          gone.push_back(std::move(v[i]));
+          v.erase(v.begin() + long(i));
+          break;
+        }
+    }
+  }
+  for (const Run& r : gone) bridge.settle(r.xorb_hex, r.src, r.run_offset, r.pending, false);
+  return gone.size();
 }
 
 size_t SettleBook::settle_all(XetBridge& bridge, bool ok) {
@@ -100,6 +155,7 @@ std::vector<TermJobResult> fetch_terms_host(XetBridge& bridge, ReconCache& recs,
   std::atomic<bool> failed{false};
   std::mutex mu;
   std::string first_err;
+  std::vector<std::pair<std::string, std::string>> quarantined;  // (file, pending) added by this call
   auto do_term = [&](const Item& it, const FetchOptions& opt, Source* src_out, std::string* peer_out) {
     const cas::Reconstruction& rec = *rec_of[it.job];
     const cas::Term& t = rec.terms[it.term];
@@ -112,8 +168,15 @@ std::vector<TermJobResult> fetch_terms_host(XetBridge& bridge, ReconCache& recs,
     auto record = [&](bool ok_now) {
       if (recorded) return;
       recorded = true;
-      if (ok_now) book.add(jobs[it.job].xet_hash, t.hash_hex, f.source, f.run_offset, f.pending);
-      else bridge.settle(t.hash_hex, f.source, f.run_offset, f.pending, false);
+      if (ok_now) {
+        book.add(jobs[it.job].xet_hash, t.hash_hex, f.source, f.run_offset, f.pending);
+        if (!f.pending.empty()) {
+          std::lock_guard<std::mutex> g(mu);
+          quarantined.emplace_back(jobs[it.job].xet_hash, f.pending);
+        }
+      } else {
+        bridge.settle(t.hash_hex, f.source, f.run_offset, f.pending, false);
+      }
     };
     try {
       const auto idx = xet::index_chunks(f.bytes(), f.size());
@@ -175,7 +238,9 @@ std::vector<TermJobResult> fetch_terms_host(XetBridge& bridge, ReconCache& recs,
   worker();
   for (auto& t : ts) t.join();
   if (failed) {
-    for (const auto& j : jobs) book.settle(bridge, j.xet_hash, false);
+    // The range is refetched by another rank: drop only the peer runs this call quarantined (they
+    // will never be Merkle-checked); cache hits and earlier calls' runs wait for the file's verdict.
+    book.discard(bridge, quarantined);
     throw Error("DownloadFailed", first_err);
   }
   return out;

@@ -40,12 +40,22 @@ struct TermShape {
   uint32_t nchunks = 0;
 };
 
+// (xorb hex, chunk range start, end) of every term of a file, in reconstruction order.
+struct TermKey {
+  std::string hex;
+  uint32_t start = 0, end = 0;
+};
+
 // Thread-safe reconstruction cache: the planner asks once per file, the fetch jobs reuse it.
 class ReconCache {
  public:
   explicit ReconCache(XetBridge& bridge) : bridge_(bridge) {}
   const cas::Reconstruction& get(const std::string& hex);
   std::vector<TermShape> shapes(const std::string& hex);
+  std::vector<TermKey> keys(const std::string& hex);
+  // Forget every reconstruction (the next pull asks the CAS again: presigned URLs expire).  Only
+  // between pulls: references handed out by get() die with it.
+  void clear();
 
  private:
   XetBridge& bridge_;
@@ -61,6 +71,8 @@ class SettleBook {
   // Publish (ok) or drop / evict (!ok) every run recorded for the file; returns how many.
   size_t settle(XetBridge& bridge, const std::string& file_hex, bool ok);
   size_t settle_all(XetBridge& bridge, bool ok);
+  // Drop the quarantined peer runs (file hex, pending path) a failed call recorded; returns how many.
+  size_t discard(XetBridge& bridge, const std::vector<std::pair<std::string, std::string>>& runs);
 
  private:
   struct Run {
@@ -72,6 +84,11 @@ class SettleBook {
   std::mutex mu_;
   std::map<std::string, std::vector<Run>> runs_;
 };
+
+// Possession check of the swarm planner: 1 per term (xorb hex, chunk range [start, end)) that the
+// local xorb cache covers, 0 otherwise; `threads` workers check terms concurrently.
+std::vector<uint8_t> cached_terms(const storage::XorbCache& cache, const std::vector<std::string>& hexes,
+                                  const std::vector<uint32_t>& starts, const std::vector<uint32_t>& ends, int threads);
 
 // Host twin of DeviceXetPull::pull_terms: `threads` workers fetch the jobs' terms, decode and hash
 // every chunk on the CPU, write the bytes at job.dst (host memory) and the keyed-BLAKE3 chunk hashes

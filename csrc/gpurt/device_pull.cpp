@@ -6,7 +6,9 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -25,10 +27,14 @@
 #include "xet_hash.h"
 #include "xorb.h"
 
-// Pipeline: batches of terms fill one of two pinned buffers (fetch threads that run on across
-// batch boundaries) while the previous batch's H2D + kernels run on a private HIP stream; a buffer
-// is refilled only after its stream event completed.  The chunk records come from the header index
-// the fetch workers build anyway while validating each run, so the GPU has no header walk to do.
+// Pipeline: batches of terms fill `slots` pinned staging buffers (fetch threads that run on across
+// batch boundaries).  A batch's H2D copies (payload + chunk records) go on a copy stream and its
+// decode/place/hash kernels on a compute stream, ordered by per-batch events only: batch b's copy
+// waits (on the device) for the kernels of batch b - slots, which read the same device staging, and
+// a releaser thread hands the host slot back to the fetch workers as soon as batch b's copy landed
+// -- no host-side wait for kernels anywhere, so the copy of batch b + 1 overlaps the kernels of
+// batch b and PCIe stays busy.  The chunk records come from the header index the fetch workers
+// build anyway while validating each run, so the GPU has no header walk to do.
 
 namespace zest::gpurt {
 
@@ -54,68 +60,94 @@ struct DevBuf {
 };
 
 struct Slot {
-  PinnedBuf pin;
+  PinnedBuf pin;            // payload staging (fetched runs, back to back)
   uint8_t* host = nullptr;  // = pin.data()
+  PinnedBuf rec_pin;        // the batch's chunk records (pinned: the records copy is async too)
+  size_t rec_cap = 0;       // records that fit rec_pin
   DevBuf<uint8_t> dev;      // device staging (padded)
   DevBuf<ZgChunk> chunks_dev;
-  std::vector<ZgChunk> chunks_host;  // chunk records of the batch, built by the fetch workers
-  hipEvent_t done = nullptr;
+  DevBuf<uint8_t> scratch;  // hash scratch of the batch's ingest launch
+  ZgChunk* recs() const { return reinterpret_cast<ZgChunk*>(rec_pin.data()); }
 };
+
+size_t env_size(const char* k, size_t dflt) {
+  const char* v = std::getenv(k);
+  return v && *v ? size_t(std::strtoull(v, nullptr, 10)) : dflt;
+}
 
 }  // namespace
 
-struct DeviceXetPull::Impl {
-  explicit Impl(const DevicePullOptions& o)
-      : cfg_(Config::from_env()), device_(o.device), cap_(o.staging_bytes), threads_(o.threads > 0 ? o.threads : 16) {
-    const std::string& repo = o.repo;
-    const std::string& revision = o.revision;
-    const std::string& repo_type = o.repo_type;
-    const bool p2p = o.p2p, dht = o.dht;
-    const auto& peers = o.peers;
-    const auto& tracker = o.tracker;
-    const auto& dht_bootstrap = o.dht_bootstrap;
+// Host side of a pipeline: Xet session, caches, swarm, reconstructions and the settle book.  Shared
+// by sibling pipelines (DeviceXetPull::sibling), so a second pipeline costs only its staging.
+struct DeviceXetPull::Shared {
+  explicit Shared(const DevicePullOptions& o) : cfg(Config::from_env()) {
     {
       trace::Span sp("device", "init: cache scan");
-      registry_.scan(cfg_);
-      cache_ = std::make_unique<storage::XorbCache>(cfg_, &registry_);
+      registry.scan(cfg);
+      cache = std::make_unique<storage::XorbCache>(cfg, &registry);
     }
+    if (cfg.cache_writes)  // ZEST_CACHE_WRITE_QUEUE_MB bounds the write-behind queue (0: synchronous)
+      if (size_t mb = env_size("ZEST_CACHE_WRITE_QUEUE_MB", 2048))
+        writer = std::make_unique<storage::CacheWriter>(cache.get(), mb << 20, 2);
     std::vector<net::Addr> boot;
-    for (auto& b : dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
+    for (auto& b : o.dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
     {
       trace::Span sp("device", "init: swarm");
-      swarm_ = std::make_unique<SwarmDownloader>(cfg_, tracker, p2p, dht && p2p, boot);
-      for (auto& p : peers) swarm_->add_direct_peer(net::Addr::parse(p, 6881));
+      swarm = std::make_unique<SwarmDownloader>(cfg, o.tracker, o.p2p, o.dht && o.p2p, boot);
+      for (auto& p : o.peers) swarm->add_direct_peer(net::Addr::parse(p, 6881));
     }
-    bridge_ = std::make_unique<XetBridge>(cfg_, cache_.get(), swarm_.get());
-    recs_ = std::make_unique<ReconCache>(*bridge_);
+    bridge = std::make_unique<XetBridge>(cfg, cache.get(), swarm.get());
+    bridge->set_writer(writer.get());
+    recs = std::make_unique<ReconCache>(*bridge);
     {
       trace::Span sp("device", "init: xet auth");
-      bridge_->authenticate(repo, repo_type, revision);
+      bridge->authenticate(o.repo, o.repo_type, o.revision);
     }
+  }
+  Config cfg;
+  storage::XorbRegistry registry;
+  std::unique_ptr<storage::XorbCache> cache;
+  std::unique_ptr<storage::CacheWriter> writer;  // destroyed (drained) before the cache
+  std::unique_ptr<SwarmDownloader> swarm;
+  std::unique_ptr<XetBridge> bridge;
+  std::unique_ptr<ReconCache> recs;
+  SettleBook book;
+};
+
+struct DeviceXetPull::Impl {
+  Impl(const DevicePullOptions& o, std::shared_ptr<Shared> shared)
+      : sh_(shared ? std::move(shared) : std::make_shared<Shared>(o)),
+        device_(o.device),
+        cap_(o.staging_bytes),
+        threads_(o.threads > 0 ? o.threads : 16),
+        nslots_(std::max<size_t>(2, o.slots > 0 ? size_t(o.slots) : env_size("ZEST_DEVICE_SLOTS", 3))) {
+    slots_.resize(nslots_);
     if (!o.defer_device) init_device();
   }
 
-  // Device half of the set-up (stream, pinned + device staging): separate from the host half above
-  // so a caller can run the Xet auth / cache scan while the HIP runtime is still coming up
-  // (gpu_worker.cpp).  The two pinned slots are page-locked concurrently.  Idempotent.
+  // Device half of the set-up (streams, pinned + device staging): separate from the host half so a
+  // caller can run the Xet auth / cache scan while the HIP runtime is still coming up
+  // (gpu_worker.cpp).  The pinned slots are page-locked concurrently.  Idempotent.
   void init_device() {
     std::lock_guard<std::mutex> g(init_mu_);
     if (device_ready_) return;
     trace::Span sp("device", "init: staging alloc");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    std::string errs[2];
-    std::thread pin1([&] {
-      if (!slots_[1].pin.alloc(cap_ + 4096)) errs[1] = "pinning the staging buffer failed";
-    });
+    hip_check(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate");
+    std::vector<std::string> errs(nslots_);
+    std::vector<std::thread> pins;
+    for (size_t i = 1; i < nslots_; ++i)
+      pins.emplace_back([&, i] {
+        if (!slots_[i].pin.alloc(cap_ + 4096)) errs[i] = "pinning the staging buffer failed";
+      });
     if (!slots_[0].pin.alloc(cap_ + 4096)) errs[0] = "pinning the staging buffer failed";
-    pin1.join();
+    for (auto& t : pins) t.join();
     for (auto& e : errs)
       if (!e.empty()) throw Error("HipError", e);
     for (auto& s : slots_) {
       s.host = s.pin.data();
       s.dev.ensure(cap_);
-      hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
     }
     err_.ensure(1);
     device_ready_ = true;
@@ -123,11 +155,24 @@ struct DeviceXetPull::Impl {
 
   ~Impl() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     for (auto& s : slots_) {
       s.pin.reset();
-      if (s.done) (void)hipEventDestroy(s.done);
+      s.rec_pin.reset();
     }
     if (stream_) (void)hipStreamDestroy(stream_);
+    if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
+  }
+
+  // `n` events for one pass (kept across calls; the previous pass synchronized its streams).
+  hipEvent_t* take_events(size_t n) {
+    while (events_.size() < n) {
+      hipEvent_t e = nullptr;
+      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      events_.push_back(e);
+    }
+    return events_.data();
   }
 
   // Pull several Xet files (hash, device pointer, size) through ONE pipeline: staging batches
@@ -140,6 +185,9 @@ struct DeviceXetPull::Impl {
   // cached ones — so one corrupt copy costs one refetch, not a permanently failing pull.
   std::vector<PullFileStats> pull_files(const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& files) {
     init_device();
+    // HIP's current device is per thread: a caller on any thread (a Python fetch pool, the CLI
+    // worker) gets this pipeline's device for the lazy allocations below
+    hip_check(hipSetDevice(device_), "hipSetDevice");
     const auto t0 = std::chrono::steady_clock::now();
     const size_t nf = files.size();
     std::vector<const cas::Reconstruction*> recs(nf);
@@ -150,7 +198,7 @@ struct DeviceXetPull::Impl {
       auto w = [&]() {
         for (size_t f; (f = k.fetch_add(1)) < nf;) {
           try {
-            recs[f] = &recs_->get(std::get<0>(files[f]));
+            recs[f] = &sh_->recs->get(std::get<0>(files[f]));
           } catch (const std::exception& e) {
             errs[f] = e.what();
           }
@@ -190,16 +238,16 @@ struct DeviceXetPull::Impl {
         todo.clear();
         break;
       }
-      if (attempt == 0) bridge_->stats().verify_failures += bad.size();
+      if (attempt == 0) sh_->bridge->stats().verify_failures += bad.size();
       else if (at.seg.ingest_err)
         throw Error("IngestError", "code " + std::to_string(at.seg.ingest_err >> 32) + " at " +
                                        std::to_string(at.seg.ingest_err & 0xFFFFFFFFu));
       std::vector<size_t> again;
       for (size_t j : bad) again.push_back(todo[j]);
-      if (attempt == 0) bridge_->stats().refetches += again.size();
+      if (attempt == 0) sh_->bridge->stats().refetches += again.size();
       todo = std::move(again);
     }
-    if (cfg_.cache_max_gb > 0) cache_->trim(uint64_t(cfg_.cache_max_gb * 1e9));  // ZEST_CACHE_MAX_GB
+    if (sh_->cfg.cache_max_gb > 0) sh_->cache->trim(uint64_t(sh_->cfg.cache_max_gb * 1e9));  // ZEST_CACHE_MAX_GB
     for (size_t f : todo)
       throw Error("HashMismatch", "device bytes hash " + got[f] + " != " + std::get<0>(files[f]));
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -224,10 +272,11 @@ struct DeviceXetPull::Impl {
   std::vector<TermJobResult> pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
                                         bool repair) {
     init_device();
+    hip_check(hipSetDevice(device_), "hipSetDevice");
     std::vector<Seg> segs;
     uint64_t next_chunk = jobs.empty() ? 0 : jobs[0].chunk0;
     for (const TermJob& j : jobs) {
-      const cas::Reconstruction& rec = recs_->get(j.xet_hash);
+      const cas::Reconstruction& rec = sh_->recs->get(j.xet_hash);
       if (j.t0 > j.t1 || j.t1 > rec.terms.size()) throw Error("RangeOutOfBounds", "term range of " + j.xet_hash);
       if (j.chunk0 != next_chunk) throw Error("InvalidArgument", "term jobs must cover consecutive chunk indices");
       for (uint32_t t = j.t0; t < j.t1; ++t) next_chunk += rec.terms[t].range.end - rec.terms[t].range.start;
@@ -254,12 +303,16 @@ struct DeviceXetPull::Impl {
         SegAttempt at = run_segments(gs, hashes, sizes, opt, attempt, {});
         auto drop = [&](size_t k) {
           for (size_t t = 0; t < at.sources[k].size(); ++t)
-            bridge_->settle(gs[k].rec->terms[gs[k].t0 + t].hash_hex, at.sources[k][t].src, at.sources[k][t].run_offset,
+            sh_->bridge->settle(gs[k].rec->terms[gs[k].t0 + t].hash_hex, at.sources[k][t].src, at.sources[k][t].run_offset,
                             at.sources[k][t].pending, false);
         };
         if (!at.fetch_err.empty()) {
-          for (size_t k = 0; k < gs.size(); ++k) drop(k);
-          for (const auto& j : jobs) book_.settle(*bridge_, j.xet_hash, false);
+          // The range is refetched elsewhere: drop the peer runs this call quarantined (never to be
+          // Merkle-checked); cache hits and earlier calls' runs wait for their file's verdict.
+          for (size_t k = 0; k < gs.size(); ++k)
+            for (const TermSource& ts : at.sources[k])
+              if (ts.src == Source::Peer && !ts.pending.empty())
+                sh_->bridge->settle(std::string(), ts.src, ts.run_offset, ts.pending, false);
           throw Error("DownloadFailed", at.fetch_err);
         }
         for (size_t k = 0; k < gs.size(); ++k) {
@@ -275,7 +328,7 @@ struct DeviceXetPull::Impl {
           for (size_t t = 0; t < at.sources[k].size(); ++t) {
             const TermSource& ts = at.sources[k][t];
             const cas::Term& term = gs[k].rec->terms[gs[k].t0 + t];
-            book_.add(jobs[i].xet_hash, term.hash_hex, ts.src, ts.run_offset, ts.pending);
+            sh_->book.add(jobs[i].xet_hash, term.hash_hex, ts.src, ts.run_offset, ts.pending);
             (ts.src == Source::Peer ? r.from_peer : ts.src == Source::Cache ? r.from_cache : r.from_cdn) +=
                 term.unpacked_length;
           }
@@ -284,17 +337,20 @@ struct DeviceXetPull::Impl {
           throw Error("IngestError", "code " + std::to_string(at.ingest_err >> 32) + " at " +
                                          std::to_string(at.ingest_err & 0xFFFFFFFFu));
       }
-      if (!bad.empty() && attempt == 0) bridge_->stats().refetches += bad.size();
+      if (!bad.empty() && attempt == 0) sh_->bridge->stats().refetches += bad.size();
       todo = std::move(bad);
     }
     if (!todo.empty()) throw Error("IngestError", "term range of " + jobs[todo[0]].xet_hash + " does not match its plan");
     return out;
   }
 
-  size_t settle(const std::string& hex, bool ok) { return book_.settle(*bridge_, hex, ok); }
-  std::vector<TermShape> term_shapes(const std::string& hex) { return recs_->shapes(hex); }
+  size_t settle(const std::string& hex, bool ok) { return sh_->book.settle(*sh_->bridge, hex, ok); }
+  void flush_cache_writes() {
+    if (sh_->writer) sh_->writer->flush();
+  }
+  std::vector<TermShape> term_shapes(const std::string& hex) { return sh_->recs->shapes(hex); }
 
-  std::string stats_json() const { return bridge_->stats_json(); }
+  std::string stats_json() const { return sh_->bridge->stats_json(); }
 
   size_t staging_bytes() const { return cap_; }
 
@@ -338,7 +394,7 @@ struct DeviceXetPull::Impl {
       const bool good = ok(j);
       for (size_t i = 0; i < at.seg.sources[j].size() && i < rec.terms.size(); ++i) {
         const TermSource& ts = at.seg.sources[j][i];
-        bridge_->settle(rec.terms[i].hash_hex, ts.src, ts.run_offset, ts.pending, good);
+        sh_->bridge->settle(rec.terms[i].hash_hex, ts.src, ts.run_offset, ts.pending, good);
       }
     }
   }
@@ -456,10 +512,10 @@ struct DeviceXetPull::Impl {
     {
       // Batches: consecutive terms whose fetched-size bounds fit one staging slot, so every term
       // has a reserved region of the pinned buffer (no refetch, no second copy pass: workers
-      // receive / copy their run straight into place).  Batch b fills slot b % 2.
+      // receive / copy their run straight into place).  Batch b fills slot b % slots.
       uint64_t max_bound = 0;
       for (size_t i = 0; i < n; ++i) max_bound = std::max(max_bound, term_bound(gt[i].ulen, gt[i].nchunks));
-      if (max_bound > cap_) grow_staging(max_bound);  // one huge term: enlarge both slots
+      if (max_bound > cap_) grow_staging(max_bound);  // one huge term: enlarge every slot
       struct Batch {
         size_t begin = 0, end = 0;
         std::vector<uint64_t> off, len, src_at;  // per term: region, fetched bytes, run start
@@ -485,22 +541,34 @@ struct DeviceXetPull::Impl {
         next = end;
       }
       const size_t nb = batches.size();
+      const size_t S = nslots_;
       auto chunk_lo = [&](size_t b) { return gt[batches[b].begin].chunk; };
       auto chunk_hi = [&](size_t b) { return batches[b].end < n ? gt[batches[b].end].chunk : nck; };
+      // every slot's pinned record table holds the largest batch (the streams are idle here: the
+      // previous pass synchronized them)
+      size_t max_recs = 1;
+      for (size_t b = 0; b < nb; ++b) max_recs = std::max<size_t>(max_recs, size_t(chunk_hi(b) - chunk_lo(b)));
+      for (auto& sl : slots_)
+        if (sl.rec_cap < max_recs) {
+          const size_t cap = std::max(max_recs, size_t(16384));
+          if (!sl.rec_pin.alloc(cap * sizeof(ZgChunk))) throw Error("HipError", "pinning the chunk records failed");
+          sl.rec_cap = cap;
+        }
+      hipEvent_t* ev = take_events(2 * nb);  // ev[2b]: batch b's copies landed; ev[2b+1]: its kernels ran
       // Continuous pipeline: the fetch workers take terms in order across batch boundaries, so the
-      // next batch's terms are already in flight while the current batch's slowest transfers finish
+      // next batches' terms are already in flight while the current batch's slowest transfers finish
       // (a per-batch join left the connections ~45 % idle: tools/direct_bench.py under ZEST_TRACE).
-      // A worker may fill slot b % 2 for batch b once ready[b % 2] >= b, i.e. once the GPU work of
-      // batch b - 2 on that slot has completed; the submitting thread (this one) waits for each
-      // batch's last term, queues its H2D + kernels, and frees the slot when they are done.
+      // A worker may fill slot b % S for batch b once ready[b % S] >= b, i.e. once the H2D copy of
+      // batch b - S out of that slot has completed (the releaser thread watches the copy events);
+      // the submitting thread (this one) waits for each batch's last term and queues its copies and
+      // kernels without waiting for the GPU.
       std::mutex mu;
       std::condition_variable cv;
-      size_t ready[2] = {0, 1};
+      std::vector<size_t> ready(S);
+      for (size_t i = 0; i < S; ++i) ready[i] = i;
       std::vector<size_t> remaining(nb);
       for (size_t b = 0; b < nb; ++b) remaining[b] = batches[b].end - batches[b].begin;
       bool abort = false;
-      for (size_t b = 0; b < std::min<size_t>(2, nb); ++b)
-        slots_[b].chunks_host.assign(size_t(chunk_hi(b) - chunk_lo(b)), ZgChunk{});
       std::atomic<size_t> k{0};
       auto fail = [&](const std::string& what) {
         std::lock_guard<std::mutex> g(mu);
@@ -514,10 +582,10 @@ struct DeviceXetPull::Impl {
           if (i >= n) return;
           const size_t b = batch_of[i];
           Batch& bt = batches[b];
-          Slot& s = slots_[b & 1];
+          Slot& s = slots_[b % S];
           {
             std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return abort || ready[b & 1] >= b; });
+            cv.wait(g, [&] { return abort || ready[b % S] >= b; });
             if (abort) return;
           }
           const size_t j = i - bt.begin;
@@ -528,7 +596,7 @@ struct DeviceXetPull::Impl {
             uint8_t* region = s.host + bt.off[j];
             const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
             auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-            XorbFetchResult r = bridge_->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
+            XorbFetchResult r = sh_->bridge->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
             at.sources[gt[i].seg][gt[i].term - segs[gt[i].seg].t0] = TermSource{r.source, r.run_offset, r.pending};
             auto idx = xet::index_chunks(r.bytes(), r.size());
             if (r.local_end > idx.size() || r.local_start >= r.local_end)
@@ -545,7 +613,7 @@ struct DeviceXetPull::Impl {
             bt.len[j] = e_end - a;
             // the device records of this term's chunks; a term that does not match its plan keeps
             // zero (no-op) records, so its file fails the Merkle check and takes the repair path
-            ZgChunk* cr = s.chunks_host.data() + (gt[i].chunk - chunk_lo(b));
+            ZgChunk* cr = s.recs() + (gt[i].chunk - chunk_lo(b));
             const uint64_t run0 = bt.src_at[j];
             uint64_t uoff = 0;
             bool ok = r.local_end - r.local_start == gt[i].nchunks;
@@ -575,9 +643,53 @@ struct DeviceXetPull::Impl {
           if (--remaining[b] == 0) cv.notify_all();
         }
       };
+      // Releaser: batch b's host slot goes back to the workers once its copies landed; with a
+      // progress callback, the batch's bytes are reported once its kernels ran.  Events are per
+      // batch, so nothing is re-recorded under its feet.
+      std::deque<size_t> issued;  // batches queued on the GPU, in order; SIZE_MAX ends the thread
+      auto releaser = [&]() {
+        (void)hipSetDevice(device_);
+        while (true) {
+          size_t b;
+          {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return !issued.empty(); });
+            b = issued.front();
+            issued.pop_front();
+          }
+          if (b == SIZE_MAX) return;
+          const bool copied = hipEventSynchronize(ev[2 * b]) == hipSuccess;
+          {
+            std::lock_guard<std::mutex> g(mu);
+            if (!copied) {
+              if (fetch_err.empty()) fetch_err = "hipEventSynchronize (H2D)";
+              abort = true;
+            }
+            ready[b % S] = b + S;
+            cv.notify_all();
+          }
+          if (progress && copied && hipEventSynchronize(ev[2 * b + 1]) == hipSuccess) {
+            // batches run in term order, and terms are in segment order: each touched segment's
+            // bytes are complete up to the end of its last term in this batch
+            const Batch& bt = batches[b];
+            for (size_t i = bt.begin; i < bt.end; ++i)
+              if (i + 1 == bt.end || gt[i + 1].seg != gt[i].seg)
+                progress(gt[i].seg, gt[i].dst + gt[i].ulen - seg_dst0[gt[i].seg]);
+          }
+        }
+      };
       std::vector<std::thread> ts;
       const int nt = int(std::min<size_t>(size_t(threads_), n));
       for (int t = 0; t < nt; ++t) ts.emplace_back(worker);
+      std::thread rel(releaser);
+      auto stop_releaser = [&]() {
+        {
+          std::lock_guard<std::mutex> g(mu);
+          issued.push_back(SIZE_MAX);
+        }
+        cv.notify_all();
+        rel.join();
+      };
       try {
         for (size_t b = 0; b < nb; ++b) {
           {
@@ -587,7 +699,7 @@ struct DeviceXetPull::Impl {
             if (abort) break;
           }
           const Batch& bt = batches[b];
-          Slot& s = slots_[b & 1];
+          Slot& s = slots_[b % S];
           uint64_t top = 0;
           for (size_t j = 0; j < bt.len.size(); ++j) {
             at.fetched += bt.len[j];
@@ -596,51 +708,53 @@ struct DeviceXetPull::Impl {
           }
           const uint64_t c0 = chunk_lo(b);
           const int nchunks = int(chunk_hi(b) - c0);
-          s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
-          trace::Span submit_span("device", "H2D + place/hash");
-          submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
-          hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, stream_), "H2D");
-          if (nchunks)
-            hip_check(hipMemcpyAsync(s.chunks_dev.p, s.chunks_host.data(), sizeof(ZgChunk) * size_t(nchunks),
-                                     hipMemcpyHostToDevice, stream_),
-                      "H2D chunk records");
           uint64_t ubytes = 0;
           for (size_t i = bt.begin; i < bt.end; ++i) ubytes += gt[i].ulen;
           bool compressed = false;
-          for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.chunks_host[size_t(c)].scheme != 0;
+          for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.recs()[c].scheme != 0;
           const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
-          hash_scratch_.ensure(hs_bytes);  // one stream: the previous batch's hash launch is ordered before
+          // the slot's device staging, records and scratch are read by batch b - S's kernels
+          if (b >= S && (s.chunks_dev.n < size_t(nchunks ? nchunks : 1) || s.scratch.n < hs_bytes))
+            hip_check(hipEventSynchronize(ev[2 * (b - S) + 1]), "hipEventSynchronize");  // growing: wait, then free
+          s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
+          s.scratch.ensure(hs_bytes);
+          trace::Span submit_span("device", "queue H2D + place/hash");
+          submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
+          if (b >= S) hip_check(hipStreamWaitEvent(copy_stream_, ev[2 * (b - S) + 1], 0), "hipStreamWaitEvent");
+          hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, copy_stream_), "H2D");
+          if (nchunks)
+            hip_check(hipMemcpyAsync(s.chunks_dev.p, s.recs(), sizeof(ZgChunk) * size_t(nchunks), hipMemcpyHostToDevice,
+                                     copy_stream_),
+                      "H2D chunk records");
+          hip_check(hipEventRecord(ev[2 * b], copy_stream_), "event");
+          hip_check(hipStreamWaitEvent(stream_, ev[2 * b], 0), "hipStreamWaitEvent");
           // decode (when the batch has compressed chunks) + one fused pass placing raw chunks and
           // hashing every chunk (csrc/gpu/blake3_flat.hip PlaceSrc)
           hip_check(zg_ingest_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, compressed ? 1 : 0, err_.p,
                                      hash_out + 32 * (hash_base + c0), size_out ? size_out + hash_base + c0 : nullptr, 0,
-                                     hash_scratch_.p, hs_bytes, stream_),
+                                     s.scratch.p, hs_bytes, stream_),
                     "ingest");
-          hip_check(hipEventRecord(s.done, stream_), "event");
-          // the slot's pinned bytes and records are free for batch b + 2 once this batch's copies ran
-          hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");
-          if (b + 2 < nb) s.chunks_host.assign(size_t(chunk_hi(b + 2) - chunk_lo(b + 2)), ZgChunk{});
+          hip_check(hipEventRecord(ev[2 * b + 1], stream_), "event");
           {
             std::lock_guard<std::mutex> g(mu);
-            ready[b & 1] = b + 2;
-            cv.notify_all();
+            issued.push_back(b);
           }
-          if (progress) {
-            // batches run in term order, and terms are in segment order: each touched segment's
-            // bytes are complete up to the end of its last term in this batch
-            for (size_t i = bt.begin; i < bt.end; ++i)
-              if (i + 1 == bt.end || gt[i + 1].seg != gt[i].seg)
-                progress(gt[i].seg, gt[i].dst + gt[i].ulen - seg_dst0[gt[i].seg]);
-          }
+          cv.notify_all();
         }
       } catch (const std::exception& e) {
         fail(e.what());
         for (auto& t : ts) t.join();
+        (void)hipStreamSynchronize(copy_stream_);
         (void)hipStreamSynchronize(stream_);
+        stop_releaser();
         throw;
       }
       for (auto& t : ts) t.join();
-      hip_check(hipStreamSynchronize(stream_), "sync");
+      const hipError_t e1 = hipStreamSynchronize(copy_stream_);
+      const hipError_t e2 = hipStreamSynchronize(stream_);
+      stop_releaser();
+      hip_check(e1, "sync copy stream");
+      hip_check(e2, "sync compute stream");
     }
     if (!fetch_err.empty()) return at;
     hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
@@ -654,7 +768,8 @@ struct DeviceXetPull::Impl {
   }
 
   void grow_staging(uint64_t bytes) {
-    hip_check(hipStreamSynchronize(stream_), "sync");  // no copy still reads the old buffers
+    hip_check(hipStreamSynchronize(copy_stream_), "sync");  // no copy still reads the old buffers
+    hip_check(hipStreamSynchronize(stream_), "sync");
     for (auto& s : slots_) {
       s.host = nullptr;
       if (!s.pin.alloc(bytes + 4096)) throw Error("HipError", "pinning the staging buffer failed");
@@ -664,31 +779,38 @@ struct DeviceXetPull::Impl {
     cap_ = bytes;
   }
 
-  Config cfg_;
+  std::shared_ptr<Shared> sh_;
   int device_;
   size_t cap_;
   int threads_;
-  storage::XorbRegistry registry_;
-  std::unique_ptr<storage::XorbCache> cache_;
-  std::unique_ptr<SwarmDownloader> swarm_;
-  std::unique_ptr<XetBridge> bridge_;
-  std::unique_ptr<ReconCache> recs_;
-  SettleBook book_;
-  hipStream_t stream_ = nullptr;
+  size_t nslots_;
+  hipStream_t stream_ = nullptr;       // kernels
+  hipStream_t copy_stream_ = nullptr;  // H2D copies
   std::mutex init_mu_;
   bool device_ready_ = false;
-  Slot slots_[2];
+  std::vector<Slot> slots_;
+  std::vector<hipEvent_t> events_;
   DevBuf<unsigned long long> err_;
   DevBuf<uint8_t> hashes_;
   DevBuf<uint64_t> sizes_;
   DevBuf<ZgMerkleJob> merkle_job_;
   DevBuf<uint8_t> merkle_scratch_;
-  DevBuf<uint8_t> hash_scratch_;
   DevBuf<uint8_t> root_;
 };
 
 
-DeviceXetPull::DeviceXetPull(const DevicePullOptions& opt) : impl_(std::make_unique<Impl>(opt)) {}
+DeviceXetPull::DeviceXetPull(const DevicePullOptions& opt) : impl_(std::make_unique<Impl>(opt, nullptr)) {}
+DeviceXetPull::DeviceXetPull(const DevicePullOptions& opt, std::shared_ptr<Shared> shared)
+    : impl_(std::make_unique<Impl>(opt, std::move(shared))) {}
+std::unique_ptr<DeviceXetPull> DeviceXetPull::sibling(size_t staging_bytes, int slots) const {
+  DevicePullOptions o;
+  o.device = impl_->device_;
+  o.staging_bytes = staging_bytes ? staging_bytes : impl_->cap_;
+  o.threads = impl_->threads_;
+  o.slots = slots;
+  o.defer_device = true;
+  return std::unique_ptr<DeviceXetPull>(new DeviceXetPull(o, impl_->sh_));
+}
 DeviceXetPull::~DeviceXetPull() = default;
 
 std::vector<PullFileStats> DeviceXetPull::pull_files(const std::vector<PullRequest>& files,
@@ -710,7 +832,21 @@ std::vector<TermJobResult> DeviceXetPull::pull_terms(const std::vector<TermJob>&
 }
 size_t DeviceXetPull::settle(const std::string& xet_hash, bool ok) { return impl_->settle(xet_hash, ok); }
 std::vector<TermShape> DeviceXetPull::term_shapes(const std::string& xet_hash) { return impl_->term_shapes(xet_hash); }
+std::vector<TermKey> DeviceXetPull::term_keys(const std::string& xet_hash) { return impl_->sh_->recs->keys(xet_hash); }
+std::vector<uint8_t> DeviceXetPull::cached_terms(const std::vector<std::string>& hexes,
+                                                 const std::vector<uint32_t>& starts, const std::vector<uint32_t>& ends) {
+  return zest::cached_terms(*impl_->sh_->cache, hexes, starts, ends, impl_->threads_);
+}
+void DeviceXetPull::reset_reconstructions() { impl_->sh_->recs->clear(); }
 void DeviceXetPull::init_device() { impl_->init_device(); }
+void DeviceXetPull::flush_cache_writes() { impl_->flush_cache_writes(); }
+std::string DeviceXetPull::cache_writer_json() const {
+  auto* w = impl_->sh_->writer.get();
+  if (!w) return "{}";
+  const auto st = w->stats();
+  return "{\"queued_bytes\":" + std::to_string(st.queued_bytes) + ",\"written_bytes\":" + std::to_string(st.written_bytes) +
+         ",\"dropped_bytes\":" + std::to_string(st.dropped_bytes) + "}";
+}
 std::string DeviceXetPull::stats_json() const { return impl_->stats_json(); }
 size_t DeviceXetPull::staging_bytes() const { return impl_->staging_bytes(); }
 

@@ -29,7 +29,8 @@ struct DevicePullOptions {
   bool dht = true;
   std::vector<std::string> dht_bootstrap;
   int device = 0;
-  size_t staging_bytes = size_t(1) << 30;  // per pinned slot (two slots)
+  size_t staging_bytes = size_t(1) << 30;  // per pinned slot
+  int slots = 0;                           // pinned staging slots (0: ZEST_DEVICE_SLOTS, default 3)
   int threads = 16;                        // fetch workers
   bool defer_device = false;  // construct the host side only; init_device() (or the first pull) does the rest
 };
@@ -47,7 +48,7 @@ struct PullFileStats {
   std::vector<uint32_t> chunk_lens;  // uncompressed size of every chunk, in file order
 };
 
-// Called on the pipeline's submit thread after a staging batch's kernels completed: file `file`
+// Called on the pipeline's releaser thread after a staging batch's kernels completed: file `file`
 // (index into the request list) now holds its verified-or-not bytes [0, bytes) in HBM.  `attempt` is
 // 0 for the first pass and 1 for the CDN repair pass of files whose Merkle root missed (which
 // overwrites their bytes).  Keep it cheap: the next batch waits for it.
@@ -71,12 +72,27 @@ class DeviceXetPull {
                                         bool repair = false);
   size_t settle(const std::string& xet_hash, bool ok);
   std::vector<TermShape> term_shapes(const std::string& xet_hash);  // (ulen, chunks) per term
+  std::vector<TermKey> term_keys(const std::string& xet_hash);      // (xorb hex, chunk range) per term
+  // Which of the terms (xorb hex, chunk range) the local xorb cache holds (planner possession check).
+  std::vector<uint8_t> cached_terms(const std::vector<std::string>& hexes, const std::vector<uint32_t>& starts,
+                                    const std::vector<uint32_t>& ends);
+  void reset_reconstructions();  // between pulls only
   std::string stats_json() const;
   size_t staging_bytes() const;
-  // Device set-up (HIP stream, pinned + device staging) when the options deferred it.  Idempotent.
+  // Device set-up (HIP streams, pinned + device staging) when the options deferred it.  Idempotent.
   void init_device();
+  // A second pipeline (own streams and staging, `staging_bytes` per slot, 0 = this one's) over the
+  // SAME host state: Xet session, caches, swarm, reconstructions and settle book.  The swarm pull
+  // fetches round k + 1 on it while round k is agreed; settle() on either settles both's runs.
+  std::unique_ptr<DeviceXetPull> sibling(size_t staging_bytes = 0, int slots = 0) const;
+  // Wait for the write-behind cache queue (runs queued by fetches, and settle operations).
+  void flush_cache_writes();
+  std::string cache_writer_json() const;  // {"queued_bytes", "written_bytes", "dropped_bytes"}
+
+  struct Shared;
 
  private:
+  DeviceXetPull(const DevicePullOptions& opt, std::shared_ptr<Shared> shared);
   struct Impl;
   std::unique_ptr<Impl> impl_;
 };

@@ -374,3 +374,151 @@ def test_swarm_plan_term_shares_and_jobs():
     assert round_weights(3 << 30, 1 << 30) == [1.0, 1.0, 1.0]
     cuts = split_bytes(ulen, 0, 40, w)
     assert cuts[0][0] == 0 and cuts[-1][1] == 40 and all(a <= b for a, b in cuts)
+
+
+def test_assign_owners_follows_possession():
+    """Ownership follows possession: nothing held -> the byte-balanced contiguous
+    split; one rank holding everything -> it owns every term (the node's seeder); every rank holding
+    everything (a shared node cache) -> balanced again; partial holdings -> holders own what they
+    hold and the rest is water-filled so totals even out."""
+    import numpy as np
+
+    from zest_amd.parallel.swarm_pull import assign_owners, rank_items
+    ulen = np.full(12, 100, dtype=np.int64)
+    assert assign_owners(ulen, None, 3).tolist() == [0] * 4 + [1] * 4 + [2] * 4
+    held = np.zeros((3, 12), dtype=bool)
+    held[0] = True
+    assert assign_owners(ulen, held, 3).tolist() == [0] * 12
+    assert assign_owners(ulen, np.ones((3, 12), dtype=bool), 3).tolist() == [0] * 4 + [1] * 4 + [2] * 4
+    held = np.zeros((3, 12), dtype=bool)
+    held[2, :6] = True          # rank 2 holds the first half
+    own = assign_owners(ulen, held, 3)
+    assert (own[:6] == 2).all()
+    # the other half goes to ranks 0 and 1 (rank 2 is already at half the model)
+    assert set(own[6:].tolist()) <= {0, 1} and sorted(np.bincount(own, minlength=3).tolist()) == [3, 3, 6]
+    # items: contiguous ranges, cut into rounds and at the gaps of a rank's share
+    own = np.array([0, 0, 1, 1, 0, 0, 0, 1, 1, 1, 0, 0])
+    assert rank_items(ulen, own, 0, [1.0]) == [(0, 2), (4, 7), (10, 12)]
+    assert rank_items(ulen, own, 1, [1.0, 1.0]) == [(2, 4), (7, 8), (8, 10)]
+    assert rank_items(ulen, own, 2, [1.0]) == []
+
+
+def _warm_worker(rank, world_size, port, repo, q, cache_dirs):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZEST_CACHE_DIR=cache_dirs[rank])
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from zest_amd.parallel import swarm_pull
+        st = {}
+        try:
+            t = swarm_pull(repo, p2p=False, dht=False, stats=st)
+            q.put((rank, "ok", {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}, st))
+        except Exception as e:
+            q.put((rank, type(e).__name__, str(e), st))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_warm(world_size, repo, cache_dirs):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_warm_worker, args=(r, world_size, port, repo, q, cache_dirs))
+             for r in range(world_size)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_swarm_pull_warm_rank_seeds_the_node(hub_env, tmp_path):
+    """BASELINE config 2 on the public path (1 seeder + N leechers): rank 0's xorb cache already
+    holds the model (an earlier pull), ranks 1 and 2 start cold.  The possession have-map makes rank
+    0 own every term: it reads them from its cache and the others receive everything over the
+    exchange -- no rank touches the CDN, and every rank still verifies every tensor."""
+    world, hub = hub_env
+    want = _expected(world)
+    dirs = [str(tmp_path / f"cache{r}") for r in range(3)]
+    first = _run_warm(1, world.spec.repo_id, dirs[:1])          # rank 0 warms its cache from the CDN
+    assert first[0][1] == "ok", first
+    before = hub.counters.get("xorb_get", 0)
+    res = _run_warm(3, world.spec.repo_id, dirs)
+    assert [r[1] for r in res] == ["ok"] * 3, res
+    total = sum(f.size for f in world.xet_files)
+    for _, _, got, st in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert st["possession"][0] == total and st["possession"][1:] == [0, 0]
+    assert hub.counters.get("xorb_get", 0) == before, "a rank fetched from the CDN"
+    r0, r1, r2 = (r[3] for r in res)
+    assert r0["from_cache"] == total and r0["from_cdn"] == 0 and r0["fetched_bytes"] == total
+    assert r1["fetched_bytes"] == 0 and r2["fetched_bytes"] == 0
+    assert r1["received_bytes"] == total and r2["p2p_ratio"] == 1.0
+
+
+def _mem_origin_worker(q, seed, compressed):
+    """A one-rank swarm_pull whose CDN is an in-process memory origin (mem:// fetch_info URLs),
+    served from a DevicePuller's origin layout -- the shape of bench.py's swarm row, on the CPU."""
+    import tempfile
+
+    import torch.distributed as dist
+
+    from zest_amd import ops
+    from zest_amd.engine import DevicePuller
+    from zest_amd.parallel import swarm_pull
+    from zest_amd.testing import FakeHub
+    try:
+        world = _sharded_world(seed)
+        contents = world.build_on_host()
+        arena = torch.zeros(world.arena_bytes + 4096, dtype=torch.uint8)[: world.arena_bytes]
+        puller = DevicePuller(world, arena, 0, 1, round_bytes=1 << 20)
+        puller.build_origin_host(contents)
+        hub = FakeHub()
+        hub.xorb_url = "mem://origin"
+        hub.start()
+        hub.add_world(world, exact=True, payload=False)
+        T = world.terms
+        ops.mem_origin_add([world.xorb_hash_hex(int(T["xorb"][t])) for t in range(len(T))],
+                           [int(T["ser0"][t]) for t in range(len(T))],
+                           [puller.origin.ptr + int(puller.term_origin_off[t]) for t in range(len(T))],
+                           [int(T["ser_len"][t]) for t in range(len(T))])
+        for k, v in hub.env(tempfile.mkdtemp()).items():
+            os.environ[k] = v
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
+        st = {}
+        t = swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st, reuse_pipeline=True)
+        got = {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}
+        st2 = {}
+        swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st2, reuse_pipeline=True)
+        from zest_amd.parallel.swarm_pull import release_pipelines
+        release_pipelines()
+        q.put(("ok", got, st, st2, hub.counters.get("xorb_get", 0), hub.counters.get("cas_v1", 0)))
+        dist.destroy_process_group()
+        hub.stop()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((type(e).__name__, traceback.format_exc(), None, None, 0, 0))
+
+
+def test_swarm_pull_from_memory_origin_and_pipeline_reuse():
+    """The bench's public-path row on the CPU: fetch_info URLs mem://origin/<xorb> are served from
+    registered host memory (no sockets, no xorb GETs), every tensor arrives intact, and a second pull
+    with reuse_pipeline=True reuses the first one's pipelines but asks the CAS for the
+    reconstructions again."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_mem_origin_worker, args=(q, 21, False))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, got, st, st2, xorb_gets, cas_calls = res
+    want = _expected(_sharded_world(21))
+    assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+    assert xorb_gets == 0  # every byte came from the memory origin
+    assert st["from_cdn"] == st["total_bytes"] and not st["reused_pipeline"] and st2["reused_pipeline"]
+    n_files = st["files"]
+    assert cas_calls >= 2 * n_files  # reconstructions fetched anew by the second pull

@@ -622,6 +622,22 @@ class DevicePuller:
     def _run_bytes(self, c0: int, n: int) -> int:
         return int(self._chunk_len_csum[c0 + n] - self._chunk_len_csum[c0])
 
+    def release_device(self) -> None:
+        """Drop this puller's device buffers (arena view, staging, tables) but keep the pinned origin:
+        bench.py's swarm row serves its CDN from the origin while swarm_pull allocates its own arena."""
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        self.arena = None
+        self.staging = []
+        self.hashes = self.sizes = self.expected = None
+        self.ws_lanes = []
+        self.xchg = None
+        for k in ("merkle_scratch", "roots", "jobs_dev", "chunk_off_dev", "chunk_len_dev"):
+            if hasattr(self, k):
+                setattr(self, k, None)
+        for rw in self.rounds:
+            rw.terms_dev = None
+
     def close(self):
         if self.is_cuda:
             # queued H2D copies still read the pinned origin and kernels the staging buffers: the

@@ -50,6 +50,30 @@ def hip():
     return _hip
 
 
+def mem_origin_add(hexes, starts, ptrs, lens) -> int:
+    """Serve fetch_info URLs mem://<name>/<xorb hex> from host memory (csrc/core/hub.h): run i is
+    bytes [starts[i], starts[i] + lens[i]) of xorb hexes[i], at address ptrs[i] (kept alive by the
+    caller).  Registered in both native modules (each links its own host core): _core's host fetches
+    and _hip's DeviceXetPull read the same origin."""
+    args = (list(hexes), [int(x) for x in starts], [int(x) for x in ptrs], [int(x) for x in lens])
+    n = _core.mem_origin_add(*args)
+    try:
+        from .. import _hip
+    except ImportError:
+        return n
+    _hip.mem_origin_add(*args)
+    return n
+
+
+def mem_origin_clear() -> None:
+    _core.mem_origin_clear()
+    try:
+        from .. import _hip
+    except ImportError:
+        return
+    _hip.mem_origin_clear()
+
+
 def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

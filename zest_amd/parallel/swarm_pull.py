@@ -100,6 +100,64 @@ def round_weights(share_bytes: int, round_bytes: int, taper: bool = True) -> lis
     return list(HEAD_TAPER) + [1.0] * mid + list(TAIL_TAPER)
 
 
+def assign_owners(ulen: np.ndarray, held: np.ndarray | None, world: int) -> np.ndarray:
+    """Owner rank of every term.  `held` (bool [world, n_terms], or None) says which rank's local
+    xorb cache already covers which term.
+
+    Possession first (the reference's per-term waterfall is cache-first, xet_bridge.zig:161-170):
+    consecutive terms held by the same set of ranks are split byte-balanced among those holders,
+    least-loaded holder first -- a rank that holds the whole model becomes the node's seeder and its
+    peers fetch nothing from the network; a cache shared by every rank is read 1/world per rank.
+    The terms nobody holds are then water-filled: cut contiguously (rank order) so that every rank's
+    total ends as close to 1/world of the model as the held shares allow.  With nothing held this is
+    the plain byte-balanced contiguous split."""
+    nt = len(ulen)
+    owner = np.full(nt, -1, dtype=np.int64)
+    load = np.zeros(world, dtype=np.float64)
+    u = ulen.astype(np.float64)
+    if held is not None and nt and held.any():
+        cols = np.ascontiguousarray(held.T.astype(bool))
+        change = np.concatenate([[True], (cols[1:] != cols[:-1]).any(axis=1)]) if nt > 1 else np.array([True])
+        starts = np.flatnonzero(change).tolist() + [nt]
+        for a, b in zip(starts[:-1], starts[1:]):
+            who = np.flatnonzero(cols[a])
+            if not len(who):
+                continue
+            order = sorted(who.tolist(), key=lambda r: (load[r], r))
+            for (x, y), r in zip(split_bytes(ulen, a, b, [1.0] * len(order)), order):
+                owner[x:y] = r
+                load[r] += u[x:y].sum()
+    free = np.flatnonzero(owner < 0)
+    if len(free):
+        total = load.sum() + u[free].sum()
+        target = np.maximum(total / world - load, 0.0)
+        if target.sum() <= 0:
+            target = np.ones(world)
+        cu = np.cumsum(u[free])
+        frac = np.cumsum(target) / target.sum()
+        cuts = [0] + [int(np.searchsorted(cu, cu[-1] * frac[k], side="left")) + 1 for k in range(world - 1)] + [len(free)]
+        cuts = np.maximum.accumulate(np.minimum(np.array(cuts), len(free)))
+        for r in range(world):
+            owner[free[cuts[r]:cuts[r + 1]]] = r
+    return owner
+
+
+def rank_items(ulen: np.ndarray, owner: np.ndarray, rank: int, weights) -> list[tuple[int, int]]:
+    """`rank`'s terms as contiguous items: its share cut into len(weights) byte-proportional rounds,
+    and additionally at every gap between its runs (an item is one contiguous term range)."""
+    idx = np.flatnonzero(owner == rank)
+    if not len(idx):
+        return []
+    cu = np.cumsum(ulen[idx].astype(np.float64))
+    frac = np.cumsum(np.asarray(weights, dtype=np.float64))
+    frac /= frac[-1]
+    cut = {int(np.searchsorted(cu, cu[-1] * frac[k], side="left")) + 1 for k in range(len(weights) - 1)}
+    gaps = set((np.flatnonzero(np.diff(idx) != 1) + 1).tolist())
+    pos = sorted({0} | {p for p in cut | gaps if 0 < p < len(idx)})
+    ends = pos[1:] + [len(idx)]
+    return [(int(idx[a]), int(idx[b - 1]) + 1) for a, b in zip(pos, ends)]
+
+
 class _Plan:
     """The repository's Xet files laid out in one arena and their terms as one global table."""
 
@@ -294,10 +352,13 @@ class _Membership:
 # ----------------------------------------------------------------------------------------------
 class _Fetcher:
     def __init__(self, repo, revision, repo_type, device, p2p, peers, tracker, dht, dht_bootstrap, staging_bytes,
-                 threads):
+                 threads, parent: "_Fetcher | None" = None, slots: int = 0):
         self.args = (repo, revision, repo_type, p2p, list(peers or []), tracker, dht, list(dht_bootstrap or []))
         self.device = device
-        self.staging_bytes, self.threads = staging_bytes, threads
+        self.staging_bytes, self.threads, self.slots = staging_bytes, threads, slots
+        # GPU: a second pipeline is a sibling of the first (own streams + staging, the same Xet
+        # session, caches, reconstructions and settle book)
+        self.parent = parent
         self._impl = None
         self._warm = None
         self._warm_err = None
@@ -334,15 +395,28 @@ class _Fetcher:
     def _make(self):
         if self._impl is None:
             repo, revision, repo_type, p2p, peers, tracker, dht, boot = self.args
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.parent is not None:
+                self._impl = self.parent.impl.sibling(self.staging_bytes, self.slots)
+            elif self.device.type == "cuda":
                 self._impl = ops.hip().DeviceXetPull(repo, revision, repo_type, p2p, peers, tracker, dht, boot,
-                                                     self.device.index or 0, self.staging_bytes, self.threads)
+                                                     self.device.index or 0, self.staging_bytes, self.threads,
+                                                     self.slots)
             else:
                 self._impl = _core.HostXetFetcher(repo, revision, repo_type, p2p, peers, tracker, dht, boot,
                                                   self.threads)
 
     def shapes(self, xet_hash: str):
         return self.impl.term_shapes(xet_hash)
+
+    def keys(self, xet_hash: str):
+        return self.impl.term_keys(xet_hash)
+
+    def reset_reconstructions(self) -> None:
+        if self._impl is not None and self.parent is None:  # siblings share the parent's
+            self._impl.reset_reconstructions()
+
+    def held(self, hexes, starts, ends) -> np.ndarray:
+        return np.frombuffer(self.impl.cached_terms(hexes, starts, ends), dtype=np.uint8).astype(bool)
 
     def fetch(self, jobs, hashes: torch.Tensor, sizes: torch.Tensor | None, repair: bool = False):
         if self.device.type == "cuda":
@@ -361,6 +435,12 @@ class _Fetcher:
 
     def stats(self) -> dict:
         return json.loads(self._impl.stats_json()) if self._impl is not None else {}
+
+    def cache_writer(self) -> dict:
+        """Write-behind cache queue counters (GPU pipelines; {} on CPU)."""
+        if self._impl is None or not hasattr(self._impl, "cache_writer_json"):
+            return {}
+        return json.loads(self._impl.cache_writer_json())
 
 
 # ----------------------------------------------------------------------------------------------
@@ -381,7 +461,7 @@ def _fault_spec() -> dict:
 
 class _Swarm:
     def __init__(self, repo, revision, group, device, *, p2p, peers, tracker, dht, dht_bootstrap, repo_type,
-                 verify_received, staging_bytes, threads, round_bytes, exchange):
+                 verify_received, staging_bytes, threads, round_bytes, exchange, reuse=False, possession=True):
         self.t0 = time.perf_counter()
         self.times: dict = {}
         self.repo, self.revision, self.repo_type = repo, revision, repo_type
@@ -395,22 +475,40 @@ class _Swarm:
         self.verify = verify_received
         self.round_bytes = int(round_bytes)
         self.exchange_req = exchange
-        self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
-                                staging_bytes, threads)
-        self.fetcher.prewarm()
         # Cross-round fetch pipelining (ZEST_SWARM_PIPELINE, default on at N > 1): round k + 1's
         # ranges are fetched on a second pipeline while round k's fetch drains and is agreed, so the
-        # connections never sit idle at a round boundary.  (The second pipeline joins no DHT: one
-        # node per process is enough, and two would contend for the DHT port.)
+        # connections never sit idle at a round boundary.  On GPUs the second pipeline is a sibling
+        # of the first (half the staging, the same Xet session, caches and reconstructions); on CPU
+        # groups it is a second host fetcher that joins no DHT (one node per process is enough).
         self.pipelined = os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
-        self.fetchers = [self.fetcher]
-        if self.pipelined:
-            f2 = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, False, dht_bootstrap,
-                          staging_bytes, threads)
-            f2.prewarm()
-            self.fetchers.append(f2)
+        self.reuse_key = (repo, revision, repo_type, str(self.device), bool(p2p), tuple(peers or []), tracker,
+                          bool(dht), tuple(dht_bootstrap or []), int(staging_bytes), int(threads), self.pipelined,
+                          os.environ.get("HF_ENDPOINT"), os.environ.get("ZEST_CACHE_DIR"))
+        self.reuse = reuse
+        kept = _PIPELINES.pop(self.reuse_key, None) if reuse else None
+        self.reused = kept is not None
+        if kept is not None:  # a previous pull's pipelines: staging pinned, session up; reconstructions anew
+            self.fetchers = kept
+            self.fetcher = kept[0]
+            for f in kept:
+                f.reset_reconstructions()
+        else:
+            self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
+                                    staging_bytes, threads)
+            self.fetcher.prewarm()
+            self.fetchers = [self.fetcher]
+            if self.pipelined:
+                if self.cuda:
+                    f2 = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, False, dht_bootstrap,
+                                  max(64 << 20, staging_bytes // 2), threads, parent=self.fetcher, slots=2)
+                else:
+                    f2 = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, False, dht_bootstrap,
+                                  staging_bytes, threads)
+                    f2.prewarm()
+                self.fetchers.append(f2)
         self._fut = None
         self.fault = _fault_spec()
+        self.possession = possession
         self.stats = {"reassigned": 0, "recovered_ranks": 0, "resent_bytes": 0, "repaired_files": 0,
                       "from_peer": 0, "from_cdn": 0, "from_cache": 0, "fetched_wire_bytes": 0}
 
@@ -468,17 +566,36 @@ class _Swarm:
                 xet = [f for f in st if f["xet_hash"]]
                 shapes = _parallel_map(lambda f: [tuple(x) for x in self.fetcher.shapes(f["xet_hash"])], xet,
                                         max(8, self.fetcher.threads))
-                obj = ("ok", commit, st, shapes)
+                # (xorb hex, chunk range) per term: every rank checks its own cache against them
+                keys = [[list(k) for k in self.fetcher.keys(f["xet_hash"])] for f in xet] if self.possession else None
+                obj = ("ok", commit, st, shapes, keys)
             except Exception as e:  # noqa: BLE001 - every rank leaves the same way
                 obj = ("err", f"{type(e).__name__}: {e}")
         obj = self._plan_from0(obj)
         if obj[0] != "ok":
             raise SwarmPullError(f"listing/planning {self.repo}@{self.revision} failed on rank 0: {obj[1]}")
-        _, self.commit, st_files, shapes = obj
+        _, self.commit, st_files, shapes, keys = obj
         self.xet_files = [f for f in st_files if f["xet_hash"]]
         self.plain_files = [f for f in st_files if not f["xet_hash"]]
         self.plan = _Plan(self.xet_files, shapes)
+        self.term_keys = [k for fk in keys for k in fk] if keys is not None else None
         self._mark("plan_s", t)
+
+    def gather_possession(self):
+        """Which terms each rank's xorb cache already covers (have-map): checked
+        locally against the planned terms' chunk ranges, then all-gathered as bitmaps on the control
+        group.  Sets self.held (bool [world, n_terms]) or None when nobody holds anything."""
+        self.held = None
+        if self.term_keys is None or not len(self.term_keys):
+            return
+        t = time.perf_counter()
+        hexes = [k[0] for k in self.term_keys]
+        mine = self.fetcher.held(hexes, [int(k[1]) for k in self.term_keys], [int(k[2]) for k in self.term_keys])
+        bits = self._gather(np.packbits(mine).tobytes())
+        nt = len(self.term_keys)
+        held = np.stack([np.unpackbits(np.frombuffer(b, dtype=np.uint8))[:nt].astype(bool) for b in bits])
+        self.held = held if held.any() else None
+        self._mark("possession_s", t)
 
     def allocate(self):
         t = time.perf_counter()
@@ -508,14 +625,11 @@ class _Swarm:
     def shard(self):
         """Per-rank queues of items (term ranges), identical on every rank."""
         P = self.plan
-        nt = len(P.t_ulen)
         W = self.m.world
-        cu = np.cumsum(P.t_ulen.astype(np.float64))
-        total = cu[-1] if nt else 0.0
-        bounds = [0] + [int(np.searchsorted(cu, total * r / W, side="left")) + 1 for r in range(1, W)] + [nt]
-        bounds = np.maximum.accumulate(np.minimum(np.array(bounds), nt))
-        shares = [(int(bounds[r]), int(bounds[r + 1])) for r in range(W)]
-        max_share = max((int(P.t_ulen[a:b].sum()) for a, b in shares), default=0)
+        held = getattr(self, "held", None)
+        self.owner = assign_owners(P.t_ulen, held, W)
+        shares = [int(P.t_ulen[self.owner == r].sum()) for r in range(W)]
+        max_share = max(shares, default=0)
         taper = os.environ.get("ZEST_ROUND_TAPER", "1") != "0"
         # One rank: nothing to overlap a fetch with, so the whole share is one pull_terms call (every
         # round boundary drains the fetch pipeline: 16 rounds of 1 GiB cost ~25 ms each on
@@ -523,11 +637,13 @@ class _Swarm:
         weights = round_weights(max_share, self.round_bytes, taper) if max_share and W > 1 else [1.0]
         self.items: list[tuple[int, int]] = []
         self.queue: list[list[int]] = [[] for _ in range(W)]
-        for r, (a, b) in enumerate(shares):
-            for ra, rb in split_bytes(P.t_ulen, a, b, weights):
-                if rb > ra:
-                    self.items.append((ra, rb))
-                    self.queue[r].append(len(self.items) - 1)
+        for r in range(W):
+            for ra, rb in rank_items(P.t_ulen, self.owner, r, weights):
+                self.items.append((ra, rb))
+                self.queue[r].append(len(self.items) - 1)
+        self.held_bytes = [int(P.t_ulen[(self.owner == r) & held[r]].sum()) if held is not None else 0
+                           for r in range(W)]
+        self.share_bytes = shares
         self.n_rounds_planned = len(weights)
         # Rank 0 holds every reconstruction from planning; the others fetch theirs now, on a side
         # thread, while the arena is mapped and the exchange autotuned, instead of in front of
@@ -685,7 +801,9 @@ class _Swarm:
     def _submit(self, nxt: list, round_no: int):
         from concurrent.futures import ThreadPoolExecutor
         if not hasattr(self, "_pool"):
-            self._pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="zest-swarm-fetch")
+            # HIP's current device is per thread: the pool's threads start on this rank's GPU
+            init = (lambda: torch.cuda.set_device(self.device)) if self.cuda else None
+            self._pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="zest-swarm-fetch", initializer=init)
         f = self.fetchers[round_no % len(self.fetchers)]
         return self._pool.submit(self._fetch_one, f, nxt[self.m.rank], round_no)
 
@@ -1015,6 +1133,17 @@ def _merged_stats(parts: list) -> dict:
     return out
 
 
+# Pipelines kept by pulls made with reuse_pipeline=True, keyed by everything that shaped them: the
+# next pull of the same repository in this process starts with its staging pinned and its Xet
+# session up (the bench times repeated pulls; a long-lived loader pulling several revisions too).
+_PIPELINES: dict = {}
+
+
+def release_pipelines() -> None:
+    """Drop the pipelines kept by reuse_pipeline=True pulls (their pinned staging is freed)."""
+    _PIPELINES.clear()
+
+
 def _parallel_map(fn, items, threads: int):
     if not items:
         return []
@@ -1027,25 +1156,39 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
                verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
                round_bytes: int | None = None, exchange: str = "auto",
-               stats: dict | None = None) -> dict[str, torch.Tensor]:
+               stats: dict | None = None, reuse_pipeline: bool | None = None,
+               possession: bool | None = None) -> dict[str, torch.Tensor]:
     """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
     full set (views into one arena per rank).  `exchange`: "auto" (measured at setup, cached per
     process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
     ZEST_SWARM_ROUND_MB, 1024 MiB): per-rank bytes per pipeline round.  `stats`, if given, is filled
     with this rank's numbers: bytes fetched / received, the exchange mode and its autotune times,
     per-phase seconds (with cross-round pipelining, `fetch_s` is the time spent waiting for a round's
-    fetch to finish, not the fetches' own duration), re-shards and recovered ranks."""
+    fetch to finish, not the fetches' own duration), re-shards and recovered ranks.
+
+    `possession` (default ZEST_SWARM_POSSESSION, on): before sharding, every rank reports which terms
+    its xorb cache already covers and holders own those terms (assign_owners) -- a rank with the
+    whole model cached is the node's seeder.  `reuse_pipeline` (default ZEST_SWARM_REUSE, off): keep
+    the fetch pipelines (pinned staging, Xet session) for the next pull of the same repository in
+    this process; release_pipelines() frees them."""
+    if reuse_pipeline is None:
+        reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
+    if possession is None:
+        possession = os.environ.get("ZEST_SWARM_POSSESSION", "1") != "0"
     if round_bytes is None:
         round_bytes = int(os.environ.get("ZEST_SWARM_ROUND_MB", "1024")) << 20
     if exchange not in ("auto",) + EXCHANGE_MODES:
         raise ValueError(f"exchange={exchange!r}")
     sw = _Swarm(repo, revision, group, device, p2p=p2p, peers=peers, tracker=tracker, dht=dht,
                 dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify_received,
-                staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange)
+                staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange,
+                reuse=reuse_pipeline, possession=possession)
+    ok = False
     try:
         while True:
             try:
                 sw.listing_and_plan()
+                sw.gather_possession()
                 break
             except _RankLost as e:
                 sw.m.rebuild()
@@ -1086,7 +1229,12 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
                 peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
                 GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
-                fetch_stats=_merged_stats([f.stats() for f in sw.fetchers]), pipelined=sw.pipelined, **sw.stats)
+                fetch_stats=_merged_stats([f.stats() for f in sw.fetchers if f.parent is None]),
+                pipelined=sw.pipelined,
+                held_bytes=sw.held_bytes[sw.m.rank], share_bytes=sw.share_bytes[sw.m.rank],
+                possession=list(sw.held_bytes), reused_pipeline=sw.reused,
+                cache_writer=sw.fetcher.cache_writer(), **sw.stats)
+        ok = True
         return out
     finally:
         if getattr(sw, "_recon_warm", None) is not None:
@@ -1101,3 +1249,5 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         for f in getattr(sw, "fetchers", [sw.fetcher]):
             f.join()
         sw.m.close()
+        if ok and sw.reuse:
+            _PIPELINES[sw.reuse_key] = sw.fetchers

@@ -112,6 +112,10 @@ class FakeHub:
         self._xorb_gets = 0
         self._delay_lock = threading.Lock()
         self.tracker_peers: dict[bytes, dict[str, float]] = {}
+        # Base of the xorb URLs handed out in fetch_info (None: this server's presigned /xorbs/ URLs).
+        # "mem://<name>" points the client's CDN fetches at an in-process memory origin
+        # (zest_amd.ops.mem_origin_add; the bench's CDN stand-in for the public swarm_pull path).
+        self.xorb_url: str | None = None
         self._srv: ThreadingHTTPServer | None = None
         self._thr: threading.Thread | None = None
 
@@ -203,10 +207,12 @@ class FakeHub:
             raise ValueError("build the world (build_on_device / build_on_host) first")
         base = len(self.xorbs)
         with self.lock:
+            # serialized sizes: header + STORED payload (a compressed world's chunks are LZ4/BG4 frames)
+            stored = world.chunk_clen if world.chunk_clen is not None else world.chunk_len
             for x in range(world.n_xorbs):
                 a = int(world.xorb_chunk0[x])
                 b = int(world.xorb_chunk0[x + 1]) if x + 1 < world.n_xorbs else world.n_chunks
-                ser = world.chunk_len[a:b].astype(np.int64) + 8
+                ser = stored[a:b].astype(np.int64) + 8
                 hx = world.xorb_hash_hex(x)
                 self.xorbs.append(_Xorb(None, hx, np.cumsum(ser).tolist(), world.chunk_len[a:b].tolist()))
                 self.xorb_index[hx] = base + x
@@ -337,6 +343,8 @@ class FakeHub:
     def _presign(self, hx: str) -> str:
         # Like S3 presigned URLs, the xorb URL carries its own authorization (clients such as hf_xet
         # fetch it without the CAS bearer token).
+        if self.xorb_url:
+            return f"{self.xorb_url}/{hx}"
         sig = hashlib.sha256(f"{self.token}:{hx}".encode()).hexdigest()[:32]
         return f"{self.url}/xorbs/default/{hx}?X-Zest-Signature={sig}"
 
