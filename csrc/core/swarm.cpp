@@ -1,6 +1,7 @@
 #include "swarm.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 #include <iomanip>
@@ -13,6 +14,8 @@ namespace zest {
 SwarmDownloader::SwarmDownloader(const Config& cfg, std::optional<std::string> tracker_url, bool enable_p2p,
                                  bool enable_dht, std::vector<net::Addr> dht_bootstrap)
     : cfg_(cfg), enabled_(enable_p2p), tracker_(std::move(tracker_url)) {
+  if (const char* v = std::getenv("ZEST_PEER_MISS_DECAY_S"))
+    miss_decay_ = std::chrono::milliseconds(int64_t(std::max(0.0, std::atof(v)) * 1000));
   pool_ = std::make_unique<bt::PeerPool>(cfg.peer_id, cfg.listen_port, cfg.max_peers, cfg.connect_timeout_ms,
                                          cfg.peer_connections);
   if (enable_p2p && enable_dht) {
@@ -163,9 +166,14 @@ std::optional<bt::ChunkResult> SwarmDownloader::try_peers(const xet::Hash& hash,
       if (tried.count(key)) continue;
       auto sc = score_.find(key);
       if (sc != score_.end() && sc->second >= 3) continue;  // banned / repeatedly failing
-      const PeerLoad& l = load_[key];
-      // a discovered peer that answered NOT_FOUND far more often than it served holds little of
-      // this repo: skip it (direct peers, named by the user, are always tried)
+      PeerLoad& l = load_[key];
+      const auto now = std::chrono::steady_clock::now();
+      if (now - l.window >= miss_decay_) {  // a new window: old NOT_FOUNDs no longer count
+        l.misses = 0;
+        l.window = now;
+      }
+      // a discovered peer that answered NOT_FOUND far more often than it served (in this window)
+      // holds little of this repo: skip it (direct peers, named by the user, are always tried)
       if (l.misses >= 8 && l.misses > 4 * (l.hits + 1) && std::find(direct_.begin(), direct_.end(), a) == direct_.end())
         continue;
       const std::pair<int, int> k{l.misses > l.hits + 2 ? 1 : 0, l.inflight};

@@ -83,7 +83,12 @@ class SwarmDownloader {
     int inflight = 0;
     uint64_t bytes = 0;
     uint32_t hits = 0, misses = 0;
+    std::chrono::steady_clock::time_point window{};  // start of the current miss-count window
   };
+  // Miss counts are forgotten every `miss_decay_` (ZEST_PEER_MISS_DECAY_S, default 30 s = the
+  // discovery TTL): a peer that missed early -- it was pulling the same model at the same time --
+  // is tried again once it may have the xorbs (the reference re-discovers on a TTL, swarm.zig:324-330).
+  std::chrono::steady_clock::duration miss_decay_ = std::chrono::seconds(30);
   std::map<std::string, PeerLoad> load_;
   void remember(const net::Addr& a);  // caller holds mu_
   std::mutex disc_mu_;

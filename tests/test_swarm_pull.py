@@ -522,3 +522,43 @@ def test_swarm_pull_from_memory_origin_and_pipeline_reuse():
     assert st["from_cdn"] == st["total_bytes"] and not st["reused_pipeline"] and st2["reused_pipeline"]
     n_files = st["files"]
     assert cas_calls >= 2 * n_files  # reconstructions fetched anew by the second pull
+
+
+def _stuck_recovery_worker(rank, world_size, port, repo, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZEST_SWARM_FAULT="exit:2:1",
+                      ZEST_SWARM_CTL_TIMEOUT="20", ZEST_SWARM_HB_STALE="3", ZEST_SWARM_FAULT_RECOVER="hang",
+                      ZEST_SWARM_RECOVER_TIMEOUT="8")
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    from zest_amd.parallel import swarm_pull
+    try:
+        swarm_pull(repo, p2p=False, dht=False, round_bytes=256 << 10)
+        q.put((rank, "ok"))
+    except Exception as e:
+        q.put((rank, type(e).__name__))
+
+
+def test_swarm_pull_stuck_recovery_exits_in_bounded_time(hub_env):
+    """the recovery after a lost rank (RCCL abort, device synchronize, new groups) runs
+    under a deadline.  Here rank 2 dies and the survivors' recovery is stubbed to hang: each exits
+    with status 3 once ZEST_SWARM_RECOVER_TIMEOUT passes, instead of waiting forever."""
+    import time as _t
+    world, hub = hub_env
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_stuck_recovery_worker, args=(r, 3, port, world.spec.repo_id, q)) for r in range(3)]
+    t0 = _t.monotonic()
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=150)
+    dt = _t.monotonic() - t0
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [3, 3, 1], codes
+    assert q.empty()  # nobody returned from the pull
+    assert dt < 120, dt

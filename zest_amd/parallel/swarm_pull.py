@@ -211,6 +211,42 @@ class _Plan:
         return sorted(set(int(x) for x in self.t_file[a:b])) if b > a else []
 
 
+class _Deadline:
+    """Bounded section: if the block has not finished within `seconds`, the process exits with
+    status 3 after a message (and, with faulthandler, every thread's stack).  For the recovery after
+    a lost rank: aborting an RCCL communicator, synchronizing the device and building new groups can
+    each wait forever on a peer that is gone; a survivor stuck there must fail, not hang the job.
+    Exit, never re-exec (a process that initialised the GPU must not replace itself)."""
+
+    def __init__(self, seconds: float, what: str):
+        self.seconds, self.what = float(seconds), what
+        self._done = threading.Event()
+        self._t = None
+
+    def _watch(self):
+        if self._done.wait(self.seconds):
+            return
+        import sys
+        print(f"[zest swarm] {self.what} did not finish within {self.seconds:.0f}s "
+              f"(ZEST_SWARM_RECOVER_TIMEOUT); exiting", file=sys.stderr, flush=True)
+        try:
+            import faulthandler
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        except Exception:  # noqa: BLE001
+            pass
+        os._exit(3)
+
+    def __enter__(self):
+        if self.seconds > 0:
+            self._t = threading.Thread(target=self._watch, daemon=True, name="zest-deadline")
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._done.set()
+        return False
+
+
 # ----------------------------------------------------------------------------------------------
 # Membership: survivors of a lost rank rebuild their groups in-process
 # ----------------------------------------------------------------------------------------------
@@ -914,7 +950,15 @@ class _Swarm:
         self.inflight_next = []
 
     def _recover(self, why: str):
-        """A rank was lost: rebuild the groups over the survivors and re-shard (see _Membership)."""
+        """A rank was lost: rebuild the groups over the survivors and re-shard (see _Membership).
+        Bounded: the whole recovery -- the membership vote, the RCCL abort, the device synchronize and
+        the new groups -- runs under a deadline (ZEST_SWARM_RECOVER_TIMEOUT, default ctl timeout +
+        60 s); a survivor that exceeds it exits with status 3 instead of hanging."""
+        bound = float(os.environ.get("ZEST_SWARM_RECOVER_TIMEOUT", str(self.m.timeout_s + 60)))
+        with _Deadline(bound, f"recovery from a lost rank ({why[:120]})"):
+            self._recover_bounded(why)
+
+    def _recover_bounded(self, why: str):
         t = time.perf_counter()
         old_world, old_granks = self.m.world, list(self.m.granks)
         # whatever the dead peer's exchanges left in flight is abandoned; only finished hashing counts
@@ -929,6 +973,8 @@ class _Swarm:
         if not lost:
             raise SwarmPullError(f"collective failed but every rank is alive: {why}")
         self.stats["recovered_ranks"] += len(lost)
+        if os.environ.get("ZEST_SWARM_FAULT_RECOVER") == "hang":  # fault injection (tests): a stuck abort/sync
+            time.sleep(1e9)
         if self.cuda:
             torch.cuda.synchronize(self.device)
         # queues of the survivors, in their new order; everything of the lost ranks is re-planned
