@@ -373,9 +373,11 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     import numpy as np
     import torch
 
+    import importlib
+
     from zest_amd import ops
-    from zest_amd.parallel import swarm_pull as sp
     from zest_amd.testing import FakeHub
+    sp = importlib.import_module("zest_amd.parallel.swarm_pull")  # the module (the package re-exports the function)
 
     world, puller = keep["world"], keep["puller"]
     cuda = device.type == "cuda"
@@ -435,10 +437,15 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             torch.cuda.synchronize()
         tdist.barrier()
         times.append(time.perf_counter() - t0)
-    el = torch.tensor(times, dtype=torch.float64, device=device if (cuda and not own_pg) else "cpu")
+    dev_t = device if (cuda and not own_pg) else "cpu"
+    el = torch.tensor(times, dtype=torch.float64, device=dev_t)
+    rx = torch.tensor([float(st.get("received_bytes", 0))], dtype=torch.float64, device=dev_t)
     if world_size > 1:
         tdist.all_reduce(el, op=tdist.ReduceOp.MAX)  # every step at its slowest rank
+        tdist.all_reduce(rx)
     wd.arm("report")
+    log(rank, f"[swarm_pull] world {st.get('world')} fetched {st.get('fetched_bytes')} received "
+              f"{st.get('received_bytes')} items {st.get('items')} rounds {st.get('rounds')} exchange {st.get('exchange')}")
     times = el.cpu().tolist()
     step_s = float(sum(times) / len(times))
     sp.release_pipelines()
@@ -451,7 +458,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             "swarm_pull_ms_per_step": round(step_s * 1e3, 3),
             "swarm_pull_step_s": [round(x, 4) for x in times],
             "swarm_pull_mode": keep.get("mode"), "swarm_pull_tensors": n_t,
-            "swarm_pull_p2p_ratio": round(float(st.get("p2p_ratio", 0.0)), 4),
+            "swarm_pull_p2p_ratio": round(float(rx.item()) / (world_size * total), 4) if total else 0.0,
             "swarm_pull_exchange": st.get("exchange"), "swarm_pull_phases": st.get("phases"),
             "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
                                                                                   "bytes_from_peer")},
@@ -553,7 +560,8 @@ def rank_main(a) -> None:
         raise SystemExit(f"refusing an nccl run over {devices} ({rccl_ranks} ranks counted by the collective)")
     spec = models.get(a.model)
     results, pick, arenas = [], None, {}
-    swarm_row = (a.swarm_row == "on" or (a.swarm_row == "auto" and world_size == 1)) and cuda and a.seeders in (0, world_size)
+    # (CPU rehearsals run it only when asked: --swarm-row on)
+    swarm_row = ((a.swarm_row == "auto" and world_size == 1 and cuda) or a.swarm_row == "on") and a.seeders in (0, world_size)
     keep = {} if swarm_row else None
     for i, mode in enumerate(a.modes):
         last = i == len(a.modes) - 1

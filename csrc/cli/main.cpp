@@ -83,7 +83,9 @@ void print_usage(std::ostream& w) {
        "  --no-verify              Skip the Xet file-hash check\n"
        "  --no-serve               Do not auto-start the background seeder\n"
        "  --gpus <n|list>          Decode + verify on n GPUs, or on the listed devices (\"0,2,5\");\n"
-       "                           one worker per GPU, RCCL. Default: $ZEST_GPUS\n"
+       "                           one independent worker per GPU, each pulling its share of the files\n"
+       "                           (no collective; for every tensor on every GPU use\n"
+       "                           zest_amd.pull(repo, device=\"all\") under torchrun). Default: $ZEST_GPUS\n"
        "  --pipeline-depth <MB>    Pinned staging per GPU worker (default: 1024)\n"
        "\n"
        "Seed options:\n"

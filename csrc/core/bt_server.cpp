@@ -2,8 +2,11 @@
 
 #include "trace.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <random>
 
 #include "bt_wire.h"
@@ -24,6 +27,7 @@ FaultSpec FaultSpec::parse(const std::string& s) {
       if (k == "drop") f.drop = std::atof(v.c_str());
       else if (k == "corrupt") f.corrupt = std::atof(v.c_str());
       else if (k == "delay") f.delay_ms = std::atoi(v.c_str());
+      else if (k == "rate") f.rate_mbps = std::max(0.0, std::atof(v.c_str()));
     }
     if (c == std::string::npos) break;
     p = c + 1;
@@ -215,12 +219,39 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
     {
       trace::Span sp("serve", "send");
       sp.arg("\"bytes\":" + std::to_string(hit->size()));
-      s.writev_all(iov, 2);
+      if (fault_.rate_mbps > 0) {
+        // paced in 1 MiB slices, so the connections of a capped server interleave on its "uplink"
+        pace(out.size());
+        s.write_all(out.data(), out.size());
+        const uint8_t* b = hit->bytes();
+        for (size_t o = 0, n = hit->size(); o < n;) {
+          const size_t k = std::min<size_t>(n - o, size_t(1) << 20);
+          pace(k);
+          s.write_all(b + o, k);
+          o += k;
+        }
+      } else {
+        s.writev_all(iov, 2);
+      }
     }
     served_++;
     bytes_ += hit->size();
     if (x.range_end > x.range_start) units_ += x.range_end - x.range_start;
   }
+}
+
+void BtServer::pace(size_t bytes) {
+  using clock = std::chrono::steady_clock;
+  const auto dur = std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(double(bytes) /
+                                                                                             (fault_.rate_mbps * 1e6)));
+  clock::time_point start;
+  {
+    std::lock_guard<std::mutex> g(rate_mu_);
+    const auto now = clock::now();
+    start = std::max(now, rate_free_);
+    rate_free_ = start + dur;
+  }
+  std::this_thread::sleep_until(start);
 }
 
 }  // namespace zest::bt

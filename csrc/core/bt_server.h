@@ -11,6 +11,7 @@
 
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <list>
 #include <memory>
@@ -44,7 +45,11 @@ struct ServerStats {
 struct FaultSpec {
   double drop = 0, corrupt = 0;
   int delay_ms = 0;
-  static FaultSpec parse(const std::string& s);  // "drop:0.1,corrupt:0.05,delay:20"
+  // Uplink cap of the whole server in MB/s (0: none), shared by all its connections: emulates a
+  // peer behind a LAN NIC (rate:1250 ~ 10 Gbps) on loopback, where striping across peers has to
+  // add bandwidth.
+  double rate_mbps = 0;
+  static FaultSpec parse(const std::string& s);  // "drop:0.1,corrupt:0.05,delay:20,rate:1250"
 };
 
 class BtServer {
@@ -82,6 +87,10 @@ class BtServer {
   std::list<Worker> workers_;
   std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0}, rejected_{0};
   FaultSpec fault_;
+  // rate cap: the time the uplink is free again (token bucket of one burst, shared by connections)
+  std::mutex rate_mu_;
+  std::chrono::steady_clock::time_point rate_free_{};
+  void pace(size_t bytes);  // wait for the uplink slot of `bytes` (rate_mbps > 0)
 };
 
 // Slice chunk run [start, end) out of a serialized xorb/partial whose first chunk is `offset`.

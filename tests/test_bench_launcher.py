@@ -79,3 +79,21 @@ def test_bench_launcher_timeout_kills_group():
                  {"ZEST_BENCH_WATCHDOG": "0", "ZEST_BENCH_FAULT": "hang:1:timed", "ZEST_BENCH_TIMEOUT": "25"})
     assert p.returncode == 124, p.stderr[-2000:]
     assert dt < 90
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_swarm_row_times_the_public_path(gpus):
+    """--swarm-row on: after the engine modes, the same world is pulled through the public
+    swarm_pull path from a mem:// memory CAS (every rank's pinned origin), and extra.swarm_pull_*
+    reports it -- here on gloo CPU ranks."""
+    p, _ = _run(["--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--modes", "random", "--swarm-row", "on",
+                 "--swarm-steps", "2", "--swarm-warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    ex = lines[0]["extra"]
+    assert ex["swarm_pull_GBps"] > 0 and len(ex["swarm_pull_step_s"]) == 2
+    assert ex["swarm_pull_mode"] == "random" and ex["swarm_pull_tensors"] > 0
+    assert ex["swarm_pull_fetch"]["bytes_from_cdn"] > 0 and not ex["swarm_pull_fetch"]["bytes_from_peer"]
+    if gpus > 1:
+        assert ex["swarm_pull_p2p_ratio"] > 0.3 and ex["swarm_pull_exchange"] in ("bcast", "allgather", "p2p")

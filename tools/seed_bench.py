@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Seed-mode benchmark (BASELINE.json config 5): a synthetic model's xorbs live in HBM and are
-served over BEP XET to concurrent loopback peers; reports chunks_served/s and GB/s.
+served over BEP XET to concurrent loopback peers; reports chunks_served/s (CHUNK_RESPONSE messages,
+the reference's unit, server.zig:196,208), GB/s, and the Xet chunks carried per second.
 
     python tools/seed_bench.py --model mixtral-8x7b --clients 16 --seconds 20
 
@@ -90,9 +91,13 @@ def main() -> None:
     dt = time.time() - t1
     st1 = srv.stats()
     units = st1["chunk_units"] - st0["chunk_units"]
-    out = {"metric": "seed chunks_served/s from HBM (loopback BEP XET peers)", "model": world.spec.repo_id,
-           "clients": a.clients, "pipeline": a.pipeline, "seconds": round(dt, 2),
-           "chunks_served_per_s": round(units / dt, 1), "GBps": round(totals["bytes"] / dt / 1e9, 3),
+    responses = st1["chunks_served"] - st0["chunks_served"]
+    # The reference's chunks_served counts CHUNK_RESPONSE messages (server.zig:196,208): that is
+    # the headline unit here too.  Xet chunks inside those responses are reported separately.
+    out = {"metric": "seed chunks_served/s (CHUNK_RESPONSEs) from HBM (loopback BEP XET peers)",
+           "model": world.spec.repo_id, "clients": a.clients, "pipeline": a.pipeline, "seconds": round(dt, 2),
+           "chunks_served_per_s": round(responses / dt, 1), "GBps": round(totals["bytes"] / dt / 1e9, 3),
+           "xet_chunks_per_s": round(totals["chunks"] / dt, 1), "chunk_units_64KiB_per_s": round(units / dt, 1),
            "requests_per_s": round(totals["reqs"] / dt, 1), "failed": totals["failed"],
            "server": st1}
     print(json.dumps(out), flush=True)

@@ -34,6 +34,10 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=int, default=2048, help="repo size (MB of random weights, 4 shards)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--trace", default=None, help="directory: each leecher writes a ZEST_TRACE Chrome trace there")
+    ap.add_argument("--rate-mbps", type=float, default=0.0,
+                    help="cap each seeder's uplink (zest serve --fault rate:<MB/s>, shared by its connections): "
+                         "1250 ~ a 10 Gbps LAN peer")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
     shard = a.mb * 1_000_000 // 4
@@ -45,7 +49,8 @@ def main() -> int:
     hub.start()
     work = Path(tempfile.mkdtemp(prefix="zest-stripe-"))
     nodes = []
-    res = {"bytes": total, "repo": "org/stripe", "data": "random bytes, 4 Xet shards, raw chunks"}
+    res = {"bytes": total, "repo": "org/stripe", "data": "random bytes, 4 Xet shards, raw chunks",
+           "seeder_rate_mbps": a.rate_mbps or None}
     try:
         hub.add_repo("org/stripe", files, xet_min_size=1000)
         seeders = [Node(hub, work, "s0")]
@@ -57,7 +62,8 @@ def main() -> int:
             seeders.append(s)
             nodes.append(s)
         for s in seeders:
-            s.spawn("serve", "--listen-port", str(s.listen_port), "--http-port", str(s.http_port))
+            extra = ["--fault", f"rate:{a.rate_mbps}"] if a.rate_mbps > 0 else []
+            s.spawn("serve", "--listen-port", str(s.listen_port), "--http-port", str(s.http_port), *extra)
         for s in seeders:
             s.wait_healthy(timeout=30)
         for label, use in (("1_seeder", seeders[:1]), ("3_seeders", seeders)):
@@ -68,7 +74,8 @@ def main() -> int:
             for s in use:
                 args += ["--peer", f"127.0.0.1:{s.listen_port}"]
             t0 = time.time()
-            r = leech.run(*args, timeout=1800)
+            env = {"ZEST_TRACE": str(Path(a.trace).resolve() / f"leech_{label}.json")} if a.trace else None
+            r = leech.run(*args, timeout=1800, env=env)
             dt = time.time() - t0
             after = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
             served = [b - a_ for a_, b in zip(before, after)]
