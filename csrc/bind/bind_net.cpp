@@ -7,6 +7,8 @@
 #include <cstring>
 #include <memory>
 #include <sstream>
+#include <thread>
+#include <atomic>
 
 #include "swarm.h"
 #include "bridge.h"
@@ -529,6 +531,26 @@ void bind_extra(py::module_& m) {
     if (range_start < 0) c.put(hex, reinterpret_cast<const uint8_t*>(d.data()), d.size());
     else c.put_partial(hex, uint32_t(range_start), reinterpret_cast<const uint8_t*>(d.data()), d.size());
   }, py::arg("hex"), py::arg("data"), py::arg("range_start") = -1);
+  m.def("cache_put_runs", [](std::vector<std::string> hexes, std::vector<uint32_t> offsets, std::vector<uintptr_t> ptrs,
+                             std::vector<uint64_t> lens, int threads) {
+    // Bulk cache fill straight from memory (e.g. a pinned origin): run i = chunks from offset[i] on.
+    if (offsets.size() != hexes.size() || ptrs.size() != hexes.size() || lens.size() != hexes.size())
+      throw std::invalid_argument("cache_put_runs: lists of different lengths");
+    Config cfg = Config::from_env();
+    storage::XorbRegistry reg;
+    storage::XorbCache c(cfg, &reg);
+    py::gil_scoped_release nogil;
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < hexes.size();)
+        c.put_run(hexes[i], offsets[i], reinterpret_cast<const uint8_t*>(ptrs[i]), lens[i], true);
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < std::max(1, threads); ++t) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+    return hexes.size();
+  }, py::arg("hexes"), py::arg("offsets"), py::arg("ptrs"), py::arg("lens"), py::arg("threads") = 8);
 
   // ---------------- BT seeder / peer client ----------------
   py::class_<PySeeder>(m, "Seeder", "BT listener serving the local xorb cache over ut_xet")

@@ -123,6 +123,13 @@ PYBIND11_MODULE(_hip, m) {
                          P<unsigned long long>(err), S(st)),
           "zg_index_terms");
   });
+  m.def("index_scratch_bytes", &zg_index_scratch_bytes);
+  m.def("index_terms_scan", [](uintptr_t src, uint64_t src_n, uintptr_t terms, int n, uintptr_t chunks, uintptr_t err,
+                               uintptr_t scratch, size_t scratch_bytes, uintptr_t st) {
+    check(zg_index_terms_scan(P<const uint8_t>(src), src_n, P<const ZgTerm>(terms), n, P<ZgChunk>(chunks),
+                              P<unsigned long long>(err), P<uint8_t>(scratch), scratch_bytes, S(st)),
+          "zg_index_terms_scan");
+  });
   m.def("place_chunks", [](uintptr_t src, uint64_t src_n, uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n,
                            uint64_t lo, uint64_t hi, uintptr_t err, uintptr_t st, uintptr_t clip_scratch) {
     check(zg_place_chunks(P<const uint8_t>(src), src_n, P<uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, lo, hi,

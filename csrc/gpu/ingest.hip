@@ -110,6 +110,174 @@ __global__ void k_index_terms(const uint8_t* __restrict__ src, const ZgTerm* __r
   walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
 }
 
+// K4a': parallel header walk ("scan, sort, link").  The walk above is one dependent HBM load per
+// chunk: ~1000 chained loads per 64 MiB xorb run, ~0.6 ms whatever the GPU's width.  Here:
+//   scan   every byte position of the span is tested in parallel for a plausible chunk header
+//          (version 0, scheme <= 2, 1 <= ulen <= 128 KiB, clen >= 1, raw => clen == ulen, payload
+//          inside its run); candidates (~one per chunk: a false positive needs ~30 bits of luck)
+//          are appended to their term's list.
+//   link   one workgroup per term sorts its candidates in LDS (bitonic) and checks that they form
+//          exactly the chain from offset 0 to the run's end with n_chunks links; then a block
+//          prefix sum of the uncompressed sizes gives every chunk's output offset and the records
+//          are written in parallel.
+// Anything else -- a false candidate, a list over capacity, a broken or short chain -- falls back
+// to the serial walk for that term, so records and error codes are exactly walk_term's.
+constexpr int kScanThreads = 256;
+constexpr uint32_t kScanBytesPerThread = 16;
+constexpr uint32_t kCandCap = 8192;  // chunks of a 64 MiB xorb at the 8 KiB CDC minimum
+constexpr int kLinkThreads = 1024;
+
+__device__ __forceinline__ bool plausible_header(uint32_t lo, uint32_t hi, uint64_t rel, uint64_t run_len) {
+  const uint32_t clen = lo >> 8, scheme = hi & 0xFF, ulen = hi >> 8;
+  return (lo & 0xFF) == 0 && scheme <= 2 && ulen >= 1 && ulen <= kMaxChunk && clen >= 1 &&
+         (scheme != 0 || clen == ulen) && rel + 8 + clen <= run_len;
+}
+
+// terms must be sorted by src (else the fast path finds no chain and the serial walk runs)
+__global__ void __launch_bounds__(kScanThreads) k_hdr_scan(const uint8_t* __restrict__ src, uint64_t src_n,
+                                                          const ZgTerm* __restrict__ terms, int n_terms,
+                                                          uint32_t* __restrict__ counts, uint32_t* __restrict__ cands) {
+  const uint64_t q = (uint64_t(blockIdx.x) * kScanThreads + threadIdx.x) * kScanBytesPerThread;
+  if (q >= src_n) return;
+  // the last term starting at or before q (binary search; terms are few)
+  int lo_t = 0, hi_t = n_terms - 1, t = -1;
+  while (lo_t <= hi_t) {
+    const int mid = (lo_t + hi_t) >> 1;
+    if (terms[mid].src <= q) {
+      t = mid;
+      lo_t = mid + 1;
+    } else {
+      hi_t = mid - 1;
+    }
+  }
+  if (t < 0) {
+    t = 0;  // q lies before the first term: positions below terms[0].src are skipped
+  }
+  uint64_t t0 = terms[t].src, t1 = t0 + terms[t].src_len;
+  uint64_t nx = t + 1 < n_terms ? terms[t + 1].src : ~uint64_t(0);
+  const uint4 v0 = *reinterpret_cast<const uint4*>(src + q);
+  const uint4 v1 = *reinterpret_cast<const uint4*>(src + q + 16);  // padded buffers: safe past the end
+  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+  for (uint32_t k = 0; k < kScanBytesPerThread; ++k) {
+    const uint64_t p = q + k;
+    while (p >= nx) {  // crossed into the next term (wave-divergent, rare)
+      ++t;
+      t0 = terms[t].src;
+      t1 = t0 + terms[t].src_len;
+      nx = t + 1 < n_terms ? terms[t + 1].src : ~uint64_t(0);
+    }
+    if (p < t0 || p + 8 > t1) continue;
+    const uint32_t j = k >> 2, sh = k & 3;
+    const uint32_t lo = sh ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) : w[j];
+    const uint32_t hi = sh ? __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], sh) : w[j + 1];
+    if (plausible_header(lo, hi, p - t0, t1 - t0)) {
+      const uint32_t i = atomicAdd(&counts[t], 1u);
+      if (i < kCandCap) cands[uint64_t(t) * kCandCap + i] = uint32_t(p - t0);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kLinkThreads) k_hdr_link(const uint8_t* __restrict__ src,
+                                                          const ZgTerm* __restrict__ terms,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ cands,
+                                                          ZgChunk* __restrict__ chunks, unsigned long long* err) {
+  __shared__ uint32_t key[kCandCap];   // candidate offsets, sorted
+  __shared__ uint32_t ul[kCandCap];    // uncompressed sizes -> exclusive prefix sums
+  __shared__ uint32_t cs[kCandCap];    // clen | scheme << 24
+  __shared__ uint32_t part[kLinkThreads / kWave];
+  __shared__ int ok;
+  const int t = blockIdx.x;
+  const ZgTerm tm = terms[t];
+  const uint32_t n = counts[t];
+  const int tid = threadIdx.x;
+  // the fast path needs exactly one candidate per planned chunk (terms of at most 4 GiB)
+  if (n != tm.n_chunks || n == 0 || n > kCandCap || tm.src_len >= (uint64_t(1) << 32)) {
+    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+    return;
+  }
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = tid; i < P; i += kLinkThreads) key[i] = i < n ? cands[uint64_t(t) * kCandCap + i] : 0xFFFFFFFFu;
+  if (tid == 0) ok = 1;
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {  // bitonic sort, ascending
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = tid; i < P; i += kLinkThreads) {
+        const uint32_t l = i ^ jj;
+        if (l > i) {
+          const uint32_t a = key[i], b = key[l];
+          if (((i & k) == 0) == (a > b)) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // link check: candidate i's payload ends exactly where candidate i + 1 starts, the first sits at
+  // offset 0 and the last ends the run
+  const uint8_t* run = src + tm.src;
+  for (uint32_t i = tid; i < n; i += kLinkThreads) {
+    uint32_t lo, hi;
+    load8(run + key[i], lo, hi);
+    const uint32_t clen = lo >> 8, ulen = hi >> 8;
+    const uint64_t end = uint64_t(key[i]) + 8 + clen;
+    const uint64_t want = i + 1 < n ? uint64_t(key[i + 1]) : tm.src_len;
+    if (end != want || (i == 0 && key[0] != 0)) ok = 0;
+    ul[i] = ulen;
+    cs[i] = clen | (hi & 0xFF) << 24;
+  }
+  __syncthreads();
+  if (!ok) {  // a false candidate or a broken chain: the serial walk decides
+    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+    return;
+  }
+  // exclusive prefix sum of ul[0, n): each thread owns a contiguous slice
+  const uint32_t per = (n + kLinkThreads - 1) / kLinkThreads;
+  const uint32_t a = min(n, tid * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += ul[i];
+  // block scan of the per-thread sums: wave inclusive scan, then the wave totals
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, kWave);
+    if (int(lane_id()) >= d) inc += y;
+  }
+  const int wv = tid / kWave;
+  if (lane_id() == kWave - 1) part[wv] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run_sum = 0;
+    for (int k = 0; k < kLinkThreads / kWave; ++k) {
+      const uint32_t x = part[k];
+      part[k] = run_sum;
+      run_sum += x;
+    }
+    if (tm.ulen != 0 && run_sum != tm.ulen) ok = 0;
+  }
+  __syncthreads();
+  if (!ok) {
+    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+    return;
+  }
+  uint32_t off = part[wv] + inc - sum;  // exclusive prefix of this thread's slice
+  for (uint32_t i = a; i < b; ++i) {
+    ZgChunk ch;
+    ch.src = tm.src + key[i] + 8;
+    ch.dst = tm.dst + off;
+    ch.clen = cs[i] & 0xFFFFFF;
+    ch.ulen = ul[i];
+    ch.scheme = cs[i] >> 24;
+    ch.term = uint32_t(t);
+    chunks[tm.chunk_base + i] = ch;
+    off += ul[i];
+  }
+}
+
 using zwv::wave_copy;  // wave64.h
 
 // K3a: place uncompressed chunks (scheme 0): one wave per chunk, clipped to [clip_lo, clip_hi).
@@ -624,6 +792,30 @@ hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, 
                           unsigned long long* err, hipStream_t stream) {
   if (n_terms <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_index_terms, dim3((n_terms + 63) / 64), dim3(64), 0, stream, src, terms, n_terms, chunks, err);
+  return hipGetLastError();
+}
+
+size_t zg_index_scratch_bytes(int n_terms) {
+  return (size_t(n_terms) * 4 + 255) / 256 * 256 + size_t(n_terms) * kCandCap * 4;
+}
+
+hipError_t zg_index_terms_scan(const uint8_t* src, uint64_t src_n, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
+                               unsigned long long* err, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (n_terms <= 0) return hipSuccess;
+  if (scratch == nullptr || scratch_bytes < zg_index_scratch_bytes(n_terms) || (reinterpret_cast<uintptr_t>(src) & 15))
+    return zg_index_terms(src, terms, n_terms, chunks, err, stream);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* cands = reinterpret_cast<uint32_t*>(scratch + (size_t(n_terms) * 4 + 255) / 256 * 256);
+  hipError_t e = hipMemsetAsync(counts, 0, size_t(n_terms) * 4, stream);
+  if (e != hipSuccess) return e;
+  const uint64_t per_block = uint64_t(kScanThreads) * kScanBytesPerThread;
+  const uint64_t blocks = (src_n + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_hdr_scan, dim3(uint32_t(blocks ? blocks : 1)), dim3(kScanThreads), 0, stream, src, src_n, terms,
+                     n_terms, counts, cands);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hdr_link, dim3(n_terms), dim3(kLinkThreads), 0, stream, src, terms, counts, cands, chunks, err);
   return hipGetLastError();
 }
 

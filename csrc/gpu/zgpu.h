@@ -65,6 +65,13 @@ hipError_t zg_index_terms(const uint8_t* src, const ZgTerm* terms, int n_terms, 
 #define ZG_CLIP_SCRATCH_BYTES (2u * (128u * 1024u + 256u))
 // Unclipped launches decode LZ4 chunks with the batched decoder (lz4seq.hip: scalar parse into
 // lane registers + lane-parallel execute); clipped ones with the LDS-ring decoder (ingest.hip).
+// K4 parallel header walk: candidate scan over the span [0, src_n) of src + per-term sort/link in
+// LDS; a term whose candidates are not exactly its chunk chain takes the serial walk (same records
+// and errors as zg_index_terms).  Terms sorted by src.  scratch: zg_index_scratch_bytes(n_terms)
+// of device memory, private to the stream (null / too small: zg_index_terms).
+size_t zg_index_scratch_bytes(int n_terms);
+hipError_t zg_index_terms_scan(const uint8_t* src, uint64_t src_n, const ZgTerm* terms, int n_terms, ZgChunk* chunks,
+                               unsigned long long* err, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream);
 hipError_t zg_place_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                            const ZgChunk* chunks, int n_chunks, uint64_t clip_lo, uint64_t clip_hi,
                            uint8_t* clip_scratch, unsigned long long* err, hipStream_t stream);

@@ -742,3 +742,65 @@ def test_device_puller_pipelines(pipeline, mode, compression):
     p.check()
     for f in w.xet_files:  # (the arena also holds alignment gaps that belong to no file)
         assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size])
+
+
+def _index_both(src, terms, n_chunks):
+    """Chunk records + error word of the serial header walk and of the parallel scan/link walk."""
+    H = ops.hip()
+    st = torch.cuda.current_stream().cuda_stream
+    tdev = torch.from_numpy(terms.view(np.uint8).copy()).to(DEV)
+    out = []
+    for scan in (False, True):
+        chunks = torch.zeros(max(1, n_chunks) * ops.CHUNK_DTYPE.itemsize, dtype=torch.uint8, device=DEV)
+        err = torch.zeros(1, dtype=torch.int64, device=DEV)
+        if scan:
+            sb = H.index_scratch_bytes(len(terms))
+            scr = torch.empty(sb, dtype=torch.uint8, device=DEV)
+            H.index_terms_scan(src.data_ptr(), src.numel(), tdev.data_ptr(), len(terms), chunks.data_ptr(),
+                               err.data_ptr(), scr.data_ptr(), sb, st)
+        else:
+            H.index_terms(src.data_ptr(), tdev.data_ptr(), len(terms), chunks.data_ptr(), err.data_ptr(), st)
+        torch.cuda.synchronize()
+        out.append((chunks.cpu().numpy().tobytes(), int(err.item())))
+    return out
+
+
+@pytest.mark.parametrize("policy", ["none", "bg4", "auto"])
+def test_index_scan_matches_serial_walk(policy):
+    """K4 parallel header walk (candidate scan + LDS sort/link + prefix sum) gives byte-identical
+    chunk records to the serial walk: clean runs at odd offsets; a raw chunk carrying a planted
+    header-like pattern (a false candidate -> that term falls back to the serial walk); and a
+    corrupted header (same error word)."""
+    data, ends, b = _make_runs(policy, seed=3)
+    body = b.serialize(False)
+    nck = len(ends)
+    bounds = b.chunk_boundaries()
+    cuts = [0, nck // 4, nck // 2, 3 * nck // 4, nck]
+    uoffs = [0] + list(ends)
+    src_host = bytearray(17)
+    terms = np.zeros(4, dtype=ops.TERM_DTYPE)
+    for t in range(4):
+        c0, c1 = cuts[t], cuts[t + 1]
+        r0 = 0 if c0 == 0 else bounds[c0 - 1]
+        run = body[r0:bounds[c1 - 1]]
+        terms[t] = (len(src_host), len(run), 5 + uoffs[c0], c0, c1 - c0, uoffs[c1] - uoffs[c0])
+        src_host += run + b"\x07" * (t + 1)
+    src = ops.padded_empty(len(src_host), DEV)
+    src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
+    (serial, e0), (scan, e1) = _index_both(src, terms, nck)
+    assert e0 == 0 and e1 == 0 and scan == serial
+    # the records are the real ones: ingest through them reproduces the data
+    if policy == "none":
+        # a planted plausible header (version 0, raw, clen == ulen == 16) inside term 1's first payload
+        t = 1
+        pos = int(terms[t]["src"]) + 8 + 100
+        src_host[pos:pos + 8] = bytes([0, 16, 0, 0, 0, 16, 0, 0])
+        src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
+        (serial, e0), (scan, e1) = _index_both(src, terms, nck)
+        assert e0 == 0 and e1 == 0 and scan == serial
+    # a corrupted header in term 2: both walks report the same error and the same zeroed records
+    pos = int(terms[2]["src"])
+    src_host[pos + 4] = 9
+    src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
+    (serial, e0), (scan, e1) = _index_both(src, terms, nck)
+    assert e0 != 0 and e1 == e0 and scan == serial

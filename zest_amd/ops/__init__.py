@@ -235,6 +235,13 @@ class IngestWorkspace:
         self._clip_scratch = None
         self.hash_scratch = HashScratch(self.device) if self.device.type == "cuda" else None
 
+    def index_scratch(self, H, n_terms: int) -> tuple[int, int]:
+        """(ptr, bytes) of this workspace's parallel header-walk scratch, grown to n_terms."""
+        need = H.index_scratch_bytes(max(1, n_terms))
+        if getattr(self, "_index_scratch", None) is None or self._index_scratch.numel() < need:
+            self._index_scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._index_scratch.data_ptr(), self._index_scratch.numel()
+
     def clip_scratch(self) -> int:
         """Device scratch for clipped decodes, private to this workspace (so to its stream)."""
         if self._clip_scratch is None:
@@ -245,11 +252,20 @@ class IngestWorkspace:
 FUSED_INGEST = os.environ.get("ZEST_FUSED_INGEST", "1") != "0"
 
 
+INDEX_SCAN = os.environ.get("ZEST_INDEX_SCAN", "1") != "0"
+
+
 def index_terms(H, src_ptr: int, src_n: int, terms_ptr: int, n_terms: int, chunks_ptr: int, err_ptr: int, stream: int,
                 ws: "IngestWorkspace | None" = None) -> None:
-    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4).  One thread per
-    term chases its headers (~0.6 ms per 1 GiB round, profiles/r4/kbench_k3pair_r4b.jsonl); a
-    candidate-scan + LDS-table walk tried in round 4 measured 10-20x slower and was removed."""
+    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4).  With a
+    workspace (its private scratch) the parallel walk runs: candidate-header scan of the span, then a
+    per-term LDS sort/link + prefix sum (csrc/gpu/ingest.hip k_hdr_scan / k_hdr_link); a term whose
+    candidates do not form exactly its chain takes the serial walk (one thread per term chasing its
+    headers, ~0.6 ms per 64 MiB run whatever the GPU's width).  ZEST_INDEX_SCAN=0: serial only."""
+    if ws is not None and INDEX_SCAN and ws.device.type == "cuda":
+        sp, sb = ws.index_scratch(H, n_terms)
+        H.index_terms_scan(src_ptr, src_n, terms_ptr, n_terms, chunks_ptr, err_ptr, sp, sb, stream)
+        return
     H.index_terms(src_ptr, terms_ptr, n_terms, chunks_ptr, err_ptr, stream)
 
 
