@@ -425,6 +425,8 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         one({})
     warm_s = time.time() - t_w
     wd.arm("timed")
+    from zest_amd import _core
+    _core.trace.roctx_push("swarm_pull timed")  # (ZEST_ROCTX=1: the window of tools/gpu/overlap.py --marker)
     times, st = [], {}
     for _ in range(a.swarm_steps):
         st = {}
@@ -437,6 +439,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             torch.cuda.synchronize()
         tdist.barrier()
         times.append(time.perf_counter() - t0)
+    _core.trace.roctx_pop()
     dev_t = device if (cuda and not own_pg) else "cpu"
     el = torch.tensor(times, dtype=torch.float64, device=dev_t)
     rx = torch.tensor([float(st.get("received_bytes", 0))], dtype=torch.float64, device=dev_t)

@@ -245,6 +245,92 @@ def test_pull_files_multi_file_pipeline(tmp_path, monkeypatch):
         hub.stop()
 
 
+def test_device_pull_sibling_pipelines_and_write_behind_cache(tmp_path, monkeypatch):
+    """DeviceXetPull with 3 staging slots (copy stream || kernels, event-ordered slot reuse) and a
+    sibling pipeline (own streams + staging, the same Xet session / reconstructions): both pull
+    byte-exact.  CDN runs reach the xorb cache through the write-behind queue (not the fetch
+    threads): after flush_cache_writes() a new pipeline pulls everything from the cache with the CDN
+    refusing every xorb."""
+    import json as _json
+
+    from zest_amd import _core, ops as zops
+
+    files = {f"model-{i:05d}.safetensors": bytes(np.random.default_rng(40 + i).integers(0, 256, 250_000 + 4099 * i,
+                                                                                        dtype=np.uint8))
+             for i in range(4)}
+    hub = FakeHub(policy="auto", max_xorb_bytes=128 << 10)
+    hub.start()
+    try:
+        hub.add_repo("org/sib", files, xet_min_size=1)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        commit, listing = _core.list_repo_files("org/sib", "main", "model")
+        listing = sorted((f for f in listing if f["xet_hash"]), key=lambda f: f["path"])
+        dp = zops.hip().DeviceXetPull("org/sib", "main", "model", False, [], None, False, [], 0, 96 << 10, 4, 3)
+        sib = dp.sibling(64 << 10, 2)
+        bufs = [zops.padded_empty(f["size"], "cuda:0")[:f["size"]] for f in listing]
+        torch.cuda.synchronize()
+        dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing[:2], bufs[:2])])
+        sib.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing[2:], bufs[2:])])
+        for f, b in zip(listing, bufs):
+            assert b.cpu().numpy().tobytes() == files[f["path"]]
+        dp.flush_cache_writes()
+        w = _json.loads(dp.cache_writer_json())
+        assert w["written_bytes"] > 0 and w["dropped_bytes"] == 0
+        assert len(_core.list_cached_xorbs()) == len(hub.xorbs)
+        st = _json.loads(dp.stats_json())
+        assert st["bytes_from_cdn"] > 0  # one session: the sibling's fetches are counted with dp's
+        del sib, dp
+        hub.fail_xorbs = {x.hash_hex for x in hub.xorbs}
+        dp2 = zops.hip().DeviceXetPull("org/sib", "main", "model", False, [], None, False, [], 0, 96 << 10, 4)
+        for b in bufs:
+            b.zero_()
+        dp2.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing, bufs)])
+        for f, b in zip(listing, bufs):
+            assert b.cpu().numpy().tobytes() == files[f["path"]]
+        assert _json.loads(dp2.stats_json())["bytes_from_cdn"] == 0
+    finally:
+        hub.stop()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_device_pull_on_second_gpu_from_another_thread(tmp_path, monkeypatch):
+    """HIP's current device is per thread.  A pipeline built for the last GPU and called
+    from a thread whose current device is 0 still allocates and runs on its own GPU."""
+    import threading
+
+    from zest_amd import _core, ops as zops
+
+    data = bytes(np.random.default_rng(9).integers(0, 256, 400_000, dtype=np.uint8))
+    hub = FakeHub(policy="auto", max_xorb_bytes=128 << 10)
+    hub.start()
+    try:
+        hub.add_repo("org/dev1", {"m.safetensors": data}, xet_min_size=1)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        last = torch.cuda.device_count() - 1
+        _, listing = _core.list_repo_files("org/dev1", "main", "model")
+        f = [x for x in listing if x["xet_hash"]][0]
+        dp = zops.hip().DeviceXetPull("org/dev1", "main", "model", False, [], None, False, [], last, 96 << 10, 4)
+        buf = zops.padded_empty(f["size"], f"cuda:{last}")[:f["size"]]
+        torch.cuda.synchronize(last)
+        err = []
+
+        def run():
+            torch.cuda.set_device(0)
+            try:
+                dp.pull_files([(f["xet_hash"], buf.data_ptr(), f["size"])])
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        t = threading.Thread(target=run)
+        t.start()
+        t.join()
+        assert not err, err
+        assert buf.cpu().numpy().tobytes() == data
+    finally:
+        hub.stop()
+
+
 def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="auto", fault="", round_bytes=None,
                            swarm_fault=""):
     import torch.distributed as dist

@@ -104,6 +104,28 @@ for step in "$@"; do
           f=$(find $OUT/pmc -name "*counter_collection.csv" | head -1)
           python tools/gpu/pmc_summary.py "$f" "${PMC_KERNEL:-lz4}" > $OUT/pmc_summary.txt 2>&1; cat $OUT/pmc_summary.txt
           rm -rf $OUT/pmc ;;
+    copytrace) # public-path swarm row under kernel + memory-copy + marker traces: does H2D overlap ingest?
+               ZEST_ROCTX=1 timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace \
+                 --output-format csv -d $OUT/ct -o ct -- python3 bench.py --model ${CT_MODEL:-llama-3.1-8b} \
+                 --modes ${CT_MODES:-random} --steps 2 --warmup 1 --swarm-steps 2 --swarm-warmup 1 > $log 2>&1 \
+                 || fail $step $? $log
+               grep -h "aggregate" $log
+               python tools/gpu/overlap.py $OUT/ct --marker "swarm_pull timed" > $OUT/overlap_swarm.txt 2>&1
+               python tools/gpu/overlap.py $OUT/ct > $OUT/overlap_all.txt 2>&1
+               cat $OUT/overlap_swarm.txt $OUT/overlap_all.txt; rm -rf $OUT/ct ;;
+    pmctable) # one counter group per rocprofv3 pass (SQ <= 8, TCC <= 4: FETCH_SIZE uses 3, WRITE_SIZE 2)
+              i=0
+              for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" \
+                         "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_INSTS_VMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+                         "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE TCC_HIT TCC_MISS"; do
+                i=$((i+1))
+                timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/pmc_$i -o p --output-format csv -- \
+                  python3 -m zest_amd.gpubench --json --mib ${PMC_MIB:-256} --runs 2 > $log.$i 2>&1 || fail $step $? $log.$i
+                timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/pmc_$i -o g --output-format csv -- \
+                  python3 tools/kbench.py --only gather --iters 2 >> $log.$i 2>&1 || fail $step $? $log.$i
+              done
+              python tools/gpu/pmc_table.py $OUT/pmc_1 $OUT/pmc_2 $OUT/pmc_3 $OUT/pmc_4 > $OUT/pmc_table.md 2>&1
+              cat $OUT/pmc_table.md; rm -rf $OUT/pmc_? ;;
     swarmtrace) ZEST_TRACE=$PWD/$OUT/swarm_trace.%p.json timeout -k 10 400 python -u tools/swarm_bench.py \
                   --model ${SWARM_MODEL:-llama-3.1-8b} --ranks 1 --out $OUT/swarm_trace_run.json > $log 2>&1 \
                   || fail $step $? $log

@@ -81,9 +81,19 @@ def main() -> int:
             served = [b - a_ for a_, b in zip(before, after)]
             res[label] = {"seconds": round(dt, 3), "GBps": round(total / dt / 1e9, 3), "p2p_ratio": p2p_ratio(r.stdout),
                           "served_share": [round(x / max(1, sum(served)), 3) for x in served]}
+            if a.trace:  # the peer-transfer phase alone (first request start .. last response end)
+                ev = json.load(open(Path(a.trace) / f"leech_{label}.json"))
+                ev = ev["traceEvents"] if isinstance(ev, dict) else ev
+                req = [e for e in ev if e.get("ph") == "X" and e.get("cat") == "peer" and e.get("name") == "request"]
+                if req:
+                    span = (max(e["ts"] + e["dur"] for e in req) - min(e["ts"] for e in req)) / 1e6
+                    res[label]["transfer_s"] = round(span, 3)
+                    res[label]["transfer_GBps"] = round(total / span / 1e9, 3)
             print(f"[{label}] {total / dt / 1e9:.2f} GB/s ({dt:.1f}s), P2P {p2p_ratio(r.stdout):.0f}%, "
                   f"seeder shares {res[label]['served_share']}", flush=True)
         res["speedup_3_vs_1"] = round(res["1_seeder"]["seconds"] / res["3_seeders"]["seconds"], 3)
+        if "transfer_s" in res["3_seeders"]:
+            res["transfer_speedup_3_vs_1"] = round(res["1_seeder"]["transfer_s"] / res["3_seeders"]["transfer_s"], 3)
         print(json.dumps(res), flush=True)
         if a.out:
             Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
