@@ -12,7 +12,12 @@
 #include <string>
 #include <vector>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "../gpu/zgpu.h"
+#include "../gpurt/pinned.h"
 
 namespace py = pybind11;
 
@@ -21,6 +26,16 @@ void bind_hip_pull(py::module_& m);  // hip_pull.cpp
 void bind_hip_vmm(py::module_& m);   // hip_vmm.cpp
 
 namespace {
+
+// host_malloc'd buffers: address -> (mapped length, registered mapping?) for host_free
+std::map<uintptr_t, std::pair<size_t, bool>>& host_allocs() {
+  static std::map<uintptr_t, std::pair<size_t, bool>> m;
+  return m;
+}
+std::mutex& host_allocs_mu() {
+  static std::mutex mu;
+  return mu;
+}
 
 template <typename T>
 T* P(uintptr_t p) {
@@ -47,17 +62,35 @@ PYBIND11_MODULE(_hip, m) {
   m.def("device_count", &zg_device_count);
   // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host
   // allocator) and raw async copies on a caller-provided stream.
+  // Pinned host memory for origins / staging: anonymous THP mapping faulted in by several threads,
+  // then hipHostRegister (gpurt/pinned.h; 72 vs 191 ms per GiB against hipHostMalloc on the box, and
+  // the same H2D rate), falling back to hipHostMalloc.
   m.def("host_malloc", [](size_t n) {
-    void* p = nullptr;
+    zest::gpurt::PinnedBuf b;
+    bool ok;
     {
       py::gil_scoped_release nogil;
-      check(hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault), "hipHostMalloc");
+      ok = b.alloc(n ? n : 1);
     }
+    if (!ok) throw std::runtime_error("host_malloc: pinning " + std::to_string(n) + " bytes failed");
+    const size_t len = b.size();
+    const bool mapped = b.mapped();
+    uint8_t* p = b.release();
+    std::lock_guard<std::mutex> g(host_allocs_mu());
+    host_allocs()[reinterpret_cast<uintptr_t>(p)] = {len, mapped};
     return reinterpret_cast<uintptr_t>(p);
   });
   m.def("host_free", [](uintptr_t p) {
+    std::pair<size_t, bool> a{0, false};
+    {
+      std::lock_guard<std::mutex> g(host_allocs_mu());
+      auto it = host_allocs().find(p);
+      if (it == host_allocs().end()) throw std::invalid_argument("host_free: not from host_malloc");
+      a = it->second;
+      host_allocs().erase(it);
+    }
     py::gil_scoped_release nogil;
-    check(hipHostFree(reinterpret_cast<void*>(p)), "hipHostFree");
+    zest::gpurt::PinnedBuf::free_raw(reinterpret_cast<uint8_t*>(p), a.first, a.second);
   });
   // Let the current device's copy engines read `peer`'s memory directly over xGMI (IPC exchange).
   m.def("enable_peer_access", [](int peer) {

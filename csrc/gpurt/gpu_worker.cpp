@@ -87,6 +87,7 @@ class WriteBack {
     uint64_t size = 0, queued = 0;
     int fd = -1;
     bool repaired = false;  // a repair pass overwrote its bytes: written again after the pull
+    size_t pending = 0;     // pieces queued or being written
     std::string err;
   };
 
@@ -126,6 +127,19 @@ class WriteBack {
     std::unique_lock<std::mutex> g(mu_);
     idle_.wait(g, [&] { return pending_ == 0; });
   }
+  // Wait until every piece queued for files `ks` is on its way to the disk (pwritten).
+  void wait_files(const std::vector<size_t>& ks) {
+    std::unique_lock<std::mutex> g(mu_);
+    idle_.wait(g, [&] {
+      for (size_t k : ks)
+        if ((*files_)[k].pending) return false;
+      return true;
+    });
+  }
+  bool repaired(size_t k) {
+    std::lock_guard<std::mutex> g(mu_);
+    return (*files_)[k].repaired;
+  }
   void stop() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -150,6 +164,7 @@ class WriteBack {
     for (uint64_t o = lo; o < hi; o += piece_) {
       q_.push_back({f, o, std::min<uint64_t>(piece_, hi - o)});
       ++pending_;
+      ++(*files_)[f].pending;
     }
     work_.notify_all();
   }
@@ -181,7 +196,9 @@ class WriteBack {
       if (e.empty()) storage::start_writeback(fl.fd, p.off, p.len);  // the disk works behind the pull
       std::lock_guard<std::mutex> g(mu_);
       if (!e.empty() && fl.err.empty()) fl.err = e;
-      if (--pending_ == 0) idle_.notify_all();
+      --fl.pending;
+      --pending_;
+      idle_.notify_all();
     }
   }
 
@@ -305,19 +322,14 @@ int run(int argc, char** argv) {
       o.staging_bytes = a.staging_mb << 20;
       o.threads = a.threads;
       o.defer_device = true;
+      // One pipeline owns the host state (Xet session, caches, write-behind queue, reconstructions);
+      // the others are its siblings: their own streams and pinned staging (2 slots each), no second
+      // auth / cache scan (DeviceXetPull::sibling).
       std::vector<std::string> errs(dps.size());
       std::vector<std::thread> mk;
-      for (size_t k = 0; k < dps.size(); ++k)
-        mk.emplace_back([&, k] {
-          try {
-            dps[k] = std::make_unique<gpurt::DeviceXetPull>(o);
-          } catch (const std::exception& e) {
-            errs[k] = e.what();
-          }
-        });
-      for (auto& t : mk) t.join();
-      for (auto& e : errs)
-        if (!e.empty()) throw Error("DeviceInit", e);
+      o.slots = env_int("ZEST_GPU_SLOTS", 2);
+      dps[0] = std::make_unique<gpurt::DeviceXetPull>(o);
+      for (size_t k = 1; k < dps.size(); ++k) dps[k] = dps[0]->sibling(o.staging_bytes, o.slots);
       hip_up.join();
       if (!hip_err.empty()) throw Error("DeviceInit", hip_err);
       mk.clear();
@@ -461,6 +473,15 @@ int run(int argc, char** argv) {
           } catch (const std::exception& e) {
             pipe_err[p] = e.what();
           }
+          if (!pipe_err[p].empty()) return;
+          // This pipeline's files are verified: write what a repair pass replaced, then make them
+          // durable now, while the other pipelines are still pulling (not all in the group's tail).
+          for (size_t k : share[p])
+            if (wb->repaired(k)) wb->post(k, 0, out[k].size);
+          wb->wait_files(share[p]);
+          for (size_t k : share[p])
+            if (out[k].err.empty() && ::fdatasync(out[k].fd) != 0)
+              out[k].err = std::string("fdatasync: ") + std::strerror(errno);
         });
       }
       for (auto& t : pipes) t.join();
@@ -469,21 +490,9 @@ int run(int argc, char** argv) {
         for (size_t k : share[p]) file_err[k] = pipe_err[p];
       t_last_pull = now_s();
       wb->drain();
-      for (size_t k = 0; k < out.size(); ++k)
-        if (out[k].repaired && file_err[k].empty()) wb->post(k, 0, out[k].size);  // the repair pass replaced its bytes
-      wb->drain();
       wb->stop();
-      // Durable before visible: the verified marker trusts size + mtime only, so a renamed file whose
-      // pages never reached the disk (crash, power loss) must not carry one.  Like the host path
-      // (downloader.cpp) the data is synced before the rename; the group's files sync concurrently.
-      {
-        std::vector<std::thread> syncs;
-        for (size_t k = 0; k < out.size(); ++k)
-          if (file_err[k].empty() && out[k].err.empty()) syncs.emplace_back([&out, k] {
-              if (::fdatasync(out[k].fd) != 0) out[k].err = std::string("fdatasync: ") + std::strerror(errno);
-            });
-        for (auto& t : syncs) t.join();
-      }
+      // (durable before visible: every pipeline fdatasync'ed its files before returning above -- the
+      // verified marker trusts size + mtime only, like the host path, downloader.cpp)
       t_last_write = now_s();
       for (size_t k = 0; k < out.size(); ++k) {
         WriteBack::File& f = out[k];

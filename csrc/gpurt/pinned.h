@@ -11,11 +11,37 @@
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <thread>
 #include <utility>
+#include <vector>
 
 namespace zest::gpurt {
+
+// Touch every page of [p, p + len) so the kernel allocates (and zeroes) it now, from several
+// threads for big buffers: one thread faults ~10 GB/s, and a 141 GB pinned origin took tens of
+// seconds of bench setup that way.
+inline void fault_in(void* p, size_t len) {
+  auto* b = static_cast<volatile uint8_t*>(p);
+  const size_t per = size_t(1) << 30;
+  const size_t nt = std::min<size_t>(16, (len + per - 1) / per);
+  auto touch = [b](size_t lo, size_t hi) {
+    for (size_t o = lo; o < hi; o += 4096) b[o] = 0;
+  };
+  if (nt <= 1) {
+    touch(0, len);
+    return;
+  }
+  std::vector<std::thread> ts;
+  const size_t step = (len / nt + 4095) / 4096 * 4096;
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t lo = t * step, hi = std::min(len, lo + step);
+    if (lo < hi) ts.emplace_back(touch, lo, hi);
+  }
+  for (auto& t : ts) t.join();
+}
 
 class PinnedBuf {
  public:
@@ -37,6 +63,23 @@ class PinnedBuf {
 
   uint8_t* data() const { return p_; }
   size_t size() const { return n_; }
+  // Hand the allocation over to the caller (freed later with free_raw(ptr, size(), mapped())).
+  bool mapped() const { return mapped_; }
+  uint8_t* release() {
+    uint8_t* p = p_;
+    p_ = nullptr;
+    n_ = 0;
+    return p;
+  }
+  static void free_raw(uint8_t* p, size_t n, bool mapped) {
+    if (!p) return;
+    if (mapped) {
+      (void)hipHostUnregister(p);
+      ::munmap(p, n);
+    } else {
+      (void)hipHostFree(p);
+    }
+  }
 
   // Returns false (and holds nothing) when neither path could pin `n` bytes.
   bool alloc(size_t n) {
@@ -47,8 +90,7 @@ class PinnedBuf {
     void* m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
       (void)::madvise(m, len, MADV_HUGEPAGE);
-      auto* b = static_cast<volatile uint8_t*>(m);
-      for (size_t o = 0; o < len; o += 4096) b[o] = 0;  // fault in (2 MiB at a time with THP)
+      fault_in(m, len);  // (2 MiB at a time with THP)
       if (hipHostRegister(m, len, hipHostRegisterDefault) == hipSuccess) {
         p_ = static_cast<uint8_t*>(m);
         n_ = len;

@@ -26,6 +26,7 @@
 #include "lz4.h"
 #include "sha1.h"
 #include "storage.h"
+#include "term_jobs.h"
 #include "tracker.h"
 #include "xet_hash.h"
 #include "xorb.h"
@@ -314,6 +315,47 @@ TEST(xorb_cache_runs) {
   CHECK(h->data.size() == body.size() - idx[4].header_off);
   CHECK(!cache.find(hx, 2, 4).has_value());
   CHECK(storage::list_cached_xorbs(cfg).size() == 1);
+}
+
+TEST(xorb_cache_covers_and_write_behind) {
+  // covers(): the planner's header-only possession check agrees with find(); the write-behind
+  // writer keeps per-xorb order (a promote queued after its quarantine write publishes it), drops
+  // runs over its byte bound instead of blocking, and flush() waits for everything queued.
+  char tmpl[] = "/tmp/zest_cpp_wb_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  setenv("ZEST_CACHE_DIR", dir, 1);
+  Config cfg = Config::from_env();
+  storage::XorbRegistry reg;
+  storage::XorbCache cache(cfg, &reg);
+  xet::XorbBuilder b(xet::CompressionPolicy::None);
+  for (uint32_t i = 0; i < 5; ++i) {
+    Bytes c = rnd(9000, 70 + i);
+    b.add_chunk(c.data(), c.size());
+  }
+  const std::string hx = xet::to_hex(b.hash());
+  Bytes body = b.body();
+  auto idx = xet::index_chunks(body.data(), body.size());
+  CHECK(!cache.covers(hx, 0, 1));
+  {
+    storage::CacheWriter w(&cache, 1 << 20, 2);
+    CHECK(w.put_run(hx, 2, body.data() + idx[2].header_off, body.size() - idx[2].header_off, false));
+    const std::string pend = w.put_pending(hx, 0, body.data(), idx[2].header_off);
+    CHECK(!pend.empty());
+    w.promote(hx, 0, pend);
+    Bytes big(2 << 20, 7);
+    CHECK(!w.put_run(hx, 9, big.data(), big.size(), false));  // over the bound: dropped, not queued
+    w.flush();
+    auto st = w.stats();
+    CHECK(st.dropped_bytes == big.size() && st.written_bytes == body.size());
+    CHECK(!storage::exists(pend));  // promoted (renamed) after its own write
+  }
+  CHECK(cache.covers(hx, 0, 2) && cache.find(hx, 0, 2).has_value());
+  CHECK(cache.covers(hx, 3, 5) && cache.find(hx, 3, 5).has_value());
+  CHECK(!cache.covers(hx, 1, 3) && !cache.find(hx, 1, 3).has_value());  // no run spans chunks 1..2
+  CHECK(!cache.covers(hx, 2, 6));
+  auto held = cached_terms(cache, {hx, hx, hx}, {0, 1, 2}, {2, 3, 5}, 2);
+  CHECK(held == std::vector<uint8_t>({1, 0, 1}));
 }
 
 TEST(xorb_cache_quarantine_per_fetch) {
