@@ -113,6 +113,14 @@ for step in "$@"; do
                python tools/gpu/overlap.py $OUT/ct --marker "swarm_pull timed" > $OUT/overlap_swarm.txt 2>&1
                python tools/gpu/overlap.py $OUT/ct > $OUT/overlap_all.txt 2>&1
                cat $OUT/overlap_swarm.txt $OUT/overlap_all.txt; rm -rf $OUT/ct ;;
+    config2) # BASELINE config 2 on the public path: rank 0 warm, rank 1 cold, ranks share the GPU (gloo)
+             ZEST_BENCH_BACKEND=gloo timeout -k 10 600 python -u tools/config2_rehearsal.py \
+               --model ${C2_MODEL:-llama-3.1-8b} --mode ${C2_MODE:-bf16} --ranks ${C2_RANKS:-2} \
+               --out $OUT/config2.json > $log 2>&1 || fail $step $? $log
+             python -c "import json,sys; d=json.load(open(sys.argv[1])); print({k: d[k] for k in ('aggregate_GBps','leecher_receive_GBps','cdn_bytes','backend')}, [(r['rank'], r['exchange'], r['from_cache'], r['received_bytes'], r['pull_s']) for r in d['per_rank']])" $OUT/config2.json ;;
+    swarmrow) timeout -k 10 600 python -u bench.py --model ${SR_MODEL:-llama-3.1-8b} --modes ${SR_MODES:-bf16,random} \
+                --steps 5 --warmup 2 --swarm-steps 3 > $log 2>&1 || fail $step $? $log
+              grep -h "GB/s aggregate\|swarm_pull" $log | cut -c1-300 ;;
     pmctable) # one counter group per rocprofv3 pass (SQ <= 8, TCC <= 4: FETCH_SIZE uses 3, WRITE_SIZE 2)
               i=0
               for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" \
