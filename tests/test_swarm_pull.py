@@ -520,6 +520,11 @@ def test_swarm_pull_from_memory_origin_and_pipeline_reuse():
     assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
     assert xorb_gets == 0  # every byte came from the memory origin
     assert st["from_cdn"] == st["total_bytes"] and not st["reused_pipeline"] and st2["reused_pipeline"]
+    # a reused pipeline reports this pull's bytes, not the session's running total (the second pull
+    # finds the first one's runs in its xorb cache: possession makes it read them from there)
+    src = ("bytes_from_cdn", "bytes_from_cache", "bytes_from_peer")
+    assert sum(st2["fetch_stats"][k] for k in src) == sum(st["fetch_stats"][k] for k in src) > 0
+    assert st2["from_cache"] == st2["total_bytes"] and st2["possession"] == [st2["total_bytes"]]
     n_files = st["files"]
     assert cas_calls >= 2 * n_files  # reconstructions fetched anew by the second pull
 

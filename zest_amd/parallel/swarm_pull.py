@@ -523,11 +523,14 @@ class _Swarm:
         self.reuse = reuse
         kept = _PIPELINES.pop(self.reuse_key, None) if reuse else None
         self.reused = kept is not None
+        self.stats_base: dict = {}
         if kept is not None:  # a previous pull's pipelines: staging pinned, session up; reconstructions anew
             self.fetchers = kept
             self.fetcher = kept[0]
             for f in kept:
                 f.reset_reconstructions()
+            # the session's counters run on across pulls: this pull reports its own share
+            self.stats_base = _merged_stats([f.stats() for f in kept if f.parent is None])
         else:
             self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
                                     staging_bytes, threads)
@@ -1190,6 +1193,23 @@ def release_pipelines() -> None:
     _PIPELINES.clear()
 
 
+def _stats_delta(now: dict, base: dict) -> dict:
+    """Counters of `now` minus `base` (numbers; nested dicts recursively; other values as in now)."""
+    out = {}
+    for k, v in now.items():
+        b = base.get(k)
+        if isinstance(v, dict):
+            out[k] = _stats_delta(v, b if isinstance(b, dict) else {})
+        elif isinstance(v, (int, float)) and not isinstance(v, bool) and isinstance(b, (int, float)):
+            out[k] = v - b
+        else:
+            out[k] = v
+    if "p2p_ratio" in out:
+        tot = sum(out.get(k, 0) for k in ("bytes_from_cache", "bytes_from_peer", "bytes_from_cdn"))
+        out["p2p_ratio"] = round(out.get("bytes_from_peer", 0) / tot, 4) if tot else 0.0
+    return out
+
+
 def _parallel_map(fn, items, threads: int):
     if not items:
         return []
@@ -1275,7 +1295,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
                 peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
                 GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
-                fetch_stats=_merged_stats([f.stats() for f in sw.fetchers if f.parent is None]),
+                fetch_stats=_stats_delta(_merged_stats([f.stats() for f in sw.fetchers if f.parent is None]),
+                                         sw.stats_base),
                 pipelined=sw.pipelined,
                 held_bytes=sw.held_bytes[sw.m.rank], share_bytes=sw.share_bytes[sw.m.rank],
                 possession=list(sw.held_bytes), reused_pipeline=sw.reused,
