@@ -81,6 +81,11 @@ for step in "$@"; do
            db=$(find $OUT/kprof -name "*.db" | head -1)
            python tools/rocpd_summary.py "$db" --title "kbench ${KBENCH_ONLY:-all} kernels" > $OUT/kernels_kbench.md 2>&1
            head -24 $OUT/kernels_kbench.md; rm -f "$db" ;;
+    gprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/gprof -o gb -- \
+             python3 -m zest_amd.gpubench --json --mib ${GPROF_MIB:-256} --runs 5 > $log 2>&1 || fail $step $? $log
+           db=$(find $OUT/gprof -name "*.db" | head -1)
+           python tools/rocpd_summary.py "$db" --title "gpubench ${GPROF_MIB:-256} MiB kernels" > $OUT/kernels_gpubench.md 2>&1
+           head -30 $OUT/kernels_gpubench.md; rm -f "$db" ;;
     benchA|benchB) v=BENCH_ENV_${step#bench}; env ${!v:-} timeout -k 10 700 python -u bench.py --modes ${BENCH_MODES:-bf16} \
                 --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
               echo "env: ${!v:-}"; grep -h "aggregate" $log ;;

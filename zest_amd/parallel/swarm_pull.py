@@ -600,17 +600,26 @@ class _Swarm:
             os._exit(1)  # fault injection (tests): this rank dies while the plan is being made
         if self.m.rank == 0:
             try:
+                t_l = time.perf_counter()
                 commit, files = _core.list_repo_files(self.repo, self.revision, self.repo_type)
+                self._mark("plan_list_s", t_l)
                 st = [f for f in files if f["path"].endswith(".safetensors")]
                 xet = [f for f in st if f["xet_hash"]]
-                shapes = _parallel_map(lambda f: [tuple(x) for x in self.fetcher.shapes(f["xet_hash"])], xet,
+                t_r = time.perf_counter()
+                impl = self.fetcher.impl  # (waits for a pipeline still being built)
+                self._mark("plan_pipeline_wait_s", t_r)
+                t_r = time.perf_counter()
+                shapes = _parallel_map(lambda f: [tuple(x) for x in impl.term_shapes(f["xet_hash"])], xet,
                                         max(8, self.fetcher.threads))
                 # (xorb hex, chunk range) per term: every rank checks its own cache against them
-                keys = [[list(k) for k in self.fetcher.keys(f["xet_hash"])] for f in xet] if self.possession else None
+                keys = [[list(k) for k in impl.term_keys(f["xet_hash"])] for f in xet] if self.possession else None
+                self._mark("plan_recon_s", t_r)
                 obj = ("ok", commit, st, shapes, keys)
             except Exception as e:  # noqa: BLE001 - every rank leaves the same way
                 obj = ("err", f"{type(e).__name__}: {e}")
+        t_b = time.perf_counter()
         obj = self._plan_from0(obj)
+        self._mark("plan_share_s", t_b)
         if obj[0] != "ok":
             raise SwarmPullError(f"listing/planning {self.repo}@{self.revision} failed on rank 0: {obj[1]}")
         _, self.commit, st_files, shapes, keys = obj
