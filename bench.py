@@ -427,6 +427,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     wd.arm("timed")
     from zest_amd import _core
     _core.trace.roctx_push("swarm_pull timed")  # (ZEST_ROCTX=1: the window of tools/gpu/overlap.py --marker)
+    mark = cuda and os.environ.get("ZEST_BENCH_MARK") == "1"
+    if mark:  # a distinctive kernel brackets the timed window in a kernel trace (overlap.py --between)
+        torch.cuda._sleep(1000)
     times, st = [], {}
     for _ in range(a.swarm_steps):
         st = {}
@@ -439,6 +442,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             torch.cuda.synchronize()
         tdist.barrier()
         times.append(time.perf_counter() - t0)
+    if mark:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     _core.trace.roctx_pop()
     dev_t = device if (cuda and not own_pg) else "cpu"
     el = torch.tensor(times, dtype=torch.float64, device=dev_t)
@@ -623,9 +629,8 @@ def rank_main(a) -> None:
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if cuda:
-        from zest_amd.engine import release_pinned_pool
-        release_pinned_pool()
+    # (the pinned origin pool is left to the process exit: unregistering ~141 GB one buffer at a time
+    # only delays it)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

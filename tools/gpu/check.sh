@@ -110,12 +110,12 @@ for step in "$@"; do
           python tools/gpu/pmc_summary.py "$f" "${PMC_KERNEL:-lz4}" > $OUT/pmc_summary.txt 2>&1; cat $OUT/pmc_summary.txt
           rm -rf $OUT/pmc ;;
     copytrace) # public-path swarm row under kernel + memory-copy + marker traces: does H2D overlap ingest?
-               ZEST_ROCTX=1 timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace \
+               ZEST_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace \
                  --output-format csv -d $OUT/ct -o ct -- python3 bench.py --model ${CT_MODEL:-llama-3.1-8b} \
                  --modes ${CT_MODES:-random} --steps 2 --warmup 1 --swarm-steps 2 --swarm-warmup 1 > $log 2>&1 \
                  || fail $step $? $log
                grep -h "aggregate" $log
-               python tools/gpu/overlap.py $OUT/ct --marker "swarm_pull timed" > $OUT/overlap_swarm.txt 2>&1
+               python tools/gpu/overlap.py $OUT/ct --between spin_kernel > $OUT/overlap_swarm.txt 2>&1
                python tools/gpu/overlap.py $OUT/ct > $OUT/overlap_all.txt 2>&1
                cat $OUT/overlap_swarm.txt $OUT/overlap_all.txt; rm -rf $OUT/ct ;;
     config2) # BASELINE config 2 on the public path: rank 0 warm, rank 1 cold, ranks share the GPU (gloo)

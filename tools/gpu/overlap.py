@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--kernel", default="ingest,place,lz4,hash,blake3,decode")
     ap.add_argument("--after-s", type=float, default=0.0)
     ap.add_argument("--marker", default="", help="restrict to the roctx range whose record contains this text")
+    ap.add_argument("--between", default="", help="restrict to the span between the first and last launch of "
+                                                 "kernels whose name contains this text")
     a = ap.parse_args()
     kt = [r for f in glob.glob(os.path.join(a.out, "**", "*kernel_trace.csv"), recursive=True) for r in csv.DictReader(open(f))]
     mc = [r for f in glob.glob(os.path.join(a.out, "**", "*memory_copy_trace.csv"), recursive=True)
@@ -67,6 +69,12 @@ def main():
             raise SystemExit(f"no roctx range containing {a.marker!r}")
         lo, hi = min(float(r["Start_Timestamp"]) for r in mk), max(float(r["End_Timestamp"]) for r in mk)
         print(f"marker {a.marker!r}: {(hi - lo) / 1e9:.3f} s")
+    if a.between:
+        mk = [r for r in kt if a.between in r.get("Kernel_Name", "")]
+        if len(mk) < 2:
+            raise SystemExit(f"fewer than two kernels named *{a.between}*")
+        lo, hi = min(float(r["End_Timestamp"]) for r in mk), max(float(r["Start_Timestamp"]) for r in mk)
+        print(f"between {a.between!r} kernels: {(hi - lo) / 1e9:.3f} s")
     h2d = [r for r in h2d if lo <= float(r["Start_Timestamp"]) <= hi]
     ks = [r for r in ks if lo <= float(r["Start_Timestamp"]) <= hi]
     if mc:
