@@ -369,6 +369,7 @@ class FakeHub:
 
         class H(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+            disable_nagle_algorithm = True  # headers and body go out without waiting for ACKs
 
             def log_message(self, *a):  # quiet
                 pass
@@ -381,7 +382,13 @@ class FakeHub:
 
             do_HEAD = do_GET
 
-        self._srv = ThreadingHTTPServer((self.host, port), H)
+        class S(ThreadingHTTPServer):
+            # socketserver's default listen backlog is 5: 16 concurrent reconstruction requests
+            # (swarm_pull's plan) overflowed it and the dropped SYNs came back after the 1 s
+            # retransmit -- the plan of a 70B pull took 1.06 s instead of ~0.1 (tools/plan_probe.py)
+            request_queue_size = 1024
+
+        self._srv = S((self.host, port), H)
         self._srv.daemon_threads = True
         self._thr = threading.Thread(target=self._srv.serve_forever, daemon=True)
         self._thr.start()
