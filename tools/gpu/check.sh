@@ -111,7 +111,7 @@ for step in "$@"; do
           rm -rf $OUT/pmc ;;
     copytrace) # public-path swarm row under kernel + memory-copy + marker traces: does H2D overlap ingest?
                ZEST_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace \
-                 --output-format csv -d $OUT/ct -o ct -- python3 bench.py --model ${CT_MODEL:-llama-3.1-8b} \
+                 -d $OUT/ct -o ct -- python3 bench.py --model ${CT_MODEL:-llama-3.1-8b} \
                  --modes ${CT_MODES:-random} --steps 2 --warmup 1 --swarm-steps 2 --swarm-warmup 1 > $log 2>&1 \
                  || fail $step $? $log
                grep -h "aggregate" $log

@@ -45,6 +45,32 @@ def inter(u1, u2):
     return s
 
 
+def from_db(out):
+    """(kernel rows, copy rows) as CSV-like dicts from a rocpd SQLite database (rocprofv3's default
+    output), or None when there is none."""
+    import sqlite3
+    dbs = glob.glob(os.path.join(out, "**", "*.db"), recursive=True)
+    if not dbs:
+        return None
+    c = sqlite3.connect(dbs[0])
+
+    def cols(view):
+        return [r[1] for r in c.execute(f"pragma table_info({view})").fetchall()]
+
+    def pick(cs, *names):
+        return next((n for n in names if n in cs), None)
+    kc, mc = cols("kernels"), cols("memory_copies")
+    ks, ke, kn = pick(kc, "start", "start_ns"), pick(kc, "end", "end_ns"), pick(kc, "name", "kernel_name")
+    kt = [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b}
+          for n, a, b in c.execute(f"select {kn}, {ks}, {ke} from kernels").fetchall()]
+    ms, me = pick(mc, "start", "start_ns"), pick(mc, "end", "end_ns")
+    mn, mz = pick(mc, "name", "direction", "kind"), pick(mc, "size", "bytes")
+    cp = [{"Direction": n, "Start_Timestamp": a, "End_Timestamp": b, "Size": z}
+          for n, a, b, z in c.execute(f"select {mn}, {ms}, {me}, {mz} from memory_copies").fetchall()]
+    print(f"rocpd db {os.path.basename(dbs[0])}: kernel columns {kc[:12]}...; copy columns {mc}")
+    return kt, cp
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
@@ -54,9 +80,14 @@ def main():
     ap.add_argument("--between", default="", help="restrict to the span between the first and last launch of "
                                                  "kernels whose name contains this text")
     a = ap.parse_args()
-    kt = [r for f in glob.glob(os.path.join(a.out, "**", "*kernel_trace.csv"), recursive=True) for r in csv.DictReader(open(f))]
-    mc = [r for f in glob.glob(os.path.join(a.out, "**", "*memory_copy_trace.csv"), recursive=True)
-          for r in csv.DictReader(open(f))]
+    db = from_db(a.out)
+    if db is not None:
+        kt, mc = db
+    else:
+        kt = [r for f in glob.glob(os.path.join(a.out, "**", "*kernel_trace.csv"), recursive=True)
+              for r in csv.DictReader(open(f))]
+        mc = [r for f in glob.glob(os.path.join(a.out, "**", "*memory_copy_trace.csv"), recursive=True)
+              for r in csv.DictReader(open(f))]
     h2d = [r for r in mc if "HOST_TO_DEVICE" in (r.get("Direction", "") + r.get("Operation", "")).upper()]
     pats = [p for p in a.kernel.split(",") if p]
     ks = [r for r in kt if any(p in r.get("Kernel_Name", "").lower() for p in pats)]
