@@ -137,7 +137,8 @@ for step in "$@"; do
                 timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/pmc_$i -o g --output-format csv -- \
                   python3 tools/kbench.py --only gather --iters 2 >> $log.$i 2>&1 || fail $step $? $log.$i
               done
-              python tools/gpu/pmc_table.py $OUT/pmc_1 $OUT/pmc_2 $OUT/pmc_3 $OUT/pmc_4 > $OUT/pmc_table.md 2>&1
+              python tools/gpu/pmc_table.py $OUT/pmc_1 $OUT/pmc_2 $OUT/pmc_3 $OUT/pmc_4 --raw $OUT/pmc_raw.json \
+                > $OUT/pmc_table.md 2>&1
               cat $OUT/pmc_table.md; rm -rf $OUT/pmc_? ;;
     swarmtrace) ZEST_TRACE=$PWD/$OUT/swarm_trace.%p.json timeout -k 10 400 python -u tools/swarm_bench.py \
                   --model ${SWARM_MODEL:-llama-3.1-8b} --ranks 1 --out $OUT/swarm_trace_run.json > $log 2>&1 \

@@ -5,10 +5,10 @@
 Each pass directory holds a counter_collection.csv (per-dispatch counters) and a kernel_trace.csv
 (per-dispatch start/end).  For every kernel: launches, mean duration, HBM bytes read / written per
 launch (FETCH_SIZE / WRITE_SIZE are KiB in rocprof's definition) and the achieved GB/s, VALU busy and
-utilization (active lanes / 64), SALU busy, LDS bank-conflict ratio, FLAT (global) vs VMEM (buffer)
-instruction counts, wait fraction.  gfx950 issues global_load/store as FLAT instructions, so
-SQ_ACTIVE_INST_VMEM / SQ_INSTS_VMEM read 0 for kernels that stream GBs through global_* -- the
-round-4 "VMEM = 0" pass was counting the wrong class; SQ_INSTS_FLAT is the one that moves.
+utilization (active lanes / 64), the fraction of wave-cycles issuing VALU / SALU instructions,
+LDS bank-conflict ratio, FLAT and VMEM instruction counts, wait fraction.  Round 4's pass used
+SQ_ACTIVE_INST_VMEM, which reads 0 on gfx950 for kernels that stream GBs through global_* loads;
+SQ_INSTS_VMEM / SQ_INSTS_FLAT count them.  Raw per-kernel counter means go to `--raw FILE` (JSON).
 """
 import collections
 import csv
@@ -39,6 +39,11 @@ def short(k):
 
 
 def main():
+    raw = None
+    if "--raw" in sys.argv:
+        i = sys.argv.index("--raw")
+        raw = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
     per = collections.defaultdict(dict)
     launches, durs = {}, collections.defaultdict(list)
     for d in sys.argv[1:]:
@@ -59,18 +64,23 @@ def main():
         gbps = (rd + wr) / (us * 1e3) if us else 0.0
         act = c.get("SQ_ACTIVE_INST_VALU", 0)
         util = 100 * c.get("SQ_THREAD_CYCLES_VALU", 0) / (act * 64) if act else 0.0
-        gui = c.get("GRBM_GUI_ACTIVE", 0)
-        cu = 256
-        valu_busy = 100 * act / cu / gui if gui else 0.0
-        salu_busy = 100 * c.get("SQ_INST_CYCLES_SALU", 0) / cu / gui if gui else 0.0
+        wcyc = c.get("SQ_WAVE_CYCLES", 0)
+        # per-wave issue fractions (independent of how rocprof sums SE / XCD instances)
+        valu_busy = 100 * act / wcyc if wcyc else 0.0
+        salu_busy = 100 * c.get("SQ_ACTIVE_INST_SCA", 0) / wcyc if wcyc else 0.0
         lds_act = c.get("SQ_LDS_IDX_ACTIVE", 0) - c.get("SQ_LDS_BANK_CONFLICT", 0)
         bank = c.get("SQ_LDS_BANK_CONFLICT", 0) / lds_act if lds_act > 0 else 0.0
         wait = 100 * c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else 0.0
         rows.append((us * launches[k], short(k), launches[k], us, rd / 1e6, wr / 1e6, gbps, valu_busy, util, salu_busy,
                      bank, c.get("SQ_INSTS_FLAT", 0), c.get("SQ_INSTS_VMEM", 0), c.get("SQ_INSTS_LDS", 0), wait))
     rows.sort(reverse=True)
-    print("| kernel | launches | us/launch | HBM rd MB | HBM wr MB | GB/s | VALU busy % | VALU util % | "
-          "SALU busy % | LDS conflict/access | FLAT insts | VMEM insts | LDS insts | wait-inst % |")
+    if raw:
+        import json
+        with open(raw, "w") as f:
+            json.dump({k: dict(v) for k, v in per.items()}, f, indent=1)
+    print("| kernel | launches | us/launch | HBM rd MB | HBM wr MB | GB/s | VALU issue % of wave-cycles | "
+          "VALU util % | SALU issue % of wave-cycles | LDS conflict/access | FLAT insts | VMEM insts | LDS insts | "
+          "wait-inst % |")
     print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for r in rows:
         print(f"| {r[1]} | {r[2]} | {r[3]:.1f} | {r[4]:.1f} | {r[5]:.1f} | {r[6]:.0f} | {r[7]:.1f} | {r[8]:.1f} | "
