@@ -404,6 +404,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     for k, v in hub.env(cache).items():
         os.environ[k] = v
     os.environ["ZEST_CACHE_WRITES"] = "0"
+    # timed HIP events around every staging batch's H2D copy and kernels: the row reports how much of
+    # the copy time ran under the decode/hash kernels (DeviceXetPull.timeline_json)
+    os.environ.setdefault("ZEST_DEVICE_TIMING", "1")
     own_pg = False
     if dist is None:  # one rank: swarm_pull is a collective over a group of one
         import torch.distributed as tdist
@@ -471,6 +474,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             "swarm_pull_exchange": st.get("exchange"), "swarm_pull_phases": st.get("phases"),
             "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
                                                                                   "bytes_from_peer")},
+            "swarm_pull_device_timeline": st.get("device_timeline"),
             "swarm_pull_setup_s": round(setup_s, 3), "swarm_pull_warmup_s": round(warm_s, 3),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}

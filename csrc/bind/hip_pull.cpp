@@ -141,6 +141,7 @@ void bind_hip_pull(py::module_& m) {
              self.flush_cache_writes();
            }, "wait for the write-behind xorb cache queue")
       .def("cache_writer_json", &DeviceXetPull::cache_writer_json)
+      .def("timeline_json", &DeviceXetPull::timeline_json)
       .def("stats_json", &DeviceXetPull::stats_json)
       .def_property_readonly("staging_bytes", &DeviceXetPull::staging_bytes);
 }

@@ -157,6 +157,7 @@ struct DeviceXetPull::Impl {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : timing_events_) (void)hipEventDestroy(e);
     for (auto& s : slots_) {
       s.pin.reset();
       s.rec_pin.reset();
@@ -555,6 +556,9 @@ struct DeviceXetPull::Impl {
           sl.rec_cap = cap;
         }
       hipEvent_t* ev = take_events(2 * nb);  // ev[2b]: batch b's copies landed; ev[2b+1]: its kernels ran
+      // ZEST_DEVICE_TIMING=1: timed events around every batch's copy and kernels (device timeline
+      // of the pass: copy / kernel busy time and how much of it overlapped, timeline_json())
+      hipEvent_t* tev = timing_ ? take_timing_events(4 * nb) : nullptr;
       // Continuous pipeline: the fetch workers take terms in order across batch boundaries, so the
       // next batches' terms are already in flight while the current batch's slowest transfers finish
       // (a per-batch join left the connections ~45 % idle: tools/direct_bench.py under ZEST_TRACE).
@@ -721,13 +725,16 @@ struct DeviceXetPull::Impl {
           trace::Span submit_span("device", "queue H2D + place/hash");
           submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
           if (b >= S) hip_check(hipStreamWaitEvent(copy_stream_, ev[2 * (b - S) + 1], 0), "hipStreamWaitEvent");
+          if (tev) hip_check(hipEventRecord(tev[4 * b], copy_stream_), "event");
           hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, copy_stream_), "H2D");
           if (nchunks)
             hip_check(hipMemcpyAsync(s.chunks_dev.p, s.recs(), sizeof(ZgChunk) * size_t(nchunks), hipMemcpyHostToDevice,
                                      copy_stream_),
                       "H2D chunk records");
           hip_check(hipEventRecord(ev[2 * b], copy_stream_), "event");
+          if (tev) hip_check(hipEventRecord(tev[4 * b + 1], copy_stream_), "event");
           hip_check(hipStreamWaitEvent(stream_, ev[2 * b], 0), "hipStreamWaitEvent");
+          if (tev) hip_check(hipEventRecord(tev[4 * b + 2], stream_), "event");
           // decode (when the batch has compressed chunks) + one fused pass placing raw chunks and
           // hashing every chunk (csrc/gpu/blake3_flat.hip PlaceSrc)
           hip_check(zg_ingest_chunks(s.dev.p, top, dst, dst_size, s.chunks_dev.p, nchunks, compressed ? 1 : 0, err_.p,
@@ -735,6 +742,7 @@ struct DeviceXetPull::Impl {
                                      s.scratch.p, hs_bytes, stream_),
                     "ingest");
           hip_check(hipEventRecord(ev[2 * b + 1], stream_), "event");
+          if (tev) hip_check(hipEventRecord(tev[4 * b + 3], stream_), "event");
           {
             std::lock_guard<std::mutex> g(mu);
             issued.push_back(b);
@@ -755,10 +763,66 @@ struct DeviceXetPull::Impl {
       stop_releaser();
       hip_check(e1, "sync copy stream");
       hip_check(e2, "sync compute stream");
+      if (tev && nb) record_timeline(tev, nb);
     }
     if (!fetch_err.empty()) return at;
     hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
     return at;
+  }
+
+  // Device timeline of the last timed pass: intervals [copy start, copy end] and [kernels start,
+  // kernels end] per batch (ms from the first copy), their unions, and the time both ran at once.
+  void record_timeline(hipEvent_t* tev, size_t nb) {
+    std::vector<std::pair<double, double>> cp, kn;
+    for (size_t b = 0; b < nb; ++b) {
+      float a = 0, c = 0, d = 0, e = 0;
+      if (hipEventElapsedTime(&a, tev[0], tev[4 * b]) != hipSuccess ||
+          hipEventElapsedTime(&c, tev[0], tev[4 * b + 1]) != hipSuccess ||
+          hipEventElapsedTime(&d, tev[0], tev[4 * b + 2]) != hipSuccess ||
+          hipEventElapsedTime(&e, tev[0], tev[4 * b + 3]) != hipSuccess)
+        return;
+      cp.emplace_back(a, c);
+      kn.emplace_back(d, e);
+    }
+    auto unite = [](std::vector<std::pair<double, double>> v) {
+      std::sort(v.begin(), v.end());
+      std::vector<std::pair<double, double>> u;
+      for (auto& x : v)
+        if (!u.empty() && x.first <= u.back().second) u.back().second = std::max(u.back().second, x.second);
+        else u.push_back(x);
+      return u;
+    };
+    auto total = [](const std::vector<std::pair<double, double>>& u) {
+      double t = 0;
+      for (auto& x : u) t += x.second - x.first;
+      return t;
+    };
+    const auto uc = unite(cp), uk = unite(kn);
+    double both = 0;
+    for (size_t i = 0, j = 0; i < uc.size() && j < uk.size();) {
+      const double lo = std::max(uc[i].first, uk[j].first), hi = std::min(uc[i].second, uk[j].second);
+      if (hi > lo) both += hi - lo;
+      (uc[i].second < uk[j].second) ? ++i : ++j;
+    }
+    const double window = std::max(uc.back().second, uk.back().second);
+    std::lock_guard<std::mutex> g(timeline_mu_);
+    timeline_ = "{\"batches\":" + std::to_string(nb) + ",\"window_ms\":" + std::to_string(window) +
+                ",\"h2d_busy_ms\":" + std::to_string(total(uc)) + ",\"kernel_busy_ms\":" + std::to_string(total(uk)) +
+                ",\"overlap_ms\":" + std::to_string(both) + "}";
+  }
+
+  hipEvent_t* take_timing_events(size_t n) {
+    while (timing_events_.size() < n) {
+      hipEvent_t e = nullptr;
+      hip_check(hipEventCreate(&e), "hipEventCreate");
+      timing_events_.push_back(e);
+    }
+    return timing_events_.data();
+  }
+
+  std::string timeline_json() {
+    std::lock_guard<std::mutex> g(timeline_mu_);
+    return timeline_.empty() ? "{}" : timeline_;
   }
 
   // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does
@@ -790,6 +854,13 @@ struct DeviceXetPull::Impl {
   bool device_ready_ = false;
   std::vector<Slot> slots_;
   std::vector<hipEvent_t> events_;
+  const bool timing_ = [] {
+    const char* v = std::getenv("ZEST_DEVICE_TIMING");
+    return v && std::string(v) == "1";
+  }();
+  std::vector<hipEvent_t> timing_events_;
+  std::mutex timeline_mu_;
+  std::string timeline_;
   DevBuf<unsigned long long> err_;
   DevBuf<uint8_t> hashes_;
   DevBuf<uint64_t> sizes_;
@@ -840,6 +911,7 @@ std::vector<uint8_t> DeviceXetPull::cached_terms(const std::vector<std::string>&
 void DeviceXetPull::reset_reconstructions() { impl_->sh_->recs->clear(); }
 void DeviceXetPull::init_device() { impl_->init_device(); }
 void DeviceXetPull::flush_cache_writes() { impl_->flush_cache_writes(); }
+std::string DeviceXetPull::timeline_json() const { return impl_->timeline_json(); }
 std::string DeviceXetPull::cache_writer_json() const {
   auto* w = impl_->sh_->writer.get();
   if (!w) return "{}";

@@ -266,6 +266,7 @@ def test_device_pull_sibling_pipelines_and_write_behind_cache(tmp_path, monkeypa
             monkeypatch.setenv(k, v)
         commit, listing = _core.list_repo_files("org/sib", "main", "model")
         listing = sorted((f for f in listing if f["xet_hash"]), key=lambda f: f["path"])
+        monkeypatch.setenv("ZEST_DEVICE_TIMING", "1")
         dp = zops.hip().DeviceXetPull("org/sib", "main", "model", False, [], None, False, [], 0, 96 << 10, 4, 3)
         sib = dp.sibling(64 << 10, 2)
         bufs = [zops.padded_empty(f["size"], "cuda:0")[:f["size"]] for f in listing]
@@ -274,6 +275,9 @@ def test_device_pull_sibling_pipelines_and_write_behind_cache(tmp_path, monkeypa
         sib.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing[2:], bufs[2:])])
         for f, b in zip(listing, bufs):
             assert b.cpu().numpy().tobytes() == files[f["path"]]
+        tl = _json.loads(dp.timeline_json())  # timed events around every batch's copy and kernels
+        assert tl["batches"] >= 2 and tl["h2d_busy_ms"] > 0 and tl["kernel_busy_ms"] > 0
+        assert 0 <= tl["overlap_ms"] <= min(tl["h2d_busy_ms"], tl["kernel_busy_ms"]) + 1e-3
         dp.flush_cache_writes()
         w = _json.loads(dp.cache_writer_json())
         assert w["written_bytes"] > 0 and w["dropped_bytes"] == 0

@@ -472,6 +472,12 @@ class _Fetcher:
     def stats(self) -> dict:
         return json.loads(self._impl.stats_json()) if self._impl is not None else {}
 
+    def timeline(self) -> dict:
+        """Device timeline of this pipeline's last pass (ZEST_DEVICE_TIMING=1; {} otherwise)."""
+        if self._impl is None or not hasattr(self._impl, "timeline_json"):
+            return {}
+        return json.loads(self._impl.timeline_json())
+
     def cache_writer(self) -> dict:
         """Write-behind cache queue counters (GPU pipelines; {} on CPU)."""
         if self._impl is None or not hasattr(self._impl, "cache_writer_json"):
@@ -1309,7 +1315,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 pipelined=sw.pipelined,
                 held_bytes=sw.held_bytes[sw.m.rank], share_bytes=sw.share_bytes[sw.m.rank],
                 possession=list(sw.held_bytes), reused_pipeline=sw.reused,
-                cache_writer=sw.fetcher.cache_writer(), **sw.stats)
+                cache_writer=sw.fetcher.cache_writer(), device_timeline=sw.fetcher.timeline(), **sw.stats)
         ok = True
         return out
     finally:
