@@ -62,9 +62,11 @@ for step in "$@"; do
     cli) timeout -k 10 700 python -u tools/direct_bench.py --model llama-3.1-8b --skip-direct --host-after \
            --out $OUT/cli_vs_host.json > $log 2>&1 || fail $step $? $log
          grep -h "^\[" $log ;;
-    stripe) timeout -k 10 600 python -u tools/stripe_bench.py --mb 4096 --out $OUT/stripe.json > $log 2>&1 \
+    stripe) mkdir -p $OUT/stripe_trace
+            timeout -k 10 600 python -u tools/stripe_bench.py --mb ${STRIPE_MB:-4096} ${STRIPE_ARGS:-} \
+              --trace $OUT/stripe_trace --out $OUT/stripe.json > $log 2>&1 \
               || fail $step $? $log
-            grep -h "^\[" $log ;;
+            grep -h "^\[" $log; rm -rf $OUT/stripe_trace ;;
     seed) timeout -k 10 600 python -u tools/seed_bench.py > $log 2>&1 || fail $step $? $log
           tail -5 $log ;;
     kbench) timeout -k 10 600 python -u tools/kbench.py ${KBENCH_ONLY:+--only $KBENCH_ONLY} > $OUT/kbench.jsonl 2> $log \
