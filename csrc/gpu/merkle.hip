@@ -14,6 +14,10 @@ namespace {
 
 constexpr int kThreads = 1024;
 constexpr int kHashThreads = 512;  // k_merkle threads that hash nodes (128-byte LDS ring each)
+// Rings sit kRingStride dwords apart: 33 (odd) puts the 64 lanes of a wave in 64 different LDS
+// banks.  With 32 every lane's ring started in the same bank, and rocprof counted 9.9 bank
+// conflicts per LDS access in k_merkle_spread (profiles/r5/pmc_table_gpubench256_r5h.md).
+constexpr int kRingStride = 33;
 constexpr uint32_t kLdsFlagWords = 4096;  // cut flags of levels with <= 131072 nodes live in LDS
 
 struct JobScratch {
@@ -323,7 +327,7 @@ __global__ void __launch_bounds__(kNodeThreads) k_merkle_spread(const uint8_t* _
                                                                 const ZgMerkleJob* __restrict__ jobs,
                                                                 uint8_t* __restrict__ scratch, uint64_t per_job,
                                                                 int level, int spread) {
-  __shared__ uint32_t s_ring[kNodeThreads * 32];
+  __shared__ uint32_t s_ring[kNodeThreads * kRingStride];
   const uint32_t jb = blockIdx.x / spread, part = blockIdx.x % spread;
   const ZgMerkleJob job = jobs[jb];
   JobScratch s = carve(scratch + per_job * jb, job.n_leaves);
@@ -336,7 +340,7 @@ __global__ void __launch_bounds__(kNodeThreads) k_merkle_spread(const uint8_t* _
     return;
   }
   const uint32_t ng = s.hdr[level - 1];
-  uint8_t* ring = reinterpret_cast<uint8_t*>(&s_ring[threadIdx.x * 32]);
+  uint8_t* ring = reinterpret_cast<uint8_t*>(&s_ring[threadIdx.x * kRingStride]);
   for (uint32_t g = part * kNodeThreads + threadIdx.x; g < ng; g += uint32_t(spread) * kNodeThreads)
     hash_node(io.in_h, io.in_s, s.starts[g], s.starts[g + 1], ring, io.out_h + 32 * size_t(g), io.out_s + g);
 }
@@ -347,7 +351,7 @@ __global__ void __launch_bounds__(kThreads) k_merkle(const uint8_t* __restrict__
                                                      const ZgMerkleJob* __restrict__ jobs, uint8_t* __restrict__ roots,
                                                      uint8_t* __restrict__ scratch, uint64_t per_job) {
   __shared__ LevelLds L;
-  __shared__ uint32_t s_ring[kHashThreads * 32];
+  __shared__ uint32_t s_ring[kHashThreads * kRingStride];
   const ZgMerkleJob job = jobs[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   uint8_t* out = roots + 32 * size_t(blockIdx.x);
@@ -364,7 +368,7 @@ __global__ void __launch_bounds__(kThreads) k_merkle(const uint8_t* __restrict__
   cur_h = s.hash_b;
   cur_s = s.size_b;
   bool into_a = true;
-  uint8_t* ring = reinterpret_cast<uint8_t*>(&s_ring[(tid % kHashThreads) * 32]);
+  uint8_t* ring = reinterpret_cast<uint8_t*>(&s_ring[(tid % kHashThreads) * kRingStride]);
   while (n > 1) {
     const uint32_t ng = level_starts(cur_h, n, s, L);
     uint8_t* nxt_h = into_a ? s.hash_a : s.hash_b;
