@@ -222,9 +222,20 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
                     arenas["peers"] = mapped
                 log(rank, f"peer arenas mapped over HIP IPC before the build: {mapped is not None}")
         world.generate_on_device(arena)
+        # One rank, compressed world: the build's compression writes the serialized chunks straight
+        # into pinned memory that becomes the origin (no second compression pass in build_origin).
+        ser_store = None
+        if comp == "bg4" and world_size == 1:
+            from zest_amd.engine import pinned_take
+            cap, ptr = pinned_take(int(world.model_bytes * 1.002) + (256 << 20))
+            ser_store = (ptr, cap)
         # N > 1: each rank chunks / hashes / compresses only its files, then the plan is all-gathered
-        world.build_on_device(arena, shard=(rank, world_size, None) if dist is not None else None)
+        world.build_on_device(arena, shard=(rank, world_size, None) if dist is not None else None,
+                              ser_store=ser_store)
         torch.cuda.synchronize()
+        if ser_store is not None and world.serialized is None:
+            from zest_amd.engine import pinned_give
+            pinned_give(ser_store[1], ser_store[0])
     else:
         contents = world.build_on_host()
         arena = torch.zeros(world.arena_bytes + 4096, dtype=torch.uint8)[: world.arena_bytes]
@@ -249,6 +260,11 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     reserve = (int(world.model_bytes * 1.002) // seeders + (256 << 20)) if rank < seeders else 0
     puller = DevicePuller(world, arena, rank, world_size, round_bytes=a.round_mb << 20, slots=a.slots,
                           seeders=seeders, origin_reserve=reserve)
+    if getattr(world, "serialized", None) is not None:  # not adopted: back to the pool
+        from zest_amd.engine import pinned_give
+        pinned_give(world.serialized[1], world.serialized[0])
+        world.serialized = None
+    phase["origin_adopted"] = bool(getattr(puller, "origin_prebuilt", False))
     ipc = False
     if want_ipc:
         ipc = mapped is not None and puller.enable_ipc(mapped)
@@ -315,6 +331,7 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     wd.arm("timed")
     barrier()
     sync()
+    hw0 = dict(puller.xchg.host_wait_s)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         puller.step()
@@ -351,6 +368,12 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         "hip_graph": bool(graph), "pipeline": getattr(puller, "pipeline", "cpu"), "seeders": seeders,
         "phase_s": phase, "exchange_rx_GBps": [round(x, 6) for x in rx],
     }
+    if world_size > 1 and puller.exchange in ("ipc", "xgmi"):
+        # host time per timed step in the peer-mapped issue path's ready-event waits + host barriers
+        # (rank 0; the GPU keeps running the next round's copy and kernels meanwhile)
+        hw = puller.xchg.host_wait_s
+        res["ipc_host_wait_ms_per_step"] = {
+            k: round((hw[k] - hw0[k]) * (1e3 if k != "calls" else 1) / max(1, a.steps), 3) for k in hw}
     if keep is not None:  # the swarm row serves its CDN from this world's pinned origin
         keep["world"], keep["puller"] = world, puller
         return res
@@ -631,6 +654,8 @@ def rank_main(a) -> None:
                    "rccl_ranks": rccl_ranks, "devices": devices, "distinct_devices": distinct,
                    "phase_s": head["phase_s"], "exchange_rx_GBps": head["exchange_rx_GBps"]},
     }
+    if "ipc_host_wait_ms_per_step" in head:
+        out["extra"]["ipc_host_wait_ms_per_step"] = head["ipc_host_wait_ms_per_step"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     # (the pinned origin pool is left to the process exit: unregistering ~141 GB one buffer at a time

@@ -628,6 +628,43 @@ def test_gpu_pull_of_bg4_compressed_world():
     p.close()
 
 
+def test_build_ser_store_is_the_origin():
+    """A compressed build with ser_store writes every chunk serialized in chunk order; a one-rank
+    DevicePuller adopts it as its origin (build_origin is then a no-op) and the bytes equal the
+    origin build_origin makes by compressing again; the pull from it is byte-exact."""
+    from zest_amd.engine import DevicePuller, pinned_take
+    from zest_amd.synthetic import SyntheticWorld
+    dev = torch.device("cuda:0")
+    w = SyntheticWorld("llama-tiny", seed=9, mode="bf16", max_xorb_bytes=1 << 20, compression="bg4")
+    arena = ops.padded_empty(w.arena_bytes, dev)
+    w.generate_on_device(arena)
+    cap, ptr = pinned_take(int(w.model_bytes * 1.002) + (16 << 20))
+    w.build_on_device(arena, ser_store=(ptr, cap))
+    assert w.serialized is not None and w.serialized[2] == int(w.chunk_clen.sum()) + 8 * w.n_chunks
+    want = arena.clone()
+    ref = DevicePuller(w, arena, 0, 1, round_bytes=1 << 20)  # adopts the store
+    assert ref.origin_prebuilt and ref.origin.ptr == ptr and w.serialized is None
+    adopted = ref.origin.array[:ref.origin.n].copy()
+    ref.origin_prebuilt = False
+    ref.origin.array[:] = 0
+    ref.build_origin()  # the old path: compress every chunk again and pack
+    torch.cuda.synchronize()
+    assert np.array_equal(ref.origin.array[:ref.origin.n], adopted)
+    for _ in range(2):
+        arena.fill_(0)
+        ref.err.zero_()
+        ref.step()
+        torch.cuda.synchronize()
+        ref.check()
+        for f in w.xet_files:
+            assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size]), f.path
+    # a ser_store too small for the build fails loudly (before any byte is copied into it)
+    w2 = SyntheticWorld("llama-tiny", seed=9, mode="bf16", max_xorb_bytes=1 << 20, compression="bg4")
+    with pytest.raises(RuntimeError, match="ser_store too small"):
+        w2.build_on_device(arena, ser_store=(ptr, 1 << 16))
+    ref.close()  # the adopted buffer goes back to the pinned pool
+
+
 @pytest.mark.parametrize("compression", ["none", "bg4"])
 def test_device_puller_hip_graph_replay(compression):
     """A whole one-GPU step captured into a HIP graph and replayed: byte-exact arena, the Merkle

@@ -33,6 +33,7 @@ from zest_amd.testing import FakeHub  # noqa: E402
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=int, default=2048, help="repo size (MB of random weights, 4 shards)")
+    ap.add_argument("--shards", type=int, default=4, help="number of weight files the repo is split into")
     ap.add_argument("--out", default=None)
     ap.add_argument("--trace", default=None, help="directory: each leecher writes a ZEST_TRACE Chrome trace there")
     ap.add_argument("--rate-mbps", type=float, default=0.0,
@@ -40,16 +41,16 @@ def main() -> int:
                          "1250 ~ a 10 Gbps LAN peer")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
-    shard = a.mb * 1_000_000 // 4
-    files = {f"model-0000{i}-of-00004.safetensors": rng.integers(0, 256, shard, dtype=np.uint8).tobytes()
-             for i in range(1, 5)}
+    shard = a.mb * 1_000_000 // a.shards
+    files = {f"model-{i:05d}-of-{a.shards:05d}.safetensors": rng.integers(0, 256, shard, dtype=np.uint8).tobytes()
+             for i in range(1, a.shards + 1)}
     files["config.json"] = b'{"model_type": "llama"}'
     total = sum(len(v) for v in files.values())
     hub = FakeHub(policy="none")
     hub.start()
     work = Path(tempfile.mkdtemp(prefix="zest-stripe-"))
     nodes = []
-    res = {"bytes": total, "repo": "org/stripe", "data": "random bytes, 4 Xet shards, raw chunks",
+    res = {"bytes": total, "repo": "org/stripe", "data": f"random bytes, {a.shards} Xet shards, raw chunks",
            "seeder_rate_mbps": a.rate_mbps or None}
     try:
         hub.add_repo("org/stripe", files, xet_min_size=1000)

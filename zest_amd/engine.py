@@ -86,23 +86,40 @@ def release_pinned_pool() -> None:
         H.host_free(_PINNED_POOL.pop()[1])
 
 
+def pinned_take(nbytes: int) -> tuple[int, int]:
+    """(cap, ptr) of pinned host memory of at least nbytes: a pooled buffer, else a new one."""
+    need = max(1, int(nbytes))
+    hit = next((i for i, (cap, _) in enumerate(_PINNED_POOL) if cap >= need), None)
+    if hit is not None:
+        return _PINNED_POOL.pop(hit)
+    release_pinned_pool()  # too small: give the pages back before pinning more
+    return need, ops.hip().host_malloc(need)
+
+
+def pinned_give(cap: int, ptr: int) -> None:
+    """Return a pinned_take buffer to the pool (freed by release_pinned_pool)."""
+    if ptr:
+        _PINNED_POOL.append((int(cap), int(ptr)))
+
+
 class OriginStore:
     """Pinned host memory holding the CDN response bytes for this rank's terms.  `reserve` (bytes)
-    over-allocates so a later store of another world can reuse the same pinned pages."""
+    over-allocates so a later store of another world can reuse the same pinned pages.  `adopt` =
+    (cap, ptr): take over a pinned buffer that already holds the bytes (a world build's
+    serialized store) instead of allocating."""
 
-    def __init__(self, nbytes: int, device: torch.device, reserve: int = 0):
+    def __init__(self, nbytes: int, device: torch.device, reserve: int = 0, adopt=None):
         self.n = int(nbytes)
         self.device = device
         if device.type == "cuda":
             self._H = ops.hip()
             need = max(1, self.n)
-            hit = next((i for i, (cap, _) in enumerate(_PINNED_POOL) if cap >= need), None)
-            if hit is not None:
-                self.cap, self.ptr = _PINNED_POOL.pop(hit)
+            if adopt is not None:
+                self.cap, self.ptr = int(adopt[0]), int(adopt[1])
+                if self.cap < need:
+                    raise ValueError("adopted origin buffer too small")
             else:
-                release_pinned_pool()  # too small: give the pages back before pinning more
-                self.cap = max(need, int(reserve))
-                self.ptr = self._H.host_malloc(self.cap)
+                self.cap, self.ptr = pinned_take(max(need, int(reserve)))
             self.array = np.ctypeslib.as_array((ctypes.c_uint8 * need).from_address(self.ptr))
         else:
             self._H = None
@@ -213,7 +230,17 @@ class DevicePuller:
         a_r, b_r = self.rank_terms[rank]
         ser_len = T["ser_len"][a_r:b_r].astype(np.int64)
         self.term_origin_off = np.concatenate([[0], np.cumsum(ser_len)]).astype(np.int64)  # relative to a_r
-        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device, origin_reserve)
+        # A one-rank origin is every chunk serialized in chunk order: exactly what a compressed world
+        # build leaves in its pinned ser_store, so adopt those bytes instead of compressing again
+        # (the second k_lz4_compress pass was ~40 s of the 70B bench's setup).
+        ser = getattr(world, "serialized", None)
+        adopt = None
+        if (ser is not None and self.is_cuda and a_r == 0 and b_r == len(T)
+                and int(ser[2]) == int(self.term_origin_off[-1])):
+            adopt = (int(ser[1]), int(ser[0]))
+            world.serialized = None
+        self.origin = OriginStore(int(self.term_origin_off[-1]), self.device, origin_reserve, adopt=adopt)
+        self.origin_prebuilt = adopt is not None
         self.rounds: list[RoundWork] = []
         max_span, max_terms, max_chunks = 0, 1, 1
         for k in range(self.n_rounds):
@@ -353,7 +380,7 @@ class DevicePuller:
         w = self.world
         T = w.terms
         a_r, b_r = self.rank_terms[self.rank]
-        if b_r <= a_r:
+        if b_r <= a_r or self.origin_prebuilt:
             return
         if not self.is_cuda:
             raise RuntimeError("CPU worlds build the origin from host contents (build_origin_host)")

@@ -338,6 +338,9 @@ class RoundExchange:
         self.mode = mode
         self.times: dict = {}
         self.bytes_moved = 0          # bytes this rank received through exchange() calls
+        # host time the peer-mapped modes spend on their ready-event wait and host barrier
+        # (the issue path's only host serialization): seconds, and calls
+        self.host_wait_s = {"event": 0.0, "barrier": 0.0, "calls": 0}
         self._gather_cap = int(gather_capacity)
         self._gather_bufs = None
         self._gather_n = 0
@@ -487,8 +490,14 @@ class RoundExchange:
             if ready is None:  # everything queued so far on this rank
                 ready = torch.cuda.Event()
                 ready.record(torch.cuda.current_stream(self.device))
+            t0 = time.perf_counter()
             ready.synchronize()
+            t1 = time.perf_counter()
             dist.barrier(group=self._host_group)
+            hw = self.host_wait_s
+            hw["event"] += t1 - t0
+            hw["barrier"] += time.perf_counter() - t1
+            hw["calls"] += 1
         H = ops.hip()
         recv = [(p, lo, hi) for p, (lo, hi) in enumerate(regions) if p != self.rank and hi > lo]
         if kernel:

@@ -113,7 +113,7 @@ class SyntheticWorld:
             data = arena[f.arena_off + len(f.header):f.arena_off + f.size]
             ops.fill_synthetic(data, f.data_seed, 0, MODES[self.mode])
 
-    def build_on_device(self, arena: torch.Tensor, hash_batch: int = 1 << 20, shard=None) -> None:
+    def build_on_device(self, arena: torch.Tensor, hash_batch: int = 1 << 20, shard=None, ser_store=None) -> None:
         """CDC + chunk hashes + file hashes (+ BG4-LZ4 stored sizes) + xorb/term plan, from content
         already in `arena`.
 
@@ -121,8 +121,18 @@ class SyntheticWorld:
         owns (byte-balanced LPT over the file sizes), then the per-file results (~49 B per chunk:
         offsets, sizes, hashes, stored sizes) are all-gathered, so every rank ends with the same plan
         at ~1/n of the GPU work (bench.py at N > 1; the content itself is regenerated on every rank,
-        which is cheap)."""
+        which is cheap).
+
+        ser_store = (ptr, cap): pinned host memory that receives every chunk serialized the way the
+        CAS serves it ([8-byte header | stored payload], chunk order) straight from this build's
+        compression, so a one-rank origin (whose layout is exactly that: engine.DevicePuller, terms
+        back to back) adopts the bytes instead of compressing every chunk a second time (compressed
+        worlds only; unsharded builds only).  On return `self.serialized` = (ptr, cap, nbytes)."""
         nf = len(self.xet_files)
+        self.serialized = None
+        self._ser_sink = None
+        if ser_store is not None and self.compression == "bg4" and (shard is None or shard[1] == 1):
+            self._ser_sink = [int(ser_store[0]), int(ser_store[1]), 0, None]  # ptr, cap, written, tmp
         if shard is None:
             own = list(range(nf))
         else:
@@ -137,6 +147,10 @@ class SyntheticWorld:
             dist.all_gather_object(objs, per_file, group=shard[2])
             for o in objs:
                 per_file.update(o)
+        if self._ser_sink is not None:
+            ptr, cap, n, _ = self._ser_sink
+            self.serialized = (ptr, cap, n)
+            self._ser_sink = None
         parts = [per_file[i] for i in range(nf)]
         self._set_chunks(np.concatenate([p["offs"] for p in parts]), np.concatenate([p["lens"] for p in parts]),
                          np.concatenate([np.full(len(p["lens"]), i, dtype=np.int32) for i, p in enumerate(parts)]))
@@ -170,12 +184,34 @@ class SyntheticWorld:
             scheme = np.zeros(len(lens), dtype=np.uint8)
             for a in range(0, len(lens), 8192):
                 b = min(len(lens), a + 8192)
-                _, flen = ops.compress_chunks(arena, offs[a:b], lens[a:b], bg4=True)
+                frames, flen = ops.compress_chunks(arena, offs[a:b], lens[a:b], bg4=True)
                 keep = flen > 0
                 clen[a:b][keep] = flen[keep]
                 scheme[a:b][keep] = 2
+                if self._ser_sink is not None:
+                    self._sink_frames(arena, frames, offs[a:b], lens[a:b], clen[a:b], scheme[a:b])
+                del frames
             out["clen"], out["scheme"] = clen, scheme
         return out
+
+    def _sink_frames(self, arena, frames, offs, lens, clen, scheme) -> None:
+        """Serialize one compressed batch ([header | frame or raw chunk] per chunk, compact) on the
+        GPU and append it to the pinned ser_store (D2H)."""
+        ser = clen.astype(np.uint64) + np.uint64(8)
+        total = int(ser.sum())
+        ptr, cap, at, tmp = self._ser_sink
+        if at + total > cap:
+            raise RuntimeError(f"ser_store too small: {at + total} > {cap} bytes")
+        if tmp is None or tmp.numel() < total:
+            tmp = ops.padded_empty(max(total, 1 << 30), arena.device)
+            self._ser_sink[3] = tmp
+        idx = np.arange(len(clen), dtype=np.uint64)
+        addr = np.where(scheme > 0, np.uint64(frames.data_ptr()) + idx * np.uint64(ops.LZ4_SLOT),
+                        np.uint64(arena.data_ptr()) + offs.astype(np.uint64))
+        ops.pack_frames(addr, clen, lens, scheme, (np.cumsum(ser) - ser).astype(np.uint64), tmp)
+        ops.hip().memcpy_async(ptr + at, tmp.data_ptr(), total, torch.cuda.current_stream(arena.device).cuda_stream)
+        torch.cuda.synchronize(arena.device)  # tmp and frames are reused / freed next batch
+        self._ser_sink[2] = at + total
 
     def pack_serialized(self, arena: torch.Tensor, a: int, b: int, out: torch.Tensor, out_off: np.ndarray) -> None:
         """Serialize chunks [a, b) ([8-byte header | stored payload], what the CAS serves) into `out`
