@@ -150,7 +150,7 @@ def test_cli_bench_gpu(tmp_path):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     names = [row["name"] for row in out["results"]]
     assert names == ["blake3_64kb_gpu", "blake3_cdc_gpu", "sha1_info_hash_gpu", "cdc_gpu", "xorb_verify_gpu", "lz4_decode_gpu",
-                     "merkle_gpu", "h2d_pinned_gpu"]
+                     "lz4_decode_gpu_hostidx", "merkle_gpu", "h2d_pinned_gpu"]
     for row in out["results"]:
         assert set(row) == {"name", "runs", "median_ns", "throughput_mbps", "bytes_processed"}
         assert row["median_ns"] > 0 and row["throughput_mbps"] > 0

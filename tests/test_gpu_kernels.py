@@ -594,6 +594,39 @@ def test_gpu_lz4_compress_roundtrip_host_decoder():
         assert gpu_total <= host_total * 1.15, (bg4, gpu_total, host_total)
 
 
+def test_gpu_lz4_compress_staged_matches_v1(monkeypatch):
+    """The default compressor (4-byte tagged table, LDS-staged output) writes exactly the frames of
+    the v1 kernel (8-byte table, direct stores): same hits, same parse, byte-identical frames,
+    across bf16 / low-entropy / random / zero / tiny / 128 KiB chunks and long literal runs."""
+    rng = np.random.default_rng(8)
+    w = (rng.standard_normal(600_000).astype(np.float32) * 0.02)
+    bf16 = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+    parts = [bf16[:65536], bf16[65536:65536 + 131072], rng.integers(0, 8, 70_000, dtype=np.uint8).tobytes(),
+             rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes(), bytes(131072), b"abc" * 9, b"x" * 12,
+             bf16[300_000:300_000 + 8191], rng.integers(0, 256, 3000, dtype=np.uint8).tobytes() * 20,
+             rng.integers(0, 256, 40_000, dtype=np.uint8).tobytes() + bytes(20_000)]
+    parts += [bf16[i * 70_000:i * 70_000 + 70_000] for i in range(8)]
+    blob = b"".join(parts)
+    offs = np.cumsum([0] + [len(p) for p in parts[:-1]]).astype(np.uint64)
+    lens = np.array([len(p) for p in parts], dtype=np.uint32)
+    buf = ops.padded_empty(len(blob), DEV)
+    buf.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+    for bg4 in (True, False):
+        monkeypatch.delenv("ZG_COMPRESS", raising=False)
+        f2, l2 = ops.compress_chunks(buf, offs, lens, bg4=bg4)
+        monkeypatch.setenv("ZG_COMPRESS", "v1")
+        f1, l1 = ops.compress_chunks(buf, offs, lens, bg4=bg4)
+        assert np.array_equal(l1, l2), (bg4, l1, l2)
+        h1, h2 = f1.cpu().numpy(), f2.cpu().numpy()
+        for i in range(len(parts)):
+            a = i * ops.LZ4_SLOT
+            assert np.array_equal(h1[a:a + int(l1[i])], h2[a:a + int(l2[i])]), (bg4, i)
+            if l2[i]:
+                fr = h2[a:a + int(l2[i])].tobytes()
+                assert C.decompress_chunk(2 if bg4 else 1, fr, len(parts[i])) == parts[i], (bg4, i)
+    monkeypatch.delenv("ZG_COMPRESS", raising=False)
+
+
 def test_gpu_pull_of_bg4_compressed_world():
     """End to end on the decode path: a bf16 world whose chunks are BG4-LZ4 frames compressed on
     the GPU (as Xet stores checkpoints) is pulled by the device engine (header walk -> LZ4/BG4 decode

@@ -16,6 +16,7 @@
 #   ipc         peer-mapped arena tests (tests/test_gpu_ipc.py)
 #   cli         `zest pull --gpus 1` vs host `zest pull` (Llama-3.1-8B from an HBM seeder, sync between)
 #   stripe      host pull from 1 vs 3 loopback seeders
+#   pin         $PIN_PROCS processes pinning $PIN_GB GB each at once (the N=8 origin setup)
 #   seed        HBM seeding throughput (Mixtral-8x7B, chunks_served/s)
 #   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group, e.g. k3pair)
 #   prof        rocprofv3 --kernel-trace --stats of the 70B bench -> per-kernel summary (markdown)
@@ -62,6 +63,9 @@ for step in "$@"; do
     cli) timeout -k 10 700 python -u tools/direct_bench.py --model llama-3.1-8b --skip-direct --host-after \
            --out $OUT/cli_vs_host.json > $log 2>&1 || fail $step $? $log
          grep -h "^\[" $log ;;
+    pin) timeout -k 10 500 python -u tools/pin_bench.py --procs ${PIN_PROCS:-8} --gb ${PIN_GB:-17.6} \
+           --out $OUT/pin_${PIN_PROCS:-8}x${PIN_GB:-17.6}.json > $log 2>&1 || fail $step $? $log
+         tail -1 $log | cut -c1-400 ;;
     stripe) mkdir -p $OUT/stripe_trace
             timeout -k 10 600 python -u tools/stripe_bench.py --mb ${STRIPE_MB:-4096} ${STRIPE_ARGS:-} \
               --trace $OUT/stripe_trace --out $OUT/stripe.json > $log 2>&1 \

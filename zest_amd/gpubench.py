@@ -11,6 +11,10 @@ row per kernel, in that schema (median over `runs` launches; throughput = bytes 
   cdc_gpu              GearHash CDC boundary candidates (K5)
   xorb_verify_gpu      header walk + placement + BLAKE3 of uncompressed xorb runs (K4 fused ingest)
   lz4_decode_gpu       the same for BG4-LZ4 bf16 weights (K3 batched decoder + K1)
+  lz4_decode_gpu_hostidx  the same batch the way the public device path (DeviceXetPull) runs it:
+                       chunk records come from the header index the fetch workers build while
+                       validating each run (host, outside the timed region), so the device work is
+                       the records' H2D upload + decode + fused place/hash -- no device header walk
   merkle_gpu           Xet Merkle file hashes over 8 x 80k leaves (K2)
   h2d_pinned_gpu       pinned host -> HBM copy (the ingest ceiling of a one-GPU pull)
   rccl_allgather_xorb  (N ranks) RCCL all-gather of 64 MiB xorb slabs over xGMI, bytes received
@@ -145,6 +149,8 @@ def run(mib: int = 1024, runs: int = 5, device="cuda:0") -> list[dict]:
         if dst[:len(raw)].cpu().numpy().tobytes() != raw:
             raise RuntimeError(f"{name}: decoded bytes differ from the input")
         rows.append(_row(name, runs, ns, len(raw)))
+        if comp:
+            rows.append(_hostidx_row(H, st, blob, raw, terms, nck, src, dst, hashes, ws, runs))
         del src, dst, hashes, ws
 
     nl = 80_000
@@ -171,6 +177,34 @@ def run(mib: int = 1024, runs: int = 5, device="cuda:0") -> list[dict]:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         rows.append(_row("rccl_allgather_xorb", runs, float(t.item()), (world - 1) * slab))
     return rows
+
+
+def _hostidx_row(H, st, blob, raw, terms, nck, src, dst, hashes, ws, runs) -> dict:
+    """lz4_decode_gpu_hostidx: records from the host header walk (_core.index_runs over the runs in
+    pinned memory, as DeviceXetPull's fetch workers produce them), then per launch: records H2D +
+    fused decode/place/hash.  Checked byte-exact and hash-equal to the device-walk row."""
+    want = hashes.clone()
+    pin = torch.frombuffer(bytearray(blob), dtype=torch.uint8).pin_memory()
+    nrec = nck * ops.CHUNK_DTYPE.itemsize
+    rec = torch.empty(nrec, dtype=torch.uint8).pin_memory()
+    th = np.ascontiguousarray(terms, dtype=ops.TERM_DTYPE)
+    e = _core.index_runs(pin.data_ptr(), len(blob), th.ctypes.data, len(th), rec.data_ptr(), nck)
+    if e:
+        raise RuntimeError(f"lz4_decode_gpu_hostidx: host header walk failed ({e:#x})")
+    sp, sb = ws.hash_scratch.get(nck, len(raw))
+
+    def launch():
+        H.memcpy_async(ws.chunks.data_ptr(), rec.data_ptr(), nrec, st)
+        H.ingest_chunks(src.data_ptr(), len(blob), dst.data_ptr(), dst.numel(), ws.chunks.data_ptr(), nck, True,
+                        ws.err.data_ptr(), hashes.data_ptr(), 0, 0, st, sp, sb)
+    dst.zero_()
+    hashes.zero_()
+    ws.err.zero_()
+    ns = _time(launch, runs)
+    ops.raise_on_error(ws.err)
+    if dst[:len(raw)].cpu().numpy().tobytes() != raw or not torch.equal(hashes, want):
+        raise RuntimeError("lz4_decode_gpu_hostidx: result differs from the device-walk ingest")
+    return _row("lz4_decode_gpu_hostidx", runs, ns, len(raw))
 
 
 def _bf16(nbytes: int) -> bytes:
