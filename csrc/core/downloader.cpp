@@ -7,7 +7,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <optional>
 #include <thread>
@@ -53,6 +55,46 @@ void pwrite_all(int fd, const uint8_t* p, size_t n, uint64_t off) {
     n -= size_t(w);
     off += uint64_t(w);
   }
+}
+
+// Run fn(part) for part in [0, parts) on parts - 1 extra threads + the caller; rethrows the first
+// exception.  Used inside one term: when the swarm's last terms land together (striped peers finish
+// at the same moment), their decode/hash/write is the whole tail of a pull, and one thread per term
+// leaves the other cores idle.
+template <class F>
+void run_parts(int parts, F&& fn) {
+  if (parts <= 1) {
+    fn(0);
+    return;
+  }
+  std::vector<std::exception_ptr> errs(static_cast<size_t>(parts));
+  std::vector<std::thread> ts;
+  for (int k = 1; k < parts; ++k)
+    ts.emplace_back([&, k] {
+      try {
+        fn(k);
+      } catch (...) {
+        errs[size_t(k)] = std::current_exception();
+      }
+    });
+  try {
+    fn(0);
+  } catch (...) {
+    errs[0] = std::current_exception();
+  }
+  for (auto& t : ts) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
+// Threads per large term (ZEST_TERM_THREADS, default 4; terms under 128 chunks use one).
+int term_threads(size_t chunks) {
+  static const int n = [] {
+    const char* e = std::getenv("ZEST_TERM_THREADS");
+    const int v = e ? std::atoi(e) : 4;
+    return std::max(1, std::min(v, 16));
+  }();
+  return chunks >= 128 ? std::min<int>(n, int(chunks / 64)) : 1;
 }
 
 // pwritev of the whole list (IOV_MAX-sized batches, partial writes resumed).
@@ -201,32 +243,40 @@ FileResult ParallelDownloader::reconstruct(const std::string& hex, const std::st
     std::vector<iovec> iov;
     Bytes dec;
     uint64_t total = 0;
+    int parts = 1;
     {
       trace::Span sp("download", "decode+hash");
       const auto idx = xet::index_chunks(f.bytes(), f.size());
       if (f.local_start > f.local_end || f.local_end > idx.size()) throw Error("RangeOutOfBounds");
-      uint64_t dec_bytes = 0;
-      for (uint32_t c = f.local_start; c < f.local_end; ++c)
-        if (idx[c].scheme != xet::Scheme::None) dec_bytes += idx[c].ulen;
-      dec.resize(dec_bytes);
-      uint8_t* dp = dec.data();
-      hs.reserve(f.local_end - f.local_start);
-      iov.reserve(f.local_end - f.local_start);
-      for (uint32_t c = f.local_start; c < f.local_end; ++c) {
-        const xet::ChunkEntry& e = idx[c];
-        const uint8_t* payload = f.bytes() + e.header_off + xet::kChunkHeaderLen;
-        const uint8_t* p = payload;
-        if (e.scheme != xet::Scheme::None) {
-          xet::decompress_chunk(e.scheme, payload, e.clen, dp, e.ulen);
-          p = dp;
-          dp += e.ulen;
-        } else if (e.clen != e.ulen) {
-          throw Error("CorruptChunk", "stored chunk length mismatch");
-        }
-        hs.push_back({xet::chunk_hash(p, e.ulen), e.ulen});
-        iov.push_back({const_cast<uint8_t*>(p), e.ulen});
+      const size_t nc = f.local_end - f.local_start;
+      // each compressed chunk's place in the decode buffer (prefix sum), so parts decode independently
+      std::vector<uint64_t> dpos(nc + 1, 0);
+      for (size_t k = 0; k < nc; ++k) {
+        const xet::ChunkEntry& e = idx[f.local_start + k];
+        dpos[k + 1] = dpos[k] + (e.scheme != xet::Scheme::None ? e.ulen : 0);
         total += e.ulen;
       }
+      dec.resize(dpos[nc]);
+      hs.resize(nc);
+      iov.resize(nc);
+      parts = term_threads(nc);
+      sp.arg("\"threads\":" + std::to_string(parts));
+      run_parts(parts, [&](int part) {
+        for (size_t k = nc * size_t(part) / size_t(parts); k < nc * size_t(part + 1) / size_t(parts); ++k) {
+          const xet::ChunkEntry& e = idx[f.local_start + k];
+          const uint8_t* payload = f.bytes() + e.header_off + xet::kChunkHeaderLen;
+          const uint8_t* p = payload;
+          if (e.scheme != xet::Scheme::None) {
+            uint8_t* dp = dec.data() + dpos[k];
+            xet::decompress_chunk(e.scheme, payload, e.clen, dp, e.ulen);
+            p = dp;
+          } else if (e.clen != e.ulen) {
+            throw Error("CorruptChunk", "stored chunk length mismatch");
+          }
+          hs[k] = {xet::chunk_hash(p, e.ulen), e.ulen};
+          iov[k] = {const_cast<uint8_t*>(p), e.ulen};
+        }
+      });
     }
     if (total != t.unpacked_length) throw Error("SizeMismatch", "term " + std::to_string(i));
     uint64_t off = offs[i];
@@ -253,7 +303,18 @@ FileResult ParallelDownloader::reconstruct(const std::string& hex, const std::st
       trace::Span sp("download", "pwrite");
       uint64_t n = 0;
       for (const iovec& v : iov) n += v.iov_len;
-      pwritev_all(fd, iov, off - skip);
+      // the term's chunks in `parts` contiguous groups, written concurrently at their own offsets
+      const int wp = std::min<int>(parts, int(iov.size()));
+      std::vector<uint64_t> at(size_t(wp) + 1, off - skip);
+      std::vector<std::vector<iovec>> groups(static_cast<size_t>(wp));
+      for (int g = 0; g < wp; ++g) {
+        const size_t a = iov.size() * size_t(g) / size_t(wp), b = iov.size() * size_t(g + 1) / size_t(wp);
+        groups[size_t(g)].assign(iov.begin() + long(a), iov.begin() + long(b));
+        uint64_t len = 0;
+        for (size_t k = a; k < b; ++k) len += iov[k].iov_len;
+        at[size_t(g) + 1] = at[size_t(g)] + len;
+      }
+      if (wp > 0) run_parts(wp, [&](int g) { pwritev_all(fd, groups[size_t(g)], at[size_t(g)]); });
       storage::start_writeback(fd, off - skip, n);
     }
     hashes[i] = std::move(hs);

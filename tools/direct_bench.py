@@ -35,6 +35,9 @@ from zest_amd.testing import FakeHub  # noqa: E402
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama-3.1-8b")
+    ap.add_argument("--mode", default="random", choices=["random", "bf16"],
+                    help="bf16: N(0,0.02) bf16 weights stored as BG4-LZ4 frames, as Xet stores checkpoints "
+                         "(the host path decodes them on the CPU, the GPU paths on the device)")
     ap.add_argument("--skip-host", action="store_true")
     ap.add_argument("--skip-gpu-cli", action="store_true")
     ap.add_argument("--skip-direct", action="store_true")
@@ -50,7 +53,7 @@ def main() -> int:
     dev = torch.device("cuda:0")
     spec = models.get(a.model)
     t0 = time.time()
-    world = SyntheticWorld(spec, seed=5)
+    world = SyntheticWorld(spec, seed=5, mode=a.mode, compression="bg4" if a.mode == "bf16" else "none")
     content = ops.padded_empty(world.arena_bytes, dev)
     world.generate_on_device(content)
     world.build_on_device(content)
@@ -69,7 +72,9 @@ def main() -> int:
     peer = f"127.0.0.1:{srv.port}"
     res = {"model": a.model, "repo": spec.repo_id, "bytes": total, "chunks": world.n_chunks, "xorbs": world.n_xorbs,
            "source": "HBM seeder over BEP XET (loopback TCP)",
-           "data": "synthetic random-byte weights, real tensor shapes"}
+           "data": ("synthetic random-byte weights, real tensor shapes" if a.mode == "random" else
+                    "synthetic N(0,0.02) bf16 weights, real tensor shapes, BG4-LZ4 frames (stored/raw "
+                    f"{float(world.chunk_clen.sum()) / float(world.chunk_len.sum()):.3f})")}
     try:
         if not a.skip_direct:
             # warm-up on the smallest Xet file (connections, allocator, kernels)

@@ -61,7 +61,7 @@ for step in "$@"; do
     ipc) timeout -k 10 400 $PYT -v tests/test_gpu_ipc.py > $log 2>&1 || fail $step $? $log
          grep -E "PASSED|FAILED|SKIPPED" $log ;;
     cli) timeout -k 10 700 python -u tools/direct_bench.py --model llama-3.1-8b --skip-direct --host-after \
-           --out $OUT/cli_vs_host.json > $log 2>&1 || fail $step $? $log
+           --mode ${CLI_MODE:-random} --out $OUT/cli_vs_host_${CLI_MODE:-random}.json > $log 2>&1 || fail $step $? $log
          grep -h "^\[" $log ;;
     pin) timeout -k 10 500 python -u tools/pin_bench.py --procs ${PIN_PROCS:-8} --gb ${PIN_GB:-17.6} \
            --out $OUT/pin_${PIN_PROCS:-8}x${PIN_GB:-17.6}.json > $log 2>&1 || fail $step $? $log
