@@ -35,6 +35,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 BASELINE_METRIC = "aggregate pull GB/s + P2P ratio, Llama-3.1-70B at 1/2/4/8 MI355X peers"
@@ -55,7 +56,7 @@ MODES = ("bf16", "random")
 # to RCCL.  ZEST_EXCHANGE_IPC=0 turns it off.
 IPC_AUTO = "1"
 PHASE_LIMITS = {"init": 180, "setup": 420, "ipc": 90, "autotune": 180, "warmup": 240, "timed": 420,
-                "report": 120}
+                "report": 120, "swarm_setup": 180, "swarm_warmup": 300, "swarm_timed": 300, "swarm_report": 120}
 
 
 def log(rank, *a):
@@ -86,7 +87,8 @@ def parse_args(argv=None):
                     help="also time the PUBLIC path, zest_amd.parallel.swarm_pull (= pull(device='all')), on the "
                          "last data mode's world, its CDN served from the same pinned origin through an "
                          "in-process memory CAS (mem:// fetch_info URLs, no sockets); reported under "
-                         "extra.swarm_pull_*.  auto: on for one GPU")
+                         "extra.swarm_pull_*.  auto: on for GPU runs (at N > 1 a failure or overrun of the row is "
+                         "recorded in extra.swarm_pull_error and never costs the headline line)")
     ap.add_argument("--swarm-steps", type=int, default=2)
     ap.add_argument("--swarm-warmup", type=int, default=1)
     a = ap.parse_args(argv)
@@ -147,21 +149,48 @@ class Watchdog:
         self.override = float(v) if v not in ("", "0") else None
         self.enabled = (enabled and v != "0") or self.override is not None
         self.rank = rank
+        # Set while an optional row runs after the headline is measured (the N > 1 swarm row): a
+        # phase that overruns then calls fallback(reason) -- rank 0 prints the headline line with the
+        # row marked failed -- and the rank exits 0, instead of losing the headline with the row.
+        self.fallback = None
+        self._timer = None
+
+    def _cancel(self) -> None:
+        import faulthandler
+        faulthandler.cancel_dump_traceback_later()
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+
+    def _expire(self, phase: str, limit: float) -> None:
+        import faulthandler
+        print(f"[bench] watchdog: phase {phase} exceeded {limit:.0f}s; stacks follow", file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        try:
+            self.fallback(f"phase {phase} exceeded {limit:.0f}s")
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
 
     def arm(self, phase: str) -> None:
         if self.enabled:
             import faulthandler
             limit = self.override or PHASE_LIMITS[phase]
-            faulthandler.cancel_dump_traceback_later()
+            self._cancel()
             log(self.rank, f"watchdog: phase {phase}, {limit:.0f}s")
-            faulthandler.dump_traceback_later(limit, exit=True)
+            if self.fallback is None:
+                faulthandler.dump_traceback_later(limit, exit=True)
+            else:
+                self._timer = threading.Timer(limit, self._expire, args=(phase, limit))
+                self._timer.daemon = True
+                self._timer.start()
         if os.environ.get("ZEST_BENCH_FAULT") == f"hang:{self.rank}:{phase}":  # fault injection (tests)
             time.sleep(1e9)
 
     def disarm(self) -> None:
         if self.enabled:
-            import faulthandler
-            faulthandler.cancel_dump_traceback_later()
+            self._cancel()
 
 
 # ------------------------------------------------------------------------------------------------
@@ -404,7 +433,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
 
     world, puller = keep["world"], keep["puller"]
     cuda = device.type == "cuda"
-    wd.arm("setup")
+    wd.arm("swarm_setup")
     t_setup = time.time()
     # the engine's device buffers go first: the swarm pull allocates its own 141 GB arena
     puller.release_device()
@@ -445,12 +474,12 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         del out
         return n
 
-    wd.arm("warmup")
+    wd.arm("swarm_warmup")
     t_w = time.time()
     for _ in range(a.swarm_warmup):
         one({})
     warm_s = time.time() - t_w
-    wd.arm("timed")
+    wd.arm("swarm_timed")
     from zest_amd import _core
     _core.trace.roctx_push("swarm_pull timed")  # (ZEST_ROCTX=1: the window of tools/gpu/overlap.py --marker)
     mark = cuda and os.environ.get("ZEST_BENCH_MARK") == "1"
@@ -478,7 +507,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     if world_size > 1:
         tdist.all_reduce(el, op=tdist.ReduceOp.MAX)  # every step at its slowest rank
         tdist.all_reduce(rx)
-    wd.arm("report")
+    wd.arm("swarm_report")
     log(rank, f"[swarm_pull] world {st.get('world')} fetched {st.get('fetched_bytes')} received "
               f"{st.get('received_bytes')} items {st.get('items')} rounds {st.get('rounds')} exchange {st.get('exchange')}")
     times = el.cpu().tolist()
@@ -597,7 +626,7 @@ def rank_main(a) -> None:
     spec = models.get(a.model)
     results, pick, arenas = [], None, {}
     # (CPU rehearsals run it only when asked: --swarm-row on)
-    swarm_row = ((a.swarm_row == "auto" and world_size == 1 and cuda) or a.swarm_row == "on") and a.seeders in (0, world_size)
+    swarm_row = ((a.swarm_row == "auto" and cuda) or a.swarm_row == "on") and a.seeders in (0, world_size)
     keep = {} if swarm_row else None
     for i, mode in enumerate(a.modes):
         last = i == len(a.modes) - 1
@@ -607,17 +636,6 @@ def rank_main(a) -> None:
         log(rank, f"[{mode}] {r['value']:.3f} GB/s aggregate, {r['step_s'] * 1e3:.1f} ms/step, "
                   f"exchange {r['exchange']}")
         results.append(r)
-    swarm = {}
-    if keep:
-        keep["mode"] = results[-1]["mode"]
-        keep["arena"] = arenas.pop("arena", None)
-        arenas.clear()
-        keep.pop("arena", None)
-        swarm = run_swarm_row(a, keep, device, rank, world_size, dist, wd)
-        log(rank, f"[swarm_pull {keep['mode']}] {swarm['swarm_pull_GBps']:.3f} GB/s aggregate, "
-                  f"{swarm['swarm_pull_ms_per_step']:.1f} ms/step (public path, memory CAS)")
-        keep["puller"].close()
-        keep.clear()
     head = results[0]
     seeders = head["seeders"]
     out = {
@@ -638,7 +656,7 @@ def rank_main(a) -> None:
         "extra": {f"{r['mode']}_GBps": round(r["value"], 3) for r in results}
         | {f"{r['mode']}_ms_per_step": round(r["step_s"] * 1e3, 3) for r in results}
         | {f"{r['mode']}_p2p_ratio": round(r["p2p_ratio"], 4) for r in results}
-        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results} | swarm,
+        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results},
         "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,
                    "parallelism": (f"swarm{world_size}" if seeders == world_size
                                    else f"seed{seeders}-leech{world_size - seeders}"),
@@ -656,8 +674,37 @@ def rank_main(a) -> None:
     }
     if "ipc_host_wait_ms_per_step" in head:
         out["extra"]["ipc_host_wait_ms_per_step"] = head["ipc_host_wait_ms_per_step"]
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    printed = [False]
+
+    def emit(extra_fields: dict) -> None:  # the one JSON line, printed once by rank 0
+        if rank == 0 and not printed[0]:
+            printed[0] = True
+            print(json.dumps(out | {"extra": out["extra"] | extra_fields}), flush=True)
+
+    if keep:
+        # The public-path row runs after the headline is measured.  At N > 1 it must not cost the
+        # headline: an exception is recorded in extra.swarm_pull_error, and a phase that overruns its
+        # deadline prints the headline line with the row marked failed and exits 0 (Watchdog.fallback).
+        keep["mode"] = results[-1]["mode"]
+        keep["arena"] = arenas.pop("arena", None)
+        arenas.clear()
+        keep.pop("arena", None)
+        if world_size > 1:
+            wd.fallback = lambda reason: emit({"swarm_pull_error": reason})
+        try:
+            swarm = run_swarm_row(a, keep, device, rank, world_size, dist, wd)
+            log(rank, f"[swarm_pull {keep['mode']}] {swarm['swarm_pull_GBps']:.3f} GB/s aggregate, "
+                      f"{swarm['swarm_pull_ms_per_step']:.1f} ms/step (public path, memory CAS)")
+        except Exception as e:  # noqa: BLE001 - the headline stands without the row
+            if world_size == 1:
+                raise
+            swarm = {"swarm_pull_error": f"{type(e).__name__}: {e}"[:400]}
+            log(rank, f"[swarm_pull] failed: {swarm['swarm_pull_error']}")
+        out["extra"].update(swarm)
+        keep["puller"].close()
+        keep.clear()
+        wd.arm("report")
+    emit({})
     # (the pinned origin pool is left to the process exit: unregistering ~141 GB one buffer at a time
     # only delays it)
     if dist is not None:

@@ -97,3 +97,29 @@ def test_bench_swarm_row_times_the_public_path(gpus):
     assert ex["swarm_pull_fetch"]["bytes_from_cdn"] > 0 and not ex["swarm_pull_fetch"]["bytes_from_peer"]
     if gpus > 1:
         assert ex["swarm_pull_p2p_ratio"] > 0.3 and ex["swarm_pull_exchange"] in ("bcast", "allgather", "p2p")
+
+
+def test_bench_swarm_row_multi_file_three_ranks():
+    """Three ranks on a 10-file model: the swarm row's term split matches the engine's per-rank
+    origin shares (every rank's CDN fetches are served by its own memory CAS)."""
+    p, _ = _run(["--gpus", "3", "--steps", "1", "--warmup", "1", "--modes", "random", "--swarm-row", "on",
+                 "--swarm-steps", "1", "--swarm-warmup", "1", "--model", "llama-tiny-sharded"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    ex = lines[0]["extra"]
+    assert "swarm_pull_error" not in ex and ex["swarm_pull_GBps"] > 0
+    assert ex["swarm_pull_p2p_ratio"] > 0.5  # each rank received the other two thirds
+
+
+def test_bench_swarm_row_overrun_keeps_the_headline():
+    """A rank that hangs inside the swarm row (after the headline was measured): the row's deadline
+    prints the headline line once, with extra.swarm_pull_error, and every rank exits 0."""
+    p, dt = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--modes", "random", "--swarm-row", "on",
+                  "--swarm-steps", "1", "--swarm-warmup", "1"],
+                 env_extra={"ZEST_BENCH_FAULT": "hang:1:swarm_timed", "ZEST_BENCH_WATCHDOG": "25"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["value"] > 0 and "swarm_timed" in lines[0]["extra"]["swarm_pull_error"]
+    assert "swarm_pull_GBps" not in lines[0]["extra"]

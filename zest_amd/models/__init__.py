@@ -222,6 +222,11 @@ def get(name: str) -> ModelSpec:
     if key in ("llama-tiny", "synthetic/llama-tiny"):
         return _llama_like("synthetic/llama-tiny", hidden=256, inter=512, layers=2, heads=4, kv_heads=2, vocab=1024,
                            max_pos=512)
+    if key in ("llama-tiny-sharded", "synthetic/llama-tiny-sharded"):  # several files / terms (multi-rank tests)
+        spec = _llama_like("synthetic/llama-tiny-sharded", hidden=256, inter=512, layers=4, heads=4, kv_heads=2,
+                           vocab=1024, max_pos=512)
+        spec.max_shard_bytes = 700_000
+        return spec
     if key in ("qwen2-7b", "qwen/qwen2-7b"):
         return _llama_like("Qwen/Qwen2-7B", hidden=3584, inter=18944, layers=28, heads=28, kv_heads=4, vocab=152064,
                            bias=True, arch="Qwen2ForCausalLM", model_type="qwen2", rope_theta=1e6, max_pos=131072)
