@@ -122,6 +122,38 @@ def test_pull_compression_policies(policy, nodes, tmp_path):
         h.stop()
 
 
+@pytest.mark.parametrize("policy", ["none", "bg4"])
+def test_pull_large_terms_split_over_threads(policy, tmp_path):
+    """Terms of >= 128 chunks are decoded, hashed and written by several threads
+    (ZEST_TERM_THREADS): byte-exact snapshots from the CDN and from a peer (quarantined runs)."""
+    import numpy as np
+    h = FakeHub(policy=policy, max_xorb_bytes=64 << 20)
+    h.start()
+    made = []
+    try:
+        rng = np.random.default_rng(4)
+        w = (rng.standard_normal(6_000_000).astype(np.float32) * 0.02)
+        files = {"config.json": b'{"model_type": "llama"}',
+                 "model.safetensors": (w.view(np.uint32) >> 16).astype(np.uint16).tobytes(),  # 12 MB bf16
+                 "other.bin": rng.integers(0, 256, 10_000_003, dtype=np.uint8).tobytes()}
+        commit = h.add_repo(REPO_ID, files, xet_min_size=100_000)
+        env = {"ZEST_TERM_THREADS": "4"}
+        a = Node(h, tmp_path, "a")
+        b = Node(h, tmp_path, "b")
+        made += [a, b]
+        a.run("pull", REPO_ID, "--no-p2p", env=env)
+        assert_snapshot(a, REPO_ID, commit, files)
+        a.spawn("serve", "--listen-port", str(a.listen_port), "--http-port", str(a.http_port))
+        a.wait_healthy()
+        out = b.run("pull", REPO_ID, "--peer", f"127.0.0.1:{a.listen_port}", "--no-dht", env=env).stdout
+        assert p2p_ratio(out) == 100.0
+        assert_snapshot(b, REPO_ID, commit, files)
+    finally:
+        for n in made:
+            n.close()
+        h.stop()
+
+
 def test_pull_revision_and_dedup(hub, nodes):
     files = sample_files()
     c1 = hub.add_repo(REPO_ID, files, xet_min_size=100_000)
