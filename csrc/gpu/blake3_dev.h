@@ -222,4 +222,68 @@ __device__ __forceinline__ void parent_cv(const uint32_t l[8], const uint32_t r[
   compress(out, m, 0, 64, mode_flags | PARENT | (root ? ROOT : 0));
 }
 
+// One wave hashes one Xet chunk (<= 128 KiB): lane l owns BLAKE3 chunks l, l + 64; chaining values
+// are merged pairwise in `cvs` (LDS, 8 words per BLAKE3 chunk, 4 KiB for 128 of them) --
+// pairwise-with-carry is BLAKE3's left-complete tree.  K1's latency path (k_hash_chunks) and the
+// fused hash at the end of the LZ4 pair decoder (lz4seq.hip).
+__device__ inline void wave_hash(const uint8_t* base, uint32_t len, const Key8& key, uint32_t mode, uint32_t* cvs,
+                          uint32_t lane, uint32_t out[8]) {
+  const uint32_t nb = len == 0 ? 1 : (len + 1023) >> 10;
+  if (nb == 1) {
+    uint32_t cv[8];
+    if (lane == 0) hash_chunk(base, len, 0, key, mode, true, cv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = __builtin_amdgcn_readfirstlane(cv[i]);
+    return;
+  }
+  for (uint32_t b = lane; b < nb; b += 64) {
+    const uint32_t seg = len - (b << 10) < 1024 ? len - (b << 10) : 1024;
+    uint32_t cv[8];
+    hash_chunk(base + (size_t(b) << 10), seg, b, key, mode, false, cv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cvs[8 * b + i] = cv[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t m = nb;
+  while (m > 2) {
+    const uint32_t pairs = m >> 1;
+    for (uint32_t i = lane; i < pairs; i += 64) {
+      uint32_t l[8], r[8], o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        l[k] = cvs[16 * i + k];
+        r[k] = cvs[16 * i + 8 + k];
+      }
+      parent_cv(l, r, key, mode, false, o);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cvs[8 * i + k] = o[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (m & 1) {
+      if (lane < 8) cvs[8 * pairs + lane] = cvs[8 * (m - 1) + lane];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    m = pairs + (m & 1);
+  }
+  uint32_t l[8], r[8], o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    l[k] = cvs[k];
+    r[k] = cvs[8 + k];
+  }
+  parent_cv(l, r, key, mode, true, o);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = o[k];
+}
+
+__device__ __forceinline__ void store_hash(uint8_t* dst, const uint32_t h[8], uint32_t lane) {
+  if (lane < 8) reinterpret_cast<uint32_t*>(dst)[lane] = h[0] * (lane == 0) + h[1] * (lane == 1) + h[2] * (lane == 2) +
+                                                          h[3] * (lane == 3) + h[4] * (lane == 4) + h[5] * (lane == 5) +
+                                                          h[6] * (lane == 6) + h[7] * (lane == 7);
+}
+
 }  // namespace zg

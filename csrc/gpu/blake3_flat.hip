@@ -122,6 +122,7 @@ struct PlaceSrc {
   uint8_t* dst;
   uint64_t dst_n;
   unsigned long long* err;
+  int skip_compressed = 0;  // the LZ4 decoder already hashed the compressed chunks (zg_lz4_decode_ingest)
   static constexpr bool kBadIsFF = false;
   static constexpr bool kPlace = true;
   __device__ __forceinline__ bool raw_ok(const ZgChunk& ch) const {
@@ -153,6 +154,8 @@ __device__ __forceinline__ uint32_t n_leaves(const Src& s, int c) {
     // as empty leaves, so its chunk hash -- and the file's Merkle check -- fails as it should.
     len = s.chunks[c].ulen;
     if (len > kMaxChunk) len = 0;
+    // a chunk with no leaves gets no hash written at all (k_hash_tree skips it)
+    if (s.skip_compressed && s.chunks[c].scheme != 0) return 0u;
   } else {
     const uint8_t* p;
     bool bad;
@@ -419,6 +422,13 @@ hipError_t zg_place_hash_flat(const uint8_t* src, uint64_t src_n, uint8_t* dst, 
                               size_t scratch_bytes, hipStream_t stream) {
   return launch_flat(PlaceSrc{chunks, src, src_n, dst, dst_n, err}, n_chunks, 0, hashes, sizes, scratch, scratch_bytes,
                      stream);
+}
+
+hipError_t zg_place_hash_flat_raw(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                  const ZgChunk* chunks, int n_chunks, unsigned long long* err, uint8_t* hashes,
+                                  uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream) {
+  return launch_flat(PlaceSrc{chunks, src, src_n, dst, dst_n, err, 1}, n_chunks, 0, hashes, sizes, scratch,
+                     scratch_bytes, stream);
 }
 
 hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n,

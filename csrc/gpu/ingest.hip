@@ -674,65 +674,8 @@ __global__ void __launch_bounds__(256, RB <= 4096 ? 8 : 5) k_decode_lz4(const ui
 // lane l owns BLAKE3 chunks l, l+64 (<= 128 for a 128 KiB Xet chunk); chaining values are merged
 // pairwise in LDS (pairwise-with-carry == BLAKE3's left-complete tree).
 // --------------------------------------------------------------------------------------------
-__device__ void wave_hash(const uint8_t* base, uint32_t len, const zg::Key8& key, uint32_t mode, uint32_t* cvs,
-                          uint32_t lane, uint32_t out[8]) {
-  const uint32_t nb = len == 0 ? 1 : (len + 1023) >> 10;
-  if (nb == 1) {
-    uint32_t cv[8];
-    if (lane == 0) zg::hash_chunk(base, len, 0, key, mode, true, cv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) out[i] = __builtin_amdgcn_readfirstlane(cv[i]);
-    return;
-  }
-  for (uint32_t b = lane; b < nb; b += kWave) {
-    const uint32_t seg = len - (b << 10) < 1024 ? len - (b << 10) : 1024;
-    uint32_t cv[8];
-    zg::hash_chunk(base + (size_t(b) << 10), seg, b, key, mode, false, cv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) cvs[8 * b + i] = cv[i];
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t m = nb;
-  while (m > 2) {
-    const uint32_t pairs = m >> 1;
-    for (uint32_t i = lane; i < pairs; i += kWave) {
-      uint32_t l[8], r[8], o[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        l[k] = cvs[16 * i + k];
-        r[k] = cvs[16 * i + 8 + k];
-      }
-      zg::parent_cv(l, r, key, mode, false, o);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int k = 0; k < 8; ++k) cvs[8 * i + k] = o[k];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (m & 1) {
-      if (lane < 8) cvs[8 * pairs + lane] = cvs[8 * (m - 1) + lane];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-    m = pairs + (m & 1);
-  }
-  uint32_t l[8], r[8], o[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    l[k] = cvs[k];
-    r[k] = cvs[8 + k];
-  }
-  zg::parent_cv(l, r, key, mode, true, o);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) out[k] = o[k];
-}
-
-__device__ __forceinline__ void store_hash(uint8_t* dst, const uint32_t h[8], uint32_t lane) {
-  if (lane < 8) reinterpret_cast<uint32_t*>(dst)[lane] = h[0] * (lane == 0) + h[1] * (lane == 1) + h[2] * (lane == 2) +
-                                                          h[3] * (lane == 3) + h[4] * (lane == 4) + h[5] * (lane == 5) +
-                                                          h[6] * (lane == 6) + h[7] * (lane == 7);
-}
+using zg::store_hash;
+using zg::wave_hash;
 
 __global__ void __launch_bounds__(256) k_hash_chunks(const uint8_t* __restrict__ dst, const ZgChunk* __restrict__ chunks,
                                                      int n_chunks, uint8_t* __restrict__ hashes,
@@ -906,12 +849,16 @@ hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, ui
                             hipStream_t stream) {
   if (n_chunks <= 0) return hipSuccess;
   if (!scratch) return hipErrorInvalidValue;
+  uint8_t* h = hashes + 32 * uint64_t(hash_index_base);
+  uint64_t* sz = sizes ? sizes + hash_index_base : nullptr;
+  int hashed = 0;  // the decoder hashed the compressed chunks itself (zg_lz4_decode_ingest)
   if (has_compressed) {
-    const hipError_t e = zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
+    const hipError_t e = zg_lz4_decode_ingest(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, &hashed, stream);
     if (e != hipSuccess) return e;
   }
-  return zg_place_hash_flat(src, src_n, dst, dst_n, chunks, n_chunks, err, hashes + 32 * uint64_t(hash_index_base),
-                            sizes ? sizes + hash_index_base : nullptr, scratch, scratch_bytes, stream);
+  if (hashed)
+    return zg_place_hash_flat_raw(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, scratch, scratch_bytes, stream);
+  return zg_place_hash_flat(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, scratch, scratch_bytes, stream);
 }
 
 hipError_t zg_hash_ranges(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lens, int n, uint8_t* hashes,

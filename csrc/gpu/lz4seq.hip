@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "blake3_dev.h"
 #include "lz4win.h"
 #include "wave64.h"
 #include "zgpu.h"
@@ -608,9 +609,19 @@ __device__ __forceinline__ bool lds_wait(PairLds& L, const uint32_t* p, uint32_t
 }
 
 // (8 waves per SIMD: see k_lz4_batched)
+//
+// hashes != nullptr: the consumer also computes each chunk's Xet BLAKE3 hash (hashes[c], 32 bytes;
+// sizes[c] = its length) as soon as the chunk is decoded -- one wave over the output it just wrote,
+// which is still in L2, with the history ring as the chaining-value scratch -- so the chunk never
+// needs a hash pass of its own (the fused place/hash pass then covers stored chunks only).  The
+// decoder issues little VALU work (~15 % of wave-cycles), so the hashing mostly fills idle issue
+// slots; only the last chunks' hashes add to the launch.  A chunk that fails hashes as all-ones.
+// (A template: kHash = false is the decode-only kernel, register allocation untouched by the hash.)
+template <bool kHash>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   const ZgChunk* __restrict__ chunks, int n_chunks,
-                                                  unsigned long long* err, uint64_t src_n, uint64_t dst_n) {
+                                                  unsigned long long* err, uint64_t src_n, uint64_t dst_n,
+                                                  uint8_t* __restrict__ hashes, uint64_t* __restrict__ sizes) {
   __shared__ PairLds L;
   const uint32_t lane = lane_id();
   const bool producer = uni(threadIdx.x >> 6) == 0;
@@ -626,12 +637,19 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     ch.ulen = uni(ch.ulen);
     ch.scheme = uni(ch.scheme);
     if (ch.scheme == 0) continue;
+    auto bad_hash = [&]() {  // (consumer) a chunk that is not decoded hashes as all-ones
+      if (!kHash) return;
+      if (lane < 8) reinterpret_cast<uint32_t*>(hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
+      if (sizes && lane == 0) sizes[c] = 0;
+    };
     if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
       if (!producer && lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
+      if (!producer) bad_hash();
       continue;
     }
     if (ch.ulen > kMaxChunk) {
       if (!producer && lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      if (!producer) bad_hash();
       continue;
     }
     Ctx X;
@@ -671,11 +689,12 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
       });
       if (!alive || !publish(kPairEnd | code, 0u, 0u, 0u)) return;
     } else {
-      bool failed = false;
+      bool failed = false, whole = false;
       while (true) {
         const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
         if (!lds_wait(L, &L.full[slot], uses + 1u, lane)) {
           if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
+          bad_hash();
           return;
         }
         Batch B;
@@ -692,6 +711,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
               if (lane == 0) report(err, code, uint32_t(c));
             } else if (X.obase != X.ulen) {
               if (lane == 0) report(err, ZG_ERR_SIZE, uint32_t(c));
+            } else {
+              whole = true;
             }
           }
           break;
@@ -700,6 +721,21 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           failed = true;
           if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
           lds_release(&L.abort, cmark, lane);
+        }
+      }
+      if (kHash) {
+        if (whole) {
+          // this wave wrote every output byte: its stores acknowledged (vmcnt also counts stores),
+          // then L1 invalidated, so the hash reads them back from L2
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          uint32_t h[8];
+          zg::wave_hash(X.out, X.ulen, zg::kDataKeyW, zg::KEYED_HASH, reinterpret_cast<uint32_t*>(L.ring), lane, h);
+          zg::store_hash(hashes + 32 * uint64_t(c), h, lane);
+          if (sizes && lane == 0) sizes[c] = X.ulen;
+          __builtin_amdgcn_wave_barrier();  // the next chunk's exec_batch reuses the ring
+        } else {
+          bad_hash();
         }
       }
     }
@@ -923,14 +959,24 @@ extern "C" hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t sr
   return hipGetLastError();
 }
 
+extern "C" hipError_t zg_lz4_pair_decode_hash(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                              const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
+                                              uint8_t* hashes, uint64_t* sizes, hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  if (grid_cap <= 0 || grid_cap > 8192) grid_cap = 4096;  // 4096 pairs = 8 waves / SIMD
+  if (hashes)
+    hipLaunchKernelGGL(k_lz4_pair<true>, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream,
+                       src, dst, chunks, n_chunks, err, src_n, dst_n, hashes, sizes);
+  else
+    hipLaunchKernelGGL(k_lz4_pair<false>, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream,
+                       src, dst, chunks, n_chunks, err, src_n, dst_n, hashes, sizes);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t zg_lz4_pair_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                          const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
                                          hipStream_t stream) {
-  if (n_chunks <= 0) return hipSuccess;
-  if (grid_cap <= 0 || grid_cap > 8192) grid_cap = 4096;  // 4096 pairs = 8 waves / SIMD
-  hipLaunchKernelGGL(k_lz4_pair, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream, src, dst,
-                     chunks, n_chunks, err, src_n, dst_n);
-  return hipGetLastError();
+  return zg_lz4_pair_decode_hash(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, nullptr, nullptr, stream);
 }
 
 extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
@@ -957,6 +1003,21 @@ extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, 
   if (pair == 1 || (pair == 2 && n_chunks < kPairBelow))
     return zg_lz4_pair_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, stream);
   return zg_lz4_batched_decode_grid(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, stream);
+}
+
+// Decode for an unclipped ingest launch.  With the pair decoder (the default) and ZG_FUSED_HASH not 0,
+// every compressed chunk is also hashed by the decoder (hashes[c], sizes[c]) and *hashed is set to
+// 1, so the following place/hash pass skips compressed chunks; else *hashed = 0.
+extern "C" hipError_t zg_lz4_decode_ingest(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                           const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                           uint8_t* hashes, uint64_t* sizes, int* hashed, hipStream_t stream) {
+  const char* v = getenv("ZG_FUSED_HASH");  // read per launch: tests A/B both paths in one process
+  const char* p = getenv("ZG_LZ4_PAIR");
+  const bool fuse = !(v && atoi(v) == 0) && !(p && std::string(p) != "1");
+  *hashed = 0;
+  if (!fuse || !hashes) return zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
+  *hashed = 1;
+  return zg_lz4_pair_decode_hash(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, hashes, sizes, stream);
 }
 
 extern "C" size_t zg_lz4_rec_scratch_bytes(int n_chunks, uint64_t src_n) {

@@ -112,6 +112,15 @@ hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, cons
 // Fused K3a + K1: uncompressed chunks are copied src -> dst by the hashing waves themselves (and
 // hashed from src); compressed ones must already be decoded into dst.  Descriptors out of bounds are
 // not placed, hash over empty leaves (never their real hash) and set ZG_ERR_RANGE (chunk index) in `err` (may be null).
+hipError_t zg_lz4_pair_decode_hash(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                   const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
+                                   uint8_t* hashes, uint64_t* sizes, hipStream_t stream);
+hipError_t zg_lz4_decode_ingest(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
+                                int n_chunks, unsigned long long* err, uint8_t* hashes, uint64_t* sizes, int* hashed,
+                                hipStream_t stream);
+hipError_t zg_place_hash_flat_raw(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                  const ZgChunk* chunks, int n_chunks, unsigned long long* err, uint8_t* hashes,
+                                  uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream);
 hipError_t zg_place_hash_flat(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
                               int n_chunks, unsigned long long* err, uint8_t* hashes, uint64_t* sizes, uint8_t* scratch,
                               size_t scratch_bytes, hipStream_t stream);

@@ -218,6 +218,54 @@ def test_ingest_matches_cpu(policy, fused):
     assert hashes.cpu().numpy().tobytes() == want
 
 
+@pytest.mark.parametrize("policy", ["bg4", "auto"])
+def test_decoder_hash_matches_place_hash(policy, monkeypatch):
+    """The LZ4 pair decoder hashing each chunk it decodes (default) vs the place/hash pass hashing
+    every chunk (ZG_FUSED_HASH=0): same bytes, hashes and sizes, at a hash index base, for a batch
+    of compressed and stored chunks; both equal the host builder's."""
+    data, ends, b = _make_runs(policy, seed=5)
+    body = b.serialize(False)
+    nck = len(ends)
+    rec = np.zeros(nck, dtype=ops.CHUNK_DTYPE)
+    H = ops.hip()
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(bytearray(body), dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, nck, len(data))
+    ws = ops.IngestWorkspace(DEV, 1, nck)
+    terms_d = torch.from_numpy(terms.view(np.uint8).copy()).to(DEV)
+    ops.index_terms(H, src.data_ptr(), len(body), terms_d.data_ptr(), 1, ws.chunks.data_ptr(), ws.err.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream, ws)
+    torch.cuda.synchronize()
+    rec[:] = np.frombuffer(ws.chunks[: nck * ops.CHUNK_DTYPE.itemsize].cpu().numpy().tobytes(), dtype=ops.CHUNK_DTYPE)
+    assert (rec["scheme"] != 0).any()
+    if policy == "auto":
+        assert (rec["scheme"] == 0).any()
+    base = 5
+    got = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("ZG_FUSED_HASH", env)
+        dst = ops.padded_empty(len(data), DEV)
+        dst.fill_(0x3C)
+        hashes = torch.full((nck + base, 32), 0x77, dtype=torch.uint8, device=DEV)
+        sizes = torch.full((nck + base,), -1, dtype=torch.int64, device=DEV)
+        err = torch.zeros(1, dtype=torch.int64, device=DEV)
+        sp, sb = ops.HashScratch(DEV).get(nck, len(data))
+        H.ingest_chunks(src.data_ptr(), len(body), dst.data_ptr(), len(data), ws.chunks.data_ptr(), nck, True,
+                        err.data_ptr(), hashes.data_ptr(), sizes.data_ptr(), base,
+                        torch.cuda.current_stream().cuda_stream, sp, sb)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert dst.cpu().numpy().tobytes() == data
+        got[env] = (hashes.cpu().numpy(), sizes.cpu().numpy())
+    monkeypatch.delenv("ZG_FUSED_HASH")
+    (h1, s1), (h0, s0) = got["1"], got["0"]
+    assert np.array_equal(h1, h0) and np.array_equal(s1, s0)
+    assert h1[base:].tobytes() == b"".join(b.chunk_hashes())
+    assert (h1[:base] == 0x77).all() and (s1[:base] == -1).all()
+    assert s1[base:].tolist() == list(np.diff([0] + list(ends)))
+
+
 def test_fused_ingest_places_exact_bytes():
     """The fused place+hash pass (zg_ingest_chunks, raw chunks copied by the hashing waves) at
     misaligned src/dst offsets: every in-bounds raw chunk lands byte-exact and hashes like the host
