@@ -16,6 +16,7 @@
 #   ipc         peer-mapped arena tests (tests/test_gpu_ipc.py)
 #   cli         `zest pull --gpus 1` vs host `zest pull` (Llama-3.1-8B from an HBM seeder, sync between)
 #   stripe      host pull from 1 vs 3 loopback seeders
+#   clipeer     `zest pull --gpus 1` vs host pull from warm `zest serve` seeders (tools/cli_peer_bench.py)
 #   pin         $PIN_PROCS processes pinning $PIN_GB GB each at once (the N=8 origin setup)
 #   seed        HBM seeding throughput (Mixtral-8x7B, chunks_served/s)
 #   kbench      per-kernel micro-benchmarks ($KBENCH_ONLY selects one group, e.g. k3pair)
@@ -63,6 +64,9 @@ for step in "$@"; do
     cli) timeout -k 10 700 python -u tools/direct_bench.py --model llama-3.1-8b --skip-direct --host-after \
            --mode ${CLI_MODE:-random} --out $OUT/cli_vs_host_${CLI_MODE:-random}.json > $log 2>&1 || fail $step $? $log
          grep -h "^\[" $log ;;
+    clipeer) timeout -k 10 900 python -u tools/cli_peer_bench.py --mb ${CLIPEER_MB:-8192} --mode ${CLI_MODE:-bf16} \
+               --seeders ${CLIPEER_SEEDERS:-1} --out $OUT/cli_peer_${CLI_MODE:-bf16}.json > $log 2>&1 || fail $step $? $log
+             grep -h "^\[" $log ;;
     pin) timeout -k 10 500 python -u tools/pin_bench.py --procs ${PIN_PROCS:-8} --gb ${PIN_GB:-17.6} \
            --out $OUT/pin_${PIN_PROCS:-8}x${PIN_GB:-17.6}.json > $log 2>&1 || fail $step $? $log
          tail -1 $log | cut -c1-400 ;;
