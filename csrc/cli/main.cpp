@@ -215,22 +215,54 @@ std::vector<WorkerResult> spawn_gpu_workers(const std::string& exe, const std::v
       out[size_t(r)].rc = 127;
     }
   }
-  for (int r = 0; r < n; ++r) {
-    if (!pids[size_t(r)]) continue;
-    int status = 0;
-    while (::waitpid(pids[size_t(r)], &status, 0) < 0 && errno == EINTR) {
-    }
-    out[size_t(r)].rc = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+  // A worker is done when its status file says complete (written after every file is durable and
+  // renamed) or when it exits.  The CLI does not wait for a completed worker's exit: tearing down a
+  // HIP process (device and pinned allocations) takes a few hundred ms the user need not wait for;
+  // the child is reaped with this process.
+  auto read_status = [&](int r) -> bool {
     const std::string st = status_base + "." + std::to_string(r);
-    if (auto b = storage::read_file(st)) {
-      try {
-        out[size_t(r)].status = json::Value::parse(std::string(b->begin(), b->end()));
-        out[size_t(r)].complete = out[size_t(r)].status["complete"].type() == json::Value::Type::Bool &&
-                                  out[size_t(r)].status["complete"].as_bool();
-      } catch (const Error&) {
-      }
+    auto b = storage::read_file(st);
+    if (!b) return false;
+    try {
+      out[size_t(r)].status = json::Value::parse(std::string(b->begin(), b->end()));
+      out[size_t(r)].complete = out[size_t(r)].status["complete"].type() == json::Value::Type::Bool &&
+                                out[size_t(r)].status["complete"].as_bool();
+    } catch (const Error&) {
+      return false;
     }
-    ::unlink(st.c_str());
+    return out[size_t(r)].complete;
+  };
+  const double spawned = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  std::vector<char> done(static_cast<size_t>(n), 0);
+  size_t left = 0;
+  for (int r = 0; r < n; ++r) left += pids[size_t(r)] ? 1 : 0;
+  while (left) {
+    for (int r = 0; r < n; ++r) {
+      if (!pids[size_t(r)] || done[size_t(r)]) continue;
+      int status = 0;
+      const pid_t w = ::waitpid(pids[size_t(r)], &status, WNOHANG);
+      if (w == pids[size_t(r)]) {
+        out[size_t(r)].rc = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+        read_status(r);
+      } else if (w == 0 && read_status(r)) {
+        out[size_t(r)].rc = out[size_t(r)].status["failed_files"].as_double() > 0 ? 1 : 0;
+        const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        const json::Value& s = out[size_t(r)].status;
+        if (s["t0_mono"].type() == json::Value::Type::Number)
+          std::cout << "[gpu " << r << "] process: exec + load " << int((s["t0_mono"].as_double() - spawned) * 1000)
+                    << " ms, run " << int((s["status_mono"].as_double() - s["t0_mono"].as_double()) * 1000)
+                    << " ms, status seen after " << int((now - s["status_mono"].as_double()) * 1000)
+                    << " ms (exit not awaited)\n" << std::flush;
+      } else if (w < 0 && errno == EINTR) {
+        continue;
+      } else if (w == 0) {
+        continue;
+      }
+      done[size_t(r)] = 1;
+      --left;
+      ::unlink((status_base + "." + std::to_string(r)).c_str());
+    }
+    if (left) std::this_thread::sleep_for(std::chrono::milliseconds(2));
   }
   return out;
 }

@@ -531,6 +531,9 @@ int run(int argc, char** argv) {
     w.key("failed_files").num_u(failed).key("bytes").num_u(done_bytes).key("files").num_u(todo.size());
     w.key("cached_files").num_u(cached).key("seconds").num(dt, 3).key("pull_s").num(t_pull, 3);
     w.key("write_s").num(t_write, 3).key("init_s").num(t_init - t0, 3).key("list_s").num(t_list - t0, 3);
+    // steady-clock instants (CLOCK_MONOTONIC, shared by the processes of one machine): the CLI times
+    // this worker's exec + load (spawn -> t0) and stops waiting as soon as this status exists
+    w.key("t0_mono").num(t0, 6).key("status_mono").num(now_s(), 6);
     w.key("stats").raw(stats).end();
     storage::write_file_atomic(status_path, w.out() + "\n", true);
   }

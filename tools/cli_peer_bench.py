@@ -57,6 +57,7 @@ def main() -> int:
     ap.add_argument("--mode", default="bf16", choices=["bf16", "random"])
     ap.add_argument("--seeders", type=int, default=1)
     ap.add_argument("--verify-bytes", action="store_true", help="also compare every snapshot byte for byte")
+    ap.add_argument("--gpu-env", default="", help="extra env for the GPU CLI runs, e.g. ZEST_GPU_STAGING_MB=256")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     shard = a.mb * 1_000_000 // a.shards
@@ -91,29 +92,32 @@ def main() -> int:
         stored = sum(p.stat().st_size for p in seeders[0].xorb_files())
         res["stored_bytes"] = stored
 
-        def run(label, extra):
+        gpu_env = dict(kv.split("=", 1) for kv in a.gpu_env.split(",") if kv)
+        res["gpu_env"] = gpu_env
+
+        def run(label, extra, env=None):
             t = time.time()
             os.sync()
             synced = time.time() - t
             leech = Node(hub, work, f"leech_{label}")
             nodes.append(leech)
             t1 = time.time()
-            r = leech.run("pull", "org/clipeer", "--no-dht", "--no-serve", *peers, *extra, timeout=3600)
+            r = leech.run("pull", "org/clipeer", "--no-dht", "--no-serve", *peers, *extra, timeout=3600, env=env)
             dt = time.time() - t1
             ratio = p2p_ratio(r.stdout) if "P2P ratio:" in r.stdout else None
             if a.verify_bytes:
                 assert_snapshot(leech, "org/clipeer", commit, files)
             res[label] = {"seconds": round(dt, 3), "GBps": round(total / dt / 1e9, 3), "p2p_ratio": ratio,
                           "presync_s": round(synced, 3),
-                          "worker": [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu")][-2:]}
+                          "worker": [ln for ln in r.stdout.splitlines() if ln.startswith("[gpu")][-3:]}
             print(f"[{label}] {total / dt / 1e9:.2f} GB/s ({dt:.2f}s), P2P {ratio}", flush=True)
             shutil.rmtree(leech.root, ignore_errors=True)
 
         run("warmup", [])  # untimed in the result: brings the seeder's cache files into the page cache
         run("host", [])
-        run("gpu_cli", ["--gpus", "1"])
+        run("gpu_cli", ["--gpus", "1"], gpu_env)
         run("host_again", [])
-        run("gpu_cli_again", ["--gpus", "1"])
+        run("gpu_cli_again", ["--gpus", "1"], gpu_env)
         host = min(res["host"]["seconds"], res["host_again"]["seconds"])
         gpu = min(res["gpu_cli"]["seconds"], res["gpu_cli_again"]["seconds"])
         res["gpu_vs_host"] = round(host / gpu, 3)

@@ -65,7 +65,8 @@ for step in "$@"; do
            --mode ${CLI_MODE:-random} --out $OUT/cli_vs_host_${CLI_MODE:-random}.json > $log 2>&1 || fail $step $? $log
          grep -h "^\[" $log ;;
     clipeer) timeout -k 10 900 python -u tools/cli_peer_bench.py --mb ${CLIPEER_MB:-8192} --mode ${CLI_MODE:-bf16} \
-               --seeders ${CLIPEER_SEEDERS:-1} --out $OUT/cli_peer_${CLI_MODE:-bf16}.json > $log 2>&1 || fail $step $? $log
+               --seeders ${CLIPEER_SEEDERS:-1} --gpu-env "${CLIPEER_GPU_ENV:-}" \
+               --out $OUT/cli_peer_${CLI_MODE:-bf16}${CLIPEER_TAG:-}.json > $log 2>&1 || fail $step $? $log
              grep -h "^\[" $log ;;
     pin) timeout -k 10 500 python -u tools/pin_bench.py --procs ${PIN_PROCS:-8} --gb ${PIN_GB:-17.6} \
            --out $OUT/pin_${PIN_PROCS:-8}x${PIN_GB:-17.6}.json > $log 2>&1 || fail $step $? $log
