@@ -57,7 +57,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   if (!fi) throw Error("NoMatchingFetchInfo", hex);
   XorbFetchResult out;
   // 1. local xorb cache: any cached run covering the term's chunks
-  if (opt.allow_cache && !opt.repair && cache_) {
+  if (opt.allow_cache && !opt.repair && cache_ && cache_->maybe_cached(hex)) {
     trace::Span sp("cache", "find");
     if (auto hit = cache_->find(hex, uint32_t(term.range.start), uint32_t(term.range.end))) {
       stats_.xorbs_from_cache++;
@@ -81,9 +81,14 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
         // file (settle), so a corrupt peer copy is never seeded on or read back as a cache hit.
         if (cache_ && cfg_.cache_writes) {
           try {
-            trace::Span sp("cache", "put_pending");
-            out.pending = writer_ ? writer_->put_pending(hex, r->chunk_offset, r->bytes(), r->size())
-                                  : cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
+            if (writer_ && opt.on_copied && r->ext) {  // copied off this thread (sink memory stays put)
+              out.pending = writer_->put_pending_ref(hex, r->chunk_offset, r->ext, r->ext_len, opt.on_copied);
+              out.copy_deferred = !out.pending.empty();
+            } else {
+              trace::Span sp("cache", "put_pending");
+              out.pending = writer_ ? writer_->put_pending(hex, r->chunk_offset, r->bytes(), r->size())
+                                    : cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
+            }
             out.run_offset = r->chunk_offset;
           } catch (const Error&) {
           }
@@ -135,8 +140,12 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   }
   if (cache_ && cfg_.cache_writes) {
     try {
-      if (writer_) writer_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
-      else cache_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
+      if (writer_ && opt.on_copied && out.ext)
+        out.copy_deferred = writer_->put_run_ref(hex, uint32_t(fi->range.start), run, run_len, opt.repair, opt.on_copied);
+      else if (writer_)
+        writer_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
+      else
+        cache_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
     } catch (const Error&) {
     }
   }

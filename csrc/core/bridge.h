@@ -12,6 +12,7 @@
 #include <mutex>
 #include <optional>
 #include <ostream>
+#include <functional>
 #include <string>
 
 #include "config.h"
@@ -36,6 +37,10 @@ struct FetchOptions {
   // CDN refetch repairing a copy that failed verification: the CDN run replaces whatever the
   // cache holds under its name (put_run normally keeps an existing longer run).
   bool repair = false;
+  // With a write-behind writer and a sink: the cache copy of a run received into sink memory is
+  // made by the writer's copy threads instead of this thread; on_copied() runs once they have it
+  // (XorbFetchResult::copy_deferred says whether it will run).  The caller keeps the sink memory.
+  std::function<void()> on_copied;
 };
 
 struct XorbFetchResult {
@@ -51,6 +56,7 @@ struct XorbFetchResult {
   // With a sink: the run was written to sink memory instead of `data`.
   uint8_t* ext = nullptr;
   size_t ext_len = 0;
+  bool copy_deferred = false;  // FetchOptions::on_copied will run (a writer copy thread owns the cache copy)
   const uint8_t* bytes() const { return ext ? ext : data.data(); }
   size_t size() const { return ext ? ext_len : data.size(); }
 };

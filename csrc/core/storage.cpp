@@ -1,4 +1,6 @@
 #include "storage.h"
+
+#include "trace.h"
 #include "xet_hash.h"
 #include "cdc.h"
 #include <thread>
@@ -303,6 +305,7 @@ bool stale_pending(const std::string& path, int64_t max_age_s) {
 // replaced by rename, never truncated in place, so a live mapping stays valid).  Only the chunk
 // headers are touched to validate coverage.
 std::optional<CacheHit> XorbCache::find(const std::string& hex, uint32_t start, uint32_t end) const {
+  if (registry_lookup_ && registry_ && !registry_->has(hex)) return std::nullopt;
   auto offs = run_offsets(hex);
   // Closest preceding run first: most likely to be the one that was fetched for this range.
   for (auto it = offs.rbegin(); it != offs.rend(); ++it) {
@@ -588,6 +591,7 @@ namespace zest::storage {
 CacheWriter::CacheWriter(XorbCache* cache, size_t max_bytes, int threads)
     : cache_(cache), max_bytes_(max_bytes), queues_(size_t(std::max(1, threads))) {
   for (int q = 0; q < int(queues_.size()); ++q) threads_.emplace_back([this, q] { worker(q); });
+  for (int k = 0; k < 2; ++k) copy_threads_.emplace_back([this] { copier(); });
 }
 
 CacheWriter::~CacheWriter() {
@@ -596,7 +600,64 @@ CacheWriter::~CacheWriter() {
     stop_ = true;
   }
   cv_.notify_all();
+  for (auto& t : copy_threads_) t.join();  // copiers first: they queue writes
+  cv_.notify_all();
   for (auto& t : threads_) t.join();  // workers drain their queues before leaving
+}
+
+void CacheWriter::copier() {
+  while (true) {
+    CopyJob j;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [&] { return stop_ || !copies_.empty(); });
+      if (copies_.empty()) return;  // stop_ and drained
+      j = std::move(copies_.front());
+      copies_.pop_front();
+      ++copy_busy_;
+    }
+    {
+      trace::Span sp("cache", j.op.kind == Op::Pending ? "quarantine copy (writer)" : "run copy (writer)");
+      j.op.data = take_buffer(j.n);
+      j.op.data.assign(j.src, j.src + j.n);
+    }
+    // queued before the caller hears the bytes are copied: a promote/discard it queues after that
+    // (same xorb, same writer) runs after this write
+    push(std::move(j.op));
+    j.on_copied();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      --copy_busy_;
+    }
+    cv_.notify_all();  // writers waiting to stop re-check
+    idle_cv_.notify_all();
+  }
+}
+
+std::string CacheWriter::put_pending_ref(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n,
+                                         std::function<void()> on_copied) {
+  if (!reserve(n)) return "";
+  CopyJob j{Op{Op::Pending, hex, cache_->pending_path(hex, chunk_offset), chunk_offset, false, {}}, data, n,
+            std::move(on_copied)};
+  std::string path = j.op.path;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    copies_.push_back(std::move(j));
+  }
+  cv_.notify_all();
+  return path;
+}
+
+bool CacheWriter::put_run_ref(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n,
+                              bool replace, std::function<void()> on_copied) {
+  if (!reserve(n)) return false;
+  CopyJob j{Op{Op::Run, hex, "", chunk_offset, replace, {}}, data, n, std::move(on_copied)};
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    copies_.push_back(std::move(j));
+  }
+  cv_.notify_all();
+  return true;
 }
 
 bool CacheWriter::reserve(size_t n) {
@@ -668,7 +729,7 @@ void CacheWriter::evict(const std::string& hex, uint32_t chunk_offset) {
 void CacheWriter::flush() {
   std::unique_lock<std::mutex> g(mu_);
   idle_cv_.wait(g, [&] {
-    if (busy_) return false;
+    if (busy_ || copy_busy_ || !copies_.empty()) return false;
     for (auto& q : queues_)
       if (!q.empty()) return false;
     return true;
@@ -685,7 +746,8 @@ void CacheWriter::worker(int q) {
     Op op;
     {
       std::unique_lock<std::mutex> g(mu_);
-      cv_.wait(g, [&] { return stop_ || !queues_[size_t(q)].empty(); });
+      // (at stop: leave only once the copy threads can queue nothing more)
+      cv_.wait(g, [&] { return !queues_[size_t(q)].empty() || (stop_ && copies_.empty() && !copy_busy_); });
       if (queues_[size_t(q)].empty()) return;  // stop_ and drained
       op = std::move(queues_[size_t(q)].front());
       queues_[size_t(q)].pop_front();

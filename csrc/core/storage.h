@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -113,6 +114,14 @@ class XorbCache {
   // `range.start == 0 && one fetch entry` rule produces, xet_bridge.zig:189-217 — the source of
   // its P2P RangeOutOfBounds failures) is never served for chunks it does not hold.
   std::optional<CacheHit> find(const std::string& hex, uint32_t start, uint32_t end) const;
+  // Pull pipelines whose registry was scanned at start: find() answers "not cached" from the
+  // registry (what was cached at the scan + what this process published since) without listing the
+  // xorb's cache directory, which a concurrent write-behind makes slow (4 ms per term in a 16-thread
+  // device pull).  Runs another process adds during the pull are not seen -- they would only have
+  // saved a fetch.  Servers keep the directory lookup.
+  void set_registry_lookup(bool on) { registry_lookup_ = on; }
+  // false: find() would answer "not cached" from the registry alone (no lookup worth tracing)
+  bool maybe_cached(const std::string& hex) const { return !(registry_lookup_ && registry_ && !registry_->has(hex)); }
   // Does a cached run cover chunks [start, end)?  The planner's possession check (swarm_pull): only
   // the chunk headers up to `end` are read (pread, no readahead of the payload), and nothing is
   // mapped or touched.  A true answer is re-validated by find() when the term is fetched.
@@ -160,6 +169,7 @@ class XorbCache {
   std::string run_path(const std::string& hex, uint32_t chunk_offset) const;
   const Config& cfg_;
   XorbRegistry* registry_;
+  bool registry_lookup_ = false;
 };
 
 // Write-behind for the xorb cache.  A device pull moves tens of GB/s; writing every fetched run to
@@ -180,6 +190,14 @@ class CacheWriter {
   bool put_run(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace);
   // The quarantine path the run will be written to, or "" when dropped.
   std::string put_pending(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n);
+  // The same without copying on the caller's thread: `data` stays valid until on_copied() runs on
+  // one of the writer's copy threads (which copy the run into a pooled buffer and queue its write;
+  // the device pull keeps the pinned staging slot holding the run until then).  on_copied runs
+  // exactly once when the call returns a path / true, never when it drops the run.
+  std::string put_pending_ref(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n,
+                              std::function<void()> on_copied);
+  bool put_run_ref(const std::string& hex, uint32_t chunk_offset, const uint8_t* data, size_t n, bool replace,
+                   std::function<void()> on_copied);
   void promote(const std::string& hex, uint32_t chunk_offset, const std::string& pending);
   void discard_pending(const std::string& pending);
   void evict(const std::string& hex, uint32_t chunk_offset);
@@ -197,10 +215,20 @@ class CacheWriter {
     bool replace = false;
     Bytes data;
   };
+  struct CopyJob {
+    Op op;  // data empty: copied from `src` by a copy thread
+    const uint8_t* src = nullptr;
+    size_t n = 0;
+    std::function<void()> on_copied;
+  };
   bool reserve(size_t n);
   Bytes take_buffer(size_t n);
   void push(Op op);
   void worker(int q);
+  void copier();
+  std::deque<CopyJob> copies_;
+  size_t copy_busy_ = 0;
+  std::vector<std::thread> copy_threads_;
   XorbCache* cache_;
   size_t max_bytes_;
   mutable std::mutex mu_;

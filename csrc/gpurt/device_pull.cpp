@@ -85,6 +85,7 @@ struct DeviceXetPull::Shared {
       trace::Span sp("device", "init: cache scan");
       registry.scan(cfg);
       cache = std::make_unique<storage::XorbCache>(cfg, &registry);
+      cache->set_registry_lookup(true);  // a miss needs no cache directory listing on a fetch thread
     }
     if (cfg.cache_writes)  // ZEST_CACHE_WRITE_QUEUE_MB bounds the write-behind queue (0: synchronous)
       if (size_t mb = env_size("ZEST_CACHE_WRITE_QUEUE_MB", 2048))
@@ -572,6 +573,14 @@ struct DeviceXetPull::Impl {
       for (size_t i = 0; i < S; ++i) ready[i] = i;
       std::vector<size_t> remaining(nb);
       for (size_t b = 0; b < nb; ++b) remaining[b] = batches[b].end - batches[b].begin;
+      // Cache copies of runs still reading batch b's host slot: the write-behind writer's copy
+      // threads take them (FetchOptions::on_copied), so the fetch threads never copy a run for the
+      // cache; the slot goes back to the workers only when its H2D landed AND these are done.
+      std::vector<size_t> copies(nb, 0);
+      auto copies_done = [&]() {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return std::all_of(copies.begin(), copies.end(), [](size_t c) { return c == 0; }); });
+      };
       bool abort = false;
       std::atomic<size_t> k{0};
       auto fail = [&](const std::string& what) {
@@ -600,7 +609,27 @@ struct DeviceXetPull::Impl {
             uint8_t* region = s.host + bt.off[j];
             const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
             auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
-            XorbFetchResult r = sh_->bridge->fetch_term(rec.terms[gt[i].term], rec, opt, sink);
+            FetchOptions topt = opt;
+            {
+              std::lock_guard<std::mutex> g(mu);
+              ++copies[b];
+            }
+            auto copied = [&mu, &cv, &copies, b]() {
+              {
+                std::lock_guard<std::mutex> g(mu);
+                --copies[b];
+              }
+              cv.notify_all();
+            };
+            if (sh_->writer) topt.on_copied = copied;
+            XorbFetchResult r;
+            try {
+              r = sh_->bridge->fetch_term(rec.terms[gt[i].term], rec, topt, sink);
+            } catch (...) {
+              copied();
+              throw;
+            }
+            if (!r.copy_deferred) copied();
             at.sources[gt[i].seg][gt[i].term - segs[gt[i].seg].t0] = TermSource{r.source, r.run_offset, r.pending};
             auto idx = xet::index_chunks(r.bytes(), r.size());
             if (r.local_end > idx.size() || r.local_start >= r.local_end)
@@ -664,11 +693,12 @@ struct DeviceXetPull::Impl {
           if (b == SIZE_MAX) return;
           const bool copied = hipEventSynchronize(ev[2 * b]) == hipSuccess;
           {
-            std::lock_guard<std::mutex> g(mu);
+            std::unique_lock<std::mutex> g(mu);
             if (!copied) {
               if (fetch_err.empty()) fetch_err = "hipEventSynchronize (H2D)";
               abort = true;
             }
+            cv.wait(g, [&] { return copies[b] == 0; });  // the writer's copy threads are done with the slot
             ready[b % S] = b + S;
             cv.notify_all();
           }
@@ -755,9 +785,11 @@ struct DeviceXetPull::Impl {
         (void)hipStreamSynchronize(copy_stream_);
         (void)hipStreamSynchronize(stream_);
         stop_releaser();
+        copies_done();  // no copy thread may still read the slots (or these counters) after return
         throw;
       }
       for (auto& t : ts) t.join();
+      copies_done();
       const hipError_t e1 = hipStreamSynchronize(copy_stream_);
       const hipError_t e2 = hipStreamSynchronize(stream_);
       stop_releaser();

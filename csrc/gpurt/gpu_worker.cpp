@@ -238,7 +238,10 @@ struct Args {
   std::optional<std::string> tracker;
   bool p2p = true, dht = true;
   int threads = 16;
-  size_t staging_mb = size_t(std::max(16, env_int("ZEST_GPU_STAGING_MB", 512)));
+  // 256 MiB per staging slot (x 2 slots x 4 pipelines): ample for H2D batches at PCIe speed, and
+  // half the pinning of 512 at start-up (8 GB bf16 from a warm seeder: device pulls 1.08 vs 1.40 s,
+  // profiles/r5/cli_peer_bf16_st256_r5o.json)
+  size_t staging_mb = size_t(std::max(16, env_int("ZEST_GPU_STAGING_MB", 256)));
 };
 
 Args parse(int argc, char** argv) {
@@ -542,6 +545,13 @@ int run(int argc, char** argv) {
   trace::flush();
   std::cout << std::flush;
   std::cerr << std::flush;
+  // Let go of the inherited stdout/stderr now: whoever reads them (a shell pipe, a harness waiting
+  // for EOF) need not wait for this process's teardown of its device and pinned memory.
+  if (const int nul = ::open("/dev/null", O_WRONLY | O_CLOEXEC); nul >= 0) {
+    ::dup2(nul, 1);
+    ::dup2(nul, 2);
+    ::close(nul);
+  }
   std::_Exit(failed ? 1 : 0);
 }
 

@@ -8,7 +8,10 @@
 
 #include <cstdio>
 #include <cstring>
+#include <chrono>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -356,6 +359,65 @@ TEST(xorb_cache_covers_and_write_behind) {
   CHECK(!cache.covers(hx, 2, 6));
   auto held = cached_terms(cache, {hx, hx, hx}, {0, 1, 2}, {2, 3, 5}, 2);
   CHECK(held == std::vector<uint8_t>({1, 0, 1}));
+}
+
+TEST(xorb_cache_write_behind_ref_copies_and_registry_lookup) {
+  // put_pending_ref / put_run_ref: the caller's bytes are copied by the writer's copy threads;
+  // on_copied runs exactly once per queued run (never for a dropped one), the written runs equal the
+  // caller's bytes even though the caller overwrites its buffer right after on_copied, and a promote
+  // queued after on_copied publishes the run.  registry lookup: find() of an unregistered xorb
+  // answers from the registry, a run published through the writer is found.
+  char tmpl[] = "/tmp/zest_cpp_wbref_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  setenv("ZEST_CACHE_DIR", dir, 1);
+  Config cfg = Config::from_env();
+  storage::XorbRegistry reg;
+  reg.scan(cfg);
+  storage::XorbCache cache(cfg, &reg);
+  cache.set_registry_lookup(true);
+  xet::XorbBuilder b(xet::CompressionPolicy::None);
+  for (uint32_t i = 0; i < 6; ++i) {
+    Bytes c = rnd(9000, 90 + i);
+    b.add_chunk(c.data(), c.size());
+  }
+  const std::string hx = xet::to_hex(b.hash());
+  const Bytes body = b.body();
+  auto idx = xet::index_chunks(body.data(), body.size());
+  CHECK(!cache.maybe_cached(hx) && !cache.find(hx, 0, 1).has_value());
+  {
+    storage::CacheWriter w(&cache, 1 << 20, 2);
+    std::mutex mu;
+    std::condition_variable cv;
+    int copied = 0;
+    auto done = [&] {
+      std::lock_guard<std::mutex> g(mu);
+      ++copied;
+      cv.notify_all();
+    };
+    Bytes buf1(body.begin(), body.begin() + long(idx[3].header_off));  // chunks 0..2, as a peer run
+    const std::string pend = w.put_pending_ref(hx, 0, buf1.data(), buf1.size(), done);
+    CHECK(!pend.empty());
+    const size_t tail = body.size() - idx[3].header_off;
+    Bytes buf2(body.begin() + long(idx[3].header_off), body.end());  // chunks 3..5, as a CDN run
+    CHECK(w.put_run_ref(hx, 3, buf2.data(), tail, false, done));
+    Bytes big(2 << 20, 7);
+    CHECK(!w.put_run_ref(hx, 9, big.data(), big.size(), false, done));  // dropped: no callback
+    {
+      std::unique_lock<std::mutex> g(mu);
+      CHECK(cv.wait_for(g, std::chrono::seconds(10), [&] { return copied == 2; }));
+    }
+    std::fill(buf1.begin(), buf1.end(), 0);  // the caller reuses its memory once copied
+    std::fill(buf2.begin(), buf2.end(), 0);
+    w.promote(hx, 0, pend);
+    w.flush();
+    CHECK(copied == 2 && w.stats().written_bytes == body.size());
+  }
+  CHECK(cache.maybe_cached(hx));
+  auto h0 = cache.find(hx, 0, 3), h1 = cache.find(hx, 3, 6);
+  CHECK(h0.has_value() && h1.has_value());
+  CHECK(h0->size() == idx[3].header_off && std::memcmp(h0->bytes(), body.data(), h0->size()) == 0);
+  CHECK(std::memcmp(h1->bytes(), body.data() + idx[3].header_off, h1->size()) == 0);
 }
 
 TEST(xorb_cache_quarantine_per_fetch) {
