@@ -138,7 +138,9 @@ PullSummary run_pull(Config& cfg, const PullOptions& opt, std::ostream& out, std
   }
   std::optional<trace::Span> setup_span(std::in_place, "pull", "cache scan + swarm + auth");
   storage::XorbRegistry registry;
+  registry.scan(cfg);
   storage::XorbCache cache(cfg, &registry);
+  cache.set_registry_lookup(true);  // misses answered from the scan + this pull's own puts (no directory listing per term)
   SwarmDownloader swarm(cfg, opt.tracker, opt.p2p, opt.dht && opt.p2p, boot);
   for (auto& p : opt.peers) {
     try {
