@@ -435,9 +435,14 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     cuda = device.type == "cuda"
     wd.arm("swarm_setup")
     t_setup = time.time()
-    # the engine's device buffers go first: the swarm pull allocates its own 141 GB arena
+    # the engine's device buffers go first: the swarm pull allocates its own 141 GB arena.  At N > 1
+    # the peers' imports of this rank's old arena must be gone too (a peer-mapped VMM chunk lives until
+    # every importer released it): every rank drops its mappings here, before swarm_pull's first
+    # collective, and gc runs so no reference cycle keeps a mapping past it.
     puller.release_device()
     keep.pop("arena", None)
+    import gc
+    gc.collect()
     if cuda:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
