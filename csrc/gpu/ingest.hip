@@ -127,10 +127,15 @@ constexpr uint32_t kScanBytesPerThread = 16;
 constexpr uint32_t kCandCap = 8192;  // chunks of a 64 MiB xorb at the 8 KiB CDC minimum
 constexpr int kLinkThreads = 1024;
 
-__device__ __forceinline__ bool plausible_header(uint32_t lo, uint32_t hi, uint64_t rel, uint64_t run_len) {
+// `pay`: the 4 bytes after the header.  A compressed chunk's payload is an LZ4 frame, so it starts
+// with the frame magic: without that test the LZ4 streams of BG4 bf16 weights (zero bytes every few
+// bytes) produced millions of header-like candidates and the scan lost to the serial walk.
+constexpr uint32_t kLz4Magic = 0x184D2204u;
+__device__ __forceinline__ bool plausible_header(uint32_t lo, uint32_t hi, uint32_t pay, uint64_t rel,
+                                                 uint64_t run_len) {
   const uint32_t clen = lo >> 8, scheme = hi & 0xFF, ulen = hi >> 8;
   return (lo & 0xFF) == 0 && scheme <= 2 && ulen >= 1 && ulen <= kMaxChunk && clen >= 1 &&
-         (scheme != 0 || clen == ulen) && rel + 8 + clen <= run_len;
+         (scheme == 0 ? clen == ulen : pay == kLz4Magic) && rel + 8 + clen <= run_len;
 }
 
 // terms must be sorted by src (else the fast path finds no chain and the serial walk runs)
@@ -171,7 +176,8 @@ __global__ void __launch_bounds__(kScanThreads) k_hdr_scan(const uint8_t* __rest
     const uint32_t j = k >> 2, sh = k & 3;
     const uint32_t lo = sh ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) : w[j];
     const uint32_t hi = sh ? __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], sh) : w[j + 1];
-    if (plausible_header(lo, hi, p - t0, t1 - t0)) {
+    const uint32_t pay = sh ? __builtin_amdgcn_alignbyte(w[j + 3], w[j + 2], sh) : w[j + 2];
+    if (plausible_header(lo, hi, pay, p - t0, t1 - t0)) {
       const uint32_t i = atomicAdd(&counts[t], 1u);
       if (i < kCandCap) cands[uint64_t(t) * kCandCap + i] = uint32_t(p - t0);
     }
