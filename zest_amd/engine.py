@@ -326,6 +326,11 @@ class DevicePuller:
         # (bench.py 20 steps: 51-52.6 GB/s vs 56.2 with 10; tools/step_times.py).  step() therefore
         # waits until at most `steps_ahead` earlier steps are still in flight (0 = unbounded).
         self.steps_ahead = int(os.environ.get("ZEST_STEPS_AHEAD", "1"))
+        # Peer-mapped exchanges: rounds queued past round k before the host waits for k to be readable
+        # (ZEST_IPC_LAG, >= 1).  With both ranks on one GPU (the only multi-rank run a one-GPU box
+        # allows) lag 1 and 2 measure the same, 279 / 294 ms per 8B bf16 step within that run's spread
+        # (profiles/r5/rehearsal_n2_r5t/); 2 keeps a copy queued on a rank that owns its PCIe link.
+        self.ipc_lag = max(1, int(os.environ.get("ZEST_IPC_LAG", "2")))
         self._inflight: collections.deque = collections.deque()
         # Header walk on the host (ZEST_HOST_INDEX, default on): the origin bytes are in host memory,
         # where the walk's pointer chase (chunk i+1's header position depends on chunk i's length)
@@ -574,11 +579,15 @@ class DevicePuller:
                     if self.n_ranks > 1:
                         if self.exchange in PEER_MAPPED_MODES:
                             # peers read round k once its kernels are done; wait for that only after
-                            # round k+1's copy and kernels are queued, so the GPU never idles on it
+                            # rounds k+1 .. k+lag are queued, so the copy engine always has a round
+                            # queued behind the one in flight while the host waits on the event and
+                            # the host barrier (lag 1 left one copy queued: the barrier's wake-up
+                            # skew became a PCIe gap every round)
                             self._ipc_done[k] = torch.cuda.Event()
                             self._ipc_done[k].record(comp)
-                            if k > 0:
-                                works += self._hash_received(k - 1, self._exchange(k - 1))
+                            if k >= self.ipc_lag:
+                                j = k - self.ipc_lag
+                                works += self._hash_received(j, self._exchange(j))
                         else:  # collectives wait for the issuing (this round's) stream
                             works += self._hash_received(k, self._exchange(k))
                 if self._rx:
@@ -587,7 +596,8 @@ class DevicePuller:
             main.wait_stream(self.side_stream)
             st = main.cuda_stream
             if self.n_ranks > 1 and self.exchange in PEER_MAPPED_MODES:
-                works += self._hash_received(self.n_rounds - 1, self._exchange(self.n_rounds - 1))
+                for j in range(max(0, self.n_rounds - self.ipc_lag), self.n_rounds):
+                    works += self._hash_received(j, self._exchange(j))
                 self._ipc_done.clear()
             if self.n_ranks > 1:
                 works.append(_StreamJoin(self.verify_stream))
