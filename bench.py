@@ -350,10 +350,13 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     try:
         warmup()
     except ops.IngestError as e:  # the error word is all-reduced: every rank takes this branch
-        if world_size == 1 or puller.exchange == "p2p":
+        # (gloo moves device tensors only through its collectives -- a batched isend/irecv of device
+        # tensors never completes -- so a gloo rehearsal falls back to its broadcasts)
+        safe = "bcast" if (cuda and dist is not None and dist.get_backend() == "gloo") else "p2p"
+        if world_size == 1 or puller.exchange == safe:  # the fallback itself failed
             raise
-        log(rank, f"exchange {puller.exchange} failed verification ({e}); falling back to p2p")
-        puller.exchange = "p2p"
+        log(rank, f"exchange {puller.exchange} failed verification ({e}); falling back to {safe}")
+        puller.exchange = safe
         warmup()
     phase["warmup_s"] = round(time.time() - t_warm, 3)
     puller.err.zero_()
@@ -401,6 +404,8 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
         # host time per timed step in the peer-mapped issue path's ready-event waits + host barriers
         # (rank 0; the GPU keeps running the next round's copy and kernels meanwhile)
         hw = puller.xchg.host_wait_s
+        # True: the exchanges waited on the GPU for the owners' ready counters (no host waits)
+        res["ipc_signals"] = bool(puller.xchg.signaled)
         res["ipc_host_wait_ms_per_step"] = {
             k: round((hw[k] - hw0[k]) * (1e3 if k != "calls" else 1) / max(1, a.steps), 3) for k in hw}
     if keep is not None:  # the swarm row serves its CDN from this world's pinned origin
@@ -679,6 +684,7 @@ def rank_main(a) -> None:
     }
     if "ipc_host_wait_ms_per_step" in head:
         out["extra"]["ipc_host_wait_ms_per_step"] = head["ipc_host_wait_ms_per_step"]
+        out["extra"]["ipc_signals"] = head.get("ipc_signals", False)
     printed = [False]
 
     def emit(extra_fields: dict) -> None:  # the one JSON line, printed once by rank 0

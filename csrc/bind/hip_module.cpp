@@ -24,6 +24,7 @@ namespace py = pybind11;
 void bind_hip_seed(py::module_& m);  // hip_seed.cpp
 void bind_hip_pull(py::module_& m);  // hip_pull.cpp
 void bind_hip_vmm(py::module_& m);   // hip_vmm.cpp
+void bind_hip_signals(py::module_& m);  // hip_signals.cpp
 
 namespace {
 
@@ -58,6 +59,7 @@ PYBIND11_MODULE(_hip, m) {
   bind_hip_seed(m);
   bind_hip_pull(m);
   bind_hip_vmm(m);
+  bind_hip_signals(m);
 
   m.def("device_count", &zg_device_count);
   // Pinned host memory (hipHostMalloc: exact size, unlike torch's power-of-two caching host

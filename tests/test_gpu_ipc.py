@@ -11,13 +11,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _rank(rank, port, q, mode, alloc="vmm"):
+def _rank(rank, port, q, mode, alloc="vmm", signals="1"):
     import faulthandler
     import sys
 
     import torch.distributed as dist
     faulthandler.dump_traceback_later(150, exit=True, file=sys.stderr)  # a stack instead of a silent hang
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZEST_IPC_SIGNALS=signals)
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
         from zest_amd import ops
@@ -42,31 +42,109 @@ def _rank(rank, port, q, mode, alloc="vmm"):
             p.check()
         same = all(torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size])
                    for f in w.xet_files)  # the alignment gaps between files are not part of any term
-        q.put((rank, ok, bool(same), p.n_rounds, p.bytes_received))
+        q.put((rank, ok, bool(same), p.n_rounds, p.bytes_received, p.xchg.signaled))
         dist.barrier()
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, False, repr(e), 0, 0))
+        q.put((rank, False, repr(e), 0, 0, None))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,alloc", [("ipc", "vmm"), ("xgmi", "vmm"), ("xgmi", "torch")])
-def test_ipc_exchange_two_ranks_one_gpu(mode, alloc):
+@pytest.mark.parametrize("mode,alloc,signals", [("ipc", "vmm", "1"), ("xgmi", "vmm", "1"), ("xgmi", "torch", "1"),
+                                                ("ipc", "vmm", "0"), ("xgmi", "vmm", "0")])
+def test_ipc_exchange_two_ranks_one_gpu(mode, alloc, signals):
     """vmm: the arena is a HIP VMM mapping shared through dmabuf fds (what bench.py uses); torch: a
-    caching-allocator tensor shared with hipIpcGetMemHandle (small arenas only, see engine.py)."""
+    caching-allocator tensor shared with hipIpcGetMemHandle (small arenas only, see engine.py).
+    signals=1: the exchanges wait on the GPU for the owners' shared ready counters; 0: host event
+    synchronize + host barrier per round."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29700 + 50 * (mode == "xgmi") + 100 * (alloc == "torch") + os.getpid() % 50
-    procs = [ctx.Process(target=_rank, args=(r, port, q, mode, alloc)) for r in range(2)]
+    port = 29700 + 50 * (mode == "xgmi") + 100 * (alloc == "torch") + 150 * (signals == "0") + os.getpid() % 50
+    procs = [ctx.Process(target=_rank, args=(r, port, q, mode, alloc, signals)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for rank, ok, equal, rounds, recv in res:
+    for rank, ok, equal, rounds, recv, signaled in res:
         assert ok is True and equal is True, res
         assert rounds > 1 and recv > 0
+        assert signaled is (signals == "1"), res
+
+
+def _signals_child(path, q):
+    """One process, two mappings of one shared page: a stream gated by hipStreamWaitValue32 runs
+    only once the counter reaches the value (not before, not at a smaller value), and set_after
+    stores a counter stream-ordered behind earlier work."""
+    import faulthandler
+    import sys
+    import time
+    faulthandler.dump_traceback_later(60, exit=True, file=sys.stderr)
+    try:
+        from zest_amd import ops
+        H = ops.hip()
+        torch.cuda.set_device(0)
+        if not H.can_stream_wait_value(0):
+            q.put("unsupported")
+            return
+        a = H.signals_open(path, 2, True, 0)
+        b = H.signals_open(path, 2, False, 0)
+        os.unlink(path)
+        x = torch.zeros(4, device="cuda:0")
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            a.wait_on(1, 5, st.cuda_stream)
+            x.fill_(7)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        time.sleep(0.2)
+        early = ev.query()
+        b.store(1, 4)
+        time.sleep(0.2)
+        below = ev.query()
+        b.store(1, 5)
+        t0 = time.time()
+        while not ev.query() and time.time() - t0 < 10:
+            time.sleep(0.005)
+        released = ev.query()
+        ok_x = released and float(x[0].item()) == 7.0
+        other = torch.cuda.Stream()
+        y = torch.randn(2048, 2048, device="cuda:0")
+        with torch.cuda.stream(other):
+            for _ in range(20):
+                y = y @ y.T / 2048.0
+            a.set_after(0, 1, other.cuda_stream)
+        with torch.cuda.stream(st):
+            a.wait_on(0, 1, st.cuda_stream)
+            ev2 = torch.cuda.Event()
+            ev2.record(st)
+        t0 = time.time()
+        while not ev2.query() and time.time() - t0 < 10:
+            time.sleep(0.005)
+        q.put((early, below, released, ok_x, ev2.query(), b.value(0), b.value(1)))
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+
+
+def test_peer_signals_gate_streams():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = f"/dev/shm/zest-sig-test-{os.getpid()}"
+    p = ctx.Process(target=_signals_child, args=(path, q))
+    p.start()
+    try:
+        got = q.get(timeout=120)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+        if os.path.exists(path):
+            os.unlink(path)
+    if got == "unsupported":
+        pytest.skip("hipStreamWaitValue32 unsupported on this device")
+    assert got == (False, False, True, True, True, 1, 5), got
 
 
 def test_peer_gather_kernel_segments():

@@ -447,12 +447,20 @@ class DevicePuller:
     def _exchange(self, k: int, mode: str | None = None):
         """Replicate round k's regions to every rank.  Peer-mapped modes wait for
         this rank's round-k kernels (event recorded by step()), then a host barrier."""
-        return self.xchg.exchange(self.regions[k], mode, ready=self._ipc_done.get(k))
+        done = self._ipc_done.get(k)
+        if isinstance(done, int):  # a ready-counter sequence number (signal_ready): GPU-side waits
+            return self.xchg.exchange(self.regions[k], mode, seq=done)
+        return self.xchg.exchange(self.regions[k], mode, ready=done)
 
     def enable_ipc(self, mapped: "PeerArenas | None" = None) -> bool:
         """Map every peer's arena into this process (HIP VMM / IPC) for the ``ipc`` / ``xgmi``
-        exchanges.  Collective; True only if every rank mapped every peer."""
-        return self.xchg.enable_ipc(mapped)
+        exchanges.  Collective; True only if every rank mapped every peer.  Also shares the ranks'
+        ready counters (RoundExchange.enable_signals), so a step's exchanges wait on the GPU for
+        the owners' rounds instead of in a host event synchronize + barrier per round."""
+        if not self.xchg.enable_ipc(mapped):
+            return False
+        self.xchg.enable_signals()
+        return True
 
     def autotune_exchange(self, modes=EXCHANGE_MODES, max_rounds: int = 4) -> dict:
         """Time each exchange strategy over the first full-size rounds and keep the fastest (setup,
@@ -553,6 +561,11 @@ class DevicePuller:
             lanes = (self.lane_stream, self.side_stream)
             for ln in lanes:
                 ln.wait_stream(main)  # hashes.zero_() above, and the caller's earlier work
+            if self.n_ranks > 1 and self.xchg.signaled and self.exchange in PEER_MAPPED_MODES:
+                # the peers' copies into this arena must land after the caller's own writes to it
+                # (the warm-up poisons the arena on the main stream): r5v's first signaled
+                # rehearsal lost that race in its second data mode (hash mismatch at index 0)
+                self.xchg.order_after(main)
             for k, rw in enumerate(self.rounds):
                 comp, ws = lanes[k % 2], self.ws_lanes[k % 2]
                 src = self.staging[k % len(self.staging)]
@@ -583,8 +596,11 @@ class DevicePuller:
                             # queued behind the one in flight while the host waits on the event and
                             # the host barrier (lag 1 left one copy queued: the barrier's wake-up
                             # skew became a PCIe gap every round)
-                            self._ipc_done[k] = torch.cuda.Event()
-                            self._ipc_done[k].record(comp)
+                            if self.xchg.signaled:
+                                self._ipc_done[k] = self.xchg.signal_ready(comp)
+                            else:
+                                self._ipc_done[k] = torch.cuda.Event()
+                                self._ipc_done[k].record(comp)
                             if k >= self.ipc_lag:
                                 j = k - self.ipc_lag
                                 works += self._hash_received(j, self._exchange(j))

@@ -346,6 +346,8 @@ class RoundExchange:
         self._gather_n = 0
         self._peer_arenas = None
         self._host_group = None
+        self._signals = None          # shared ready counters (enable_signals)
+        self._sig_sent = 0            # signal_ready calls so far (= this rank's counter value)
 
     # -- helpers ------------------------------------------------------------------------------
     def backend(self) -> str:
@@ -380,20 +382,101 @@ class RoundExchange:
         self._ipc_streams = [role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
         return True
 
+    # -- device-side readiness (csrc/bind/hip_signals.cpp) ------------------------------------
+    @property
+    def signaled(self) -> bool:
+        return self._signals is not None
+
+    def enable_signals(self) -> bool:
+        """Collective over the mapped ranks: share one page of ready counters (one per rank) so that
+        peer-mapped exchanges wait on the GPU (hipStreamWaitValue32 on the owner's counter) instead
+        of a host event synchronize + host barrier per round.  Off with ZEST_IPC_SIGNALS=0; False
+        (and nothing changes) unless every rank mapped the page and its device can wait on a value."""
+        import uuid
+
+        import torch.distributed as dist
+        if self._peer_arenas is None or self._host_group is None:
+            return False
+        if os.environ.get("ZEST_IPC_SIGNALS", "1") == "0":
+            return False
+        H = ops.hip()
+        dev = self.device.index or 0
+        try:
+            ok = int(bool(H.can_stream_wait_value(dev)))
+        except Exception:  # noqa: BLE001
+            ok = 0
+        g = self._host_group
+
+        def agree(v: int) -> int:
+            t = torch.tensor([v], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
+            return int(t.item())
+
+        box = [f"/dev/shm/zest-sig-{uuid.uuid4().hex}" if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_process_group_ranks(g)[0], group=g)
+        path = box[0]
+        sig = None
+        if self.rank == 0 and ok:
+            try:
+                sig = H.signals_open(path, self.n_ranks, True, dev)
+            except Exception:  # noqa: BLE001
+                ok = 0
+        ok = agree(ok)  # the page exists (or nobody opens it)
+        if ok and self.rank != 0:
+            try:
+                sig = H.signals_open(path, self.n_ranks, False, dev)
+            except Exception:  # noqa: BLE001
+                sig, ok = None, 0
+        ok = agree(ok)  # everyone mapped it: the name is no longer needed
+        if self.rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+        if not ok:
+            return False
+        self._signals = sig
+        self._sig_sent = 0
+        self._signal_stream = role_stream(self.device, "signal")
+        return True
+
+    def order_after(self, stream) -> None:
+        """With ready counters the exchange streams wait only for the owners' counters, not for this
+        rank's host: a caller that writes the receiving regions itself (bench.py's warm-up poisons
+        the arena on the main stream before each step) orders the exchange streams after that work
+        with this.  (The host-synchronized path got the ordering from its event synchronize.)"""
+        for st in getattr(self, "_ipc_streams", ()):
+            st.wait_stream(stream)
+
+    def signal_ready(self, stream) -> int:
+        """This rank's next region is complete once `stream`'s queued work is: queue the counter
+        update behind it (on the signal stream, so `stream` never waits for the host function).
+        Returns the sequence number the peers' exchange() must be given for that region.  Every
+        rank calls this once per region, in the same order (ranks with empty regions included)."""
+        self._sig_sent += 1
+        ss = self._signal_stream
+        ss.wait_stream(stream)
+        self._signals.set_after(self.rank, self._sig_sent, ss.cuda_stream)
+        return self._sig_sent
+
     # -- one exchange -------------------------------------------------------------------------
-    def exchange(self, regions, mode: str | None = None, ready=None, synced: bool = False) -> list:
+    def exchange(self, regions, mode: str | None = None, ready=None, synced: bool = False, seq: int | None = None) -> list:
         """Replicate `regions` ([lo, hi) per rank; empty = that rank sends nothing) to every rank.
         Returns work handles to wait on (stream-ordered on the GPU).
 
         Peer-mapped modes read the owners' arenas directly, so the owners' regions must be complete:
-        `ready` (an event recorded after this rank's region was written) is host-synchronized and a
-        host barrier follows; `synced=True` says the caller already synchronized every owner (e.g.
-        a control-plane all_gather after blocking fetches) and skips both."""
+        with shared ready counters (enable_signals) and `seq` (what every owner's signal_ready
+        returned for these regions) the exchange streams wait on the GPU for each owner's counter;
+        otherwise `ready` (an event recorded after this rank's region was written) is
+        host-synchronized and a host barrier follows; `synced=True` says the caller already
+        synchronized every owner (e.g. a control-plane all_gather after blocking fetches) and skips
+        both."""
         mode = mode or self.mode
         regions = [(int(lo), int(hi)) for lo, hi in regions]
         self.bytes_moved += sum(hi - lo for p, (lo, hi) in enumerate(regions) if p != self.rank and hi > lo)
         if mode in PEER_MAPPED_MODES:
-            return self._exchange_ipc(regions, kernel=(mode == "xgmi"), ready=ready, synced=synced)
+            return self._exchange_ipc(regions, kernel=(mode == "xgmi"), ready=ready, synced=synced,
+                                      seq=seq if self._signals is not None else None)
         if mode == "bcast":
             return self._exchange_bcast(regions)
         if mode == "allgather":
@@ -482,11 +565,13 @@ class RoundExchange:
         self._gather_used[b] = True
         return [StreamJoin(self._unpack_stream)]
 
-    def _exchange_ipc(self, regions, kernel: bool = False, ready=None, synced: bool = False):
+    def _exchange_ipc(self, regions, kernel: bool = False, ready=None, synced: bool = False, seq=None):
         """Pull every peer's region from its mapped arena: DMA copies (``ipc``) or one K8 gather
-        kernel (``xgmi``)."""
+        kernel (``xgmi``).  With `seq`, each exchange stream first waits (on the GPU) for the
+        counters of the owners it reads."""
         import torch.distributed as dist
-        if not synced:
+        sig = self._signals if seq is not None else None
+        if sig is None and not synced:
             if ready is None:  # everything queued so far on this rank
                 ready = torch.cuda.Event()
                 ready.record(torch.cuda.current_stream(self.device))
@@ -503,6 +588,9 @@ class RoundExchange:
         if kernel:
             segs = [(self._peer_arenas[p].data_ptr() + lo, self.arena.data_ptr() + lo, hi - lo) for p, lo, hi in recv]
             st = self._ipc_streams[0]
+            if sig is not None:
+                for p, _, _ in recv:
+                    sig.wait_on(p, int(seq), st.cuda_stream)
             for i in range(0, len(segs), 16):
                 part = segs[i:i + 16]
                 H.peer_gather([a for a, _, _ in part], [b for _, b, _ in part], [n for _, _, n in part],
@@ -510,10 +598,14 @@ class RoundExchange:
             self._inject_gather_fault(recv, st)
             return [StreamJoin(st)] if segs else []
         used = []
-        for p, lo, hi in recv:
-            st = self._ipc_streams[len(used) % len(self._ipc_streams)]
+        for i, (p, lo, hi) in enumerate(recv):
+            # peers dealt round-robin over the streams (7 peers on 4 streams: 2/2/2/1 copies each;
+            # picking by len(used) put peers 5-7 behind peer 1 on the first stream)
+            st = self._ipc_streams[i % len(self._ipc_streams)]
             if st not in used:
                 used.append(st)
+            if sig is not None:
+                sig.wait_on(p, int(seq), st.cuda_stream)
             H.memcpy_async(self.arena.data_ptr() + lo, self._peer_arenas[p].data_ptr() + lo, hi - lo, st.cuda_stream)
         if used:
             self._inject_gather_fault(recv, used[-1], used)

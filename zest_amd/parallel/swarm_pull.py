@@ -595,7 +595,10 @@ class _Swarm:
             # (a root that has not stamped its first heartbeat yet counts from when this wait began)
             if time.time() - max(m._last_beat(root), t0) > m.stale_s:
                 raise _RankLost(f"rank {root} stopped while listing {self.repo}")  # survivors re-plan
-            time.sleep(0.05)
+            # 2 ms polls for the first second (a plan is usually ready in tens of ms; a fixed 50 ms
+            # poll left the other ranks up to 50 ms behind rank 0, which then waited for them in the
+            # possession gather: 44 ms of a 0.44 s 2-rank pull, profiles/r5/rehearsal_n2_r5t/lag2.log)
+            time.sleep(0.002 if time.time() - t0 < 1.0 else 0.05)
         return json.loads(m.store.get(key))
 
     # -- setup --------------------------------------------------------------------------------
