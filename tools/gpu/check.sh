@@ -128,7 +128,8 @@ for step in "$@"; do
                grep -h "aggregate" $log
                python tools/gpu/overlap.py $OUT/ct --between spin_kernel > $OUT/overlap_swarm.txt 2>&1
                python tools/gpu/overlap.py $OUT/ct > $OUT/overlap_all.txt 2>&1
-               cat $OUT/overlap_swarm.txt $OUT/overlap_all.txt; rm -rf $OUT/ct ;;
+               python tools/gpu/copy_rates.py $OUT/ct > $OUT/copy_rates.txt 2>&1
+               cat $OUT/overlap_swarm.txt $OUT/overlap_all.txt $OUT/copy_rates.txt; rm -rf $OUT/ct ;;
     config2) # BASELINE config 2 on the public path: rank 0 warm, rank 1 cold, ranks share the GPU (gloo)
              ZEST_BENCH_BACKEND=gloo timeout -k 10 600 python -u tools/config2_rehearsal.py \
                --model ${C2_MODEL:-llama-3.1-8b} --mode ${C2_MODE:-bf16} --ranks ${C2_RANKS:-2} \
