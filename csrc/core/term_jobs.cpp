@@ -246,4 +246,18 @@ std::vector<TermJobResult> fetch_terms_host(XetBridge& bridge, ReconCache& recs,
   return out;
 }
 
+std::vector<std::pair<uint64_t, uint64_t>> copy_ranges(const std::vector<uint64_t>& at,
+                                                       const std::vector<uint64_t>& len, uint64_t max_gap) {
+  std::vector<std::pair<uint64_t, uint64_t>> r;
+  for (size_t i = 0; i < at.size() && i < len.size(); ++i)
+    if (len[i]) r.emplace_back(at[i], at[i] + len[i]);
+  std::sort(r.begin(), r.end());
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  for (const auto& x : r) {
+    if (!out.empty() && x.first <= out.back().second + max_gap) out.back().second = std::max(out.back().second, x.second);
+    else out.push_back(x);
+  }
+  return out;
+}
+
 }  // namespace zest

@@ -15,6 +15,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "bridge.h"
@@ -98,5 +99,11 @@ std::vector<uint8_t> cached_terms(const storage::XorbCache& cache, const std::ve
 std::vector<TermJobResult> fetch_terms_host(XetBridge& bridge, ReconCache& recs, SettleBook& book,
                                             const std::vector<TermJob>& jobs, uint8_t* hashes, int threads,
                                             bool repair);
+
+// [lo, hi) byte ranges covering the runs (at[i], len[i]) of a staging slot, in address order, with
+// neighbours whose gap is at most max_gap merged (one copy command instead of two); empty runs are
+// skipped.  The device pull copies only these to the GPU, not the holes between reserved regions.
+std::vector<std::pair<uint64_t, uint64_t>> copy_ranges(const std::vector<uint64_t>& at,
+                                                       const std::vector<uint64_t>& len, uint64_t max_gap);
 
 }  // namespace zest

@@ -582,6 +582,7 @@ struct DeviceXetPull::Impl {
         cv.wait(g, [&] { return std::all_of(copies.begin(), copies.end(), [](size_t c) { return c == 0; }); });
       };
       bool abort = false;
+      uint64_t h2d_bytes = 0;  // payload bytes queued for H2D this pass (timeline)
       std::atomic<size_t> k{0};
       auto fail = [&](const std::string& what) {
         std::lock_guard<std::mutex> g(mu);
@@ -756,7 +757,20 @@ struct DeviceXetPull::Impl {
           submit_span.arg("\"terms\":" + std::to_string(bt.end - bt.begin) + ",\"bytes\":" + std::to_string(top));
           if (b >= S) hip_check(hipStreamWaitEvent(copy_stream_, ev[2 * (b - S) + 1], 0), "hipStreamWaitEvent");
           if (tev) hip_check(hipEventRecord(tev[4 * b], copy_stream_), "event");
-          hip_check(hipMemcpyAsync(s.dev.p, s.host, top, hipMemcpyHostToDevice, copy_stream_), "H2D");
+          // Only the fetched bytes cross PCIe: each term owns a region sized for its worst case
+          // (term_bound: every chunk stored raw), and a compressed run fills ~88 % of it on bf16
+          // weights, so one copy of [0, top) moved the holes too (70B bf16 public path: 141 GB over
+          // PCIe for 123.6 GB of runs, 55.2 GB/s against the engine's 64.3).  Runs are copied to
+          // the same offsets (the chunk records address the slot), merging neighbours whose gap is
+          // under 1 MiB.
+          // (ZEST_H2D_WHOLE_SPAN=1: the old single copy of [0, top), for A/B runs)
+          static const bool whole_span = env_size("ZEST_H2D_WHOLE_SPAN", 0) != 0;
+          const auto ranges = whole_span ? std::vector<std::pair<uint64_t, uint64_t>>{{0, top}}
+                                         : copy_ranges(bt.src_at, bt.len, uint64_t(1) << 20);
+          for (const auto& [lo, hi] : ranges) {
+            hip_check(hipMemcpyAsync(s.dev.p + lo, s.host + lo, hi - lo, hipMemcpyHostToDevice, copy_stream_), "H2D");
+            h2d_bytes += hi - lo;
+          }
           if (nchunks)
             hip_check(hipMemcpyAsync(s.chunks_dev.p, s.recs(), sizeof(ZgChunk) * size_t(nchunks), hipMemcpyHostToDevice,
                                      copy_stream_),
@@ -795,7 +809,7 @@ struct DeviceXetPull::Impl {
       stop_releaser();
       hip_check(e1, "sync copy stream");
       hip_check(e2, "sync compute stream");
-      if (tev && nb) record_timeline(tev, nb);
+      if (tev && nb) record_timeline(tev, nb, h2d_bytes);
     }
     if (!fetch_err.empty()) return at;
     hip_check(hipMemcpy(&at.ingest_err, err_.p, sizeof at.ingest_err, hipMemcpyDeviceToHost), "err D2H");
@@ -804,7 +818,7 @@ struct DeviceXetPull::Impl {
 
   // Device timeline of the last timed pass: intervals [copy start, copy end] and [kernels start,
   // kernels end] per batch (ms from the first copy), their unions, and the time both ran at once.
-  void record_timeline(hipEvent_t* tev, size_t nb) {
+  void record_timeline(hipEvent_t* tev, size_t nb, uint64_t h2d_bytes) {
     std::vector<std::pair<double, double>> cp, kn;
     for (size_t b = 0; b < nb; ++b) {
       float a = 0, c = 0, d = 0, e = 0;
@@ -840,7 +854,8 @@ struct DeviceXetPull::Impl {
     std::lock_guard<std::mutex> g(timeline_mu_);
     timeline_ = "{\"batches\":" + std::to_string(nb) + ",\"window_ms\":" + std::to_string(window) +
                 ",\"h2d_busy_ms\":" + std::to_string(total(uc)) + ",\"kernel_busy_ms\":" + std::to_string(total(uk)) +
-                ",\"overlap_ms\":" + std::to_string(both) + "}";
+                ",\"overlap_ms\":" + std::to_string(both) + ",\"h2d_bytes\":" + std::to_string(h2d_bytes) +
+                ",\"h2d_GBps_busy\":" + std::to_string(total(uc) > 0 ? double(h2d_bytes) / total(uc) / 1e6 : 0.0) + "}";
   }
 
   hipEvent_t* take_timing_events(size_t n) {

@@ -90,7 +90,7 @@ class DeviceXetPull {
   std::string cache_writer_json() const;  // {"queued_bytes", "written_bytes", "dropped_bytes"}
   // ZEST_DEVICE_TIMING=1: the last pass's device timeline from timed HIP events around every
   // batch's H2D copy and kernels: {"batches", "window_ms", "h2d_busy_ms", "kernel_busy_ms",
-  // "overlap_ms"} ({} otherwise)
+  // "overlap_ms", "h2d_bytes", "h2d_GBps_busy"} ({} otherwise)
   std::string timeline_json() const;
 
   struct Shared;

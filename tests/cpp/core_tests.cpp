@@ -471,6 +471,17 @@ TEST(xorb_cache_quarantine_per_fetch) {
   CHECK(cache.sweep_pending(3600) == 2 && storage::exists(live));
 }
 
+TEST(copy_ranges_skip_holes) {
+  using R = std::vector<std::pair<uint64_t, uint64_t>>;
+  // three reserved regions of 100 bytes holding runs of 90, 0 and 70 bytes; one run starts mid-region
+  CHECK((zest::copy_ranges({0, 100, 210}, {90, 0, 70}, 0) == R{{0, 90}, {210, 280}}));
+  // gaps of at most max_gap merge; out-of-order input is sorted first
+  CHECK((zest::copy_ranges({210, 0}, {70, 90}, 120) == R{{0, 280}}));
+  CHECK((zest::copy_ranges({0, 95}, {90, 5}, 5) == R{{0, 100}}));
+  CHECK((zest::copy_ranges({0, 96}, {90, 5}, 5) == R{{0, 90}, {96, 101}}));
+  CHECK(zest::copy_ranges({}, {}, 1).empty());
+}
+
 TEST(peer_pool_leases) {
   // Lease accounting of the connection pool against a loopback seeding server: a lease raises its
   // session's user count by exactly one for its lifetime, busy sessions make the pool open more
