@@ -114,16 +114,19 @@ __global__ void k_index_terms(const uint8_t* __restrict__ src, const ZgTerm* __r
 // chunk: ~1000 chained loads per 64 MiB xorb run, ~0.6 ms whatever the GPU's width.  Here:
 //   scan   every byte position of the span is tested in parallel for a plausible chunk header
 //          (version 0, scheme <= 2, 1 <= ulen <= 128 KiB, clen >= 1, raw => clen == ulen, payload
-//          inside its run); candidates (~one per chunk: a false positive needs ~30 bits of luck)
-//          are appended to their term's list.
-//   link   one workgroup per term sorts its candidates in LDS (bitonic) and checks that they form
-//          exactly the chain from offset 0 to the run's end with n_chunks links; then a block
-//          prefix sum of the uncompressed sizes gives every chunk's output offset and the records
-//          are written in parallel.
-// Anything else -- a false candidate, a list over capacity, a broken or short chain -- falls back
-// to the serial walk for that term, so records and error codes are exactly walk_term's.
+//          inside its run, a compressed payload starting with the LZ4 frame magic); candidates
+//          (one per chunk, plus a few look-alikes per 256 MiB) are appended to their term's list.
+//   link   one workgroup per term sorts its candidates in LDS (bitonic), picks the chain from
+//          offset 0 to the run's end out of them (successor lookups, see k_hdr_link) and checks
+//          it has n_chunks links; block prefix sums give every chunk's index and output offset and
+//          the records are written in parallel.
+// Anything else -- a list over capacity, a broken, ambiguous or short chain -- falls back to the
+// serial walk for that term, so records and error codes are exactly walk_term's.
 constexpr int kScanThreads = 256;
-constexpr uint32_t kScanBytesPerThread = 16;
+// 64 positions per thread from 80 loaded bytes (5 x 16 B): 1.25 loads per position byte instead of
+// 2 with 16 positions from 32 bytes
+constexpr uint32_t kScanBytesPerThread = 64;
+constexpr uint32_t kScanWords = (kScanBytesPerThread + 16) / 4;
 constexpr uint32_t kCandCap = 8192;  // chunks of a 64 MiB xorb at the 8 KiB CDC minimum
 constexpr int kLinkThreads = 1024;
 
@@ -160,9 +163,15 @@ __global__ void __launch_bounds__(kScanThreads) k_hdr_scan(const uint8_t* __rest
   }
   uint64_t t0 = terms[t].src, t1 = t0 + terms[t].src_len;
   uint64_t nx = t + 1 < n_terms ? terms[t + 1].src : ~uint64_t(0);
-  const uint4 v0 = *reinterpret_cast<const uint4*>(src + q);
-  const uint4 v1 = *reinterpret_cast<const uint4*>(src + q + 16);  // padded buffers: safe past the end
-  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t w[kScanWords];
+#pragma unroll
+  for (uint32_t i = 0; i < kScanWords / 4; ++i) {  // padded buffers: safe past the end
+    const uint4 v = *reinterpret_cast<const uint4*>(src + q + 16 * i);
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kScanBytesPerThread; ++k) {
     const uint64_t p = q + k;
@@ -184,23 +193,52 @@ __global__ void __launch_bounds__(kScanThreads) k_hdr_scan(const uint8_t* __rest
   }
 }
 
+// Link.  The candidates are sorted, then every candidate's successor (its offset + 8 + clen) is
+// looked up among them.  False candidates do occur: LZ4 streams of BG4 bf16 weights hold a few
+// raw-header look-alikes ([00 x y z 00 x y z], clen == ulen) per 256 MiB, so demanding exactly
+// n_chunks candidates sent every term of a 256 MiB batch back to the serial walk.  The chain is
+// instead picked out of the candidate set G' = {candidates with a successor (a candidate, or the
+// run's end) that sit at offset 0 or are some candidate's successor}.  If G' contains offset 0, is
+// closed under the successor, and has exactly n_chunks members, it IS the true chain: the true
+// chain starts at 0 and follows successors, so closure puts all of it in G', and the count leaves
+// room for nothing else.  Otherwise the serial walk decides (records and error codes stay exactly
+// walk_term's).
+constexpr uint32_t kEnd = 0xFFFFFFFEu, kNone = 0xFFFFFFFFu;
+constexpr uint32_t kPointed = 1u << 31, kGood = 1u << 30;
+constexpr uint32_t kFellBack = 1u << 31;  // in counts[t] after the link: term t took the serial walk
+
+__device__ __forceinline__ uint32_t lds_find(const uint32_t* key, uint32_t n, uint32_t v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && key[lo] == v ? lo : kNone;
+}
+
 __global__ void __launch_bounds__(kLinkThreads) k_hdr_link(const uint8_t* __restrict__ src,
                                                           const ZgTerm* __restrict__ terms,
-                                                          const uint32_t* __restrict__ counts,
+                                                          uint32_t* __restrict__ counts,  // kFellBack marks a serial-walk term
                                                           const uint32_t* __restrict__ cands,
                                                           ZgChunk* __restrict__ chunks, unsigned long long* err) {
   __shared__ uint32_t key[kCandCap];   // candidate offsets, sorted
-  __shared__ uint32_t ul[kCandCap];    // uncompressed sizes -> exclusive prefix sums
-  __shared__ uint32_t cs[kCandCap];    // clen | scheme << 24
-  __shared__ uint32_t part[kLinkThreads / kWave];
+  __shared__ uint32_t ul[kCandCap];    // uncompressed sizes
+  __shared__ uint32_t cs[kCandCap];    // clen | scheme << 24 | kPointed | kGood
+  __shared__ uint32_t nx[kCandCap];    // index of the successor candidate, kEnd or kNone
+  __shared__ uint32_t part_n[kLinkThreads / kWave];
+  __shared__ uint32_t part_u[kLinkThreads / kWave];
   __shared__ int ok;
   const int t = blockIdx.x;
   const ZgTerm tm = terms[t];
   const uint32_t n = counts[t];
   const int tid = threadIdx.x;
-  // the fast path needs exactly one candidate per planned chunk (terms of at most 4 GiB)
-  if (n != tm.n_chunks || n == 0 || n > kCandCap || tm.src_len >= (uint64_t(1) << 32)) {
-    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+  // the fast path needs at least one candidate per planned chunk (terms of at most 4 GiB)
+  if (n < tm.n_chunks || n == 0 || n > kCandCap || tm.src_len >= (uint64_t(1) << 32)) {
+    if (tid == 0) {
+      counts[t] = n | kFellBack;
+      walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+    }
     return;
   }
   uint32_t P = 1;
@@ -223,63 +261,84 @@ __global__ void __launch_bounds__(kLinkThreads) k_hdr_link(const uint8_t* __rest
       __syncthreads();
     }
   }
-  // link check: candidate i's payload ends exactly where candidate i + 1 starts, the first sits at
-  // offset 0 and the last ends the run
+  // successors
   const uint8_t* run = src + tm.src;
   for (uint32_t i = tid; i < n; i += kLinkThreads) {
     uint32_t lo, hi;
     load8(run + key[i], lo, hi);
-    const uint32_t clen = lo >> 8, ulen = hi >> 8;
+    const uint32_t clen = lo >> 8;
     const uint64_t end = uint64_t(key[i]) + 8 + clen;
-    const uint64_t want = i + 1 < n ? uint64_t(key[i + 1]) : tm.src_len;
-    if (end != want || (i == 0 && key[0] != 0)) ok = 0;
-    ul[i] = ulen;
+    nx[i] = end == tm.src_len ? kEnd : end < tm.src_len ? lds_find(key, n, uint32_t(end)) : kNone;
+    ul[i] = hi >> 8;
     cs[i] = clen | (hi & 0xFF) << 24;
   }
   __syncthreads();
-  if (!ok) {  // a false candidate or a broken chain: the serial walk decides
-    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
-    return;
-  }
-  // exclusive prefix sum of ul[0, n): each thread owns a contiguous slice
+  for (uint32_t i = tid; i < n; i += kLinkThreads)
+    if (nx[i] < n) atomicOr(&cs[nx[i]], kPointed);
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kLinkThreads)
+    if (nx[i] != kNone && (key[i] == 0 || (cs[i] & kPointed))) atomicOr(&cs[i], kGood);
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kLinkThreads)  // closed under the successor
+    if ((cs[i] & kGood) && nx[i] != kEnd && !(cs[nx[i]] & kGood)) ok = 0;
+  if (tid == 0 && (key[0] != 0 || !(cs[0] & kGood))) ok = 0;
+  // exclusive prefix sums (chunk count, uncompressed bytes) over the chain members: each thread
+  // owns a contiguous slice, then a wave scan and the wave totals
   const uint32_t per = (n + kLinkThreads - 1) / kLinkThreads;
   const uint32_t a = min(n, tid * per), b = min(n, a + per);
-  uint32_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += ul[i];
-  // block scan of the per-thread sums: wave inclusive scan, then the wave totals
-  uint32_t inc = sum;
+  uint32_t cnt = 0, sum = 0;
+  for (uint32_t i = a; i < b; ++i)
+    if (cs[i] & kGood) {
+      ++cnt;
+      sum += ul[i];
+    }
+  uint32_t inc_n = cnt, inc_u = sum;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, kWave);
-    if (int(lane_id()) >= d) inc += y;
+    const uint32_t yn = __shfl_up(inc_n, d, kWave), yu = __shfl_up(inc_u, d, kWave);
+    if (int(lane_id()) >= d) {
+      inc_n += yn;
+      inc_u += yu;
+    }
   }
   const int wv = tid / kWave;
-  if (lane_id() == kWave - 1) part[wv] = inc;
+  if (lane_id() == kWave - 1) {
+    part_n[wv] = inc_n;
+    part_u[wv] = inc_u;
+  }
   __syncthreads();
   if (tid == 0) {
-    uint32_t run_sum = 0;
+    uint32_t rn = 0, ru = 0;
     for (int k = 0; k < kLinkThreads / kWave; ++k) {
-      const uint32_t x = part[k];
-      part[k] = run_sum;
-      run_sum += x;
+      const uint32_t xn = part_n[k], xu = part_u[k];
+      part_n[k] = rn;
+      part_u[k] = ru;
+      rn += xn;
+      ru += xu;
     }
-    if (tm.ulen != 0 && run_sum != tm.ulen) ok = 0;
+    if (rn != tm.n_chunks || (tm.ulen != 0 && ru != tm.ulen)) ok = 0;
   }
   __syncthreads();
-  if (!ok) {
-    if (tid == 0) walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+  if (!ok) {  // a broken or ambiguous chain: the serial walk decides
+    if (tid == 0) {
+      counts[t] = n | kFellBack;
+      walk_term(tm, t, chunks, err, GlobalHdr{src + tm.src});
+    }
     return;
   }
-  uint32_t off = part[wv] + inc - sum;  // exclusive prefix of this thread's slice
+  uint32_t c = part_n[wv] + inc_n - cnt;  // this slice's first chunk index
+  uint32_t off = part_u[wv] + inc_u - sum;
   for (uint32_t i = a; i < b; ++i) {
+    if (!(cs[i] & kGood)) continue;
     ZgChunk ch;
     ch.src = tm.src + key[i] + 8;
     ch.dst = tm.dst + off;
     ch.clen = cs[i] & 0xFFFFFF;
     ch.ulen = ul[i];
-    ch.scheme = cs[i] >> 24;
+    ch.scheme = (cs[i] >> 24) & 0x3F;
     ch.term = uint32_t(t);
-    chunks[tm.chunk_base + i] = ch;
+    chunks[tm.chunk_base + c] = ch;
+    ++c;
     off += ul[i];
   }
 }

@@ -862,8 +862,12 @@ def test_device_puller_pipelines(pipeline, mode, compression):
         assert torch.equal(arena[f.arena_off:f.arena_off + f.size], want[f.arena_off:f.arena_off + f.size])
 
 
-def _index_both(src, terms, n_chunks):
-    """Chunk records + error word of the serial header walk and of the parallel scan/link walk."""
+FELL_BACK = 1 << 31  # k_hdr_link's mark in the scan's per-term candidate counts
+
+
+def _index_both(src, terms, n_chunks, fallbacks=None):
+    """Chunk records + error word of the serial header walk and of the parallel scan/link walk;
+    `fallbacks` (a list) receives, per term, whether the link handed it to the serial walk."""
     H = ops.hip()
     st = torch.cuda.current_stream().cuda_stream
     tdev = torch.from_numpy(terms.view(np.uint8).copy()).to(DEV)
@@ -880,15 +884,19 @@ def _index_both(src, terms, n_chunks):
             H.index_terms(src.data_ptr(), tdev.data_ptr(), len(terms), chunks.data_ptr(), err.data_ptr(), st)
         torch.cuda.synchronize()
         out.append((chunks.cpu().numpy().tobytes(), int(err.item())))
+        if scan and fallbacks is not None:
+            cnt = scr[:4 * len(terms)].cpu().numpy().view(np.uint32)
+            fallbacks[:] = [bool(int(c) & FELL_BACK) for c in cnt]
     return out
 
 
 @pytest.mark.parametrize("policy", ["none", "bg4", "auto"])
 def test_index_scan_matches_serial_walk(policy):
     """K4 parallel header walk (candidate scan + LDS sort/link + prefix sum) gives byte-identical
-    chunk records to the serial walk: clean runs at odd offsets; a raw chunk carrying a planted
-    header-like pattern (a false candidate -> that term falls back to the serial walk); and a
-    corrupted header (same error word)."""
+    chunk records to the serial walk: clean runs at odd offsets (no term falls back); a raw chunk
+    carrying a planted header-like pattern (a false candidate: the link picks the chain around it,
+    no fallback); two planted look-alikes where the first points at the second (an ambiguous set:
+    that term falls back to the serial walk); and a corrupted header (same error word)."""
     data, ends, b = _make_runs(policy, seed=3)
     body = b.serialize(False)
     nck = len(ends)
@@ -905,8 +913,10 @@ def test_index_scan_matches_serial_walk(policy):
         src_host += run + b"\x07" * (t + 1)
     src = ops.padded_empty(len(src_host), DEV)
     src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
-    (serial, e0), (scan, e1) = _index_both(src, terms, nck)
+    fb = []
+    (serial, e0), (scan, e1) = _index_both(src, terms, nck, fb)
     assert e0 == 0 and e1 == 0 and scan == serial
+    assert fb == [False] * 4, fb
     # the records are the real ones: ingest through them reproduces the data
     if policy == "none":
         # a planted plausible header (version 0, raw, clen == ulen == 16) inside term 1's first payload
@@ -914,8 +924,28 @@ def test_index_scan_matches_serial_walk(policy):
         pos = int(terms[t]["src"]) + 8 + 100
         src_host[pos:pos + 8] = bytes([0, 16, 0, 0, 0, 16, 0, 0])
         src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
-        (serial, e0), (scan, e1) = _index_both(src, terms, nck)
+        (serial, e0), (scan, e1) = _index_both(src, terms, nck, fb)
         assert e0 == 0 and e1 == 0 and scan == serial
+        assert fb == [False] * 4, fb
+        # term 3: look-alike A (clen 16) whose successor is look-alike B (clen 24): B is some
+        # candidate's successor, so the chosen set has one member too many -> the serial walk
+        t = 3
+        pa = int(terms[t]["src"]) + 8 + 200
+        pb = pa + 8 + 16
+        src_host[pa:pa + 8] = bytes([0, 16, 0, 0, 0, 16, 0, 0])
+        src_host[pb:pb + 8] = bytes([0, 24, 0, 0, 0, 24, 0, 0])
+        # ...and B's successor is a real header (the chunk after the first one), so B passes the
+        # successor test: only the member count can reject the set
+        first = int(bounds[int(terms[t]["chunk_base"])]) - (0 if int(terms[t]["chunk_base"]) == 0
+                                                           else int(bounds[int(terms[t]["chunk_base"]) - 1]))
+        nxt = int(terms[t]["src"]) + first
+        if nxt - (pb + 8) > 0 and nxt - (pb + 8) < (1 << 17):
+            cl = nxt - (pb + 8)
+            src_host[pb:pb + 8] = bytes([0, cl & 0xFF, (cl >> 8) & 0xFF, cl >> 16, 0, cl & 0xFF, (cl >> 8) & 0xFF, cl >> 16])
+        src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
+        (serial, e0), (scan, e1) = _index_both(src, terms, nck, fb)
+        assert e0 == 0 and e1 == 0 and scan == serial
+        assert fb == [False, False, False, True], fb
     # a corrupted header in term 2: both walks report the same error and the same zeroed records
     pos = int(terms[2]["src"])
     src_host[pos + 4] = 9

@@ -252,20 +252,25 @@ class IngestWorkspace:
 FUSED_INGEST = os.environ.get("ZEST_FUSED_INGEST", "1") != "0"
 
 
-# Opt-in (ZEST_INDEX_SCAN=1): measured slower than the serial walk on the box (gpubench 256 MiB:
-# xorb_verify_gpu 958 -> 1042 us, lz4_decode_gpu 3.96 -> 9.69 ms -- LZ4 streams of BG4 bf16 weights
-# are full of header-like byte patterns, so candidates run into the millions and their per-term
-# atomic counter serializes; profiles/r5/gpubench256_scan_r5c.json).
-INDEX_SCAN = os.environ.get("ZEST_INDEX_SCAN", "0") == "1"
+# The parallel header walk is the default (ZEST_INDEX_SCAN=0: the serial walk).  History: it was
+# opt-in after it measured slower than the serial walk (gpubench 256 MiB lz4_decode_gpu 3.96 -> 9.69
+# ms, profiles/r5/gpubench256_scan_r5c.json): LZ4 streams of BG4 bf16 weights are full of header-like
+# byte patterns.  Compressed candidates now need the LZ4 frame magic (millions of candidates -> a
+# few), and the link picks the chain out of the candidates instead of handing any term with a
+# look-alike to the serial walk (which every term of a 256 MiB batch had): scan 112 us + link 32 us
+# against the serial walk's 761 us; lz4_decode_gpu 69.0 -> 85.4 GB/s, xorb_verify_gpu 267 -> 575
+# GiB/s; the 70B engine bench is unchanged (64.34 / 64.30 GB/s serial / parallel: the walk is hidden
+# under each round's H2D copy either way) (profiles/r5/index_scan_r5ab/).
+INDEX_SCAN = os.environ.get("ZEST_INDEX_SCAN", "1") == "1"
 
 
 def index_terms(H, src_ptr: int, src_n: int, terms_ptr: int, n_terms: int, chunks_ptr: int, err_ptr: int, stream: int,
                 ws: "IngestWorkspace | None" = None) -> None:
-    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4): one thread per
-    term chases its headers (~0.5 ms per 64 MiB run whatever the GPU's width).  ZEST_INDEX_SCAN=1
-    (with a workspace for its scratch): the parallel walk instead -- candidate-header scan of the
-    span, per-term LDS sort/link + prefix sum (csrc/gpu/ingest.hip k_hdr_scan / k_hdr_link), serial
-    fallback per term -- identical records, measured slower (INDEX_SCAN above)."""
+    """Device header walk of n_terms runs in src[0, src_n) into chunk records (K4).  With a workspace
+    for its scratch (and ZEST_INDEX_SCAN not 0): the parallel walk -- candidate-header scan of the
+    span, per-term LDS sort/link + prefix sums (csrc/gpu/ingest.hip k_hdr_scan / k_hdr_link), serial
+    fallback per term; identical records.  Otherwise one thread per term chases its headers (~0.5 ms
+    per 64 MiB run whatever the GPU's width)."""
     if ws is not None and INDEX_SCAN and ws.device.type == "cuda":
         sp, sb = ws.index_scratch(H, n_terms)
         H.index_terms_scan(src_ptr, src_n, terms_ptr, n_terms, chunks_ptr, err_ptr, sp, sb, stream)
