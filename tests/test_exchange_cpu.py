@@ -66,6 +66,16 @@ def _worker(rank, world, port, q):
         xc = X.RoundExchange(arena, rank, world, None, "p2p")
         t = xc.autotune(rounds[:2], modes=("p2p", "bcast", "allgather"))
         res["tuned"] = (xc.mode, sorted(t), X.tuned_mode(world, "gloo", False))
+        # GPU-side readiness needs peer-mapped arenas: on a CPU group it stays off, the exchange
+        # keeps its host path, and a seq handed to exchange() is ignored
+        res["signals"] = (xc.enable_signals(), xc.signaled)
+        xc.order_after(None)  # no exchange streams: a no-op
+        arena = torch.zeros(n, dtype=torch.uint8)
+        xc = X.RoundExchange(arena, rank, world, None, "bcast")
+        _fill(arena, rounds[0], rank, 0)
+        for w in xc.exchange(rounds[0], seq=5):
+            w.wait()
+        res["seq_ignored"] = bool(torch.equal(arena[:9000], _want(n, rounds[0], 0)[:9000]))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -90,3 +100,6 @@ def test_round_exchange_modes_subgroup_and_autotune():
     for r in range(3):
         mode, timed, cached = res[r]["tuned"]
         assert timed == ["allgather", "bcast", "p2p"] and cached == mode
+    for r in range(3):
+        assert res[r]["signals"] == (False, False), res[r]
+        assert res[r]["seq_ignored"], res[r]
