@@ -486,8 +486,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
 
     wd.arm("swarm_warmup")
     t_w = time.time()
-    for _ in range(a.swarm_warmup):
-        one({})
+    warm_st: dict = {}
+    for i in range(a.swarm_warmup):
+        one(warm_st if i == 0 else {})  # the first call's phases: what a user's first pull costs
     warm_s = time.time() - t_w
     wd.arm("swarm_timed")
     from zest_amd import _core
@@ -538,6 +539,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
                                                                                   "bytes_from_peer")},
             "swarm_pull_device_timeline": st.get("device_timeline"),
             "swarm_pull_setup_s": round(setup_s, 3), "swarm_pull_warmup_s": round(warm_s, 3),
+            "swarm_pull_first_call_phases": warm_st.get("phases", {}),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
 

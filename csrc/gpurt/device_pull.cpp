@@ -761,12 +761,16 @@ struct DeviceXetPull::Impl {
           // (term_bound: every chunk stored raw), and a compressed run fills ~88 % of it on bf16
           // weights, so one copy of [0, top) moved the holes too (70B bf16 public path: 141 GB over
           // PCIe for 123.6 GB of runs, 55.2 GB/s against the engine's 64.3).  Runs are copied to
-          // the same offsets (the chunk records address the slot), merging neighbours whose gap is
-          // under 1 MiB.
+          // the same offsets (the chunk records address the slot).
           // (ZEST_H2D_WHOLE_SPAN=1: the old single copy of [0, top), for A/B runs)
           static const bool whole_span = env_size("ZEST_H2D_WHOLE_SPAN", 0) != 0;
+          // Neighbours merge across gaps of at most 64 KiB (ZEST_H2D_MERGE_GAP): small terms share a
+          // copy, while a 64 MiB term's ~0.6 MB of worst-case slack stays off PCIe -- with 1 MiB
+          // the random-bytes 70B pull moved 142.3 GB for 141.1 (public path 54.2 vs 54.8 GB/s with
+          // no merging, same box; the per-term copies cost nothing visible: 56.3 GB/s busy).
+          static const uint64_t merge_gap = env_size("ZEST_H2D_MERGE_GAP", size_t(64) << 10);
           const auto ranges = whole_span ? std::vector<std::pair<uint64_t, uint64_t>>{{0, top}}
-                                         : copy_ranges(bt.src_at, bt.len, uint64_t(1) << 20);
+                                         : copy_ranges(bt.src_at, bt.len, merge_gap);
           for (const auto& [lo, hi] : ranges) {
             hip_check(hipMemcpyAsync(s.dev.p + lo, s.host + lo, hi - lo, hipMemcpyHostToDevice, copy_stream_), "H2D");
             h2d_bytes += hi - lo;
