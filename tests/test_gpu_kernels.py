@@ -952,3 +952,57 @@ def test_index_scan_matches_serial_walk(policy):
     src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
     (serial, e0), (scan, e1) = _index_both(src, terms, nck)
     assert e0 != 0 and e1 == e0 and scan == serial
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_index_scan_random_lookalikes(seed):
+    """The parallel walk against the serial walk with header look-alikes planted at random payload
+    positions: lone ones (the link must see past them), chains of two, and ones whose successor is a
+    real header (both kinds make the chosen set ambiguous -> that term falls back).  Records and the
+    error word must equal the serial walk's whatever path each term took."""
+    rng = random.Random(seed)
+    data, ends, b = _make_runs("none" if seed % 2 else "auto", seed=seed)
+    body = b.serialize(False)
+    nck = len(ends)
+    bounds = list(b.chunk_boundaries())
+    cuts = [0, nck // 3, 2 * nck // 3, nck]
+    uoffs = [0] + list(ends)
+    src_host = bytearray(3)
+    terms = np.zeros(3, dtype=ops.TERM_DTYPE)
+    for t in range(3):
+        c0, c1 = cuts[t], cuts[t + 1]
+        r0 = 0 if c0 == 0 else bounds[c0 - 1]
+        terms[t] = (len(src_host), bounds[c1 - 1] - r0, uoffs[c0], c0, c1 - c0, uoffs[c1] - uoffs[c0])
+        src_host += body[r0:bounds[c1 - 1]] + b"\x00" * 5
+    hdr_pos = {int(terms[t]["src"]) + (0 if c == cuts[t] else bounds[c - 1] - (0 if cuts[t] == 0 else bounds[cuts[t] - 1]))
+               for t in range(3) for c in range(cuts[t], cuts[t + 1])}
+
+    def raw_hdr(n):
+        return bytes([0, n & 0xFF, (n >> 8) & 0xFF, n >> 16, 0, n & 0xFF, (n >> 8) & 0xFF, n >> 16])
+
+    def plant(pos, n):  # only inside payloads, never over a real header
+        if any(h - 8 < pos < h + 8 for h in hdr_pos):
+            return False
+        src_host[pos:pos + 8] = raw_hdr(n)
+        return True
+
+    for _ in range(rng.randint(1, 6)):
+        t = rng.randrange(3)
+        lo = int(terms[t]["src"]) + 16
+        pos = rng.randrange(lo, lo + int(terms[t]["src_len"]) - 64)
+        kind = rng.randrange(3)
+        if kind == 0:  # lone look-alike
+            plant(pos, rng.randint(1, 4096))
+        elif kind == 1:  # a chain of two
+            n1 = rng.randint(1, 512)
+            if plant(pos, n1):
+                plant(pos + 8 + n1, rng.randint(1, 512))
+        else:  # a look-alike whose successor is the next real header
+            nxt = min((h for h in hdr_pos if h > pos + 16), default=None)
+            if nxt is not None and nxt - pos - 8 <= 131072:
+                plant(pos, nxt - pos - 8)
+    src = ops.padded_empty(len(src_host), DEV)
+    src.copy_(torch.frombuffer(bytes(src_host), dtype=torch.uint8))
+    fb = []
+    (serial, e0), (scan, e1) = _index_both(src, terms, nck, fb)
+    assert e0 == 0 and e1 == e0 and scan == serial, (fb, e0, e1)
