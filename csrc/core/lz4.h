@@ -22,6 +22,8 @@ size_t block_bound(size_t n);
 size_t compress_block(const uint8_t* src, size_t n, uint8_t* dst, size_t cap);
 // Decompress a block into dst[dst_pos .. dst_cap); matches may reference dst[0 .. dst_pos)
 // (dependent-block prefix).  Returns bytes produced; throws Error("CorruptLz4") on malformed input.
+// Decodes into dst[dst_pos, ...) and returns the bytes produced.  May write scratch bytes past the
+// produced output, anywhere below dst_cap: pass the end of the region this block's output owns.
 size_t decompress_block(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_pos, size_t dst_cap);
 
 // Frame format.

@@ -538,6 +538,28 @@ def test_start_opens_dashboard(nodes, tmp_path):
     a.run("stop")
 
 
+def _free_port_range(n: int) -> int:
+    """First port of n consecutive TCP ports that can all be bound on 127.0.0.1 right now."""
+    import random
+    import socket
+    rng = random.Random(os.getpid())
+    for _ in range(200):
+        base = rng.randrange(20000, 60000 - n)
+        socks = []
+        try:
+            for p in range(base, base + n):
+                sk = socket.socket()
+                socks.append(sk)
+                sk.bind(("127.0.0.1", p))
+            return base
+        except OSError:
+            continue
+        finally:
+            for sk in socks:
+                sk.close()
+    raise RuntimeError(f"no {n} consecutive free ports")
+
+
 def test_p2p_cluster_script_local(tmp_path):
     """scripts/p2p_cluster_test.sh --local 3 (the reference's hetzner / docker P2P suites): CDN-only
     baseline, two seeders, pulls from both and from one — each snapshot identical, 100 % P2P."""
@@ -545,7 +567,7 @@ def test_p2p_cluster_script_local(tmp_path):
     if shutil.which("curl") is None:
         pytest.skip("curl not installed")
     env = dict(os.environ, TMPDIR=str(tmp_path), PYTHONPATH=str(ROOT))
-    base = 20000 + (os.getpid() % 500) * 40
+    base = _free_port_range(40)  # a pid-derived base collided with other xdist workers' ports now and then
     r = subprocess.run(["bash", str(ROOT / "scripts" / "p2p_cluster_test.sh"), "--local", "3", "--bt-port", str(base),
                         "--http-port", str(base + 5)],
                        capture_output=True, text=True, timeout=300, env=env)
