@@ -539,7 +539,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
                                                                                   "bytes_from_peer")},
             "swarm_pull_device_timeline": st.get("device_timeline"),
             "swarm_pull_setup_s": round(setup_s, 3), "swarm_pull_warmup_s": round(warm_s, 3),
-            "swarm_pull_first_call_phases": warm_st.get("phases", {}),
+            "swarm_pull_first_call_phases": warm_st.get("phases", {}), "swarm_pull_first_call_alloc": warm_st.get("alloc", {}),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
 

@@ -661,6 +661,10 @@ class _Swarm:
         want_map = (self.cuda and self.m.world > 1 and os.environ.get("ZEST_EXCHANGE_IPC", "1") != "0"
                     and self.exchange_req in ("auto", "ipc", "xgmi"))
         self.arena = None
+        # (device memory free before the arena, and the arena's own allocation time: a pull after
+        # another pull in the same process spent 4.5 s here, profiles/r5/bench70b_r5ai.log)
+        self.alloc_info = {"free_before_GB": round(torch.cuda.mem_get_info(self.device)[0] / 1e9, 2)} if self.cuda else {}
+        t_a = time.perf_counter()
         if want_map:
             try:
                 self.arena = ops.vmm_empty(n, self.device)
@@ -668,6 +672,7 @@ class _Swarm:
                 self.arena = None
         if self.arena is None:
             self.arena = ops.padded_empty(n, self.device) if self.cuda else torch.empty(n + ops.PAD, dtype=torch.uint8)[:n]
+        self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
         nck = max(1, P.n_chunks)
         self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
@@ -1318,7 +1323,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 pipelined=sw.pipelined,
                 held_bytes=sw.held_bytes[sw.m.rank], share_bytes=sw.share_bytes[sw.m.rank],
                 possession=list(sw.held_bytes), reused_pipeline=sw.reused,
-                cache_writer=sw.fetcher.cache_writer(), device_timeline=sw.fetcher.timeline(), **sw.stats)
+                cache_writer=sw.fetcher.cache_writer(), device_timeline=sw.fetcher.timeline(),
+                alloc=getattr(sw, "alloc_info", {}), **sw.stats)
         ok = True
         return out
     finally:
