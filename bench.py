@@ -422,8 +422,10 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     every term's CDN fetch served from this rank's pinned origin through a mem:// memory CAS (the
     same cache -> P2P -> CDN waterfall, the bytes copied into the pinned staging like a NIC's DMA),
     then DeviceXetPull's pipeline (copy stream H2D || GPU decode + BLAKE3), the exchange at N > 1 and
-    the Merkle check of every file.  A step is one whole swarm_pull call; the fetch pipelines are
-    kept between calls (reuse_pipeline), reconstructions are asked for anew every call.  The xorb
+    the Merkle check of every file.  A step is one whole swarm_pull call; the fetch pipelines and
+    the arena (peer-mapped at N > 1) are kept between calls (reuse_pipeline, reuse_arena: each call's
+    tensors are dropped before the next; the warm-up call lands in a fresh arena, so its exchange is
+    verified against bytes no earlier pull wrote), reconstructions are asked for anew every call.  The xorb
     cache is empty and cache writes are off (a device pull into HBM; nothing is read from disk)."""
     import tempfile
 
@@ -479,7 +481,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
 
     def one(st):
         out = sp.swarm_pull(world.spec.repo_id, device=device if cuda else None, p2p=False, dht=False,
-                            round_bytes=a.round_mb << 20, stats=st, reuse_pipeline=True)
+                            round_bytes=a.round_mb << 20, stats=st, reuse_pipeline=True, reuse_arena=True)
         n = len(out)
         del out
         return n
@@ -540,6 +542,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             "swarm_pull_device_timeline": st.get("device_timeline"),
             "swarm_pull_setup_s": round(setup_s, 3), "swarm_pull_warmup_s": round(warm_s, 3),
             "swarm_pull_first_call_phases": warm_st.get("phases", {}), "swarm_pull_first_call_alloc": warm_st.get("alloc", {}),
+            "swarm_pull_arena_reused": bool(st.get("alloc", {}).get("reused", False)),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
 

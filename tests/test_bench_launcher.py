@@ -93,6 +93,7 @@ def test_bench_swarm_row_times_the_public_path(gpus):
     assert len(lines) == 1, p.stdout
     ex = lines[0]["extra"]
     assert ex["swarm_pull_GBps"] > 0 and len(ex["swarm_pull_step_s"]) == 2
+    assert ex["swarm_pull_arena_reused"]  # timed pulls land in the warm-up pull's arena
     assert ex["swarm_pull_mode"] == "random" and ex["swarm_pull_tensors"] > 0
     assert ex["swarm_pull_fetch"]["bytes_from_cdn"] > 0 and not ex["swarm_pull_fetch"]["bytes_from_peer"]
     if gpus > 1:
@@ -110,6 +111,7 @@ def test_bench_swarm_row_multi_file_three_ranks():
     ex = lines[0]["extra"]
     assert "swarm_pull_error" not in ex and ex["swarm_pull_GBps"] > 0
     assert ex["swarm_pull_p2p_ratio"] > 0.5  # each rank received the other two thirds
+    assert ex["swarm_pull_arena_reused"]
 
 
 def test_bench_swarm_row_overrun_keeps_the_headline():

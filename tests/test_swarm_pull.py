@@ -489,12 +489,18 @@ def _mem_origin_worker(q, seed, compressed):
             os.environ[k] = v
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
         st = {}
-        t = swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st, reuse_pipeline=True)
+        t = swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st, reuse_pipeline=True, reuse_arena=True)
         got = {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t.items()}
+        base = next(iter(t.values())).untyped_storage().data_ptr()
+        del t
         st2 = {}
-        swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st2, reuse_pipeline=True)
+        t2 = swarm_pull(world.spec.repo_id, p2p=False, dht=False, stats=st2, reuse_pipeline=True, reuse_arena=True)
+        got2 = {k: v.contiguous().view(torch.uint8).numpy().tobytes() for k, v in t2.items()}
+        st2["same_arena"] = next(iter(t2.values())).untyped_storage().data_ptr() == base
+        del t2
         from zest_amd.parallel.swarm_pull import release_pipelines
         release_pipelines()
+        st2["got2_equal"] = got2 == got
         q.put(("ok", got, st, st2, hub.counters.get("xorb_get", 0), hub.counters.get("cas_v1", 0)))
         dist.destroy_process_group()
         hub.stop()
@@ -507,7 +513,7 @@ def test_swarm_pull_from_memory_origin_and_pipeline_reuse():
     """The bench's public-path row on the CPU: fetch_info URLs mem://origin/<xorb> are served from
     registered host memory (no sockets, no xorb GETs), every tensor arrives intact, and a second pull
     with reuse_pipeline=True reuses the first one's pipelines but asks the CAS for the
-    reconstructions again."""
+    reconstructions again; with reuse_arena=True it lands in the first pull's arena."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_mem_origin_worker, args=(q, 21, False))
@@ -520,6 +526,8 @@ def test_swarm_pull_from_memory_origin_and_pipeline_reuse():
     assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
     assert xorb_gets == 0  # every byte came from the memory origin
     assert st["from_cdn"] == st["total_bytes"] and not st["reused_pipeline"] and st2["reused_pipeline"]
+    # reuse_arena: the second pull lands in the first one's arena, and intact
+    assert not st["alloc"].get("reused") and st2["alloc"].get("reused") and st2["same_arena"] and st2["got2_equal"]
     # a reused pipeline reports this pull's bytes, not the session's running total (the second pull
     # finds the first one's runs in its xorb cache: possession makes it read them from there)
     src = ("bytes_from_cdn", "bytes_from_cache", "bytes_from_peer")

@@ -665,6 +665,24 @@ class _Swarm:
         # another pull in the same process spent 4.5 s here, profiles/r5/bench70b_r5ai.log)
         self.alloc_info = {"free_before_GB": round(torch.cuda.mem_get_info(self.device)[0] / 1e9, 2)} if self.cuda else {}
         t_a = time.perf_counter()
+        # reuse_arena: the arena (and, peer-mapped, every peer's mapping of it) of this process's
+        # previous pull of at least this size, when every rank has one -- the caller holds no tensor
+        # of that pull any more.  A fresh 141 GB arena per pull costs the driver's reclaim of the last
+        # one (~4 s, profiles/r5/alloc_probe_141g_r5aj.log) and, peer-mapped, a new export/import.
+        key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks), want_map)
+        cached = _ARENAS.get(key) if self.reuse_arena else None
+        have = int(cached is not None and cached[0].numel() >= n and (cached[1] is not None or not want_map))
+        if self.reuse_arena and self.m.world > 1:
+            have = int(all(self._gather(have)))
+        if have:
+            full, self.mapped = cached
+            self.arena = full[:n]
+            self.alloc_info["reused"] = True
+            self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
+            self._alloc_tables(P)
+            self._mark("alloc_s", t)
+            return
+        _ARENAS.pop(key, None)  # (a smaller cached arena is dropped before the new one is made)
         if want_map:
             try:
                 self.arena = ops.vmm_empty(n, self.device)
@@ -673,16 +691,21 @@ class _Swarm:
         if self.arena is None:
             self.arena = ops.padded_empty(n, self.device) if self.cuda else torch.empty(n + ops.PAD, dtype=torch.uint8)[:n]
         self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
-        nck = max(1, P.n_chunks)
-        self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
-        self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
-        self.lens = np.zeros(nck, dtype=np.uint32)   # every chunk's size, filled as rounds are agreed
+        self._alloc_tables(P)
         self.mapped = None
         if want_map and self.exchange_req != "p2p":
             t_map = time.perf_counter()
             self.mapped = map_peer_arenas(self.arena, self.m.rank, self.m.world, self.m.data)
             self._mark("map_s", t_map)
+        if self.reuse_arena:
+            _ARENAS[key] = (self.arena, self.mapped)
         self._mark("alloc_s", t)
+
+    def _alloc_tables(self, P):
+        nck = max(1, P.n_chunks)
+        self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
+        self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
+        self.lens = np.zeros(nck, dtype=np.uint32)   # every chunk's size, filled as rounds are agreed
 
     def shard(self):
         """Per-rank queues of items (term ranges), identical on every rank."""
@@ -1211,9 +1234,16 @@ def _merged_stats(parts: list) -> dict:
 _PIPELINES: dict = {}
 
 
+# Arenas kept by pulls made with reuse_arena=True: (arena, peer mappings or None), keyed by device,
+# world size, member ranks and whether the arena is peer-mapped.
+_ARENAS: dict = {}
+
+
 def release_pipelines() -> None:
-    """Drop the pipelines kept by reuse_pipeline=True pulls (their pinned staging is freed)."""
+    """Drop the pipelines kept by reuse_pipeline=True pulls (their pinned staging is freed) and the
+    arenas kept by reuse_arena=True pulls."""
     _PIPELINES.clear()
+    _ARENAS.clear()
 
 
 def _stats_delta(now: dict, base: dict) -> dict:
@@ -1246,7 +1276,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
                round_bytes: int | None = None, exchange: str = "auto",
                stats: dict | None = None, reuse_pipeline: bool | None = None,
-               possession: bool | None = None) -> dict[str, torch.Tensor]:
+               possession: bool | None = None, reuse_arena: bool = False) -> dict[str, torch.Tensor]:
     """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
     full set (views into one arena per rank).  `exchange`: "auto" (measured at setup, cached per
     process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
@@ -1259,7 +1289,10 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     its xorb cache already covers and holders own those terms (assign_owners) -- a rank with the
     whole model cached is the node's seeder.  `reuse_pipeline` (default ZEST_SWARM_REUSE, off): keep
     the fetch pipelines (pinned staging, Xet session) for the next pull of the same repository in
-    this process; release_pipelines() frees them."""
+    this process; release_pipelines() frees them.  `reuse_arena` (off): the pull lands in the
+    arena of this process's previous reuse_arena pull (same group, large enough) instead of a fresh
+    one -- that pull's tensors are overwritten, so only for a caller that dropped them (bench.py's
+    repeated pulls); release_pipelines() frees the kept arena."""
     if reuse_pipeline is None:
         reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
     if possession is None:
@@ -1272,6 +1305,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify_received,
                 staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange,
                 reuse=reuse_pipeline, possession=possession)
+    sw.reuse_arena = bool(reuse_arena)
     ok = False
     try:
         while True:
