@@ -1,8 +1,8 @@
 """The `ipc` / `xgmi` exchanges on a real GPU: two ranks map each other's HBM arena (HIP IPC over
 dmabuf) and pull their peer's regions with DMA copies (`ipc`) or the K8 gather kernel (`xgmi`).  Both ranks share the box's one GPU (gloo carries
 the control messages; RCCL refuses two ranks on one device), which exercises the handle exchange,
-the per-round host barrier and the copy streams; xGMI bandwidth is measured by bench.py on the
-8-GPU node."""
+the per-round readiness (GPU-side ready counters, or the host barrier with ZEST_IPC_SIGNALS=0) and the
+copy streams; xGMI bandwidth is measured by bench.py on the 8-GPU node."""
 import os
 
 import pytest
