@@ -471,6 +471,40 @@ TEST(xorb_cache_quarantine_per_fetch) {
   CHECK(cache.sweep_pending(3600) == 2 && storage::exists(live));
 }
 
+TEST(lz4_decoder_exact_buffers_and_corrupt_input) {
+  // The decoder's fast paths copy 8/16 bytes at a time inside checked slack: round trips into
+  // exact-size heap buffers (an ASan build catches any byte past them) and corrupt / truncated
+  // blocks that must raise or stay in bounds (python tools/build.py --asan && build/asan/core_tests).
+  std::mt19937_64 rng(7);
+  for (int it = 0; it < 1500; ++it) {
+    const size_t n = rng() % 70000;
+    std::vector<uint8_t> d(n);
+    const int kind = it % 5;
+    for (size_t i = 0; i < n; ++i) {
+      if (kind == 0) d[i] = uint8_t(rng());
+      else if (kind == 1) d[i] = uint8_t(rng() % 3);
+      else if (kind == 2) d[i] = uint8_t((i % (1 + it % 7)) * 17);
+      else if (kind == 3) d[i] = 0;
+      else d[i] = (rng() % 4 == 0) ? uint8_t(rng()) : (i ? d[i - 1] : 1);
+    }
+    std::vector<uint8_t> blk(lz4::block_bound(n) + 1);
+    const size_t c = n ? lz4::compress_block(d.data(), n, blk.data(), blk.size()) : 0;
+    if (n) {
+      std::vector<uint8_t> out(n);
+      CHECK(lz4::decompress_block(blk.data(), c, out.data(), 0, n) == n && out == d);
+    }
+    std::vector<uint8_t> bad(blk.begin(), blk.begin() + (c ? c : 1));
+    for (int k = 0; k < 3 && !bad.empty(); ++k) bad[rng() % bad.size()] ^= uint8_t(1 + rng() % 255);
+    const size_t cut = bad.empty() ? 0 : rng() % (bad.size() + 1);
+    const size_t cap = 1 + rng() % (n + 64);
+    std::vector<uint8_t> src(bad.begin(), bad.begin() + cut), out(cap);
+    try {
+      CHECK(lz4::decompress_block(src.data(), src.size(), out.data(), 0, cap) <= cap);
+    } catch (const std::exception&) {
+    }
+  }
+}
+
 TEST(copy_ranges_skip_holes) {
   using R = std::vector<std::pair<uint64_t, uint64_t>>;
   // three reserved regions of 100 bytes holding runs of 90, 0 and 70 bytes; one run starts mid-region
