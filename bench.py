@@ -477,6 +477,8 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
         own_pg = True
     import torch.distributed as tdist
+    if world_size > 1 and rank == 0:
+        _log_split_check(world, puller, world_size, sp)
     setup_s = time.time() - t_setup
 
     def one(st):
@@ -545,6 +547,33 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             "swarm_pull_arena_reused": bool(st.get("alloc", {}).get("reused", False)),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
+
+
+def _log_split_check(world, puller, world_size, sp) -> None:
+    """Diagnostics (rank 0, N > 1): the public path's term owners -- computed the way swarm_pull will,
+    on the files in the order the hub lists them -- against the engine's per-rank origin shares that
+    each rank's memory CAS serves.  A term owned by a rank whose origin lacks it is a 404 in the row."""
+    import numpy as np
+
+    from zest_amd import _core
+    try:
+        _, files = _core.list_repo_files(world.spec.repo_id, "main", "model")
+        by_hash = {world.file_hash_hex(i): i for i in range(len(world.xet_files))}
+        order = [by_hash[f["xet_hash"]] for f in files if f["path"].endswith(".safetensors") and f["xet_hash"]]
+        T = world.terms
+        idx = np.concatenate([np.flatnonzero(T["file"] == i) for i in order]) if order else np.zeros(0, np.int64)
+        owner = sp.assign_owners(T["ulen"][idx], None, world_size)
+        rt = puller.rank_terms
+        eng = np.empty(len(T), dtype=np.int64)
+        for r, (a, b) in enumerate(rt):
+            eng[a:b] = r
+        bad = np.flatnonzero(eng[idx] != owner)
+        log(0, f"[swarm_pull] split check: {len(idx)} of {len(T)} terms planned, files in listing order "
+               f"{order[:8]}{'...' if len(order) > 8 else ''}, engine shares {rt}; {len(bad)} terms owned "
+               f"elsewhere" + (f" (first: plan term {int(bad[0])} = world term {int(idx[bad[0]])}, "
+                               f"swarm rank {int(owner[bad[0]])}, engine rank {int(eng[idx[bad[0]]])})" if len(bad) else ""))
+    except Exception as e:  # noqa: BLE001 - diagnostics only
+        log(0, f"[swarm_pull] split check failed: {type(e).__name__}: {e}")
 
 
 def _data_note(r: dict) -> str:

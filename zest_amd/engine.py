@@ -150,14 +150,9 @@ def plan_rank_terms(world: SyntheticWorld, n_ranks: int, seeders: int | None = N
     if k < n_ranks:
         own = plan_rank_terms(world, k)
         return own + [(len(T), len(T))] * (n_ranks - k)
-    cu = np.cumsum(T["ulen"].astype(np.float64))
-    total = cu[-1] if len(cu) else 0.0
-    bounds = [0]
-    for r in range(1, n_ranks):
-        bounds.append(int(np.searchsorted(cu, total * r / n_ranks, side="left")) + 1)
-    bounds.append(len(T))
-    bounds = np.maximum.accumulate(np.minimum(np.array(bounds), len(T)))
-    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(n_ranks)]
+    from .parallel.split import even_bounds  # (the same cut as swarm_pull's owners)
+    bounds = even_bounds(T["ulen"], n_ranks)
+    return [(bounds[r], bounds[r + 1]) for r in range(n_ranks)]
 
 
 HEAD_TAPER = (0.25, 0.5)        # first rounds, as fractions of a full round

@@ -59,6 +59,7 @@ import torch.distributed as dist
 from .. import _core, ops
 from .. import device as zdev
 from .exchange import EXCHANGE_MODES, PEER_MAPPED_MODES, RoundExchange, map_peer_arenas, role_stream, tuned_mode
+from .split import even_bounds
 
 FILE_ALIGN = 4096
 HEAD_TAPER = (0.25, 0.5)
@@ -113,6 +114,13 @@ def assign_owners(ulen: np.ndarray, held: np.ndarray | None, world: int) -> np.n
     the plain byte-balanced contiguous split."""
     nt = len(ulen)
     owner = np.full(nt, -1, dtype=np.int64)
+    if held is None or not nt or not held.any():
+        # nothing held: the plain byte-balanced contiguous split, cut exactly where the bench
+        # engine cuts its origin shares (split.even_bounds, integer arithmetic)
+        b = even_bounds(ulen, world)
+        for r in range(world):
+            owner[b[r]:b[r + 1]] = r
+        return owner
     load = np.zeros(world, dtype=np.float64)
     u = ulen.astype(np.float64)
     if held is not None and nt and held.any():
