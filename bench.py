@@ -453,6 +453,16 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     if cuda:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    if dist is not None and world_size > 1:
+        # A peer-mapped arena's memory is freed only once every importer has released its mapping:
+        # wait until every rank has dropped its mappings before any rank allocates the row's arena.
+        # Without this a rank could hold its old 141 GB arena (kept alive by a slower peer's import)
+        # next to the new one; the 8-rank one-GPU rehearsal ran out of device memory exactly so
+        # (hipMalloc in a fetch pipeline, profiles/r5/rehearsal_n8_r5am.log).
+        dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
     hub = FakeHub()
     hub.xorb_url = "mem://origin"
     hub.start()
@@ -743,7 +753,7 @@ def rank_main(a) -> None:
         except Exception as e:  # noqa: BLE001 - the headline stands without the row
             if world_size == 1:
                 raise
-            swarm = {"swarm_pull_error": f"{type(e).__name__}: {e}"[:400]}
+            swarm = {"swarm_pull_error": f"{type(e).__name__}: {e}"[:1000]}
             log(rank, f"[swarm_pull] failed: {swarm['swarm_pull_error']}")
         out["extra"].update(swarm)
         keep["puller"].close()

@@ -949,6 +949,8 @@ class _Swarm:
                     continue
                 g = self.m.granks[r]
                 if e:
+                    if not getattr(self, "first_fetch_error", None):
+                        self.first_fetch_error = e  # (named in the final error if the item finds no owner)
                     self.fails[g] = self.fails.get(g, 0) + 1
                     self.tried.setdefault(item, set()).add(g)
                     moves = [item]
@@ -960,7 +962,8 @@ class _Swarm:
                                  if self.fails.get(self.m.granks[q], 0) < 2 and self.m.granks[q] not in self.tried.get(mv, set())]
                         if not cands:
                             fatal.append(e if mv == item else f"no owner left for terms {self.items[mv]} "
-                                                              f"(rank {g} dropped)")
+                                                              f"(rank {g} dropped; first fetch error: "
+                                                              f"{self.first_fetch_error})")
                             continue
                         load = [sum(int(P.t_ulen[self.items[x][0]:self.items[x][1]].sum()) for x in self.queue[q])
                                 for q in range(self.m.world)]
