@@ -424,8 +424,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     then DeviceXetPull's pipeline (copy stream H2D || GPU decode + BLAKE3), the exchange at N > 1 and
     the Merkle check of every file.  A step is one whole swarm_pull call; the fetch pipelines and
     the arena (peer-mapped at N > 1) are kept between calls (reuse_pipeline, reuse_arena: each call's
-    tensors are dropped before the next; the warm-up call lands in a fresh arena, so its exchange is
-    verified against bytes no earlier pull wrote), reconstructions are asked for anew every call.  The xorb
+    tensors are dropped before the next; the arena is the engine's, poisoned before the warm-up
+    call, so the row's exchange is verified against bytes no earlier pull wrote), reconstructions
+    are asked for anew every call.  The xorb
     cache is empty and cache writes are off (a device pull into HBM; nothing is read from disk)."""
     import tempfile
 
@@ -446,13 +447,27 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     # the peers' imports of this rank's old arena must be gone too (a peer-mapped VMM chunk lives until
     # every importer released it): every rank drops its mappings here, before swarm_pull's first
     # collective, and gc runs so no reference cycle keeps a mapping past it.
+    free0 = torch.cuda.mem_get_info(device)[0] if cuda else 0
     puller.release_device()
-    keep.pop("arena", None)
+    arena, mapped = keep.pop("arena", None), keep.pop("peers", None)
+    # The row's pulls land in the engine's arena (and, peer-mapped, its peers' mappings of it):
+    # freeing 141 GB and allocating it again costs the driver's reclaim (~4 s), and in the 4-rank
+    # rehearsal a released peer-mapped arena stayed counted as used, so a fresh one did not fit next
+    # to the others (8 ranks: out of device memory).  The arena is poisoned first, on every rank
+    # before the barrier below, so the row's first exchange is verified against bytes no earlier
+    # pull wrote.
+    if arena is not None and (world_size == 1 or mapped is not None):
+        if cuda:
+            arena.fill_(0xA5)
+            torch.cuda.synchronize()
+        sp.adopt_arena(arena, mapped if world_size > 1 else None)
+    del arena, mapped
     import gc
     gc.collect()
     if cuda:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    free1 = torch.cuda.mem_get_info(device)[0] if cuda else 0
     if dist is not None and world_size > 1:
         # A peer-mapped arena's memory is freed only once every importer has released its mapping:
         # wait until every rank has dropped its mappings before any rank allocates the row's arena.
@@ -463,6 +478,18 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         if cuda:
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+    if cuda:
+        # The driver reclaims (clears) freed device memory asynchronously, ~35 GB/s
+        # (profiles/r5/alloc_probe_141g_r5aj.log): the engine's 141 GB arena is still counted as used
+        # for seconds after its last reference went, and an allocation in that window can fail
+        # instead of waiting (the 8-rank one-GPU rehearsal: hipMalloc out of memory with every VMM
+        # mapping already released).  Wait until the free device memory stops growing.
+        _wait_device_reclaim(device)
+    if cuda:  # (device memory free before / after the engine's buffers were released, and after the barrier)
+        own, imp = ops.hip().vmm_live()
+        log(rank, f"[swarm_pull] device free GB: {free0 / 1e9:.1f} -> {free1 / 1e9:.1f} -> "
+                  f"{torch.cuda.mem_get_info(device)[0] / 1e9:.1f}; live VMM mappings: own {own / 1e9:.1f} GB, "
+                  f"imported {imp / 1e9:.1f} GB")
     hub = FakeHub()
     hub.xorb_url = "mem://origin"
     hub.start()
@@ -557,6 +584,22 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
             "swarm_pull_arena_reused": bool(st.get("alloc", {}).get("reused", False)),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
+
+
+def _wait_device_reclaim(device, timeout_s: float = 30.0, quiet_s: float = 0.5) -> float:
+    """Poll the device's free memory until it has not grown for `quiet_s` (or `timeout_s` passed);
+    returns the seconds waited."""
+    import torch
+    t0 = time.time()
+    last, since = torch.cuda.mem_get_info(device)[0], time.time()
+    while time.time() - t0 < timeout_s:
+        time.sleep(0.05)
+        free = torch.cuda.mem_get_info(device)[0]
+        if free > last:
+            last, since = free, time.time()
+        elif time.time() - since >= quiet_s:
+            break
+    return time.time() - t0
 
 
 def _log_split_check(world, puller, world_size, sp) -> None:
@@ -742,8 +785,8 @@ def rank_main(a) -> None:
         # deadline prints the headline line with the row marked failed and exits 0 (Watchdog.fallback).
         keep["mode"] = results[-1]["mode"]
         keep["arena"] = arenas.pop("arena", None)
+        keep["peers"] = arenas.pop("peers", None)
         arenas.clear()
-        keep.pop("arena", None)
         if world_size > 1:
             wd.fallback = lambda reason: emit({"swarm_pull_error": reason})
         try:

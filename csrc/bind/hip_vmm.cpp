@@ -20,6 +20,7 @@
 #include <pybind11/stl.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
@@ -50,15 +51,20 @@ size_t granularity(int device) {
   return g ? g : 4096;
 }
 
+// Bytes of live mappings in this process, own and imported (vmm_live(): leak diagnostics).
+std::atomic<int64_t> g_live_own{0}, g_live_imported{0};
+
 // One contiguous virtual range mapped onto n physical chunks (own or imported).
 struct VmmMapping {
   uint8_t* va = nullptr;
   size_t chunk = 0, size = 0;
   int device = 0;  // device that accesses it (owner's device, or the importer's)
   bool imported = false;
+  bool counted = false;
   std::vector<hipMemGenericAllocationHandle_t> h;
 
   ~VmmMapping() {
+    if (counted) (imported ? g_live_imported : g_live_own) -= int64_t(size);
     if (!va) return;
     (void)hipDeviceSynchronize();  // no kernel or copy may still touch the range
     for (size_t k = 0; k < h.size(); ++k) {
@@ -75,6 +81,10 @@ struct VmmMapping {
     va = static_cast<uint8_t*>(p);
   }
   void grant() {
+    if (!counted) {
+      (imported ? g_live_imported : g_live_own) += int64_t(size);
+      counted = true;
+    }
     hipMemAccessDesc acc{};
     acc.location.type = hipMemLocationTypeDevice;
     acc.location.id = device;
@@ -225,6 +235,8 @@ void bind_hip_vmm(py::module_& m) {
       })
       .def("dlpack", &vmm_dlpack, py::arg("nbytes"));
   m.def("vmm_granularity", &granularity, py::arg("device"));
+  m.def("vmm_live", [] { return py::make_tuple(g_live_own.load(), g_live_imported.load()); },
+        "bytes of live (own, imported) VMM mappings in this process");
   m.def("runtime_version", [] {
     int v = 0;
     vcheck(hipRuntimeGetVersion(&v), "hipRuntimeGetVersion");

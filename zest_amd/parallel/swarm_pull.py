@@ -1250,6 +1250,18 @@ _PIPELINES: dict = {}
 _ARENAS: dict = {}
 
 
+def adopt_arena(arena: torch.Tensor, mapped=None, group=None) -> None:
+    """Seed the reuse_arena cache with an arena the caller already holds (with `mapped`, the
+    PeerArenas of it when peer-mapped): the next reuse_arena pull over `group` of at most its size
+    lands in it instead of allocating.  bench.py hands its engine's arena to the public-path row:
+    freeing 141 GB and allocating it again costs the driver's reclaim, and a freed peer-mapped arena
+    stayed counted as used in the 4-rank rehearsal (profiles/r5/rehearsal_n4_reclaim_r5ao.log)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    granks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(world))
+    dev = arena.device.index if arena.device.type == "cuda" else -1
+    _ARENAS[(dev, world, granks, mapped is not None)] = (arena, mapped)
+
+
 def release_pipelines() -> None:
     """Drop the pipelines kept by reuse_pipeline=True pulls (their pinned staging is freed) and the
     arenas kept by reuse_arena=True pulls."""
