@@ -361,6 +361,76 @@ def _swarm_pull_gpu_worker(rank, world_size, port, repo, backend, q, exchange="a
             dist.destroy_process_group()
 
 
+def _swarm_repeat_worker(rank, world_size, port, repo, q):
+    """Three pulls in one process with peer-mapped arenas and the default reuse_arena: the second
+    lands in the first one's arena (its tensors were dropped); the third gets a fresh one because
+    the second's tensors are still held -- and they stay intact."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from zest_amd.parallel import swarm_pull
+
+        def pull():
+            st = {}
+            t = swarm_pull(repo, device="cuda:0", p2p=False, dht=False, stats=st, exchange="xgmi",
+                           round_bytes=512 << 10)
+            return t, st
+
+        def host(t):
+            return {k: v.contiguous().view(torch.uint8).cpu().numpy().tobytes() for k, v in t.items()}
+        t1, st1 = pull()
+        got1 = host(t1)
+        del t1
+        t2, st2 = pull()
+        got2 = host(t2)
+        t3, st3 = pull()  # t2 still held
+        torch.cuda.synchronize()
+        kept2 = host(t2)
+        got3 = host(t3)
+        from zest_amd.parallel.swarm_pull import release_pipelines
+        del t2, t3
+        release_pipelines()
+        q.put((rank, got1, [st1["alloc"], st2["alloc"], st3["alloc"]], got2 == got1, kept2 == got1, got3 == got1))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_swarm_pull_reuses_peer_mapped_arena_when_free(tmp_path, monkeypatch):
+    import dataclasses
+
+    import torch.multiprocessing as mp
+
+    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
+    world = SyntheticWorld(spec, seed=23, mode="bf16")
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = free_port()
+        procs = [ctx.Process(target=_swarm_repeat_worker, args=(r, 2, port, world.spec.repo_id, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=240) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+        for rank, got1, allocs, same2, kept2, same3 in res:
+            assert isinstance(got1, dict), got1
+            assert not allocs[0].get("reused") and allocs[1].get("reused") and not allocs[2].get("reused"), allocs
+            assert same2 and kept2 and same3
+    finally:
+        hub.stop()
+
+
 @pytest.mark.parametrize("world_size,backend,exchange,fault", [
     (1, "nccl", "auto", ""), (2, "gloo", "auto", ""), (2, "gloo", "xgmi", ""), (2, "gloo", "ipc", ""),
     (2, "gloo", "allgather", ""), (2, "gloo", "auto", "import"), (2, "gloo", "auto", "sentinel"),

@@ -197,3 +197,20 @@ def test_round_plan_taper_covers_every_term_once():
             assert sizes[0] < full and sizes[-1] < full
     assert round_weights(3 << 20, 1 << 20) == [1.0] * 3          # short plans are not tapered
     assert round_weights(40 << 20, 1 << 20, taper=False) == [1.0] * 40
+
+
+def test_arena_in_use_counts_views():
+    """swarm_pull's automatic arena reuse only takes a kept arena when no tensor of the earlier pull
+    still views it (storage reference count beyond the cached tensor)."""
+    import torch
+
+    from zest_amd.parallel.swarm_pull import _arena_in_use, _storage_refs
+    base = torch.empty(1 << 16, dtype=torch.uint8)
+    full = base[: 1 << 15]
+    del base
+    entry = (full, None, _storage_refs(full))  # as swarm_pull keeps it
+    assert not _arena_in_use(entry)
+    views = {"a": full[:100].view(torch.int32), "b": full[4096:8192]}
+    assert _arena_in_use(entry)
+    del views
+    assert not _arena_in_use(entry)

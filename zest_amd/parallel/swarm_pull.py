@@ -678,12 +678,17 @@ class _Swarm:
         # of that pull any more.  A fresh 141 GB arena per pull costs the driver's reclaim of the last
         # one (~4 s, profiles/r5/alloc_probe_141g_r5aj.log) and, peer-mapped, a new export/import.
         key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks), want_map)
-        cached = _ARENAS.get(key) if self.reuse_arena else None
-        have = int(cached is not None and cached[0].numel() >= n and (cached[1] is not None or not want_map))
-        if self.reuse_arena and self.m.world > 1:
+        # reuse_arena None (default): peer-mapped arenas are kept and reused whenever no tensor of the
+        # previous pull is alive (a released peer-mapped arena stayed counted as used on the box,
+        # ARCHITECTURE 15.8, so a fresh one per pull would pile up); True: reuse regardless.
+        use_cache = self.reuse_arena is True or (self.reuse_arena is None and want_map)
+        cached = _ARENAS.get(key) if use_cache else None
+        have = int(cached is not None and cached[0].numel() >= n and (cached[1] is not None or not want_map)
+                   and (self.reuse_arena is True or not _arena_in_use(cached)))
+        if use_cache and self.m.world > 1:
             have = int(all(self._gather(have)))
         if have:
-            full, self.mapped = cached
+            full, self.mapped, _ = cached
             self.arena = full[:n]
             self.alloc_info["reused"] = True
             self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
@@ -705,8 +710,8 @@ class _Swarm:
             t_map = time.perf_counter()
             self.mapped = map_peer_arenas(self.arena, self.m.rank, self.m.world, self.m.data)
             self._mark("map_s", t_map)
-        if self.reuse_arena:
-            _ARENAS[key] = (self.arena, self.mapped)
+        if use_cache:
+            _ARENAS[key] = (self.arena, self.mapped, _storage_refs(self.arena))
         self._mark("alloc_s", t)
 
     def _alloc_tables(self, P):
@@ -1245,9 +1250,21 @@ def _merged_stats(parts: list) -> dict:
 _PIPELINES: dict = {}
 
 
-# Arenas kept by pulls made with reuse_arena=True: (arena, peer mappings or None), keyed by device,
-# world size, member ranks and whether the arena is peer-mapped.
+# Arenas kept between pulls (reuse_arena): (arena, peer mappings or None, storage references when
+# kept), keyed by device, world size, member ranks and whether the arena is peer-mapped.
 _ARENAS: dict = {}
+
+
+def _storage_refs(t: torch.Tensor) -> int:
+    """References to t's storage (tensors viewing it, view bases, and the probe's own storage
+    object)."""
+    return int(torch._C._storage_Use_Count(t.untyped_storage()._cdata))
+
+
+def _arena_in_use(entry) -> bool:
+    """Whether any tensor besides the kept arena still views its storage (a caller's tensor of an
+    earlier pull): more references than when the arena was kept."""
+    return _storage_refs(entry[0]) > entry[2]
 
 
 def adopt_arena(arena: torch.Tensor, mapped=None, group=None) -> None:
@@ -1259,7 +1276,7 @@ def adopt_arena(arena: torch.Tensor, mapped=None, group=None) -> None:
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     granks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(world))
     dev = arena.device.index if arena.device.type == "cuda" else -1
-    _ARENAS[(dev, world, granks, mapped is not None)] = (arena, mapped)
+    _ARENAS[(dev, world, granks, mapped is not None)] = (arena, mapped, _storage_refs(arena))
 
 
 def release_pipelines() -> None:
@@ -1299,7 +1316,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
                round_bytes: int | None = None, exchange: str = "auto",
                stats: dict | None = None, reuse_pipeline: bool | None = None,
-               possession: bool | None = None, reuse_arena: bool = False) -> dict[str, torch.Tensor]:
+               possession: bool | None = None, reuse_arena: bool | None = None) -> dict[str, torch.Tensor]:
     """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
     full set (views into one arena per rank).  `exchange`: "auto" (measured at setup, cached per
     process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
@@ -1312,10 +1329,13 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     its xorb cache already covers and holders own those terms (assign_owners) -- a rank with the
     whole model cached is the node's seeder.  `reuse_pipeline` (default ZEST_SWARM_REUSE, off): keep
     the fetch pipelines (pinned staging, Xet session) for the next pull of the same repository in
-    this process; release_pipelines() frees them.  `reuse_arena` (off): the pull lands in the
-    arena of this process's previous reuse_arena pull (same group, large enough) instead of a fresh
-    one -- that pull's tensors are overwritten, so only for a caller that dropped them (bench.py's
-    repeated pulls); release_pipelines() frees the kept arena."""
+    this process; release_pipelines() frees them.  `reuse_arena`: True -- the pull lands in the
+    arena kept from this process's previous pull over the same group (large enough) instead of a
+    fresh one, overwriting that pull's tensors (bench.py's repeated pulls); None (default) -- the
+    same for peer-mapped arenas (N > 1), but only when no tensor of the previous pull is still alive
+    (a fresh peer-mapped arena per pull would pile up: a released one stayed counted as used on the
+    box); False -- always a fresh arena.  Kept arenas hold their memory until the next pull or
+    release_pipelines()."""
     if reuse_pipeline is None:
         reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
     if possession is None:
@@ -1328,7 +1348,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify_received,
                 staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange,
                 reuse=reuse_pipeline, possession=possession)
-    sw.reuse_arena = bool(reuse_arena)
+    sw.reuse_arena = reuse_arena
     ok = False
     try:
         while True:
