@@ -531,6 +531,14 @@ class _Swarm:
         # of the first (half the staging, the same Xet session, caches and reconstructions); on CPU
         # groups it is a second host fetcher that joins no DHT (one node per process is enough).
         self.pipelined = os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
+        if self.m.world > 1 and self.cuda and not os.environ.get("ZEST_SWARM_STAGING_MB"):
+            # At N > 1 every round is one pull_terms call, and a call drains its pipeline before it
+            # returns: with 1 GiB staging slots a 1 GiB round was a single batch (its H2D and its
+            # kernels in series).  Slots of a quarter round keep 4 batches in flight within a round:
+            # public-path row 81.0 -> 92.4 GB/s at 2 ranks, 108.6 -> 133.8 at 4 (one shared GPU,
+            # 8B random, profiles/r5/swarm_staging_r5as/).  N = 1 pulls its share in one call and
+            # keeps the large slots.
+            staging_bytes = min(int(staging_bytes), max(64 << 20, self.round_bytes // 4))
         self.reuse_key = (repo, revision, repo_type, str(self.device), bool(p2p), tuple(peers or []), tracker,
                           bool(dht), tuple(dht_bootstrap or []), int(staging_bytes), int(threads), self.pipelined,
                           os.environ.get("HF_ENDPOINT"), os.environ.get("ZEST_CACHE_DIR"))
@@ -1338,6 +1346,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     release_pipelines()."""
     if reuse_pipeline is None:
         reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
+    if os.environ.get("ZEST_SWARM_STAGING_MB"):  # per-slot staging of the fetch pipelines (A/B knob)
+        staging_bytes = int(os.environ["ZEST_SWARM_STAGING_MB"]) << 20
     if possession is None:
         possession = os.environ.get("ZEST_SWARM_POSSESSION", "1") != "0"
     if round_bytes is None:
