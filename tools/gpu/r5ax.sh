@@ -1,0 +1,6 @@
+# round-5 call ax: closing check at HEAD: full `pytest -m gpu`, smoke, 8-rank one-GPU rehearsal
+# (8 ranks now keep 1 GiB staging slots)
+set -o pipefail
+export ZEST_SKIP_BUILD=1 TMPDIR=/tmp
+RANKS=8 bash tools/gpu/check.sh r5ax tests smoke rehearsal || exit 1
+grep '^{"metric' gpurun_out/r5ax/rehearsal.log | tail -1 | python -c "import json,sys; d=json.JSONDecoder().raw_decode(sys.stdin.read())[0]; e=d['extra']; print(d['value'], {k: e[k] for k in e if k in ('bf16_GBps','random_GBps','ipc_signals','swarm_pull_GBps','swarm_pull_step_s','swarm_pull_arena_reused','swarm_pull_error')})"
