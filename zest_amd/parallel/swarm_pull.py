@@ -66,6 +66,25 @@ HEAD_TAPER = (0.25, 0.5)
 TAIL_TAPER = (0.5, 0.25, 0.125)
 
 
+def staging_slot_bytes(staging_bytes: int, round_bytes: int, world: int) -> int:
+    """Staging slot size of a device swarm pull at `world` ranks.
+
+    At N > 1 every round is one pull_terms call, and a call drains its pipeline before it
+    returns: with 1 GiB staging slots a 1 GiB round was a single batch (its H2D and its
+    kernels in series).  Slots of a quarter round keep 4 batches in flight within a round:
+    public-path row 81.0 -> 92.4 GB/s at 2 ranks, 108.6 -> 133.8 at 4 (one shared GPU,
+    8B random, profiles/r5/swarm_staging_r5as/).  At 8 ranks quarter slots stalled one
+    pull in three or five for ~2.5 s (three runs, cause not found) while half-round slots
+    never did in 10 pulls and still beat 1 GiB: 159.3 / 161.8 vs 144.3 GB/s
+    (profiles/r5/swarm_staging_r5av/), so worlds above 4 take half-round slots.  N = 1
+    pulls its share in one call and keeps the large slots.
+    """
+    if world <= 1:
+        return int(staging_bytes)
+    split = 4 if world <= 4 else 2
+    return min(int(staging_bytes), max(64 << 20, int(round_bytes) // split))
+
+
 class SwarmPullError(RuntimeError):
     pass
 
@@ -531,18 +550,8 @@ class _Swarm:
         # of the first (half the staging, the same Xet session, caches and reconstructions); on CPU
         # groups it is a second host fetcher that joins no DHT (one node per process is enough).
         self.pipelined = os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
-        if self.m.world > 1 and self.cuda and not os.environ.get("ZEST_SWARM_STAGING_MB"):
-            # At N > 1 every round is one pull_terms call, and a call drains its pipeline before it
-            # returns: with 1 GiB staging slots a 1 GiB round was a single batch (its H2D and its
-            # kernels in series).  Slots of a quarter round keep 4 batches in flight within a round:
-            # public-path row 81.0 -> 92.4 GB/s at 2 ranks, 108.6 -> 133.8 at 4 (one shared GPU,
-            # 8B random, profiles/r5/swarm_staging_r5as/).  At 8 ranks quarter slots stalled one
-            # pull in three or five for ~2.5 s (three runs, cause not found) while half-round slots
-            # never did in 10 pulls and still beat 1 GiB: 159.3 / 161.8 vs 144.3 GB/s
-            # (profiles/r5/swarm_staging_r5av/), so worlds above 4 take half-round slots.  N = 1
-            # pulls its share in one call and keeps the large slots.
-            split = 4 if self.m.world <= 4 else 2
-            staging_bytes = min(int(staging_bytes), max(64 << 20, self.round_bytes // split))
+        if self.cuda and not os.environ.get("ZEST_SWARM_STAGING_MB"):
+            staging_bytes = staging_slot_bytes(staging_bytes, self.round_bytes, self.m.world)
         self.reuse_key = (repo, revision, repo_type, str(self.device), bool(p2p), tuple(peers or []), tracker,
                           bool(dht), tuple(dht_bootstrap or []), int(staging_bytes), int(threads), self.pipelined,
                           os.environ.get("HF_ENDPOINT"), os.environ.get("ZEST_CACHE_DIR"))
