@@ -76,12 +76,14 @@ def staging_slot_bytes(staging_bytes: int, round_bytes: int, world: int) -> int:
     8B random, profiles/r5/swarm_staging_r5as/).  At 8 ranks quarter slots stalled one
     pull in three or five for ~2.5 s (three runs, cause not found) while half-round slots
     never did in 10 pulls and still beat 1 GiB: 159.3 / 161.8 vs 144.3 GB/s
-    (profiles/r5/swarm_staging_r5av/), so worlds above 4 take half-round slots.  N = 1
-    pulls its share in one call and keeps the large slots.
+    (profiles/r5/swarm_staging_r5av/).  A 4-rank rehearsal then stalled the same way with quarter
+    slots (steps 2.41 / 0.53 s, profiles/r5/rehearsal_n2_n4_r5bb/), so only 2 ranks take quarter
+    slots and larger worlds half-round slots.  N = 1 pulls its share in one call and keeps the
+    large slots.
     """
     if world <= 1:
         return int(staging_bytes)
-    split = 4 if world <= 4 else 2
+    split = 4 if world <= 2 else 2
     return min(int(staging_bytes), max(64 << 20, int(round_bytes) // split))
 
 
