@@ -138,6 +138,10 @@ PYBIND11_MODULE(_hip, m) {
     check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault, S(st)),
           "hipMemcpyAsync");
   });
+  // Stream-order `st` after a raw hipEvent_t (DeviceXetPull.wait_item's item events).
+  m.def("stream_wait_event", [](uintptr_t st, uintptr_t ev) {
+    check(hipStreamWaitEvent(S(st), reinterpret_cast<hipEvent_t>(ev), 0), "hipStreamWaitEvent");
+  });
   // K8 (xgmi exchange): one launch pulls every (peer src, local dst, bytes) segment.
   m.def("peer_gather", [](const std::vector<uint64_t>& src, const std::vector<uint64_t>& dst,
                           const std::vector<uint64_t>& n, uintptr_t st) {

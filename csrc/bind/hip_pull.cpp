@@ -129,6 +129,41 @@ void bind_hip_pull(py::module_& m) {
            py::arg("jobs"), py::arg("hashes_ptr"), py::arg("sizes_ptr") = 0, py::arg("repair") = false,
            "[(xet_hash, t0, t1, dst_ptr, chunk0), ...]: fetch term ranges, GPU decode + chunk-hash them into "
            "place (hashes/sizes: device tables indexed by chunk); consecutive chunk indices required")
+      .def("submit_terms",
+           [](DeviceXetPull& self, const std::vector<zest::TermJobTuple>& v, uintptr_t hashes, uintptr_t sizes) {
+             const auto jobs = zest::term_jobs_of(v);
+             py::gil_scoped_release nogil;
+             return self.submit_terms(jobs, reinterpret_cast<uint8_t*>(hashes), reinterpret_cast<uint64_t*>(sizes));
+           },
+           py::arg("jobs"), py::arg("hashes_ptr"), py::arg("sizes_ptr") = 0,
+           "pull_terms as one item of the persistent streaming pipeline (no drain between items): returns a "
+           "ticket at once; wait_item(ticket) collects it")
+      .def("wait_item",
+           [](DeviceXetPull& self, uint64_t ticket) {
+             DeviceXetPull::ItemResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = self.wait_item(ticket);
+             }
+             return py::make_tuple(r.err, r.err.empty() ? zest::term_results_py(r.results) : py::list(), r.event);
+           },
+           py::arg("ticket"),
+           "(error, results, event): blocks until the item's kernels are queued (or it failed); event is a "
+           "hipEvent_t (int) completing with them -- order exchanges after it with stream_wait_event")
+      .def("item_error",
+           [](DeviceXetPull& self, uint64_t ticket) {
+             py::gil_scoped_release nogil;
+             return self.item_error(ticket);
+           },
+           py::arg("ticket"), "the item's device decode error word (0 = clean); waits for its kernels")
+      .def("stream_reset",
+           [](DeviceXetPull& self, bool cancel) {
+             py::gil_scoped_release nogil;
+             self.stream_reset(cancel);
+           },
+           py::arg("cancel") = false,
+           "wait for every submitted item and forget them (between pulls); cancel: abandon the ones still "
+           "fetching first")
       .def("settle", [](DeviceXetPull& self, const std::string& hex, bool ok) {
              py::gil_scoped_release nogil;
              return self.settle(hex, ok);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -155,6 +156,7 @@ struct DeviceXetPull::Impl {
   }
 
   ~Impl() {
+    s_stop();
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
@@ -387,6 +389,75 @@ struct DeviceXetPull::Impl {
     std::string fetch_err;
   };
 
+  // A term of a pass in segment order: its segment, term index, output offset from the pass's base
+  // address, first chunk (pass-relative), chunk count and unpacked size.
+  struct GTerm {
+    size_t seg, term;
+    uint64_t dst;
+    uint64_t chunk;
+    uint32_t nchunks;
+    uint64_t ulen;
+  };
+  struct TermFetch {
+    uint64_t src_at = 0, len = 0;  // the run's chunk span in the slot: offset, bytes
+    TermSource src;
+    bool planned = true;           // the run matched the term's plan (else its records stay zero)
+  };
+  // One term of a pass: fetch its run through the cache -> P2P -> CDN waterfall into `region` (the
+  // term's reserved part of a pinned staging slot, `room` bytes, at `region_off` in the slot) and
+  // write its chunks' device records into `cr` and their sizes into `lens`.  A run that does not
+  // match the plan keeps zero (no-op) records, so its file fails the Merkle check and takes the
+  // repair path.  `copied` runs once no writer copy thread reads the region any more (now, unless
+  // the fetch deferred the cache copy to the writer).  Throws on a fetch error.
+  TermFetch fetch_term_into(const cas::Reconstruction& rec, const GTerm& g, const FetchOptions& topt,
+                            const std::function<void()>& copied, uint8_t* region, uint64_t room, uint64_t region_off,
+                            uint32_t tag, ZgChunk* cr, uint32_t* lens, TermSource& src_out) {
+    auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
+    XorbFetchResult r;
+    try {
+      r = sh_->bridge->fetch_term(rec.terms[g.term], rec, topt, sink);
+    } catch (...) {
+      copied();
+      throw;
+    }
+    if (!r.copy_deferred) copied();
+    TermFetch tf;
+    tf.src = TermSource{r.source, r.run_offset, r.pending};
+    src_out = tf.src;  // (recorded before any check below throws: a quarantined run is dropped on failure)
+    auto idx = xet::index_chunks(r.bytes(), r.size());
+    if (r.local_end > idx.size() || r.local_start >= r.local_end)
+      throw Error("RangeOutOfBounds", rec.terms[g.term].hash_hex);
+    const uint64_t a = idx[r.local_start].header_off;
+    const uint64_t e_end = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
+    if (r.ext) {
+      tf.src_at = region_off + a;  // already in place
+    } else {
+      if (e_end - a > room) throw Error("TermTooLarge", "term " + std::to_string(g.term) + " exceeds its bound");
+      std::memcpy(region, r.data.data() + a, e_end - a);
+      tf.src_at = region_off;
+    }
+    tf.len = e_end - a;
+    const uint64_t run0 = tf.src_at;
+    uint64_t uoff = 0;
+    bool ok = r.local_end - r.local_start == g.nchunks;
+    for (uint32_t c = r.local_start; ok && c < r.local_end; ++c) {
+      const xet::ChunkEntry& e = idx[c];
+      const uint32_t sc = uint32_t(e.scheme);
+      if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
+        ok = false;
+        break;
+      }
+      cr[c - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, g.dst + uoff, e.clen, e.ulen, sc, tag};
+      lens[c - r.local_start] = e.ulen;
+      uoff += e.ulen;
+    }
+    if (!ok || uoff != g.ulen) {
+      std::fill(cr, cr + g.nchunks, ZgChunk{});
+      tf.planned = false;
+    }
+    return tf;
+  }
+
   // Publish (ok) or drop/evict (!ok) the cache runs behind every term of the attempt's files.
   template <typename OkFn>
   void settle_all(const Attempt& at, const std::vector<const cas::Reconstruction*>& recs,
@@ -465,6 +536,7 @@ struct DeviceXetPull::Impl {
   SegAttempt run_segments(const std::vector<Seg>& segs, uint8_t* hash_out, uint64_t* size_out, const FetchOptions& opt,
                           int attempt, const std::function<void(size_t, uint64_t)>& progress) {
     (void)attempt;
+    s_drain();  // the streaming engine shares the slots and streams: nothing of it may be in flight
     const size_t ns = segs.size();
     SegAttempt at;
     at.sources.resize(ns);
@@ -472,13 +544,6 @@ struct DeviceXetPull::Impl {
     at.planned_ok.assign(ns, 1);
     at.seg_fetched.assign(ns, 0);
     // Global term list in segment order; chunk indices are relative to segs[0].chunk0.
-    struct GTerm {
-      size_t seg, term;
-      uint64_t dst;    // device address offset from `base`
-      uint64_t chunk;  // index of the term's first chunk (pass-relative)
-      uint32_t nchunks;
-      uint64_t ulen;
-    };
     std::vector<GTerm> gt;
     std::vector<uint64_t> seg_chunk0(ns + 1, 0), seg_dst0(ns, 0);
     uintptr_t base = UINTPTR_MAX, top_addr = 0;
@@ -609,7 +674,6 @@ struct DeviceXetPull::Impl {
             // fits (no intermediate heap buffer); otherwise only its chunk span is copied in.
             uint8_t* region = s.host + bt.off[j];
             const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
-            auto sink = [&](size_t nbytes) -> uint8_t* { return nbytes <= room ? region : nullptr; };
             FetchOptions topt = opt;
             {
               std::lock_guard<std::mutex> g(mu);
@@ -623,49 +687,13 @@ struct DeviceXetPull::Impl {
               cv.notify_all();
             };
             if (sh_->writer) topt.on_copied = copied;
-            XorbFetchResult r;
-            try {
-              r = sh_->bridge->fetch_term(rec.terms[gt[i].term], rec, topt, sink);
-            } catch (...) {
-              copied();
-              throw;
-            }
-            if (!r.copy_deferred) copied();
-            at.sources[gt[i].seg][gt[i].term - segs[gt[i].seg].t0] = TermSource{r.source, r.run_offset, r.pending};
-            auto idx = xet::index_chunks(r.bytes(), r.size());
-            if (r.local_end > idx.size() || r.local_start >= r.local_end)
-              throw Error("RangeOutOfBounds", rec.terms[gt[i].term].hash_hex);
-            const uint64_t a = idx[r.local_start].header_off;
-            const uint64_t e_end = idx[r.local_end - 1].header_off + xet::kChunkHeaderLen + idx[r.local_end - 1].clen;
-            if (r.ext) {
-              bt.src_at[j] = bt.off[j] + a;  // already in place
-            } else {
-              if (e_end - a > room) throw Error("TermTooLarge", "term " + std::to_string(i) + " exceeds its bound");
-              std::memcpy(region, r.data.data() + a, e_end - a);
-              bt.src_at[j] = bt.off[j];
-            }
-            bt.len[j] = e_end - a;
-            // the device records of this term's chunks; a term that does not match its plan keeps
-            // zero (no-op) records, so its file fails the Merkle check and takes the repair path
             ZgChunk* cr = s.recs() + (gt[i].chunk - chunk_lo(b));
-            const uint64_t run0 = bt.src_at[j];
-            uint64_t uoff = 0;
-            bool ok = r.local_end - r.local_start == gt[i].nchunks;
             uint32_t* lens = at.chunk_lens[gt[i].seg].data() + (gt[i].chunk - seg_chunk0[gt[i].seg]);
-            for (uint32_t c = r.local_start; ok && c < r.local_end; ++c) {
-              const xet::ChunkEntry& e = idx[c];
-              const uint32_t sc = uint32_t(e.scheme);
-              if (sc > 2 || (sc == 0 && e.clen != e.ulen) || e.ulen > 128u * 1024u) {
-                ok = false;
-                break;
-              }
-              cr[c - r.local_start] = ZgChunk{run0 + (e.header_off - a) + xet::kChunkHeaderLen, gt[i].dst + uoff,
-                                               e.clen, e.ulen, sc, uint32_t(j)};
-              lens[c - r.local_start] = e.ulen;
-              uoff += e.ulen;
-            }
-            if (!ok || uoff != gt[i].ulen) {
-              std::fill(cr, cr + gt[i].nchunks, ZgChunk{});
+            const TermFetch tf = fetch_term_into(rec, gt[i], topt, copied, region, room, bt.off[j], uint32_t(j), cr, lens,
+                                                 at.sources[gt[i].seg][gt[i].term - segs[gt[i].seg].t0]);
+            bt.src_at[j] = tf.src_at;
+            bt.len[j] = tf.len;
+            if (!tf.planned) {
               std::lock_guard<std::mutex> g(mu);
               at.planned_ok[gt[i].seg] = 0;
             }
@@ -820,16 +848,549 @@ struct DeviceXetPull::Impl {
     return at;
   }
 
+
+  // ---------------------------------------------------------------------------------------------
+  // Streaming submission (the swarm pull's rounds at N > 1).  pull_terms() is one pass that drains
+  // its streams before it returns, so a caller issuing one call per round serialized every round
+  // boundary.  submit_terms() instead appends an item -- one round's term
+  // ranges -- to ONE continuous pipeline whose fetch workers, submitter and releaser threads, pinned
+  // slots and copy / compute streams persist across items: the workers take terms in submission
+  // order across item boundaries, the submitter queues every staging batch's H2D copy and
+  // decode/place/hash kernels as soon as its terms are in, and the releaser hands a host slot back
+  // once its copy landed.  Nothing waits for the GPU between items.  wait_item(ticket) returns once
+  // the item's last kernels are queued, with a HIP event that completes with them; the caller
+  // orders the item's exchange after that event (stream wait, or a peer ready counter) without ever
+  // blocking on the device.  Batches never cross items, and a failed item (a fetch that fails from
+  // every source, or a run that does not match its plan) skips its remaining fetches and GPU work,
+  // so the caller can hand it to another rank.  Device decode errors are reported per item by
+  // item_error() (an error word per item, copied back behind its kernels).
+  struct SItem {
+    uint64_t ticket = 0;
+    std::vector<TermJob> jobs;
+    std::vector<Seg> segs;
+    std::vector<GTerm> gt;
+    std::vector<uint64_t> seg_chunk0;
+    uint8_t* dst = nullptr;  // base device address (the item's lowest output byte)
+    uint64_t dst_size = 0;
+    uint8_t* hash_out = nullptr;  // hashes + 32 * chunk0 of the item
+    uint64_t* size_out = nullptr;
+    SegAttempt at;
+    size_t b0 = 0, nb = 0;  // global batches [b0, b0 + nb)
+    bool failed = false;
+    std::string err;
+    bool queued = false;     // the submitter passed the item's last batch (done event recorded)
+    bool collected = false;  // wait_item() ran
+    hipEvent_t done = nullptr;
+    size_t eslot = 0;        // error word index
+  };
+  struct SBatch {
+    SItem* item = nullptr;
+    size_t begin = 0, end = 0;  // terms [begin, end) of item->gt
+    std::vector<uint64_t> off, len, src_at;
+    uint64_t c_lo = 0, c_hi = 0;  // item-relative chunk range
+    size_t remaining = 0;
+    size_t copies = 0;
+    bool gpu = false;  // its H2D + kernels were queued
+    uint64_t h2d = 0;  // bytes copied
+    std::array<hipEvent_t, 4> tev{};  // ZEST_DEVICE_TIMING: copy start / end, kernels start / end
+  };
+  static constexpr size_t kErrRing = 4096;
+
+  void s_start() {
+    if (s_started_) return;
+    init_device();
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    const size_t S = nslots_;
+    sh2d_.assign(S, nullptr);
+    skern_.assign(S, nullptr);
+    skern_set_.assign(S, 0);
+    sready_.resize(S);
+    for (size_t i = 0; i < S; ++i) {
+      hip_check(hipEventCreateWithFlags(&sh2d_[i], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&skern_[i], hipEventDisableTiming), "hipEventCreate");
+      sready_[i] = i;
+    }
+    serr_.ensure(kErrRing);
+    if (!serr_host_.alloc(kErrRing * sizeof(unsigned long long))) throw Error("HipError", "pinning the error words failed");
+    std::memset(serr_host_.data(), 0, kErrRing * sizeof(unsigned long long));
+    const int nt = threads_ > 0 ? threads_ : 16;
+    for (int t = 0; t < nt; ++t) sworkers_.emplace_back([this] { s_worker(); });
+    ssubmitter_ = std::thread([this] { s_submitter(); });
+    sreleaser_ = std::thread([this] { s_releaser(); });
+    s_started_ = true;
+  }
+
+  void s_stop() {
+    if (!s_started_) return;
+    {
+      std::lock_guard<std::mutex> g(smu_);
+      sstop_ = true;
+    }
+    scv_.notify_all();
+    for (auto& t : sworkers_) t.join();
+    ssubmitter_.join();
+    sreleaser_.join();
+    sworkers_.clear();
+    (void)hipStreamSynchronize(copy_stream_);
+    (void)hipStreamSynchronize(stream_);
+    for (auto& it : sitems_)
+      if (it->done) (void)hipEventDestroy(it->done);
+    sitems_.clear();
+    for (hipEvent_t e : sh2d_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : skern_) (void)hipEventDestroy(e);
+    sh2d_.clear();
+    skern_.clear();
+    s_started_ = false;
+  }
+
+  // Every submitted batch released (fetched, queued, copy landed, slot back) and both streams idle.
+  void s_drain() {
+    if (!s_started_) return;
+    {
+      std::unique_lock<std::mutex> g(smu_);
+      scv_.wait(g, [&] { return sreleased_ == sbatch_total_; });
+    }
+    hip_check(hipStreamSynchronize(copy_stream_), "sync copy stream");
+    hip_check(hipStreamSynchronize(stream_), "sync compute stream");
+  }
+
+  // Forget every item (their events too): between pulls, once the caller waited for all of them.
+  // `cancel`: items still fetching are marked failed first, so their remaining terms are skipped.
+  void s_reset(bool cancel) {
+    if (!s_started_) return;
+    if (cancel) {
+      {
+        std::lock_guard<std::mutex> g(smu_);
+        for (auto& it : sitems_)
+          if (!it->queued && !it->failed) {
+            it->failed = true;
+            it->err = "cancelled";
+          }
+      }
+      scv_.notify_all();
+    }
+    s_drain();
+    std::lock_guard<std::mutex> g(smu_);
+    if (timing_) {  // the streamed pass's device timeline (timeline_json), then its events go
+      std::vector<std::array<hipEvent_t, 4>> tev;
+      uint64_t h2d = 0;
+      for (auto& b : sbatches_)
+        if (b.gpu && b.tev[0]) {
+          tev.push_back(b.tev);
+          h2d += b.h2d;
+        }
+      record_timeline(tev, h2d);
+      for (auto& b : sbatches_)
+        for (auto& e : b.tev)
+          if (e) (void)hipEventDestroy(e);
+    }
+    for (auto& it : sitems_)
+      if (it->done) (void)hipEventDestroy(it->done);
+    sitems_.clear();
+    sbatches_.clear();
+    swork_.clear();
+    swork_next_ = 0;
+    sb0_ = sbatch_total_;
+  }
+
+  SItem* s_find(uint64_t ticket) {
+    for (auto& it : sitems_)
+      if (it->ticket == ticket) return it.get();
+    throw Error("InvalidArgument", "unknown pull ticket " + std::to_string(ticket));
+  }
+
+  uint64_t submit_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes) {
+    s_start();
+    auto item = std::make_unique<SItem>();
+    SItem& it = *item;
+    it.jobs = jobs;
+    uint64_t next_chunk = jobs.empty() ? 0 : jobs[0].chunk0;
+    for (const TermJob& j : jobs) {
+      const cas::Reconstruction& rec = sh_->recs->get(j.xet_hash);
+      if (j.t0 > j.t1 || j.t1 > rec.terms.size()) throw Error("RangeOutOfBounds", "term range of " + j.xet_hash);
+      if (j.chunk0 != next_chunk) throw Error("InvalidArgument", "term jobs must cover consecutive chunk indices");
+      for (uint32_t t = j.t0; t < j.t1; ++t) next_chunk += rec.terms[t].range.end - rec.terms[t].range.start;
+      it.segs.push_back({&rec, j.t0, j.t1, j.dst, j.chunk0});
+    }
+    const size_t ns = it.segs.size();
+    it.at.sources.resize(ns);
+    it.at.chunk_lens.resize(ns);
+    it.at.planned_ok.assign(ns, 1);
+    it.at.seg_fetched.assign(ns, 0);
+    uintptr_t base = UINTPTR_MAX, top_addr = 0;
+    for (const Seg& sg : it.segs) {
+      uint64_t bytes = 0;
+      for (uint32_t t = sg.t0; t < sg.t1; ++t) bytes += sg.rec->terms[t].unpacked_length;
+      base = std::min(base, sg.dst);
+      top_addr = std::max<uintptr_t>(top_addr, sg.dst + bytes);
+    }
+    it.seg_chunk0.assign(ns + 1, 0);
+    for (size_t sidx = 0; sidx < ns; ++sidx) {
+      const Seg& sg = it.segs[sidx];
+      it.at.sources[sidx].resize(sg.t1 - sg.t0);
+      uint64_t off = 0, c = it.seg_chunk0[sidx];
+      for (uint32_t i = sg.t0; i < sg.t1; ++i) {
+        const auto& t = sg.rec->terms[i];
+        const uint32_t n = uint32_t(t.range.end - t.range.start);
+        it.gt.push_back({sidx, i, sg.dst - base + off, c, n, t.unpacked_length});
+        off += t.unpacked_length;
+        c += n;
+      }
+      it.seg_chunk0[sidx + 1] = c;
+      it.at.chunk_lens[sidx].assign(size_t(c - it.seg_chunk0[sidx]), 0);
+    }
+    const size_t n = it.gt.size();
+    const uint64_t nck = it.seg_chunk0[ns];
+    it.dst = ns ? reinterpret_cast<uint8_t*>(base) : nullptr;
+    it.dst_size = ns ? uint64_t(top_addr - base) : 0;
+    it.hash_out = hashes + 32 * (ns ? it.segs[0].chunk0 : 0);
+    it.size_out = sizes ? sizes + (ns ? it.segs[0].chunk0 : 0) : nullptr;
+    // batches of whole terms that fit a slot (as in run_segments); a term larger than a slot grows
+    // every slot, and the slots' record tables / device buffers grow to the largest batch -- both
+    // only with the pipeline idle
+    uint64_t max_bound = 0;
+    for (size_t i = 0; i < n; ++i) max_bound = std::max(max_bound, term_bound(it.gt[i].ulen, it.gt[i].nchunks));
+    if (max_bound > cap_) {
+      s_drain();
+      grow_staging(max_bound);
+    }
+    std::vector<SBatch> bs;
+    for (size_t next = 0; next < n;) {
+      SBatch bt;
+      bt.item = &it;
+      bt.begin = next;
+      uint64_t pos = 0;
+      size_t end = next;
+      while (end < n) {
+        const uint64_t bound = term_bound(it.gt[end].ulen, it.gt[end].nchunks);
+        if (pos + bound > cap_ && end > next) break;
+        bt.off.push_back(pos);
+        pos += bound;
+        ++end;
+      }
+      bt.end = end;
+      bt.len.assign(end - next, 0);
+      bt.src_at.assign(end - next, 0);
+      bt.c_lo = it.gt[next].chunk;
+      bt.c_hi = end < n ? it.gt[end].chunk : nck;
+      bt.remaining = end - next;
+      bs.push_back(std::move(bt));
+      next = end;
+    }
+    size_t max_recs = 1, max_hs = 1;
+    for (const SBatch& bt : bs) {
+      uint64_t ub = 0;
+      for (size_t i = bt.begin; i < bt.end; ++i) ub += it.gt[i].ulen;
+      max_recs = std::max<size_t>(max_recs, size_t(bt.c_hi - bt.c_lo));
+      max_hs = std::max(max_hs, zg_hash_scratch_bytes(int(bt.c_hi - bt.c_lo), ub));
+    }
+    bool grow = false;
+    for (const auto& sl : slots_) grow |= sl.rec_cap < max_recs || sl.chunks_dev.n < max_recs || sl.scratch.n < max_hs;
+    if (grow) {
+      s_drain();
+      for (auto& sl : slots_) {
+        if (sl.rec_cap < max_recs) {
+          const size_t cap = std::max(max_recs, size_t(16384));
+          if (!sl.rec_pin.alloc(cap * sizeof(ZgChunk))) throw Error("HipError", "pinning the chunk records failed");
+          sl.rec_cap = cap;
+        }
+        sl.chunks_dev.ensure(std::max(max_recs, sl.rec_cap));
+        sl.scratch.ensure(max_hs);
+      }
+    }
+    hip_check(hipEventCreateWithFlags(&it.done, hipEventDisableTiming), "hipEventCreate");
+    uint64_t ticket;
+    {
+      std::lock_guard<std::mutex> g(smu_);
+      size_t unread = 0;
+      for (auto& x : sitems_) unread += !x->collected;
+      if (unread >= kErrRing) {
+        (void)hipEventDestroy(it.done);
+        throw Error("InvalidArgument", "too many pull items in flight");
+      }
+      ticket = ++sticket_;
+      it.ticket = ticket;
+      it.eslot = size_t(ticket % kErrRing);
+      it.b0 = sbatch_total_;
+      it.nb = bs.size();
+      for (size_t k = 0; k < bs.size(); ++k) {
+        for (size_t i = bs[k].begin; i < bs[k].end; ++i) swork_.emplace_back(sbatch_total_ + k, i);
+        sbatches_.push_back(std::move(bs[k]));
+      }
+      sbatch_total_ += it.nb;
+      if (it.nb == 0) it.queued = true;  // nothing to fetch (the caller still gets a done event)
+      sitems_.push_back(std::move(item));
+    }
+    if (it.nb == 0) hip_check(hipEventRecord(it.done, stream_), "event");
+    scv_.notify_all();
+    return ticket;
+  }
+
+  void s_worker() {
+    (void)hipSetDevice(device_);
+    const size_t S = nslots_;
+    while (true) {
+      size_t g, i;
+      SBatch* bp;
+      {
+        std::unique_lock<std::mutex> lk(smu_);
+        scv_.wait(lk, [&] { return sstop_ || swork_next_ < swork_.size(); });
+        if (sstop_) return;
+        std::tie(g, i) = swork_[swork_next_++];
+        bp = &sbatches_[g - sb0_];
+        SItem& it = *bp->item;
+        scv_.wait(lk, [&] { return sstop_ || it.failed || sready_[g % S] >= g; });
+        if (sstop_) return;
+        if (it.failed) {  // the item is lost: its other terms need no fetch
+          if (--bp->remaining == 0) scv_.notify_all();
+          continue;
+        }
+        ++bp->copies;
+      }
+      SBatch& bt = *bp;
+      SItem& it = *bt.item;
+      Slot& s = slots_[g % S];
+      const size_t j = i - bt.begin;
+      try {
+        const GTerm& gti = it.gt[i];
+        const cas::Reconstruction& rec = *it.segs[gti.seg].rec;
+        uint8_t* region = s.host + bt.off[j];
+        const uint64_t room = (i + 1 < bt.end ? bt.off[j + 1] : cap_) - bt.off[j];
+        FetchOptions topt;
+        auto copied = [this, bp]() {
+          {
+            std::lock_guard<std::mutex> lk(smu_);
+            --bp->copies;
+          }
+          scv_.notify_all();
+        };
+        if (sh_->writer) topt.on_copied = copied;
+        ZgChunk* cr = s.recs() + (gti.chunk - bt.c_lo);
+        uint32_t* lens = it.at.chunk_lens[gti.seg].data() + (gti.chunk - it.seg_chunk0[gti.seg]);
+        const TermFetch tf = fetch_term_into(rec, gti, topt, copied, region, room, bt.off[j], uint32_t(j), cr, lens,
+                                             it.at.sources[gti.seg][gti.term - it.segs[gti.seg].t0]);
+        bt.src_at[j] = tf.src_at;
+        bt.len[j] = tf.len;
+        std::lock_guard<std::mutex> lk(smu_);
+        if (!tf.planned) {
+          it.at.planned_ok[gti.seg] = 0;
+          if (!it.failed) {
+            it.failed = true;
+            it.err = "term range of " + it.jobs[gti.seg].xet_hash + " does not match its plan";
+          }
+        }
+        if (--bt.remaining == 0) scv_.notify_all();
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(smu_);
+        if (!it.failed) {
+          it.failed = true;
+          it.err = e.what();
+        }
+        if (--bt.remaining == 0) scv_.notify_all();
+      }
+    }
+  }
+
+  void s_submitter() {
+    (void)hipSetDevice(device_);
+    const size_t S = nslots_;
+    while (true) {
+      size_t g;
+      SBatch* bp;
+      bool failed;
+      {
+        std::unique_lock<std::mutex> lk(smu_);
+        scv_.wait(lk, [&] {
+          if (sstop_) return true;
+          if (ssubmit_next_ >= sb0_ + sbatches_.size() || ssubmit_next_ < sb0_) return false;
+          const SBatch& b = sbatches_[ssubmit_next_ - sb0_];
+          return b.remaining == 0 && sready_[ssubmit_next_ % S] >= ssubmit_next_;
+        });
+        if (sstop_) return;
+        g = ssubmit_next_++;
+        bp = &sbatches_[g - sb0_];
+        failed = bp->item->failed;
+      }
+      SBatch& bt = *bp;
+      SItem& it = *bt.item;
+      const size_t slot = g % S;
+      Slot& s = slots_[slot];
+      const bool first = g == it.b0, last = g + 1 == it.b0 + it.nb;
+      std::string err;
+      try {
+        trace::Span sp("device", "stream: queue H2D + place/hash");
+        if (first) hip_check(hipMemsetAsync(serr_.p + it.eslot, 0, sizeof(unsigned long long), stream_), "hipMemset");
+        if (!failed) {
+          uint64_t top = 0, fetched = 0;
+          for (size_t j = 0; j < bt.len.size(); ++j) {
+            top = std::max<uint64_t>(top, bt.src_at[j] + bt.len[j]);
+            fetched += bt.len[j];
+            it.at.seg_fetched[it.gt[bt.begin + j].seg] += bt.len[j];
+          }
+          it.at.fetched += fetched;
+          const int nchunks = int(bt.c_hi - bt.c_lo);
+          uint64_t ubytes = 0;
+          for (size_t i = bt.begin; i < bt.end; ++i) ubytes += it.gt[i].ulen;
+          bool compressed = false;
+          for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.recs()[c].scheme != 0;
+          const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
+          if (skern_set_[slot]) hip_check(hipStreamWaitEvent(copy_stream_, skern_[slot], 0), "hipStreamWaitEvent");
+          if (timing_)
+            for (auto& e : bt.tev) hip_check(hipEventCreate(&e), "hipEventCreate");
+          if (timing_) hip_check(hipEventRecord(bt.tev[0], copy_stream_), "event");
+          static const uint64_t merge_gap = env_size("ZEST_H2D_MERGE_GAP", size_t(64) << 10);
+          for (const auto& [lo, hi] : copy_ranges(bt.src_at, bt.len, merge_gap)) {
+            hip_check(hipMemcpyAsync(s.dev.p + lo, s.host + lo, hi - lo, hipMemcpyHostToDevice, copy_stream_), "H2D");
+            bt.h2d += hi - lo;
+          }
+          if (nchunks)
+            hip_check(hipMemcpyAsync(s.chunks_dev.p, s.recs(), sizeof(ZgChunk) * size_t(nchunks), hipMemcpyHostToDevice,
+                                     copy_stream_),
+                      "H2D chunk records");
+          hip_check(hipEventRecord(sh2d_[slot], copy_stream_), "event");
+          if (timing_) hip_check(hipEventRecord(bt.tev[1], copy_stream_), "event");
+          hip_check(hipStreamWaitEvent(stream_, sh2d_[slot], 0), "hipStreamWaitEvent");
+          if (timing_) hip_check(hipEventRecord(bt.tev[2], stream_), "event");
+          hip_check(zg_ingest_chunks(s.dev.p, top, it.dst, it.dst_size, s.chunks_dev.p, nchunks, compressed ? 1 : 0,
+                                     serr_.p + it.eslot, it.hash_out + 32 * bt.c_lo,
+                                     it.size_out ? it.size_out + bt.c_lo : nullptr, 0, s.scratch.p, hs_bytes, stream_),
+                    "ingest");
+          if (timing_) hip_check(hipEventRecord(bt.tev[3], stream_), "event");
+          hip_check(hipEventRecord(skern_[slot], stream_), "event");
+          skern_set_[slot] = 1;
+          bt.gpu = true;
+        }
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      if (last) {
+        (void)hipMemcpyAsync(reinterpret_cast<unsigned long long*>(serr_host_.data()) + it.eslot, serr_.p + it.eslot,
+                             sizeof(unsigned long long), hipMemcpyDeviceToHost, stream_);
+        if (hipEventRecord(it.done, stream_) != hipSuccess && err.empty()) err = "hipEventRecord (item done)";
+      }
+      {
+        std::lock_guard<std::mutex> lk(smu_);
+        if (!err.empty() && !it.failed) {
+          it.failed = true;
+          it.err = err;
+        }
+        sissued_.push_back(g);
+        if (last) it.queued = true;
+      }
+      scv_.notify_all();
+    }
+  }
+
+  void s_releaser() {
+    (void)hipSetDevice(device_);
+    const size_t S = nslots_;
+    while (true) {
+      size_t g;
+      SBatch* bp;
+      {
+        std::unique_lock<std::mutex> lk(smu_);
+        scv_.wait(lk, [&] { return sstop_ || !sissued_.empty(); });
+        if (sissued_.empty()) return;  // stopping
+        g = sissued_.front();
+        sissued_.pop_front();
+        bp = &sbatches_[g - sb0_];
+      }
+      const bool ok = !bp->gpu || hipEventSynchronize(sh2d_[g % S]) == hipSuccess;
+      {
+        std::unique_lock<std::mutex> lk(smu_);
+        if (!ok && !bp->item->failed) {
+          bp->item->failed = true;
+          bp->item->err = "hipEventSynchronize (H2D)";
+        }
+        // the write-behind writer's copy threads are done with the slot
+        scv_.wait(lk, [&] { return sstop_ || bp->copies == 0; });
+        sready_[g % S] = g + S;
+        ++sreleased_;
+      }
+      scv_.notify_all();
+    }
+  }
+
+  struct ItemResult {
+    std::string err;                      // empty: every term fetched and matched its plan
+    std::vector<TermJobResult> results;   // per job
+    uintptr_t event = 0;                  // hipEvent_t: the item's kernels (and error word copy) done
+  };
+
+  // Blocks until the item's last batch is queued on the GPU (or the item failed).  Settles the
+  // bookkeeping like pull_terms: runs go to the settle book, or a failed item's quarantined peer
+  // runs (and the runs of ranges that did not match their plan) are dropped.
+  ItemResult wait_item(uint64_t ticket) {
+    SItem* itp;
+    {
+      std::unique_lock<std::mutex> lk(smu_);
+      itp = s_find(ticket);
+      scv_.wait(lk, [&] { return itp->queued; });
+      if (itp->collected) throw Error("InvalidArgument", "pull ticket " + std::to_string(ticket) + " already waited");
+      itp->collected = true;
+    }
+    SItem& it = *itp;
+    ItemResult out;
+    out.event = reinterpret_cast<uintptr_t>(it.done);
+    out.results.resize(it.segs.size());
+    if (it.failed) {
+      out.err = it.err.empty() ? "fetch failed" : it.err;
+      for (size_t k = 0; k < it.segs.size(); ++k)
+        for (size_t t = 0; t < it.at.sources[k].size(); ++t) {
+          const TermSource& ts = it.at.sources[k][t];
+          if (!it.at.planned_ok[k])
+            sh_->bridge->settle(it.segs[k].rec->terms[it.segs[k].t0 + t].hash_hex, ts.src, ts.run_offset, ts.pending,
+                                false);
+          else if (ts.src == Source::Peer && !ts.pending.empty())
+            sh_->bridge->settle(std::string(), ts.src, ts.run_offset, ts.pending, false);
+        }
+      return out;
+    }
+    for (size_t k = 0; k < it.segs.size(); ++k) {
+      TermJobResult& r = out.results[k];
+      r.chunk_lens = std::move(it.at.chunk_lens[k]);
+      r.fetched = it.at.seg_fetched[k];
+      for (size_t t = 0; t < it.at.sources[k].size(); ++t) {
+        const TermSource& ts = it.at.sources[k][t];
+        const cas::Term& term = it.segs[k].rec->terms[it.segs[k].t0 + t];
+        sh_->book.add(it.jobs[k].xet_hash, term.hash_hex, ts.src, ts.run_offset, ts.pending);
+        (ts.src == Source::Peer ? r.from_peer : ts.src == Source::Cache ? r.from_cache : r.from_cdn) +=
+            term.unpacked_length;
+      }
+    }
+    return out;
+  }
+
+  // The item's device error word (0: every chunk decoded and placed); waits for its kernels.
+  unsigned long long item_error(uint64_t ticket) {
+    SItem* itp;
+    {
+      std::lock_guard<std::mutex> lk(smu_);
+      itp = s_find(ticket);
+      if (!itp->queued) throw Error("InvalidArgument", "item_error before wait_item");
+    }
+    hip_check(hipEventSynchronize(itp->done), "hipEventSynchronize (item)");
+    return reinterpret_cast<volatile unsigned long long*>(serr_host_.data())[itp->eslot];
+  }
+
   // Device timeline of the last timed pass: intervals [copy start, copy end] and [kernels start,
   // kernels end] per batch (ms from the first copy), their unions, and the time both ran at once.
   void record_timeline(hipEvent_t* tev, size_t nb, uint64_t h2d_bytes) {
+    std::vector<std::array<hipEvent_t, 4>> ev(nb);
+    for (size_t b = 0; b < nb; ++b) ev[b] = {tev[4 * b], tev[4 * b + 1], tev[4 * b + 2], tev[4 * b + 3]};
+    record_timeline(ev, h2d_bytes);
+  }
+  // (copy start, copy end, kernels start, kernels end) per batch, relative to the first copy start
+  void record_timeline(const std::vector<std::array<hipEvent_t, 4>>& tev, uint64_t h2d_bytes) {
+    const size_t nb = tev.size();
+    if (!nb) return;
     std::vector<std::pair<double, double>> cp, kn;
     for (size_t b = 0; b < nb; ++b) {
       float a = 0, c = 0, d = 0, e = 0;
-      if (hipEventElapsedTime(&a, tev[0], tev[4 * b]) != hipSuccess ||
-          hipEventElapsedTime(&c, tev[0], tev[4 * b + 1]) != hipSuccess ||
-          hipEventElapsedTime(&d, tev[0], tev[4 * b + 2]) != hipSuccess ||
-          hipEventElapsedTime(&e, tev[0], tev[4 * b + 3]) != hipSuccess)
+      if (hipEventElapsedTime(&a, tev[0][0], tev[b][0]) != hipSuccess ||
+          hipEventElapsedTime(&c, tev[0][0], tev[b][1]) != hipSuccess ||
+          hipEventElapsedTime(&d, tev[0][0], tev[b][2]) != hipSuccess ||
+          hipEventElapsedTime(&e, tev[0][0], tev[b][3]) != hipSuccess)
         return;
       cp.emplace_back(a, c);
       kn.emplace_back(d, e);
@@ -913,6 +1474,25 @@ struct DeviceXetPull::Impl {
   std::mutex timeline_mu_;
   std::string timeline_;
   DevBuf<unsigned long long> err_;
+  // streaming engine (submit_terms)
+  bool s_started_ = false;
+  std::mutex smu_;
+  std::condition_variable scv_;
+  bool sstop_ = false;
+  std::deque<std::unique_ptr<SItem>> sitems_;
+  std::deque<SBatch> sbatches_;                   // global batch g at sbatches_[g - sb0_]
+  size_t sb0_ = 0, sbatch_total_ = 0, sreleased_ = 0, ssubmit_next_ = 0;
+  std::deque<std::pair<size_t, size_t>> swork_;  // (global batch, item term) in fetch order
+  size_t swork_next_ = 0;
+  std::deque<size_t> sissued_;                   // batches queued on the GPU, for the releaser
+  std::vector<size_t> sready_;                   // per slot: first batch allowed to fill it
+  std::vector<hipEvent_t> sh2d_, skern_;         // per slot: last batch's H2D landed / kernels ran
+  std::vector<uint8_t> skern_set_;
+  std::vector<std::thread> sworkers_;
+  std::thread ssubmitter_, sreleaser_;
+  DevBuf<unsigned long long> serr_;
+  PinnedBuf serr_host_;
+  uint64_t sticket_ = 0;
   DevBuf<uint8_t> hashes_;
   DevBuf<uint64_t> sizes_;
   DevBuf<ZgMerkleJob> merkle_job_;
@@ -952,6 +1532,15 @@ std::vector<TermJobResult> DeviceXetPull::pull_terms(const std::vector<TermJob>&
                                                      bool repair) {
   return impl_->pull_terms(jobs, hashes, sizes, repair);
 }
+uint64_t DeviceXetPull::submit_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes) {
+  return impl_->submit_terms(jobs, hashes, sizes);
+}
+DeviceXetPull::ItemResult DeviceXetPull::wait_item(uint64_t ticket) {
+  auto r = impl_->wait_item(ticket);
+  return ItemResult{std::move(r.err), std::move(r.results), r.event};
+}
+unsigned long long DeviceXetPull::item_error(uint64_t ticket) { return impl_->item_error(ticket); }
+void DeviceXetPull::stream_reset(bool cancel) { impl_->s_reset(cancel); }
 size_t DeviceXetPull::settle(const std::string& xet_hash, bool ok) { return impl_->settle(xet_hash, ok); }
 std::vector<TermShape> DeviceXetPull::term_shapes(const std::string& xet_hash) { return impl_->term_shapes(xet_hash); }
 std::vector<TermKey> DeviceXetPull::term_keys(const std::string& xet_hash) { return impl_->sh_->recs->keys(xet_hash); }

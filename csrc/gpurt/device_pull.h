@@ -70,6 +70,21 @@ class DeviceXetPull {
   // check: the caller verifies each whole file, then settle(file, ok) publishes or drops the runs.
   std::vector<TermJobResult> pull_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes,
                                         bool repair = false);
+  // Streaming form of pull_terms (the swarm pull's rounds): the jobs become one item of a continuous
+  // pipeline that persists across items (no stream drain between them); returns a ticket at once.
+  uint64_t submit_terms(const std::vector<TermJob>& jobs, uint8_t* hashes, uint64_t* sizes);
+  struct ItemResult {
+    std::string err;                     // empty: every term fetched and matched its plan
+    std::vector<TermJobResult> results;  // per job (valid when err is empty)
+    uintptr_t event = 0;                 // hipEvent_t completing with the item's kernels
+  };
+  // Blocks until the item's kernels are queued (not run) or it failed; once per ticket.
+  ItemResult wait_item(uint64_t ticket);
+  // The item's device decode error word (0 = clean); waits for its kernels.
+  unsigned long long item_error(uint64_t ticket);
+  // Wait for every submitted item (GPU included) and forget them and their events; `cancel` first
+  // abandons the items still fetching (their remaining terms are skipped).
+  void stream_reset(bool cancel = false);
   size_t settle(const std::string& xet_hash, bool ok);
   std::vector<TermShape> term_shapes(const std::string& xet_hash);  // (ulen, chunks) per term
   std::vector<TermKey> term_keys(const std::string& xet_hash);      // (xorb hex, chunk range) per term

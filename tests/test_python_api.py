@@ -70,6 +70,32 @@ def test_pull_as_tensors_cpu(world_hub):
         assert t.contiguous().view(torch.uint8).numpy().tobytes() == raw
 
 
+def test_pull_device_defaults_to_direct(world_hub, tmp_path):
+    """A device pull is device-direct by default (as from_pretrained): tensors straight into device
+    memory, no snapshot on disk unless save_snapshot=True; direct=False is the snapshot path;
+    include (suffixes) filters the files."""
+    import inspect
+
+    world, hub, commit = world_hub
+    assert inspect.signature(zest_amd.pull).parameters["direct"].default is None
+    hf = tmp_path / "hf"
+
+    def snaps():
+        return sorted(p.name for p in hf.rglob("*.safetensors")) if hf.exists() else []
+    exp = _expected_tensors(world)
+    got = zest_amd.pull(world.spec.repo_id, device="cpu", p2p=False, dht=False)
+    assert set(got) == set(exp) and snaps() == []
+    one = world.xet_files[0].path
+    part = zest_amd.pull(world.spec.repo_id, device="cpu", p2p=False, dht=False, include=[one])
+    assert part and set(part) <= set(exp)
+    assert zest_amd.pull(world.spec.repo_id, device="cpu", p2p=False, dht=False, include=["no-such.bin"]) == {}
+    got = zest_amd.pull(world.spec.repo_id, device="cpu", p2p=False, dht=False, save_snapshot=True)
+    assert set(got) == set(exp) and snaps() == sorted(os.path.basename(f.path) for f in world.files
+                                                        if f.path.endswith(".safetensors"))
+    legacy = zest_amd.pull(world.spec.repo_id, device="cpu", direct=False, p2p=False)
+    assert set(legacy) == set(exp)
+
+
 def test_load_snapshot_detects_corruption(world_hub):
     world, hub, commit = world_hub
     client = zest_amd.client.ZestClient()

@@ -248,6 +248,20 @@ def _run_elastic(world_size, repo, fault, round_bytes, expect_dead=()):
     return sorted(res, key=lambda r: r[0]), [p.exitcode for p in procs], dt
 
 
+def test_swarm_pull_round_synchronous_loop(hub_env, monkeypatch):
+    """ZEST_SWARM_STREAM=0: the round-synchronous loop (agree, then exchange; two alternating
+    pipelines) still pulls every tensor -- it is also what the streamed phase falls back to for
+    reassigned ranges."""
+    monkeypatch.setenv("ZEST_SWARM_STREAM", "0")
+    world, hub = hub_env
+    want = _expected(world)
+    res, codes, _ = _run_elastic(3, world.spec.repo_id, "", 256 << 10)
+    assert codes == [0, 0, 0] and [r[1] for r in res] == ["ok"] * 3, res
+    for _, _, got, st in res:
+        assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+        assert st["pipelined"] and not st["streamed"]
+
+
 def test_swarm_pull_term_shards_and_stats(hub_env):
     """Ranks own byte-balanced *term* ranges (not whole files): each rank fetches ~1/3 of the model,
     in several rounds, and the stats say which exchange replicated them."""
@@ -260,7 +274,8 @@ def test_swarm_pull_term_shards_and_stats(hub_env):
         assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
         assert st["exchange"] in ("bcast", "allgather", "p2p") and st["world"] == 3
         assert st["rounds"] >= 2 and st["items"] >= 6
-        assert st["pipelined"]  # round k + 1 fetched on the second pipeline while round k is agreed
+        # streamed rounds (default): one persistent pipeline, exchanges issued before agreement
+        assert st["streamed"] and not st["pipelined"]
         assert st["fetched_bytes"] + st["received_bytes"] == total
         assert abs(st["fetched_bytes"] - total / 3) < 0.2 * total, st["fetched_bytes"]
         assert set(st["phases"]) >= {"plan_s", "fetch_s", "agree_s", "verify_s", "pull_s"}

@@ -55,7 +55,7 @@ def disable() -> None:
 
 def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = False, verify: bool = True,
          p2p: bool = True, peers=None, tracker=None, dht: bool = True, dht_bootstrap=None, include=None,
-         group=None, repo_type: str = "model", verbose: bool = False, direct: bool = False,
+         group=None, repo_type: str = "model", verbose: bool = False, direct: bool | None = None,
          save_snapshot: bool = False, threads: int = 16, staging_bytes: int = 1 << 30, stats: dict | None = None,
          exchange: str = "auto", round_bytes: int | None = None):
     """Download `repo@revision` via zest.
@@ -71,10 +71,14 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
       Merkle-checked on every rank; no snapshot is written (zest_amd.parallel.swarm_pull).
       `stats` (a dict) receives the exchange mode used, bytes fetched / received, per-phase
       seconds, re-shards and recovered ranks.
-    * direct=True with a GPU device: Xet files bypass the disk — fetched compressed through the
+    * device="cuda:N" / "cpu" pulls are device-direct by default (`direct=None` -> True, like
+      from_pretrained): Xet files bypass the disk -- fetched compressed through the
       cache/peer/CDN waterfall and decoded + hash-verified on the GPU into HBM (zest_amd.direct);
-      `threads` fetch workers fill two pinned staging buffers of `staging_bytes` each.  With
-      device="cpu" the same pull lands in CPU tensors (host decode + verification, no disk).
+      `threads` fetch workers fill pinned staging buffers of `staging_bytes` each.  With
+      device="cpu" the same pull lands in CPU tensors (host decode + verification, no disk).  No
+      snapshot is written unless `save_snapshot=True`; `include` (file-name suffixes) filters the
+      safetensors files.  direct=False: the reference's path -- the CLI writes the HF-cache
+      snapshot, which is then loaded and (verify=True) hash-checked on the device.
     """
     _init()
     kw = dict(p2p=p2p, peers=peers, tracker=tracker, dht=dht, dht_bootstrap=dht_bootstrap, include=include,
@@ -88,12 +92,14 @@ def pull(repo: str, revision: str = "main", *, device=None, as_tensors: bool = F
                           dht_bootstrap=dht_bootstrap, repo_type=repo_type, verify_received=verify,
                           staging_bytes=staging_bytes, threads=threads, stats=stats, exchange=exchange,
                           round_bytes=round_bytes)
+    if direct is None:
+        direct = True  # weights straight into device memory (the north star); direct=False: via disk
     if direct:
         from .direct import pull_to_device
 
         return pull_to_device(repo, revision, device or "cuda:0", p2p=p2p, peers=peers, tracker=tracker, dht=dht,
                               dht_bootstrap=dht_bootstrap, repo_type=repo_type, save_snapshot=save_snapshot,
-                              threads=threads, staging_bytes=staging_bytes)
+                              threads=threads, staging_bytes=staging_bytes, include=include)
     from .device import load_snapshot
 
     res = _client.pull_detailed(repo, revision, **kw)

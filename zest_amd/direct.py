@@ -24,11 +24,13 @@ from . import device as zdev
 
 def pull_to_device(repo: str, revision: str = "main", device="cuda:0", *, p2p: bool = True, peers=None,
                    tracker=None, dht: bool = True, dht_bootstrap=None, repo_type: str = "model",
-                   save_snapshot: bool = False, staging_bytes: int = 1 << 30, threads: int = 16):
+                   save_snapshot: bool = False, staging_bytes: int = 1 << 30, threads: int = 16, include=None):
     dev = torch.device(device)
     if dev.type not in ("cuda", "cpu"):
         raise ValueError("pull_to_device needs a GPU or the CPU")
     commit, files = _core.list_repo_files(repo, revision, repo_type)
+    if include:  # file-name suffixes, as `zest pull --include` (csrc/core/pull.cpp)
+        files = [f for f in files if any(f["path"].endswith(x) for x in include)]
     st_files = [f for f in files if f["path"].endswith(".safetensors")]
     xet = [f for f in st_files if f["xet_hash"]]
     plain = [f for f in st_files if not f["xet_hash"]]

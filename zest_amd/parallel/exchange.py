@@ -76,10 +76,14 @@ def role_stream(device: torch.device, role: str, priority: int = 0):
 @dataclass
 class PeerArenas:
     """Every peer's arena mapped into this process (``peers[rank]`` is None), plus the gloo group the
-    ``ipc`` exchange's host barriers use."""
+    ``ipc`` exchange's host barriers use.  ``signals`` / ``sig_sent``: the ready-counter page shared
+    over these ranks (RoundExchange.enable_signals) and this rank's last counter value, kept with the
+    mapping so later exchanges over it (the next pull reusing the arena) reuse the page."""
     arena: "torch.Tensor"
     peers: list
     host_group: object
+    signals: object = None
+    sig_sent: int = 0
 
 
 def map_peer_arenas(arena, rank: int, n_ranks: int, group=None, deadline_s: float | None = None):
@@ -348,6 +352,7 @@ class RoundExchange:
         self._host_group = None
         self._signals = None          # shared ready counters (enable_signals)
         self._sig_sent = 0            # signal_ready calls so far (= this rank's counter value)
+        self._pa = None               # the PeerArenas of enable_ipc
 
     # -- helpers ------------------------------------------------------------------------------
     def backend(self) -> str:
@@ -379,6 +384,7 @@ class RoundExchange:
             return False
         self._host_group = mapped.host_group
         self._peer_arenas = mapped.peers
+        self._pa = mapped
         self._ipc_streams = [role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
         return True
 
@@ -401,17 +407,30 @@ class RoundExchange:
             return False
         H = ops.hip()
         dev = self.device.index or 0
+        g = self._host_group
+
+        def agree(v: int, op=dist.ReduceOp.MIN) -> int:
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=op, group=g)
+            return int(t.item())
+
+        pa = self._pa
+        if agree(int(pa is not None and pa.signals is not None)):
+            # the mapping's page from an earlier exchange over it (a previous pull): every rank's
+            # counter continues from the highest value any rank reached, so a wait of this pull can
+            # never be satisfied by an earlier one, whatever the earlier pull left behind
+            self.sync()  # no host function of ours may still store an older value
+            top = agree(int(pa.sig_sent), dist.ReduceOp.MAX)
+            pa.signals.store(self.rank, top)
+            pa.sig_sent = top
+            dist.barrier(group=g)
+            self._signals, self._sig_sent = pa.signals, top
+            self._signal_stream = role_stream(self.device, "signal")
+            return True
         try:
             ok = int(bool(H.can_stream_wait_value(dev)))
         except Exception:  # noqa: BLE001
             ok = 0
-        g = self._host_group
-
-        def agree(v: int) -> int:
-            t = torch.tensor([v], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
-            return int(t.item())
-
         box = [f"/dev/shm/zest-sig-{uuid.uuid4().hex}" if self.rank == 0 else None]
         dist.broadcast_object_list(box, src=dist.get_process_group_ranks(g)[0], group=g)
         path = box[0]
@@ -437,8 +456,24 @@ class RoundExchange:
             return False
         self._signals = sig
         self._sig_sent = 0
+        if pa is not None:
+            pa.signals, pa.sig_sent = sig, 0
         self._signal_stream = role_stream(self.device, "signal")
         return True
+
+    def release_signals(self) -> None:
+        """Open every ready counter (0xFFFFFFFF) so that no exchange stream waits any more -- a lost
+        rank's counter would never advance -- and stop using the page (the mapping forgets it: its
+        sequence is broken).  Copies already queued read whatever the dead owner left; the caller
+        re-sends or re-fetches those ranges."""
+        sig = self._signals
+        if sig is None:
+            return
+        for i in range(self.n_ranks):
+            sig.store(i, 0xFFFFFFFF)
+        self._signals = None
+        if self._pa is not None and self._pa.signals is sig:
+            self._pa.signals = None
 
     def order_after(self, stream) -> None:
         """With ready counters the exchange streams wait only for the owners' counters, not for this
@@ -454,10 +489,45 @@ class RoundExchange:
         Returns the sequence number the peers' exchange() must be given for that region.  Every
         rank calls this once per region, in the same order (ranks with empty regions included)."""
         self._sig_sent += 1
+        if self._pa is not None:
+            self._pa.sig_sent = self._sig_sent
         ss = self._signal_stream
-        ss.wait_stream(stream)
+        if stream is not None:
+            ss.wait_stream(stream)
         self._signals.set_after(self.rank, self._sig_sent, ss.cuda_stream)
         return self._sig_sent
+
+    def exchange_after(self, regions, event=None, mode: str | None = None) -> list:
+        """exchange(regions) once this rank's own region is complete, without a host wait: `event`
+        is a raw hipEvent_t recorded after the work writing it (DeviceXetPull.wait_item; None: the
+        region is complete on the host, CPU groups, or with the current stream's queued work).
+        Peer-mapped modes with ready counters signal after the event and wait for the owners' counters
+        on the GPU; without counters the event is host-synchronized and a host barrier follows; the
+        RCCL modes issue their collective from a stream ordered after the event.  Every rank calls
+        this for every round, in the same order."""
+        mode = mode or self.mode
+        if not self.is_cuda:
+            return self.exchange(regions, mode)
+        H = ops.hip()
+        cur = torch.cuda.current_stream(self.device)
+        if mode in PEER_MAPPED_MODES:
+            if self._signals is not None:
+                ss = self._signal_stream
+                ss.wait_stream(cur)
+                if event:
+                    H.stream_wait_event(ss.cuda_stream, int(event))
+                return self.exchange(regions, mode, seq=self.signal_ready(None))
+            ready = torch.cuda.Event()
+            if event:
+                H.stream_wait_event(cur.cuda_stream, int(event))
+            ready.record(cur)
+            return self.exchange(regions, mode, ready=ready)
+        xs = role_stream(self.device, "xissue")
+        xs.wait_stream(cur)
+        if event:
+            H.stream_wait_event(xs.cuda_stream, int(event))
+        with torch.cuda.stream(xs):
+            return self.exchange(regions, mode)
 
     # -- one exchange -------------------------------------------------------------------------
     def exchange(self, regions, mode: str | None = None, ready=None, synced: bool = False, seq: int | None = None) -> list:

@@ -46,11 +46,13 @@ its only failure handling is the per-term waterfall (CONTRIBUTING.md:92-99).
 """
 from __future__ import annotations
 
+import collections
 import json
 import os
 import threading
 import time
 import uuid
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -89,6 +91,19 @@ def staging_slot_bytes(staging_bytes: int, round_bytes: int, world: int) -> int:
 
 class SwarmPullError(RuntimeError):
     pass
+
+
+@dataclass
+class _Agree:
+    """One streamed round's pending agreement (see _Swarm._rounds_streamed)."""
+    rno: int
+    items: list      # item per rank (None: nothing)
+    err: str         # this rank's fetch error text ("" = ok)
+    info: dict       # this rank's fetch counters
+    works: list      # the round's exchange works (the received chunks are hashed after them)
+    outs: list       # gathered [status, sizes...] per rank
+    work: object     # the async all_gather
+    nck: list        # chunks of each rank's item
 
 
 class _RankLost(RuntimeError):
@@ -428,6 +443,7 @@ class _Fetcher:
         self._warm = None
         self._warm_err = None
         self._lock = threading.Lock()  # `impl` is reached from the reconstruction warm-up thread too
+        self._serial = None            # CPU: the side thread of submit()
 
     def prewarm(self) -> None:
         """Build the pipeline (Xet auth, pinned staging, cache scan, swarm) on a side thread, so it
@@ -488,6 +504,40 @@ class _Fetcher:
             return self.impl.pull_terms(jobs, hashes.data_ptr(), sizes.data_ptr() if sizes is not None else 0, repair)
         return self.impl.fetch_terms(jobs, hashes.data_ptr(), repair)
 
+    # -- streaming submission (the streamed round loop) ----------------------------------------
+    def submit(self, jobs, hashes: torch.Tensor, sizes: torch.Tensor | None):
+        """Queue one item (a round's term ranges) behind the ones already submitted; returns a
+        ticket.  GPU: the persistent pipeline of DeviceXetPull.submit_terms (no drain between
+        items); CPU: the host fetches run one item at a time, in order, on a side thread."""
+        if self.device.type == "cuda":
+            return ("dev", self.impl.submit_terms(jobs, hashes.data_ptr(), sizes.data_ptr() if sizes is not None else 0))
+        if self._serial is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._serial = ThreadPoolExecutor(max_workers=1, thread_name_prefix="zest-swarm-item")
+        impl = self.impl
+        return ("host", self._serial.submit(impl.fetch_terms, jobs, hashes.data_ptr(), False))
+
+    def wait(self, ticket):
+        """(error text, results, event): blocks until the item's kernels are queued (GPU; `event`
+        is a raw hipEvent_t that completes with them) or its host fetch returned (CPU; no event)."""
+        kind, t = ticket
+        if kind == "dev":
+            err, res, ev = self.impl.wait_item(t)
+            return err, res, ev
+        try:
+            return "", t.result(), None
+        except Exception as e:  # noqa: BLE001 - reported through the agreement
+            return f"{type(e).__name__}: {e}", [], None
+
+    def drain(self, cancel: bool = False) -> None:
+        """Wait for every submitted item and forget them (end of a pull).  `cancel`: items whose
+        fetches have not finished are abandoned first (an abandoned streamed phase)."""
+        if self._impl is not None and hasattr(self._impl, "stream_reset"):
+            self._impl.stream_reset(cancel)
+        if self._serial is not None:
+            self._serial.shutdown(wait=True)
+            self._serial = None
+
     def join(self) -> None:
         """Wait for a prewarm still running (a rank that never fetched)."""
         w = self._warm
@@ -542,21 +592,34 @@ class _Swarm:
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.backend = backend
+        t_m = time.perf_counter()
         self.m = _Membership(group, backend, self.device)
+        self._mark("membership_s", t_m)
         self.verify = verify_received
         self.round_bytes = int(round_bytes)
         self.exchange_req = exchange
-        # Cross-round fetch pipelining (ZEST_SWARM_PIPELINE, default on at N > 1): round k + 1's
-        # ranges are fetched on a second pipeline while round k's fetch drains and is agreed, so the
-        # connections never sit idle at a round boundary.  On GPUs the second pipeline is a sibling
-        # of the first (half the staging, the same Xet session, caches and reconstructions); on CPU
-        # groups it is a second host fetcher that joins no DHT (one node per process is enough).
-        self.pipelined = os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
+        # Streamed rounds (ZEST_SWARM_STREAM, default on at N > 1, _rounds_streamed): one persistent
+        # fetch pipeline streams this rank's whole share; exchanges are ordered on the device and the
+        # agreement lags.  Its staging: 4 slots of half a round, two rounds buffered ahead of the copy
+        # engine.  ZEST_SWARM_STREAM=0 keeps the round-synchronous loop (below), which the streamed
+        # phase also falls back to for reassigned ranges.
+        self.streamed = os.environ.get("ZEST_SWARM_STREAM", "1") != "0" and self.m.world > 1
+        # Cross-round fetch pipelining of the synchronous loop (ZEST_SWARM_PIPELINE, default on at
+        # N > 1 when not streamed): round k + 1's ranges are fetched on a second pipeline while round
+        # k's fetch drains and is agreed.  On GPUs the second pipeline is a sibling of the first (half
+        # the staging, the same Xet session, caches and reconstructions); on CPU groups it is a second
+        # host fetcher that joins no DHT (one node per process is enough).
+        self.pipelined = (os.environ.get("ZEST_SWARM_PIPELINE", "1") != "0" and self.m.world > 1
+                          and not self.streamed)
+        slots = int(os.environ.get("ZEST_SWARM_SLOTS", "4")) if self.streamed else 0
         if self.cuda and not os.environ.get("ZEST_SWARM_STAGING_MB"):
-            staging_bytes = staging_slot_bytes(staging_bytes, self.round_bytes, self.m.world)
+            if self.streamed:
+                staging_bytes = min(int(staging_bytes), max(64 << 20, self.round_bytes // 2))
+            else:
+                staging_bytes = staging_slot_bytes(staging_bytes, self.round_bytes, self.m.world)
         self.reuse_key = (repo, revision, repo_type, str(self.device), bool(p2p), tuple(peers or []), tracker,
                           bool(dht), tuple(dht_bootstrap or []), int(staging_bytes), int(threads), self.pipelined,
-                          os.environ.get("HF_ENDPOINT"), os.environ.get("ZEST_CACHE_DIR"))
+                          self.streamed, slots, os.environ.get("HF_ENDPOINT"), os.environ.get("ZEST_CACHE_DIR"))
         self.reuse = reuse
         kept = _PIPELINES.pop(self.reuse_key, None) if reuse else None
         self.reused = kept is not None
@@ -570,7 +633,7 @@ class _Swarm:
             self.stats_base = _merged_stats([f.stats() for f in kept if f.parent is None])
         else:
             self.fetcher = _Fetcher(repo, revision, repo_type, self.device, p2p, peers, tracker, dht, dht_bootstrap,
-                                    staging_bytes, threads)
+                                    staging_bytes, threads, slots=slots)
             self.fetcher.prewarm()
             self.fetchers = [self.fetcher]
             if self.pipelined:
@@ -793,8 +856,9 @@ class _Swarm:
         t = time.perf_counter()
         W = self.m.world
         self.xchg = RoundExchange(self.arena, self.m.rank, W, self.m.data, "p2p")
-        if self.mapped is not None:
-            self.xchg.enable_ipc(self.mapped)
+        if self.mapped is not None and self.xchg.enable_ipc(self.mapped) and self.streamed:
+            # streamed rounds wait for the owners on the GPU (ready counters), not in host barriers
+            self.xchg.enable_signals()
         self.verify_stream = role_stream(self.device, "verify") if self.cuda else None
         self._hash_scratch = ops.HashScratch(self.device) if self.cuda else None
         if W == 1:
@@ -878,12 +942,220 @@ class _Swarm:
         offs = (P.t_dst[term_of].astype(np.uint64) + start_in_term).astype(np.uint64)
         return offs, lens, int(P.t_c0[a])
 
+    def _apply_meta(self, meta, info: dict):
+        """Apply one round's agreement -- every rank's (item, error text, chunk sizes) -- on this
+        rank (every rank derives the same result): a failed item is reassigned to a rank that has
+        not tried it (least queued bytes), a rank failing twice hands its queue to the others; the
+        rest is recorded (owner, chunk sizes, this rank's fetch counters from `info`).  Returns
+        (fatal errors, the round's regions per rank with failed ones empty, items to receive)."""
+        P = self.plan
+        me = self.m.rank
+        fatal, regions, recv = [], [], []
+        for r, (item, e, ls) in enumerate(meta):
+            if item is None:
+                regions.append((0, 0))
+                continue
+            g = self.m.granks[r]
+            if e:
+                if not getattr(self, "first_fetch_error", None):
+                    self.first_fetch_error = e  # (named in the final error if the item finds no owner)
+                self.fails[g] = self.fails.get(g, 0) + 1
+                self.tried.setdefault(item, set()).add(g)
+                moves = [item]
+                if self.fails[g] >= 2:   # a repeatedly failing owner: hand its queue to the others
+                    moves += self.queue[r]
+                    self.queue[r] = []
+                for mv in moves:
+                    cands = [q for q in range(self.m.world)
+                             if self.fails.get(self.m.granks[q], 0) < 2 and self.m.granks[q] not in self.tried.get(mv, set())]
+                    if not cands:
+                        fatal.append(e if mv == item else f"no owner left for terms {self.items[mv]} "
+                                                          f"(rank {g} dropped; first fetch error: "
+                                                          f"{self.first_fetch_error})")
+                        continue
+                    load = [sum(int(P.t_ulen[self.items[x][0]:self.items[x][1]].sum()) for x in self.queue[q])
+                            for q in range(self.m.world)]
+                    q = min(cands, key=lambda q: (load[q], q))
+                    self.queue[q].append(mv)
+                    self.stats["reassigned"] += 1
+                regions.append((0, 0))
+                continue
+            self.item_lens[item] = ls
+            first_time = item not in self.owner_of
+            self.owner_of.setdefault(item, g)
+            regions.append(P.region(*self.items[item]))
+            if r == me:
+                if first_time and info:
+                    a, b = self.items[item]
+                    self.fetched_bytes += int(P.t_ulen[a:b].sum())
+                    self.stats["fetched_wire_bytes"] += info["fetched"]
+                    for k in ("from_peer", "from_cdn", "from_cache"):
+                        self.stats[k] += info[k]
+                self.have.add(item)
+            elif item not in self.have:  # (a re-send also reaches ranks holding it: same bytes)
+                recv.append(item)
+            if not first_time and r == me:
+                a, b = self.items[item]
+                self.stats["resent_bytes"] += int(P.t_ulen[a:b].sum())
+        return fatal, regions, recv
+
+    # -- streamed rounds (N > 1) ----------------------------------------------------------------
+    def _rounds_streamed(self):
+        """The engine's shape on the public path, N > 1:
+
+          * every round's item of this rank is submitted up front to ONE persistent fetch pipeline
+            (_Fetcher.submit -> DeviceXetPull.submit_terms), which streams them with no drain
+            between rounds;
+          * round k's exchange is issued as soon as this rank's item k is queued on the GPU and is
+            ordered after it on the device -- the owners' ready counters for the peer-mapped modes
+            (hipStreamWaitValue32), a stream wait on the item's event for RCCL.  The schedule is
+            fixed at planning, so nothing has to be agreed first;
+          * the agreement (a status word + the item's chunk sizes) is an asynchronous gloo
+            all_gather of one small tensor per rank, waited for only when more than
+            ZEST_SWARM_AGREE_LAG (default 3) rounds are pending; a round's received chunks are
+            hashed once their sizes are agreed.
+
+        A range whose fetch failed is exchanged anyway (its bytes are never hashed, so never
+        trusted) and is reassigned exactly as in the synchronous loop; run() then re-fetches and
+        re-sends the reassigned ranges with _rounds()."""
+        P = self.plan
+        me = self.m.rank
+        rounds = []
+        while any(self.queue):
+            rounds.append(self._pop_round())
+        self.unagreed = [list(x) for x in rounds]   # popped, not agreed (re-queued by _recover)
+        self.item_ready_s = []  # per round: seconds into the pull when this rank's item was queued
+        base = self.arena.data_ptr()
+        tickets, injected = [None] * len(rounds), set()
+        for k, items in enumerate(rounds):
+            it = items[me]
+            if it is None:
+                continue
+            if (self.m.me, self.round_no + k) in self.fault["fail"]:
+                injected.add(k)  # fault injection (tests): this fetch "fails"
+                continue
+            a, b = self.items[it]
+            tickets[k] = self.fetcher.submit(P.jobs(a, b, base), self.hashes, self.sizes)
+        self._tickets = tickets
+        if self.cuda and self.xchg.mode in PEER_MAPPED_MODES:
+            # peer-mapped exchanges write this arena from the exchange streams, which wait only for
+            # the owners' counters: order them after whatever the caller queued on the arena
+            self.xchg.order_after(torch.cuda.current_stream(self.device))
+        lag = max(0, int(os.environ.get("ZEST_SWARM_AGREE_LAG", "3")))
+        pending = collections.deque()
+        for k, items in enumerate(rounds):
+            rno = self.round_no
+            if (self.m.me, rno) in self.fault["exit"]:
+                os._exit(1)  # fault injection: this rank dies mid-pull (tests)
+            it = items[me]
+            t = time.perf_counter()
+            err, lens, info, ev = "", b"", {}, None
+            if it is not None:
+                if k in injected:
+                    err = f"rank {self.m.me}: RuntimeError: injected fetch failure (round {rno})"
+                else:
+                    e, res, ev = self.fetcher.wait(tickets[k])
+                    tickets[k] = None
+                    if e:
+                        err = f"rank {self.m.me}: {e}"
+                    else:
+                        lens = b"".join(r["chunk_lens"] for r in res)
+                        info = {x: sum(r[x] for r in res) for x in ("fetched", "from_peer", "from_cdn", "from_cache")}
+            self._mark("fetch_s", t)
+            t = time.perf_counter()
+            self.item_ready_s.append(round(t - getattr(self, "t_pull", t), 4))
+            regions = [P.region(*self.items[x]) if x is not None else (0, 0) for x in items]
+            works = []
+            if any(hi > lo for lo, hi in regions):
+                try:
+                    works = self.xchg.exchange_after(regions, ev)
+                except Exception as e:  # noqa: BLE001
+                    raise _RankLost(str(e)) from e
+            self._mark("exchange_issue_s", t)
+            pending.append(self._post_agree(rno, items, err, lens, info, works))
+            self.round_no += 1
+            t = time.perf_counter()
+            while pending and (len(pending) > lag or pending[0].work.is_completed()):
+                self._finish_agree(pending.popleft())
+            self._mark("agree_s", t)
+        t = time.perf_counter()
+        while pending:
+            self._finish_agree(pending.popleft())
+        self._mark("agree_s", t)
+        self._tickets = []
+
+    def _post_agree(self, rno: int, items: list, err: str, lens: bytes, info: dict, works: list) -> "_Agree":
+        """Start round rno's agreement: an async all_gather of [status, chunk sizes...] per rank
+        (status 0 ok, 1 failed, 2 nothing to fetch), padded to the round's largest item."""
+        P = self.plan
+        me = self.m.rank
+        nck = [int(P.t_nck[self.items[x][0]:self.items[x][1]].sum()) if x is not None else 0 for x in items]
+        mine = torch.zeros(1 + max(nck), dtype=torch.int32)
+        if items[me] is None:
+            mine[0] = 2
+        elif not err:
+            arr = np.frombuffer(lens, dtype=np.int32)
+            if len(arr) != nck[me]:
+                err = f"rank {self.m.me}: {len(arr)} chunk sizes for a range of {nck[me]} chunks"
+            else:
+                mine[1:1 + len(arr)] = torch.from_numpy(arr.copy())
+        if err:
+            mine[0] = 1
+        outs = [torch.empty_like(mine) for _ in range(self.m.world)]
+        try:
+            work = dist.all_gather(outs, mine, group=self.m.ctl, async_op=True)
+        except Exception as e:  # noqa: BLE001
+            raise _RankLost(str(e)) from e
+        return _Agree(rno, list(items), err, info, works, outs, work, nck)
+
+    def _finish_agree(self, ag: "_Agree") -> None:
+        try:
+            ag.work.wait()
+        except Exception as e:  # noqa: BLE001 - a dead or stuck peer
+            raise _RankLost(str(e)) from e
+        me = self.m.rank
+        meta = []
+        for r, x in enumerate(ag.items):
+            st = int(ag.outs[r][0])
+            if x is None:
+                meta.append((None, "", b""))
+            elif st != 0:
+                meta.append((x, ag.err if r == me and ag.err else
+                             f"rank {self.m.granks[r]}: fetch failed (round {ag.rno})", b""))
+            else:
+                meta.append((x, "", ag.outs[r][1:1 + ag.nck[r]].numpy().tobytes()))
+        fatal, _, recv = self._apply_meta(meta, ag.info)
+        if self.unagreed:
+            self.unagreed.pop(0)  # rounds are agreed in order
+        if fatal:
+            self._settle_received()
+            raise SwarmPullError("; ".join(sorted(set(fatal))))
+        if recv:
+            ev = self._hash_received(recv, ag.works)
+            if ev is not None:
+                self.pending_events.append((ev, recv))
+        elif not self.cuda:
+            for w in ag.works:
+                w.wait()
+
     # -- main loop ----------------------------------------------------------------------------
     def run(self):
         self.round_no = 0
         self.pending_events: list = []   # (event, items) of received rounds not yet known to be hashed
+        self.unagreed: list = []
+        streamed = self.streamed
         while True:
             try:
+                if streamed:
+                    streamed = False
+                    self._rounds_streamed()
+                    if any(self.queue):
+                        # reassigned ranges follow on the synchronous loop: their exchanges must land
+                        # after the streamed ones that wrote the same regions (with a failed owner's
+                        # bytes) on other streams
+                        self._settle_received()
+                        if self.cuda:
+                            torch.cuda.synchronize(self.device)
                 self._rounds()
                 self._settle_received()
                 return
@@ -929,13 +1201,18 @@ class _Swarm:
         return self._pool.submit(self._fetch_one, f, nxt[self.m.rank], round_no)
 
     def _join_fetch(self):
-        """Wait for a fetch still in flight (its result is dropped: its item is re-queued)."""
+        """Wait for a fetch still in flight (its result is dropped: its item is re-queued), and cancel
+        and drain the streamed items not yet collected."""
         if self._fut is not None:
             try:
                 self._fut.result()
             except Exception:  # noqa: BLE001
                 pass
             self._fut = None
+        if getattr(self, "_tickets", None):
+            self._tickets = []
+            for f in self.fetchers:
+                f.drain(cancel=True)
 
     def _rounds(self):
         P = self.plan
@@ -970,53 +1247,7 @@ class _Swarm:
             t = time.perf_counter()
             meta = self._gather((it, err, lens))
             self._mark("agree_s", t)
-            fatal, regions, recv = [], [], []
-            for r, (item, e, ls) in enumerate(meta):
-                if item is None:
-                    regions.append((0, 0))
-                    continue
-                g = self.m.granks[r]
-                if e:
-                    if not getattr(self, "first_fetch_error", None):
-                        self.first_fetch_error = e  # (named in the final error if the item finds no owner)
-                    self.fails[g] = self.fails.get(g, 0) + 1
-                    self.tried.setdefault(item, set()).add(g)
-                    moves = [item]
-                    if self.fails[g] >= 2:   # a repeatedly failing owner: hand its queue to the others
-                        moves += self.queue[r]
-                        self.queue[r] = []
-                    for mv in moves:
-                        cands = [q for q in range(self.m.world)
-                                 if self.fails.get(self.m.granks[q], 0) < 2 and self.m.granks[q] not in self.tried.get(mv, set())]
-                        if not cands:
-                            fatal.append(e if mv == item else f"no owner left for terms {self.items[mv]} "
-                                                              f"(rank {g} dropped; first fetch error: "
-                                                              f"{self.first_fetch_error})")
-                            continue
-                        load = [sum(int(P.t_ulen[self.items[x][0]:self.items[x][1]].sum()) for x in self.queue[q])
-                                for q in range(self.m.world)]
-                        q = min(cands, key=lambda q: (load[q], q))
-                        self.queue[q].append(mv)
-                        self.stats["reassigned"] += 1
-                    regions.append((0, 0))
-                    continue
-                self.item_lens[item] = ls
-                first_time = item not in self.owner_of
-                self.owner_of.setdefault(item, g)
-                regions.append(P.region(*self.items[item]))
-                if r == me:
-                    if first_time and info:
-                        a, b = self.items[item]
-                        self.fetched_bytes += int(P.t_ulen[a:b].sum())
-                        self.stats["fetched_wire_bytes"] += info["fetched"]
-                        for k in ("from_peer", "from_cdn", "from_cache"):
-                            self.stats[k] += info[k]
-                    self.have.add(item)
-                elif item not in self.have:  # (a re-send also reaches ranks holding it: same bytes)
-                    recv.append(item)
-                if not first_time and r == me:
-                    a, b = self.items[item]
-                    self.stats["resent_bytes"] += int(P.t_ulen[a:b].sum())
+            fatal, regions, recv = self._apply_meta(meta, info)
             self.inflight = []
             if fatal:
                 self._join_fetch()
@@ -1057,6 +1288,10 @@ class _Swarm:
         self.have.update(done)
         self.pending_events = []
         self._join_fetch()  # (its range is re-queued below with the other unagreed ones)
+        if self.cuda and getattr(self, "xchg", None) is not None:
+            # exchange streams still waiting (on the GPU) for a dead owner's ready counter would never
+            # finish: open every counter, abandoning those copies, before anything synchronizes
+            self.xchg.release_signals()
         lost = self.m.rebuild()
         if not lost:
             raise SwarmPullError(f"collective failed but every rank is alive: {why}")
@@ -1069,8 +1304,10 @@ class _Swarm:
         keep = {g: self.queue[old_granks.index(g)] for g in self.m.granks}
         orphan = [x for i in lost for x in self.queue[i]]
         # ranges popped but never agreed (the failed round's, and the next round's already handed to
-        # the other pipeline): back to their owner, in order, or orphaned
-        for popped in (getattr(self, "inflight_next", []), getattr(self, "inflight", [])):
+        # the other pipeline; the streamed phase's pending rounds): back to their owner, in order, or
+        # orphaned
+        for popped in list(reversed(getattr(self, "unagreed", []))) + [getattr(self, "inflight_next", []),
+                                                                      getattr(self, "inflight", [])]:
             for i, x in enumerate(popped):
                 if x is not None and x not in self.owner_of:
                     if old_granks[i] in keep:
@@ -1080,6 +1317,7 @@ class _Swarm:
                         orphan.append(x)
         self.inflight = []
         self.inflight_next = []
+        self.unagreed = []
         self.queue = [keep[g] for g in self.m.granks]
         # which items does every survivor hold?  (fetched ones, and received ones already hashed)
         fetched = sorted(self.owner_of)
@@ -1388,7 +1626,10 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         sw.shard()
         sw.setup_exchange()
         t_pull = time.perf_counter()
+        sw.t_pull = t_pull
         sw.run()
+        for f in sw.fetchers:
+            f.drain()  # (streamed items: every one was waited for; their events go, the timeline is made)
         if sw.cuda:
             torch.cuda.synchronize(sw.device)
         sw._mark("pull_s", t_pull)
@@ -1400,6 +1641,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
             sw.repair(bad)
             bad = sw.verify_files()
         nf = len(sw.xet_files)
+        t_t = time.perf_counter()
         sw.settle(set(range(nf)) - set(bad))
         if bad:
             raise zdev.VerifyError(f"rank {sw.m.me}: files failed their Xet hash after repair: "
@@ -1408,6 +1650,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         out = sw.tensors(plain)
         if sw.cuda:
             torch.cuda.synchronize(sw.device)
+        sw._mark("tensors_s", t_t)
         if stats is not None:
             total = sum(f["size"] for f in sw.xet_files) + sum(f["size"] for f in sw.plain_files)
             wall = time.perf_counter() - sw.t0
@@ -1422,7 +1665,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 GBps=round(total / wall / 1e9, 4) if wall > 0 else 0.0, phases=dict(sw.times),
                 fetch_stats=_stats_delta(_merged_stats([f.stats() for f in sw.fetchers if f.parent is None]),
                                          sw.stats_base),
-                pipelined=sw.pipelined,
+                pipelined=sw.pipelined, streamed=sw.streamed, item_ready_s=getattr(sw, "item_ready_s", []),
                 held_bytes=sw.held_bytes[sw.m.rank], share_bytes=sw.share_bytes[sw.m.rank],
                 possession=list(sw.held_bytes), reused_pipeline=sw.reused,
                 cache_writer=sw.fetcher.cache_writer(), device_timeline=sw.fetcher.timeline(),
@@ -1440,6 +1683,11 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         if getattr(sw, "_pool", None) is not None:
             sw._pool.shutdown(wait=True)
         for f in getattr(sw, "fetchers", [sw.fetcher]):
+            try:
+                f.drain(cancel=not ok)  # (streamed items: every one was waited for unless the pull failed)
+            except Exception:  # noqa: BLE001 - the pull already failed
+                if ok:
+                    raise
             f.join()
         sw.m.close()
         if ok and sw.reuse:
