@@ -618,11 +618,19 @@ void bind_extra(py::module_& m) {
       .def("fetch_many_bytes", [](bt::PeerSession& s, std::vector<py::bytes> hashes, std::vector<uint32_t> starts,
                                   std::vector<uint32_t> ends, int timeout_ms) {
         // Pipelined; returns total payload bytes (the data is discarded: for load generation).
+        // Load generation: every payload is received into one reused per-thread buffer (like iperf's
+        // receiver), so the client does not pay a fresh 64 MiB allocation's page faults per response.
+        thread_local std::vector<uint8_t> scratch;
+        auto sink = [](size_t n) -> uint8_t* {
+          if (scratch.size() < n) scratch.resize(n);
+          return scratch.data();
+        };
         std::vector<bt::XetRequest> reqs(hashes.size());
         for (size_t i = 0; i < hashes.size(); ++i) {
           reqs[i].xorb_hash = arr_of<32>(hashes[i], "xorb hash");
           reqs[i].range_start = starts.at(i);
           reqs[i].range_end = ends.at(i);
+          reqs[i].sink = sink;
         }
         uint64_t total = 0;
         size_t failed = 0;
@@ -631,7 +639,7 @@ void bind_extra(py::module_& m) {
           std::vector<std::string> errs;
           auto res = s.request_many(reqs, timeout_ms, &errs);
           for (size_t i = 0; i < res.size(); ++i) {
-            total += res[i].data.size();
+            total += res[i].ext ? res[i].ext_len : res[i].data.size();
             if (i < errs.size() && !errs[i].empty()) failed++;
           }
         }

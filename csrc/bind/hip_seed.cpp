@@ -9,6 +9,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <shared_mutex>
 #include <stdexcept>
@@ -32,15 +34,26 @@ struct XorbLoc {
   uint32_t first = 0;               // xorb chunk index of the run's first chunk (partial runs)
 };
 
+// Per connection thread: pinned staging for one response, the stream its D2H copies run on, and one
+// event per piece.  A thread serves one request at a time, so the next response reuses them only after
+// the previous one was sent.
 struct Staging {
   uint8_t* host = nullptr;
   size_t cap = 0;
   hipStream_t stream = nullptr;
+  std::vector<hipEvent_t> ev;
   ~Staging() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (host) (void)hipHostFree(host);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  void ensure(size_t n) {
+  void ensure(size_t n, size_t pieces) {
+    while (ev.size() < pieces) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw Error("HipError", "hipEventCreate");
+      ev.push_back(e);
+    }
     if (n <= cap) return;
     if (host) (void)hipHostFree(host);
     host = nullptr;
@@ -115,16 +128,36 @@ class HbmSeeder {
       if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess)
         throw Error("HipError", "hipStreamCreate");
     }
+    // The response is copied HBM -> pinned in pieces of kPiece (ZEST_SEED_PIECE_MB, default 8)
+    // queued back to back, each followed by an event: the server sends piece k while piece k + 1 is
+    // still in flight (ready() waits for the piece a slice needs), instead of copying the whole
+    // run (up to 64 MiB) and synchronizing before the first byte goes out.
+    static const size_t kPiece = [] {
+      const char* v = std::getenv("ZEST_SEED_PIECE_MB");
+      const size_t mb = v && *v ? size_t(std::strtoull(v, nullptr, 10)) : 8;
+      return std::max<size_t>(1, mb) << 20;
+    }();
     const size_t len = size_t(hi - lo);
-    st->ensure(len);
-    if (hipMemcpyAsync(st->host, arena_ + lo, len, hipMemcpyDeviceToHost, st->stream) != hipSuccess ||
-        hipStreamSynchronize(st->stream) != hipSuccess)
-      throw Error("HipError", "HBM -> host copy");
+    const size_t pieces = std::max<size_t>(1, (len + kPiece - 1) / kPiece);
+    st->ensure(len, pieces);
+    for (size_t k = 0; k < pieces; ++k) {
+      const size_t o = k * kPiece, n = std::min(kPiece, len - o);
+      if ((n && hipMemcpyAsync(st->host + o, arena_ + lo + o, n, hipMemcpyDeviceToHost, st->stream) != hipSuccess) ||
+          hipEventRecord(st->ev[k], st->stream) != hipSuccess)
+        throw Error("HipError", "HBM -> host copy");
+    }
     storage::CacheHit h;
     h.chunk_offset = a;
     h.ext = st->host;
     h.ext_len = len;
     h.keep = st;
+    Staging* sp = st.get();
+    h.ready = [sp](size_t upto) {
+      if (!upto) return;
+      const size_t k = (upto - 1) / kPiece;
+      if (hipEventSynchronize(sp->ev[std::min(k, sp->ev.size() - 1)]) != hipSuccess)
+        throw Error("HipError", "HBM -> host copy");
+    };
     return h;
   }
 
@@ -164,6 +197,9 @@ void bind_hip_seed(py::module_& m) {
         d["bytes_served"] = st.bytes_served;
         d["not_found"] = st.not_found;
         d["rejected"] = st.rejected;
+        d["lookup_s"] = double(st.lookup_ns) / 1e9;
+        d["wait_s"] = double(st.wait_ns) / 1e9;
+        d["send_s"] = double(st.send_ns) / 1e9;
         return d;
       });
 }

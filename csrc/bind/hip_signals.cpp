@@ -50,10 +50,19 @@ struct PeerSignals {
   ~PeerSignals() {
     if (!host) return;
     if (registered) {
-      (void)hipDeviceSynchronize();  // no wait command may still poll the page
+      // No wait command may still poll the page when it is unmapped, so the device is synchronized
+      // -- after every slot is opened (0xFFFFFFFF), so that a wait on a rank that will never signal
+      // again (it died, or this pull failed) cannot hang the teardown.  Safe for the other
+      // ranks: a page is dropped only after a pull ended on every rank (the end of a pull is a
+      // collective) or after a failure, and the next pull agrees on a fresh page.
+      release();
+      (void)hipDeviceSynchronize();
       (void)hipHostUnregister(host);
     }
     munmap(host, bytes);
+  }
+  void release() {
+    for (int i = 0; i < n; ++i) __atomic_store_n(slot(i), 0xFFFFFFFFu, __ATOMIC_RELEASE);
   }
   uint32_t* slot(int i) const {
     if (i < 0 || i >= n) throw std::out_of_range("signal slot");
@@ -114,6 +123,8 @@ void bind_hip_signals(py::module_& m) {
       .def_readonly("n", &PeerSignals::n)
       .def("value", [](const PeerSignals& s, int i) { return __atomic_load_n(s.slot(i), __ATOMIC_ACQUIRE); })
       .def("store", [](const PeerSignals& s, int i, uint32_t v) { __atomic_store_n(s.slot(i), v, __ATOMIC_RELEASE); })
+      // Open every slot: no wait on this page blocks any more (a lost rank, a failed pull).
+      .def("release", [](PeerSignals& s) { s.release(); })
       // Queue on `stream`: store `value` into slot i once everything queued before it has completed.
       .def("set_after",
            [](const PeerSignals& s, int i, uint32_t v, uintptr_t stream) {

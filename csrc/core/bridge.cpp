@@ -1,5 +1,9 @@
 #include "bridge.h"
 
+#include <tuple>
+
+#include <algorithm>
+
 #include <cstring>
 #include <iomanip>
 
@@ -89,6 +93,7 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
               out.pending = writer_ ? writer_->put_pending(hex, r->chunk_offset, r->bytes(), r->size())
                                     : cache_->put_pending(hex, r->chunk_offset, r->bytes(), r->size());
             }
+            if (writer_ && out.pending.empty()) defer(hex, *fi, false);  // the writer's queue was full
             out.run_offset = r->chunk_offset;
           } catch (const Error&) {
           }
@@ -140,11 +145,12 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   }
   if (cache_ && cfg_.cache_writes) {
     try {
-      if (writer_ && opt.on_copied && out.ext)
+      if (writer_ && opt.on_copied && out.ext) {
         out.copy_deferred = writer_->put_run_ref(hex, uint32_t(fi->range.start), run, run_len, opt.repair, opt.on_copied);
-      else if (writer_)
-        writer_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
-      else
+        if (!out.copy_deferred) defer(hex, *fi, opt.repair);  // the writer's queue was full
+      } else if (writer_) {
+        if (!writer_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair)) defer(hex, *fi, opt.repair);
+      } else
         cache_->put_run(hex, uint32_t(fi->range.start), run, run_len, opt.repair);
     } catch (const Error&) {
     }
@@ -154,6 +160,44 @@ XorbFetchResult XetBridge::fetch_term(const cas::Term& term, const cas::Reconstr
   out.local_end = uint32_t(term.range.end - fi->range.start);
   out.source = Source::Cdn;
   return out;
+}
+
+void XetBridge::defer(const std::string& hex, const cas::FetchInfo& fi, bool repair) {
+  std::lock_guard<std::mutex> g(deferred_mu_);
+  deferred_.push_back(Deferred{hex, fi, repair});
+}
+
+size_t XetBridge::deferred_count() const {
+  std::lock_guard<std::mutex> g(deferred_mu_);
+  return deferred_.size();
+}
+
+size_t XetBridge::fill_deferred() {
+  std::vector<Deferred> todo;
+  {
+    std::lock_guard<std::mutex> g(deferred_mu_);
+    todo.swap(deferred_);
+  }
+  if (todo.empty() || !cache_ || !cas_) return 0;
+  if (writer_) writer_->flush();  // the quarantined runs' promote/discard ops ran first
+  std::sort(todo.begin(), todo.end(), [](const Deferred& a, const Deferred& b) {
+    return std::tie(a.hex, a.fi.range.start) < std::tie(b.hex, b.fi.range.start);
+  });
+  size_t done = 0;
+  for (size_t i = 0; i < todo.size(); ++i) {
+    const Deferred& d = todo[i];
+    if (i && d.hex == todo[i - 1].hex && d.fi.range.start == todo[i - 1].fi.range.start) continue;
+    if (!d.repair && cache_->find(d.hex, uint32_t(d.fi.range.start), uint32_t(d.fi.range.end))) continue;
+    try {
+      trace::Span sp("cache", "refill dropped run");
+      Bytes body = cas_->fetch(d.fi);
+      cache_->put_run(d.hex, uint32_t(d.fi.range.start), body.data(), body.size(), d.repair);
+      ++done;
+    } catch (const std::exception&) {
+      // best effort: a run that cannot be refetched only costs a later miss
+    }
+  }
+  return done;
 }
 
 void XetBridge::settle(const std::string& xorb_hex, Source src, uint32_t run_offset, const std::string& pending,

@@ -86,14 +86,29 @@ class XetBridge {
   // through a write-behind queue instead of the fetch thread (device pulls; see storage::CacheWriter).
   void set_writer(storage::CacheWriter* w) { writer_ = w; }
   storage::CacheWriter* writer() const { return writer_; }
+  // Runs the write-behind queue had no room for (dropped instead of stalling the fetch): recorded
+  // here, and fill_deferred() fetches them again from the CDN -- the trusted origin, so a dropped
+  // quarantined peer run is replaced by a verified one -- and writes them into the cache once the
+  // pull's hot path is over.  Seed-while-downloading then misses nothing (the
+  // reference always caches after a fetch, swarm.zig:416-420).  Returns the runs written.
+  size_t fill_deferred();
+  size_t deferred_count() const;
 
  private:
+  void defer(const std::string& hex, const cas::FetchInfo& fi, bool repair);
   const Config& cfg_;
   storage::XorbCache* cache_;
   SwarmDownloader* swarm_;
   storage::CacheWriter* writer_ = nullptr;
   std::unique_ptr<cas::CasClient> cas_;
   FetchStats stats_;
+  struct Deferred {
+    std::string hex;
+    cas::FetchInfo fi;
+    bool repair = false;
+  };
+  mutable std::mutex deferred_mu_;
+  std::vector<Deferred> deferred_;
 };
 
 }  // namespace zest

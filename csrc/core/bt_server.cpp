@@ -94,6 +94,9 @@ ServerStats BtServer::stats() const {
   s.not_found = nf_.load();
   s.chunk_units = units_.load();
   s.rejected = rejected_.load();
+  s.lookup_ns = lookup_ns_.load();
+  s.wait_ns = wait_ns_.load();
+  s.send_ns = send_ns_.load();
   return s;
 }
 
@@ -198,9 +201,15 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
     if (fault_.delay_ms) std::this_thread::sleep_for(std::chrono::milliseconds(fault_.delay_ms));
     if (fault_.drop > 0 && u01(rng) < fault_.drop) return;  // injected connection drop
     std::optional<storage::CacheHit> hit;
+    using clk = std::chrono::steady_clock;
+    auto ns_since = [](clk::time_point t) {
+      return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t).count());
+    };
     {
       trace::Span sp("serve", "lookup");
+      const auto t0 = clk::now();
       hit = lookup(x.hash, x.range_start, x.range_end);
+      lookup_ns_ += ns_since(t0);
     }
     out.clear();
     if (!hit) {
@@ -221,6 +230,7 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
       sp.arg("\"bytes\":" + std::to_string(hit->size()));
       if (fault_.rate_mbps > 0) {
         // paced in 1 MiB slices, so the connections of a capped server interleave on its "uplink"
+        hit->wait_all();
         pace(out.size());
         s.write_all(out.data(), out.size());
         const uint8_t* b = hit->bytes();
@@ -230,8 +240,31 @@ void BtServer::handle(net::Socket s, net::Addr peer) {
           s.write_all(b + o, k);
           o += k;
         }
+      } else if (hit->ready && hit->ext) {
+        // slice by slice behind the provider's copies: slice k + 1 lands while slice k is sent
+        constexpr size_t kSlice = size_t(8) << 20;
+        const uint8_t* b = hit->bytes();
+        const size_t n = hit->size();
+        auto t = clk::now();
+        s.write_all(out.data(), out.size());
+        send_ns_ += ns_since(t);
+        for (size_t o = 0; o < n;) {
+          const size_t k = std::min(n - o, kSlice);
+          t = clk::now();
+          hit->ready(o + k);
+          wait_ns_ += ns_since(t);
+          t = clk::now();
+          s.write_all(b + o, k);
+          send_ns_ += ns_since(t);
+          o += k;
+        }
       } else {
+        const auto t = clk::now();
+        hit->wait_all();
+        wait_ns_ += ns_since(t);
+        const auto t1 = clk::now();
         s.writev_all(iov, 2);
+        send_ns_ += ns_since(t1);
       }
     }
     served_++;

@@ -40,6 +40,10 @@ struct ServerStats {
   uint64_t not_found = 0;
   uint64_t chunk_units = 0;  // Xet chunks delivered (sum of requested range lengths)
   uint64_t rejected = 0;     // connections closed at accept: max_inbound already being served
+  // Where a response's time goes, summed over connections (ns): the piece provider (lookup; for
+  // the HBM seeder: queueing its D2H copies), waiting for provider bytes to land (ready()), and the
+  // socket writes.
+  uint64_t lookup_ns = 0, wait_ns = 0, send_ns = 0;
 };
 
 struct FaultSpec {
@@ -86,6 +90,7 @@ class BtServer {
   std::set<int> conns_;
   std::list<Worker> workers_;
   std::atomic<uint64_t> active_{0}, total_{0}, served_{0}, bytes_{0}, nf_{0}, units_{0}, rejected_{0};
+  std::atomic<uint64_t> lookup_ns_{0}, wait_ns_{0}, send_ns_{0};
   FaultSpec fault_;
   // rate cap: the time the uplink is free again (token bucket of one burst, shared by connections)
   std::mutex rate_mu_;

@@ -232,6 +232,9 @@ Reconstruction CasClient::get_reconstruction(const std::string& file_hash_hex) c
 }
 
 Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
+  if (fi.url_range.end < fi.url_range.start || fi.url_range.end - fi.url_range.start >= (uint64_t(1) << 40))
+    throw Error("InvalidRange", "xorb url_range " + std::to_string(fi.url_range.start) + "-" +
+                                    std::to_string(fi.url_range.end));
   const uint64_t want = fi.url_range.end - fi.url_range.start + 1;
   if (is_mem_url(fi.url)) {
     const uint8_t* p = mem_origin_find(fi.url, fi.url_range.start, fi.url_range.end);
@@ -261,6 +264,7 @@ Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
 }
 
 size_t CasClient::fetch_into(const FetchInfo& fi, uint8_t* dst, size_t room, int timeout_ms) const {
+  if (fi.url_range.end < fi.url_range.start) throw Error("InvalidRange", "xorb url_range end before start");
   const uint64_t want = fi.url_range.end - fi.url_range.start + 1;
   if (!dst || want > room) return 0;
   if (is_mem_url(fi.url)) {
@@ -330,8 +334,11 @@ const uint8_t* mem_origin_find(const std::string& url, uint64_t start, uint64_t 
   auto it = g_mem.upper_bound({hex, start});
   if (it == g_mem.begin()) return nullptr;
   --it;  // the run starting at or before `start`
-  if (it->first.first != hex || end_inclusive + 1 > it->first.second + it->second.len) return nullptr;
-  return it->second.data + (start - it->first.second);
+  if (it->first.first != hex || end_inclusive < start) return nullptr;
+  // [start, end_inclusive] inside [run_start, run_start + len), without overflowing on a hostile range
+  const uint64_t skip = start - it->first.second, len = it->second.len;
+  if (skip >= len || end_inclusive - start >= len - skip) return nullptr;
+  return it->second.data + skip;
 }
 
 }  // namespace zest::cas

@@ -59,9 +59,20 @@ struct CacheHit {
   const uint8_t* ext = nullptr;
   size_t ext_len = 0;
   std::shared_ptr<void> keep;
+  // A view still being filled (e.g. HBM -> pinned copies in flight): ready(n) blocks until bytes
+  // [0, n) of `ext` are valid.  Empty: all of it is.  A server sends slice by slice behind it, so
+  // the copy of one slice overlaps the send of the previous one.
+  std::function<void(size_t)> ready;
   const uint8_t* bytes() const { return ext ? ext : data.data(); }
   size_t size() const { return ext ? ext_len : data.size(); }
+  void wait_all() {
+    if (ready) {
+      ready(ext_len);
+      ready = nullptr;
+    }
+  }
   void materialize() {  // copy an external view into `data`
+    wait_all();
     if (ext) {
       data.assign(ext, ext + ext_len);
       ext = nullptr;

@@ -89,8 +89,10 @@ struct DeviceXetPull::Shared {
       cache->set_registry_lookup(true);  // a miss needs no cache directory listing on a fetch thread
     }
     if (cfg.cache_writes)  // ZEST_CACHE_WRITE_QUEUE_MB bounds the write-behind queue (0: synchronous)
-      if (size_t mb = env_size("ZEST_CACHE_WRITE_QUEUE_MB", 2048))
-        writer = std::make_unique<storage::CacheWriter>(cache.get(), mb << 20, 2);
+      if (size_t mb = env_size("ZEST_CACHE_WRITE_QUEUE_MB", 2048)) {
+        const size_t bytes = env_size("ZEST_CACHE_WRITE_QUEUE_BYTES", 0);  // (tests: a queue that overflows)
+        writer = std::make_unique<storage::CacheWriter>(cache.get(), bytes ? bytes : mb << 20, 2);
+      }
     std::vector<net::Addr> boot;
     for (auto& b : o.dht_bootstrap) boot.push_back(net::Addr::parse(b, 6881));
     {
@@ -104,6 +106,15 @@ struct DeviceXetPull::Shared {
     {
       trace::Span sp("device", "init: xet auth");
       bridge->authenticate(o.repo, o.repo_type, o.revision);
+    }
+  }
+  ~Shared() {
+    // runs the write-behind queue dropped are fetched again and cached before the pipeline goes
+    // (ZEST_CACHE_REFILL=0: left out); the writer drains first
+    try {
+      if (writer) writer->flush();
+      if (bridge && env_size("ZEST_CACHE_REFILL", 1)) bridge->fill_deferred();
+    } catch (...) {
     }
   }
   Config cfg;
@@ -351,6 +362,7 @@ struct DeviceXetPull::Impl {
   size_t settle(const std::string& hex, bool ok) { return sh_->book.settle(*sh_->bridge, hex, ok); }
   void flush_cache_writes() {
     if (sh_->writer) sh_->writer->flush();
+    sh_->bridge->fill_deferred();  // runs the full write-behind queue dropped: refetched and cached now
   }
   std::vector<TermShape> term_shapes(const std::string& hex) { return sh_->recs->shapes(hex); }
 
@@ -1139,7 +1151,21 @@ struct DeviceXetPull::Impl {
         std::tie(g, i) = swork_[swork_next_++];
         bp = &sbatches_[g - sb0_];
         SItem& it = *bp->item;
-        scv_.wait(lk, [&] { return sstop_ || it.failed || sready_[g % S] >= g; });
+        // Start-up: until the pass's first batch is queued, only its terms are fetched -- with every
+        // worker free to run ahead, the first batch shared the host's copy bandwidth with 15 later
+        // terms and the copy engine idled ~30 ms (4-rank rehearsal, profiles/r6/).  Afterwards the
+        // workers run as far ahead as the free slots allow.  ZEST_STREAM_AHEAD = A > 0 keeps a
+        // window of A batches past the oldest unqueued one for the whole pass; 0 turns both off.
+        static const long ahead = [] {
+          const char* v = std::getenv("ZEST_STREAM_AHEAD");
+          return v && *v ? std::strtol(v, nullptr, 10) : -1L;
+        }();
+        scv_.wait(lk, [&] {
+          if (sstop_ || it.failed) return true;
+          if (sready_[g % S] < g) return false;
+          if (ahead > 0) return g < ssubmit_next_ + size_t(ahead);
+          return ahead == 0 || ssubmit_next_ > sb0_ || g == sb0_;
+        });
         if (sstop_) return;
         if (it.failed) {  // the item is lost: its other terms need no fetch
           if (--bp->remaining == 0) scv_.notify_all();
@@ -1557,7 +1583,8 @@ std::string DeviceXetPull::cache_writer_json() const {
   if (!w) return "{}";
   const auto st = w->stats();
   return "{\"queued_bytes\":" + std::to_string(st.queued_bytes) + ",\"written_bytes\":" + std::to_string(st.written_bytes) +
-         ",\"dropped_bytes\":" + std::to_string(st.dropped_bytes) + "}";
+         ",\"dropped_bytes\":" + std::to_string(st.dropped_bytes) +
+         ",\"deferred_runs\":" + std::to_string(impl_->sh_->bridge->deferred_count()) + "}";
 }
 std::string DeviceXetPull::stats_json() const { return impl_->stats_json(); }
 size_t DeviceXetPull::staging_bytes() const { return impl_->staging_bytes(); }

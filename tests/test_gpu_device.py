@@ -297,6 +297,49 @@ def test_device_pull_sibling_pipelines_and_write_behind_cache(tmp_path, monkeypa
         hub.stop()
 
 
+def test_dropped_cache_runs_are_refilled_and_served(tmp_path, monkeypatch):
+    """a write-behind queue with no room drops runs instead of stalling the
+    device pull -- they are recorded, refetched from the CDN by flush_cache_writes() (and when the
+    pipeline goes), and then every xorb of the repository is served from the cache by a `zest serve`
+    seeder, byte-exact."""
+    import json as _json
+
+    from zest_amd import _core, ops as zops
+
+    files = {f"model-{i:05d}.safetensors": bytes(np.random.default_rng(70 + i).integers(0, 256, 300_000 + 5003 * i,
+                                                                                        dtype=np.uint8))
+             for i in range(3)}
+    hub = FakeHub(policy="auto", max_xorb_bytes=128 << 10)
+    hub.start()
+    try:
+        hub.add_repo("org/refill", files, xet_min_size=1)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("ZEST_CACHE_WRITE_QUEUE_BYTES", "1")  # every run overflows the queue
+        commit, listing = _core.list_repo_files("org/refill", "main", "model")
+        listing = sorted((f for f in listing if f["xet_hash"]), key=lambda f: f["path"])
+        dp = zops.hip().DeviceXetPull("org/refill", "main", "model", False, [], None, False, [], 0, 1 << 20, 4)
+        bufs = [zops.padded_empty(f["size"], "cuda:0")[:f["size"]] for f in listing]
+        torch.cuda.synchronize()
+        dp.pull_files([(f["xet_hash"], b.data_ptr(), f["size"]) for f, b in zip(listing, bufs)])
+        for f, b in zip(listing, bufs):
+            assert b.cpu().numpy().tobytes() == files[f["path"]]
+        w = _json.loads(dp.cache_writer_json())
+        assert w["dropped_bytes"] > 0 and w["deferred_runs"] == len(hub.xorbs), w
+        dp.flush_cache_writes()  # the dropped runs are fetched again and cached
+        assert _json.loads(dp.cache_writer_json())["deferred_runs"] == 0
+        assert len(_core.list_cached_xorbs()) == len(hub.xorbs)
+        seeder = _core.Seeder(0)
+        try:
+            for x in hub.xorbs:
+                data, off, _ = _core.peer_fetch(f"127.0.0.1:{seeder.port}", _core.from_xet_hex(x.hash_hex), 0, 0)
+                assert off == 0 and data == x.data, x.hash_hex
+        finally:
+            seeder.stop()
+    finally:
+        hub.stop()
+
+
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
 def test_device_pull_on_second_gpu_from_another_thread(tmp_path, monkeypatch):
     """HIP's current device is per thread.  A pipeline built for the last GPU and called

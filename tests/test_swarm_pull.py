@@ -590,3 +590,28 @@ def test_swarm_pull_stuck_recovery_exits_in_bounded_time(hub_env):
     assert codes == [3, 3, 1], codes
     assert q.empty()  # nobody returned from the pull
     assert dt < 120, dt
+
+
+def test_single_command_replicated_pull(hub_env, tmp_path):
+    """`python -m zest_amd pull <repo> --gpus 3 --device all --save-snapshot` (here --cpu: host
+    memory, gloo): one command starts 3 rank processes, every rank ends with every tensor verified,
+    each prints its status line, and rank 0 writes the HF-cache snapshot once."""
+    import subprocess
+    import sys
+
+    world, hub = hub_env
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "zest_amd", "pull", world.spec.repo_id, "--gpus", "3", "--device", "all", "--cpu",
+           "--save-snapshot", "--no-p2p", "--no-dht", "--round-mb", "1", "--timeout", "240"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=root))
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("[rank ")]
+    assert len(lines) == 3 and all("tensors" in ln and "verified" in ln for ln in lines), r.stdout
+    n_t = len(_expected(world))
+    assert all(f"{n_t} tensors" in ln for ln in lines), lines
+    snaps = sorted((tmp_path / "hf").rglob("snapshots/*/*.safetensors"))
+    assert {p.name for p in snaps} == {os.path.basename(f.path) for f in world.xet_files}
+    for f in world.xet_files:
+        p = next(x for x in snaps if x.name == os.path.basename(f.path))
+        assert p.read_bytes() == world.file_bytes_host(f)

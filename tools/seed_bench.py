@@ -99,6 +99,9 @@ def main() -> None:
            "chunks_served_per_s": round(responses / dt, 1), "GBps": round(totals["bytes"] / dt / 1e9, 3),
            "xet_chunks_per_s": round(totals["chunks"] / dt, 1), "chunk_units_64KiB_per_s": round(units / dt, 1),
            "requests_per_s": round(totals["reqs"] / dt, 1), "failed": totals["failed"],
+           # where the server's connection threads spent the window (seconds summed over connections):
+           # queueing the HBM -> pinned copies, waiting for copied pieces, writing the sockets
+           "server_split_s": {k: round(st1.get(k, 0.0) - st0.get(k, 0.0), 3) for k in ("lookup_s", "wait_s", "send_s")},
            "server": st1}
     print(json.dumps(out), flush=True)
     srv.stop()

@@ -11,7 +11,7 @@ step, with the process's open fd count, for these modes (--modes, comma list):
   map       + the peer imports and maps the chunks (map_peer_arenas)    -> the swarm pull's path
   map_rev   like map, but the owners release before the importers
 
-Usage: python tools/experiments/vmm_leak_probe.py [--gb 4] [--iters 3] [--modes alloc,export,map,map_rev]
+Usage: python tools/vmm_leak_probe.py [--gb 4] [--iters 3] [--modes alloc,export,map,map_rev]
 Prints one JSON line per rank and mode.
 """
 from __future__ import annotations
@@ -23,7 +23,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 

@@ -393,7 +393,7 @@ class RoundExchange:
     def signaled(self) -> bool:
         return self._signals is not None
 
-    def enable_signals(self) -> bool:
+    def enable_signals(self, agreed=None) -> bool:
         """Collective over the mapped ranks: share one page of ready counters (one per rank) so that
         peer-mapped exchanges wait on the GPU (hipStreamWaitValue32 on the owner's counter) instead
         of a host event synchronize + host barrier per round.  Off with ZEST_IPC_SIGNALS=0; False
@@ -415,6 +415,17 @@ class RoundExchange:
             return int(t.item())
 
         pa = self._pa
+        if agreed is not None and agreed[0] and pa is not None and pa.signals is not None:
+            # the caller already agreed (one control all-gather) that every rank keeps this mapping's
+            # page, and on the highest counter value any rank reached: no collective here.  Every
+            # counter continues from there, so no wait of this pull can be satisfied by an earlier
+            # one; no barrier is needed (each rank only raises its own counter, to at most `top`).
+            top = int(agreed[1])
+            pa.signals.store(self.rank, top)
+            pa.sig_sent = top
+            self._signals, self._sig_sent = pa.signals, top
+            self._signal_stream = role_stream(self.device, "signal")
+            return True
         if agree(int(pa is not None and pa.signals is not None)):
             # the mapping's page from an earlier exchange over it (a previous pull): every rank's
             # counter continues from the highest value any rank reached, so a wait of this pull can
@@ -469,8 +480,7 @@ class RoundExchange:
         sig = self._signals
         if sig is None:
             return
-        for i in range(self.n_ranks):
-            sig.store(i, 0xFFFFFFFF)
+        sig.release()
         self._signals = None
         if self._pa is not None and self._pa.signals is sig:
             self._pa.signals = None

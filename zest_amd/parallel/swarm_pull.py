@@ -129,12 +129,21 @@ def split_bytes(ulen: np.ndarray, a: int, b: int, weights) -> list[tuple[int, in
 
 def round_weights(share_bytes: int, round_bytes: int, taper: bool = True) -> list[float]:
     """Relative sizes of a share's rounds: full rounds of `round_bytes`, with geometrically shrinking
-    first and last rounds (nothing overlaps the first fetch or the last exchange)."""
+    first and last rounds (nothing overlaps the first fetch or the last exchange).
+    ZEST_SWARM_HEAD_TAPER / ZEST_SWARM_TAIL_TAPER (comma lists of round fractions) override the
+    tapers."""
+    head = _taper_env("ZEST_SWARM_HEAD_TAPER", HEAD_TAPER)
+    tail = _taper_env("ZEST_SWARM_TAIL_TAPER", TAIL_TAPER)
     n = max(1, -(-int(share_bytes) // int(round_bytes)))
     if not taper or n < 4:
         return [1.0] * n
-    mid = max(1, -(-int(share_bytes - (sum(HEAD_TAPER) + sum(TAIL_TAPER)) * round_bytes) // round_bytes))
-    return list(HEAD_TAPER) + [1.0] * mid + list(TAIL_TAPER)
+    mid = max(1, -(-int(share_bytes - (sum(head) + sum(tail)) * round_bytes) // round_bytes))
+    return list(head) + [1.0] * mid + list(tail)
+
+
+def _taper_env(name: str, default) -> tuple:
+    v = os.environ.get(name, "").strip()
+    return tuple(float(x) for x in v.split(",") if x.strip()) if v else tuple(default)
 
 
 def assign_owners(ulen: np.ndarray, held: np.ndarray | None, world: int) -> np.ndarray:
@@ -735,25 +744,56 @@ class _Swarm:
     def gather_possession(self):
         """Which terms each rank's xorb cache already covers (have-map): checked
         locally against the planned terms' chunk ranges, then all-gathered as bitmaps on the control
-        group.  Sets self.held (bool [world, n_terms]) or None when nobody holds anything."""
+        group.  Sets self.held (bool [world, n_terms]) or None when nobody holds anything.
+        The same all-gather carries what allocate() and setup_exchange() need agreed -- whether every
+        rank can reuse its kept arena, and the state of its ready-counter page -- so a repeated pull
+        pays one control collective here instead of three."""
         self.held = None
-        if self.term_keys is None or not len(self.term_keys):
-            return
         t = time.perf_counter()
-        hexes = [k[0] for k in self.term_keys]
-        mine = self.fetcher.held(hexes, [int(k[1]) for k in self.term_keys], [int(k[2]) for k in self.term_keys])
-        bits = self._gather(np.packbits(mine).tobytes())
-        nt = len(self.term_keys)
-        held = np.stack([np.unpackbits(np.frombuffer(b, dtype=np.uint8))[:nt].astype(bool) for b in bits])
-        self.held = held if held.any() else None
+        self._arena_local()
+        bits = None
+        if self.term_keys is not None and len(self.term_keys):
+            hexes = [k[0] for k in self.term_keys]
+            mine = self.fetcher.held(hexes, [int(k[1]) for k in self.term_keys], [int(k[2]) for k in self.term_keys])
+            bits = np.packbits(mine).tobytes()
+        mine_v = (bits, self._have_local, self._sig_local[0], self._sig_local[1])
+        allv = self._gather(mine_v) if self.m.world > 1 else [mine_v]
+        self._have_all = int(all(v[1] for v in allv))
+        self._sig_agreed = (bool(all(v[2] for v in allv)), max(int(v[3]) for v in allv))
+        if bits is not None:
+            nt = len(self.term_keys)
+            held = np.stack([np.unpackbits(np.frombuffer(v[0], dtype=np.uint8))[:nt].astype(bool) for v in allv])
+            self.held = held if held.any() else None
         self._mark("possession_s", t)
+
+    def _arena_local(self):
+        """This rank's side of the arena reuse decision (agreed in gather_possession)."""
+        n = max(1, self.plan.arena_bytes)
+        self._want_map = (self.cuda and self.m.world > 1 and os.environ.get("ZEST_EXCHANGE_IPC", "1") != "0"
+                          and self.exchange_req in ("auto", "ipc", "xgmi"))
+        # reuse_arena None (default): peer-mapped arenas are kept and reused whenever no tensor of the
+        # previous pull is alive (a released peer-mapped arena stayed counted as used on the box,
+        # ARCHITECTURE 15.8, so a fresh one per pull would pile up); True: reuse regardless.
+        self._use_cache = self.reuse_arena is True or (self.reuse_arena is None and self._want_map)
+        self._arena_key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks), self._want_map)
+        cached = _ARENAS.get(self._arena_key) if self._use_cache else None
+        self._cached = cached
+        self._have_local = int(cached is not None and cached[0].numel() >= n
+                               and (cached[1] is not None or not self._want_map)
+                               and (self.reuse_arena is True or not _arena_in_use(cached)))
+        pa = cached[1] if cached is not None else None
+        self._sig_local = (bool(self._have_local and pa is not None and getattr(pa, "signals", None) is not None),
+                           int(getattr(pa, "sig_sent", 0) if pa is not None else 0))
 
     def allocate(self):
         t = time.perf_counter()
         P = self.plan
         n = max(1, P.arena_bytes)
-        want_map = (self.cuda and self.m.world > 1 and os.environ.get("ZEST_EXCHANGE_IPC", "1") != "0"
-                    and self.exchange_req in ("auto", "ipc", "xgmi"))
+        if not hasattr(self, "_have_all"):  # (no possession gather ran: agree on the arena here)
+            self._arena_local()
+            self._have_all = int(all(self._gather(self._have_local))) if self.m.world > 1 else self._have_local
+            self._sig_agreed = (False, 0)
+        want_map = self._want_map
         self.arena = None
         # (device memory free before the arena, and the arena's own allocation time: a pull after
         # another pull in the same process spent 4.5 s here, profiles/r5/bench70b_r5ai.log)
@@ -763,16 +803,9 @@ class _Swarm:
         # previous pull of at least this size, when every rank has one -- the caller holds no tensor
         # of that pull any more.  A fresh 141 GB arena per pull costs the driver's reclaim of the last
         # one (~4 s, profiles/r5/alloc_probe_141g_r5aj.log) and, peer-mapped, a new export/import.
-        key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks), want_map)
-        # reuse_arena None (default): peer-mapped arenas are kept and reused whenever no tensor of the
-        # previous pull is alive (a released peer-mapped arena stayed counted as used on the box,
-        # ARCHITECTURE 15.8, so a fresh one per pull would pile up); True: reuse regardless.
-        use_cache = self.reuse_arena is True or (self.reuse_arena is None and want_map)
-        cached = _ARENAS.get(key) if use_cache else None
-        have = int(cached is not None and cached[0].numel() >= n and (cached[1] is not None or not want_map)
-                   and (self.reuse_arena is True or not _arena_in_use(cached)))
-        if use_cache and self.m.world > 1:
-            have = int(all(self._gather(have)))
+        key, use_cache, cached = self._arena_key, self._use_cache, self._cached
+        have = self._have_all if use_cache else 0
+        self.reused_arena = bool(have)
         if have:
             full, self.mapped, _ = cached
             self.arena = full[:n]
@@ -818,7 +851,16 @@ class _Swarm:
         # One rank: nothing to overlap a fetch with, so the whole share is one pull_terms call (every
         # round boundary drains the fetch pipeline: 16 rounds of 1 GiB cost ~25 ms each on
         # Llama-3.1-8B, profiles/r4/swarm_pull_r4b.json).
-        weights = round_weights(max_share, self.round_bytes, taper) if max_share and W > 1 else [1.0]
+        rb = self.round_bytes
+        if self.streamed and max_share:
+            # streamed rounds cost no drain and no blocking agreement, so the share is cut finer: at
+            # least ZEST_SWARM_MIN_ROUNDS (8) rounds per rank (>= 64 MiB each), so the first exchange
+            # starts early and the last one is short (8 ranks of an 8B model: 2 GB shares were 2
+            # rounds of 1 GiB, the first exchange waiting ~0.3 s, profiles/r6/)
+            k = max(1, int(os.environ.get("ZEST_SWARM_MIN_ROUNDS", "8")))
+            rb = min(rb, max(64 << 20, -(-max_share // k)))
+        self.round_bytes_used = rb
+        weights = round_weights(max_share, rb, taper) if max_share and W > 1 else [1.0]
         self.items: list[tuple[int, int]] = []
         self.queue: list[list[int]] = [[] for _ in range(W)]
         for r in range(W):
@@ -857,8 +899,9 @@ class _Swarm:
         W = self.m.world
         self.xchg = RoundExchange(self.arena, self.m.rank, W, self.m.data, "p2p")
         if self.mapped is not None and self.xchg.enable_ipc(self.mapped) and self.streamed:
-            # streamed rounds wait for the owners on the GPU (ready counters), not in host barriers
-            self.xchg.enable_signals()
+            # streamed rounds wait for the owners on the GPU (ready counters), not in host barriers;
+            # a kept arena's page continues from the counter values agreed in gather_possession
+            self.xchg.enable_signals(agreed=self._sig_agreed if getattr(self, "reused_arena", False) else None)
         self.verify_stream = role_stream(self.device, "verify") if self.cuda else None
         self._hash_scratch = ops.HashScratch(self.device) if self.cuda else None
         if W == 1:
@@ -1577,7 +1620,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                verify_received: bool = True, staging_bytes: int = 1 << 30, threads: int = 16,
                round_bytes: int | None = None, exchange: str = "auto",
                stats: dict | None = None, reuse_pipeline: bool | None = None,
-               possession: bool | None = None, reuse_arena: bool | None = None) -> dict[str, torch.Tensor]:
+               possession: bool | None = None, reuse_arena: bool | None = None,
+               files_out: dict | None = None) -> dict[str, torch.Tensor]:
     """Collective over `group`: returns {tensor_name: tensor} on this rank's device, every rank the
     full set (views into one arena per rank).  `exchange`: "auto" (measured at setup, cached per
     process) or one of p2p / bcast / allgather / ipc / xgmi.  `round_bytes` (default
@@ -1596,7 +1640,8 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     same for peer-mapped arenas (N > 1), but only when no tensor of the previous pull is still alive
     (a fresh peer-mapped arena per pull would pile up: a released one stayed counted as used on the
     box); False -- always a fresh arena.  Kept arenas hold their memory until the next pull or
-    release_pipelines()."""
+    release_pipelines().  `files_out`, if given, receives {path: uint8 tensor} -- every pulled
+    safetensors file's verified bytes (views of the arena), e.g. for writing a snapshot."""
     if reuse_pipeline is None:
         reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
     if os.environ.get("ZEST_SWARM_STAGING_MB"):  # per-slot staging of the fetch pipelines (A/B knob)
@@ -1612,6 +1657,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 staging_bytes=staging_bytes, threads=threads, round_bytes=round_bytes, exchange=exchange,
                 reuse=reuse_pipeline, possession=possession)
     sw.reuse_arena = reuse_arena
+    sw._mark("init_s", sw.t0)
     ok = False
     try:
         while True:
@@ -1623,8 +1669,12 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 sw.m.rebuild()
                 del e
         sw.allocate()
+        t_s = time.perf_counter()
         sw.shard()
+        sw._mark("shard_s", t_s)
+        t_s = time.perf_counter()
         sw.setup_exchange()
+        sw._mark("setup_exchange_s", t_s)
         t_pull = time.perf_counter()
         sw.t_pull = t_pull
         sw.run()
@@ -1648,6 +1698,11 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                                    f"{[sw.xet_files[i]['path'] for i in bad]}")
         plain = sw.plain()
         out = sw.tensors(plain)
+        if files_out is not None:
+            for f, o in zip(sw.xet_files, sw.plan.file_off):
+                files_out[f["path"]] = sw.arena[o:o + f["size"]]
+            for f, b in zip(sw.plain_files, plain):
+                files_out[f["path"]] = b
         if sw.cuda:
             torch.cuda.synchronize(sw.device)
         sw._mark("tensors_s", t_t)
@@ -1659,6 +1714,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 received_bytes=total - sw.fetched_bytes, total_bytes=total,
                 p2p_ratio=(total - sw.fetched_bytes) / total if total else 0.0,
                 rounds=sw.round_no, planned_rounds=sw.n_rounds_planned, items=len(sw.items),
+                round_bytes=getattr(sw, "round_bytes_used", sw.round_bytes),
                 exchange=round_mode, repair_exchange=sw.xchg.mode if sw.stats["repaired_files"] else None,
                 exchange_autotune_s={k: round(v, 4) for k, v in sw.xchg.times.items()},
                 peer_mapped=sw.xchg.mapped, world=sw.m.world, seconds=round(wall, 4),
@@ -1673,6 +1729,10 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         ok = True
         return out
     finally:
+        if not ok and sw.cuda and getattr(sw, "xchg", None) is not None:
+            # a failed pull may leave exchange streams waiting for counters that will never move:
+            # open them before anything below synchronizes (the page is not reused)
+            sw.xchg.release_signals()
         if getattr(sw, "_recon_warm", None) is not None:
             sw._recon_warm.join()
         if getattr(sw, "_fut", None) is not None:
