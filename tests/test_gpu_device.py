@@ -325,7 +325,7 @@ def test_dropped_cache_runs_are_refilled_and_served(tmp_path, monkeypatch):
         for f, b in zip(listing, bufs):
             assert b.cpu().numpy().tobytes() == files[f["path"]]
         w = _json.loads(dp.cache_writer_json())
-        assert w["dropped_bytes"] > 0 and w["deferred_runs"] == len(hub.xorbs), w
+        assert w["dropped_bytes"] > 0 and w["deferred_runs"] >= len(hub.xorbs), w  # (a xorb per term)
         dp.flush_cache_writes()  # the dropped runs are fetched again and cached
         assert _json.loads(dp.cache_writer_json())["deferred_runs"] == 0
         assert len(_core.list_cached_xorbs()) == len(hub.xorbs)
@@ -333,7 +333,8 @@ def test_dropped_cache_runs_are_refilled_and_served(tmp_path, monkeypatch):
         try:
             for x in hub.xorbs:
                 data, off, _ = _core.peer_fetch(f"127.0.0.1:{seeder.port}", _core.from_xet_hex(x.hash_hex), 0, 0)
-                assert off == 0 and data == x.data, x.hash_hex
+                # the served run is the xorb's chunk section (the hub's object also carries the footer)
+                assert off == 0 and len(data) == x.boundaries[-1] and data == x.data[:len(data)], x.hash_hex
         finally:
             seeder.stop()
     finally:
@@ -540,6 +541,57 @@ def test_swarm_pull_device_direct(tmp_path, monkeypatch, world_size, backend, ex
             assert all(r[2]["repaired_files"] == 0 for r in res)
         print(f"[swarm_pull {world_size}x{backend} {exchange}{'/' + fault if fault else ''}] mode {mode} "
               f"autotune {res[0][2]['exchange_autotune_s']} phases {res[0][2]['phases']}")
+    finally:
+        hub.stop()
+
+
+@pytest.mark.parametrize("world_size", [1, 2])
+def test_swarm_pull_hash_table_ordered_before_ingest(tmp_path, monkeypatch, world_size):
+    """Round 5's 2.4-3.4 s stall: the hash table was zero-filled on torch's
+    current stream while the native pipeline's ingest kernels -- on a stream of their own --
+    already wrote chunk hashes into it; when the zero-fill ran late it wiped them, the Merkle check
+    failed and the pull paid a CDN repair.  Here the current stream is held busy (~0.25 s) before the
+    zero-fill: the pull must still verify on its first check (no repair)."""
+    import dataclasses
+    import json
+    import struct
+
+    import torch.multiprocessing as mp
+
+    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
+    world = SyntheticWorld(spec, seed=29, mode="bf16")
+    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    hub.start()
+    try:
+        hub.add_world(world)
+        for k, v in hub.env(str(tmp_path)).items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("ZEST_LISTEN_PORT", str(free_port()))
+        monkeypatch.setenv("ZEST_SWARM_FAULT_SLOWZERO", "500000000")
+        want = {}
+        for f in world.xet_files:
+            data = world.file_bytes_host(f)
+            (hlen,) = struct.unpack("<Q", data[:8])
+            for name, ent in json.loads(data[8:8 + hlen]).items():
+                if name != "__metadata__":
+                    a, b = ent["data_offsets"]
+                    want[name] = data[8 + hlen + a:8 + hlen + b]
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = free_port()
+        backend = "nccl" if world_size == 1 else "gloo"
+        procs = [ctx.Process(target=_swarm_pull_gpu_worker,
+                             args=(r, world_size, port, world.spec.repo_id, backend, q, "auto", "", 512 << 10))
+                 for r in range(world_size)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=180) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+        for rank, got, st in res:
+            assert isinstance(got, dict), got
+            assert got.keys() == want.keys() and all(got[k] == want[k] for k in want)
+            assert st["first_verify_bad_files"] == 0 and st["repaired_files"] == 0, st
     finally:
         hub.stop()
 

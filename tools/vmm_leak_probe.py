@@ -10,6 +10,7 @@ step, with the process's open fd count, for these modes (--modes, comma list):
   export    + export every chunk as a dmabuf fd, close the fds          -> does an export pin memory?
   map       + the peer imports and maps the chunks (map_peer_arenas)    -> the swarm pull's path
   map_rev   like map, but the owners release before the importers
+  map_fresh like map, the importer moving every received fd to a never-used fd number first
 
 Usage: python tools/vmm_leak_probe.py [--gb 4] [--iters 3] [--modes alloc,export,map,map_rev]
 Prints one JSON line per rank and mode.
@@ -53,7 +54,7 @@ def _settle(torch, dev, quiet=0.5, limit=20.0) -> float:
 
 
 def worker(rank, world, port, gb, iters, modes, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZEST_IPC_DEBUG="1")
     import torch
     import torch.distributed as dist
     dev = torch.device("cuda", 0)
@@ -71,16 +72,26 @@ def worker(rank, world, port, gb, iters, modes, q):
             rec["base_GB"] = round(base, 2)
             for it in range(iters):
                 arena = ops.vmm_empty(int(gb * (1 << 30)), dev)
-                arena.fill_(rank + 1)
                 torch.cuda.synchronize()
                 a_free = _free(torch, dev)
                 mapped = None
                 if mode == "export":
                     for fd in ops.vmm_mapping(arena).export_fds():
                         os.close(fd)
-                elif mode in ("map", "map_rev"):
+                elif mode in ("map", "map_rev", "map_fresh"):
+                    # (mapped while fresh, as the swarm pull and the bench do)
+                    os.environ["ZEST_VMM_FRESH_FDS"] = "1" if mode == "map_fresh" else "0"
                     mapped = map_peer_arenas(arena, rank, world)
-                    assert mapped is not None, "mapping failed"
+                mapped_ok = mapped is not None or mode in ("alloc", "export")
+                arena.fill_(rank + 1)
+                reads_ok = None
+                if mapped is not None:  # the peer's bytes read back through the mapping
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                    peer = mapped.peers[1 - rank]
+                    reads_ok = int(peer[:16].cpu()[0]) == 2 - rank
+                    del peer
+                torch.cuda.synchronize()
                 dist.barrier()
                 m_free = _free(torch, dev)
                 fds_mapped = _fds()
@@ -104,7 +115,8 @@ def worker(rank, world, port, gb, iters, modes, q):
                 dist.barrier()
                 f = _settle(torch, dev)
                 own, imp = H.vmm_live()
-                rec["steps"].append({"iter": it, "after_alloc_GB": round(a_free, 2), "after_map_GB": round(m_free, 2),
+                rec["steps"].append({"iter": it, "mapped": mapped_ok, "reads_ok": reads_ok,
+                                     "after_alloc_GB": round(a_free, 2), "after_map_GB": round(m_free, 2),
                                      "after_release_GB": round(f, 2), "leaked_GB": round(base - f, 2),
                                      "fds_mapped": fds_mapped, "fds_after": _fds(),
                                      "vmm_live_own": own, "vmm_live_imported": imp})
@@ -120,7 +132,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=4.0)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--modes", default="alloc,export,map,map_rev")
+    ap.add_argument("--modes", default="alloc,export,map,map_rev,map_fresh")
     a = ap.parse_args()
     import socket
 
@@ -138,8 +150,8 @@ def main():
     for p in ps:
         p.join(timeout=60)
     worst = max((s["leaked_GB"] for r in res for rec in r for s in rec["steps"]), default=0.0)
-    print(json.dumps({"summary": {rec["mode"]: [s["leaked_GB"] for s in rec["steps"]] for r in res for rec in r
-                                  if rec["rank"] == 0}, "worst_leak_GB": worst}), flush=True)
+    print(json.dumps({"summary": {rec["mode"]: [(s["leaked_GB"], s["mapped"], s["reads_ok"]) for s in rec["steps"]]
+                                  for r in res for rec in r if rec["rank"] == 0}, "worst_leak_GB": worst}), flush=True)
 
 
 if __name__ == "__main__":

@@ -189,6 +189,27 @@ def _vmm_check(t, numel: int, token: str, p: int) -> bool:
     return torch.equal(got, _vmm_sentinel(token, p))
 
 
+_FD_FLOOR = [4096]
+
+
+def _fresh_fds(fds: list[int]) -> list[int]:
+    """Move received fds to numbers this process never used before (F_DUPFD above a rising floor),
+    closing the originals: an import must not be told a dmabuf by a recycled fd number
+    (ZEST_VMM_FRESH_FDS=1; tools/vmm_leak_probe.py)."""
+    import fcntl
+    out = []
+    for fd in fds:
+        try:
+            nfd = fcntl.fcntl(fd, fcntl.F_DUPFD_CLOEXEC, _FD_FLOOR[0])
+        except OSError:
+            out.append(fd)
+            continue
+        _FD_FLOOR[0] = nfd + 1
+        os.close(fd)
+        out.append(nfd)
+    return out
+
+
 def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadline_s) -> bool:
     """VMM half of :func:`map_peer_arenas`: serve this rank's chunk fds, import every peer's.
 
@@ -264,6 +285,8 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
                             raise RuntimeError(f"rank {p} closed the fd stream early")
                         fds += got
                     dbg(f"received {len(fds)} fds from rank {p}; importing")
+                    if os.environ.get("ZEST_VMM_FRESH_FDS", "0") == "1":
+                        fds = _fresh_fds(fds)
                     try:
                         if vmm_fault() == "import":
                             raise RuntimeError("injected import failure (ZEST_VMM_FAULT=import)")

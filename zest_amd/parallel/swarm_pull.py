@@ -339,6 +339,7 @@ class _Membership:
             self.data = dist.new_group(ranks=self.granks, backend=backend, use_local_synchronization=group is not None)
             self._own_data = True
         self.epoch = 0
+        self.pulls = 0  # pulls made with this membership (a kept one serves several; store keys per pull)
         self.store = None
         self._stop = threading.Event()
         self._hb = None
@@ -602,7 +603,15 @@ class _Swarm:
         self.cuda = self.device.type == "cuda"
         self.backend = backend
         t_m = time.perf_counter()
-        self.m = _Membership(group, backend, self.device)
+        # reuse_pipeline pulls also keep their membership (control group, data group, store clients,
+        # heartbeat) for the next pull over the same group, unless a rank was lost under it
+        self.member_key = (tuple(dist.get_process_group_ranks(group)) if group is not None
+                           else tuple(range(dist.get_world_size())), backend, str(self.device))
+        kept_m = _MEMBERS.pop(self.member_key, None) if reuse else None
+        self.m = kept_m if kept_m is not None and kept_m.epoch == 0 else _Membership(group, backend, self.device)
+        if kept_m is not None and kept_m is not self.m:
+            kept_m.close()
+        self.m.pulls += 1
         self._mark("membership_s", t_m)
         self.verify = verify_received
         self.round_bytes = int(round_bytes)
@@ -689,7 +698,7 @@ class _Swarm:
         m = self.m
         if not m.enabled:
             return self._bcast_from0(obj)
-        key = f"{m.prefix}/e{m.epoch}/plan"
+        key = f"{m.prefix}/e{m.epoch}/p{m.pulls}/plan"
         if m.rank == 0:
             m.store.set(key, json.dumps(obj))
             return obj
@@ -835,9 +844,25 @@ class _Swarm:
 
     def _alloc_tables(self, P):
         nck = max(1, P.n_chunks)
+        if self.cuda and os.environ.get("ZEST_SWARM_FAULT_SLOWZERO"):
+            # fault injection (tests): the current stream is busy for a while, so the zero-fill below
+            # runs late -- a pipeline not ordered after it would write chunk hashes that get zeroed
+            torch.cuda._sleep(int(os.environ["ZEST_SWARM_FAULT_SLOWZERO"]))
         self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
         self.lens = np.zeros(nck, dtype=np.uint32)   # every chunk's size, filled as rounds are agreed
+        if self.cuda:
+            # The fetch pipelines write these tables (and the arena) from streams of their own
+            # (DeviceXetPull's compute stream), which are not ordered after torch's current stream:
+            # the zero-fill must have run before the first ingest kernel, or it wipes the chunk hashes
+            # that kernel wrote and the file fails its Merkle check -> a ~2.5 s CDN repair.  That race
+            # was round 5's unexplained 2.4-3.4 s stall: it showed whenever the device ran the two
+            # streams concurrently (other staging sizes, other rank counts; at will with 16 hardware
+            # queues per process, profiles/r6/), and tests/test_gpu_device.py pins it with a delayed
+            # zero-fill (ZEST_SWARM_FAULT_SLOWZERO; ZEST_SWARM_UNORDERED_TABLES=1 brings the race back for
+            # that test's negative control).
+            if os.environ.get("ZEST_SWARM_UNORDERED_TABLES") != "1":
+                torch.cuda.current_stream(self.device).synchronize()
 
     def shard(self):
         """Per-rank queues of items (term ranges), identical on every rank."""
@@ -1583,10 +1608,18 @@ def adopt_arena(arena: torch.Tensor, mapped=None, group=None) -> None:
     _ARENAS[(dev, world, granks, mapped is not None)] = (arena, mapped, _storage_refs(arena))
 
 
+# Memberships kept by reuse_pipeline pulls (control / data groups, heartbeat), keyed by the group's
+# ranks, backend and device.
+_MEMBERS: dict = {}
+
+
 def release_pipelines() -> None:
     """Drop the pipelines kept by reuse_pipeline=True pulls (their pinned staging is freed) and the
     arenas kept by reuse_arena=True pulls."""
     _PIPELINES.clear()
+    for m in _MEMBERS.values():
+        m.close()
+    _MEMBERS.clear()
     _ARENAS.clear()
 
 
@@ -1685,6 +1718,7 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
         sw._mark("pull_s", t_pull)
         round_mode = sw.xchg.mode
         bad = sw.verify_files()
+        sw.stats["first_verify_bad_files"] = len(bad)
         for _ in range(2):
             if not bad:
                 break
@@ -1749,6 +1783,9 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
                 if ok:
                     raise
             f.join()
-        sw.m.close()
+        if ok and sw.reuse and sw.m.epoch == 0:
+            _MEMBERS[sw.member_key] = sw.m
+        else:
+            sw.m.close()
         if ok and sw.reuse:
             _PIPELINES[sw.reuse_key] = sw.fetchers
