@@ -408,7 +408,10 @@ extern "C" {
 size_t zg_hash_scratch_bytes(int n, uint64_t total_bytes) {
   if (n <= 0) return 0;
   const uint64_t cap = total_bytes / 1024 + uint64_t(n) + 64;
-  return size_t(cv_offset(n, cap) + 32 * cap);
+  const size_t hash = size_t(cv_offset(n, cap) + 32 * cap);
+  // the same buffer serves an ingest launch's BG4 decode staging first (zg_ingest_chunks)
+  const size_t stage = zg_lz4_stage_bytes(n);
+  return hash > stage ? hash : stage;
 }
 
 hipError_t zg_hash_chunks_flat(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,

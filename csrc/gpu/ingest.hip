@@ -918,7 +918,10 @@ hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, ui
   uint64_t* sz = sizes ? sizes + hash_index_base : nullptr;
   int hashed = 0;  // the decoder hashed the compressed chunks itself (zg_lz4_decode_ingest)
   if (has_compressed) {
-    const hipError_t e = zg_lz4_decode_ingest(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, &hashed, stream);
+    // the hash scratch doubles as the BG4 staging of the decoder (which finishes before the place/hash
+    // pass below uses it: one stream); zg_hash_scratch_bytes sizes it for both
+    const hipError_t e = zg_lz4_decode_ingest(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, &hashed, scratch,
+                                              scratch_bytes, stream);
     if (e != hipSuccess) return e;
   }
   if (hashed)

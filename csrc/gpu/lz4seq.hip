@@ -557,6 +557,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 }
 
+// BG4 staging.  Decoding a BG4 chunk straight into its interleaved place writes
+// every output line in four passes a quarter-chunk apart (group g's byte p lands at 4 p + g), so each
+// 128 B line reached HBM up to four times: 1105 MB of writes for 268 MB of output on 256 MiB of bf16
+// (profiles/r5/pmc_table_gpubench256_merkle_stride33_r5i.md).  With a staging slice (one per block,
+// kMaxChunk bytes) the consumer decodes the grouped stream there -- contiguous stores, far matches
+// read back contiguously, the slice reused chunk after chunk so it stays in L2 / MALL -- and then
+// writes the chunk's final bytes once, whole lines at a time: lane i of each step gathers bytes
+// 4i .. 4i + 3 of the four groups (one dword each when the group start allows, else bytes) and
+// stores the 16 interleaved output bytes.  The fused hash then reads the final bytes from L2.
+__device__ __forceinline__ uint32_t load4(const uint8_t* p, bool aligned) {
+  if (aligned) return *reinterpret_cast<const uint32_t*>(p);
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+
+__device__ void ungroup_bg4(const uint8_t* __restrict__ st, uint8_t* __restrict__ out, uint32_t ulen, uint32_t g1,
+                            uint32_t g2, uint32_t g3, uint32_t lane) {
+  const uint32_t q = ulen >> 2, r = ulen & 3;
+  const bool a1 = (g1 & 3) == 0, a2 = (g2 & 3) == 0, a3 = (g3 & 3) == 0;  // group starts (slice is aligned)
+  const bool oal = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const uint32_t q4 = q & ~3u;  // whole 4-index steps
+  for (uint32_t p0 = 4 * lane; p0 < q4; p0 += 4 * kWave) {
+    const uint32_t a = *reinterpret_cast<const uint32_t*>(st + p0);
+    const uint32_t b = load4(st + g1 + p0, a1), c = load4(st + g2 + p0, a2), d = load4(st + g3 + p0, a3);
+    const uint32_t d0 = (a & 0xFFu) | (b & 0xFFu) << 8 | (c & 0xFFu) << 16 | (d & 0xFFu) << 24;
+    const uint32_t d1 = (a >> 8 & 0xFFu) | (b & 0xFF00u) | (c & 0xFF00u) << 8 | (d & 0xFF00u) << 16;
+    const uint32_t d2 = (a >> 16 & 0xFFu) | (b >> 8 & 0xFF00u) | (c & 0xFF0000u) | (d & 0xFF0000u) << 8;
+    const uint32_t d3 = (a >> 24) | (b >> 16 & 0xFF00u) | (c >> 8 & 0xFF0000u) | (d & 0xFF000000u);
+    uint8_t* o = out + 4 * p0;
+    if (oal) {
+      *reinterpret_cast<uint4*>(o) = make_uint4(d0, d1, d2, d3);
+    } else {
+      const uint32_t w[4] = {d0, d1, d2, d3};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
+    }
+  }
+  // the last q - q4 indices of every group, then the r leftover bytes (groups 0 .. r-1 hold one more)
+  const uint32_t tail = 4 * (q - q4) + r;
+  if (lane < tail) {
+    const uint32_t pos = 4 * q4 + lane;  // output position
+    const uint32_t g = pos & 3, p = pos >> 2;
+    const uint32_t gs = g == 0 ? 0u : g == 1 ? g1 : g == 2 ? g2 : g3;
+    out[pos] = st[gs + p];
+  }
+}
+
 // -----------------------------------------------------------------------------------------------
 // Producer/consumer pairs (k_lz4_pair): two waves per chunk.  The one-wave decoder alternates its
 // scalar parse of 64 sequences with their lane-parallel execution, so a chunk's latency is the SUM of
@@ -621,7 +667,8 @@ template <bool kHash>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   const ZgChunk* __restrict__ chunks, int n_chunks,
                                                   unsigned long long* err, uint64_t src_n, uint64_t dst_n,
-                                                  uint8_t* __restrict__ hashes, uint64_t* __restrict__ sizes) {
+                                                  uint8_t* __restrict__ hashes, uint64_t* __restrict__ sizes,
+                                                  uint8_t* __restrict__ stage) {
   __shared__ PairLds L;
   const uint32_t lane = lane_id();
   const bool producer = uni(threadIdx.x >> 6) == 0;
@@ -666,6 +713,13 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     X.obase = 0;
     X.heads = L.heads;
     X.ring = L.ring;
+    // BG4 with a staging slice: decode the grouped stream contiguously into it (see ungroup_bg4)
+    uint8_t* const final_out = X.out;
+    const bool staged = stage != nullptr && X.bg4;
+    if (staged) {
+      X.out = stage + size_t(blockIdx.x) * kMaxChunk;
+      X.bg4 = false;
+    }
     const uint32_t cmark = uint32_t(c) + 1u;
     if (producer) {
       bool alive = true;
@@ -722,6 +776,19 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
           lds_release(&L.abort, cmark, lane);
         }
+      }
+      if (staged) {
+        if (whole) {
+          // the staged stream is complete in L2 (this wave's stores acknowledged, L1 dropped): write
+          // the chunk's final bytes once
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          ungroup_bg4(X.out, final_out, X.ulen, X.g1, X.g2, X.g3, lane);
+        }
+        X.out = final_out;
+        // the next chunk of this block decodes into the same slice: every lane's reads of it done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
       }
       if (kHash) {
         if (whole) {
@@ -959,18 +1026,41 @@ extern "C" hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t sr
   return hipGetLastError();
 }
 
+constexpr int kPairGrid = 4096;  // 4096 pairs = 8 waves / SIMD
+
+// Staging bytes for BG4 chunks of a pair launch over n chunks (one kMaxChunk slice per block).
+extern "C" size_t zg_lz4_stage_bytes(int n_chunks) {
+  if (n_chunks <= 0) return 0;
+  return size_t(n_chunks < kPairGrid ? n_chunks : kPairGrid) * kMaxChunk;
+}
+
+static bool stage_enabled() {
+  const char* v = getenv("ZG_BG4_STAGE");  // read per launch: tests A/B both paths in one process
+  return !(v && atoi(v) == 0);
+}
+
+extern "C" hipError_t zg_lz4_pair_decode_hash_staged(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                                     const ZgChunk* chunks, int n_chunks, unsigned long long* err,
+                                                     int grid_cap, uint8_t* hashes, uint64_t* sizes, uint8_t* stage,
+                                                     size_t stage_bytes, hipStream_t stream) {
+  if (n_chunks <= 0) return hipSuccess;
+  if (grid_cap <= 0 || grid_cap > 8192) grid_cap = kPairGrid;
+  const int grid = n_chunks < grid_cap ? n_chunks : grid_cap;
+  if (!stage_enabled() || !stage || stage_bytes < size_t(grid) * kMaxChunk) stage = nullptr;
+  if (hashes)
+    hipLaunchKernelGGL(k_lz4_pair<true>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
+                       src_n, dst_n, hashes, sizes, stage);
+  else
+    hipLaunchKernelGGL(k_lz4_pair<false>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
+                       src_n, dst_n, hashes, sizes, stage);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t zg_lz4_pair_decode_hash(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                               const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
                                               uint8_t* hashes, uint64_t* sizes, hipStream_t stream) {
-  if (n_chunks <= 0) return hipSuccess;
-  if (grid_cap <= 0 || grid_cap > 8192) grid_cap = 4096;  // 4096 pairs = 8 waves / SIMD
-  if (hashes)
-    hipLaunchKernelGGL(k_lz4_pair<true>, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream,
-                       src, dst, chunks, n_chunks, err, src_n, dst_n, hashes, sizes);
-  else
-    hipLaunchKernelGGL(k_lz4_pair<false>, dim3(n_chunks < grid_cap ? n_chunks : grid_cap), dim3(2 * kWave), 0, stream,
-                       src, dst, chunks, n_chunks, err, src_n, dst_n, hashes, sizes);
-  return hipGetLastError();
+  return zg_lz4_pair_decode_hash_staged(src, src_n, dst, dst_n, chunks, n_chunks, err, grid_cap, hashes, sizes,
+                                        nullptr, 0, stream);
 }
 
 extern "C" hipError_t zg_lz4_pair_decode(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
@@ -1010,14 +1100,16 @@ extern "C" hipError_t zg_lz4_batched_decode(const uint8_t* src, uint64_t src_n, 
 // 1, so the following place/hash pass skips compressed chunks; else *hashed = 0.
 extern "C" hipError_t zg_lz4_decode_ingest(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                            const ZgChunk* chunks, int n_chunks, unsigned long long* err,
-                                           uint8_t* hashes, uint64_t* sizes, int* hashed, hipStream_t stream) {
+                                           uint8_t* hashes, uint64_t* sizes, int* hashed, uint8_t* stage,
+                                           size_t stage_bytes, hipStream_t stream) {
   const char* v = getenv("ZG_FUSED_HASH");  // read per launch: tests A/B both paths in one process
   const char* p = getenv("ZG_LZ4_PAIR");
   const bool fuse = !(v && atoi(v) == 0) && !(p && std::string(p) != "1");
   *hashed = 0;
   if (!fuse || !hashes) return zg_lz4_batched_decode(src, src_n, dst, dst_n, chunks, n_chunks, err, stream);
   *hashed = 1;
-  return zg_lz4_pair_decode_hash(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, hashes, sizes, stream);
+  return zg_lz4_pair_decode_hash_staged(src, src_n, dst, dst_n, chunks, n_chunks, err, 0, hashes, sizes, stage,
+                                        stage_bytes, stream);
 }
 
 extern "C" size_t zg_lz4_rec_scratch_bytes(int n_chunks, uint64_t src_n) {

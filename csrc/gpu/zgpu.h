@@ -115,9 +115,16 @@ hipError_t zg_hash_ranges_flat(const uint8_t* buf, const uint64_t* offsets, cons
 hipError_t zg_lz4_pair_decode_hash(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                    const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
                                    uint8_t* hashes, uint64_t* sizes, hipStream_t stream);
+// `stage` (>= zg_lz4_stage_bytes(n) of device memory, or null): BG4 chunks decode their grouped
+// stream there and are written to dst once, whole lines at a time (ZG_BG4_STAGE=0 turns it off).
 hipError_t zg_lz4_decode_ingest(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks,
                                 int n_chunks, unsigned long long* err, uint8_t* hashes, uint64_t* sizes, int* hashed,
-                                hipStream_t stream);
+                                uint8_t* stage, size_t stage_bytes, hipStream_t stream);
+size_t zg_lz4_stage_bytes(int n_chunks);
+hipError_t zg_lz4_pair_decode_hash_staged(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
+                                          const ZgChunk* chunks, int n_chunks, unsigned long long* err, int grid_cap,
+                                          uint8_t* hashes, uint64_t* sizes, uint8_t* stage, size_t stage_bytes,
+                                          hipStream_t stream);
 hipError_t zg_place_hash_flat_raw(const uint8_t* src, uint64_t src_n, uint8_t* dst, uint64_t dst_n,
                                   const ZgChunk* chunks, int n_chunks, unsigned long long* err, uint8_t* hashes,
                                   uint64_t* sizes, uint8_t* scratch, size_t scratch_bytes, hipStream_t stream);

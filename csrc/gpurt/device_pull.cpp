@@ -606,9 +606,12 @@ struct DeviceXetPull::Impl {
         bt.begin = next;
         uint64_t pos = 0;
         size_t end = next;
+        // the pass's first batch is small (ZEST_FIRST_BATCH_MB, 128): nothing overlaps its fetch, so
+        // the copy engine starts after ~128 MiB has arrived instead of a whole slot
+        const uint64_t cap_b = batches.empty() ? first_batch_cap() : cap_;
         while (end < n) {
           const uint64_t bound = term_bound(gt[end].ulen, gt[end].nchunks);
-          if (pos + bound > cap_ && end > next) break;
+          if (pos + bound > cap_b && end > next) break;
           bt.off.push_back(pos);
           pos += bound;
           batch_of[end++] = uint32_t(batches.size());
@@ -1067,15 +1070,21 @@ struct DeviceXetPull::Impl {
       grow_staging(max_bound);
     }
     std::vector<SBatch> bs;
+    bool first_of_pass;
+    {
+      std::lock_guard<std::mutex> g(smu_);
+      first_of_pass = sbatch_total_ == sb0_;  // nothing submitted since the last reset
+    }
     for (size_t next = 0; next < n;) {
       SBatch bt;
       bt.item = &it;
       bt.begin = next;
       uint64_t pos = 0;
       size_t end = next;
+      const uint64_t cap_b = first_of_pass && bs.empty() ? first_batch_cap() : cap_;
       while (end < n) {
         const uint64_t bound = term_bound(it.gt[end].ulen, it.gt[end].nchunks);
-        if (pos + bound > cap_ && end > next) break;
+        if (pos + bound > cap_b && end > next) break;
         bt.off.push_back(pos);
         pos += bound;
         ++end;
@@ -1461,6 +1470,11 @@ struct DeviceXetPull::Impl {
   std::string timeline_json() {
     std::lock_guard<std::mutex> g(timeline_mu_);
     return timeline_.empty() ? "{}" : timeline_;
+  }
+
+  uint64_t first_batch_cap() const {
+    static const uint64_t mb = env_size("ZEST_FIRST_BATCH_MB", 128);
+    return mb ? std::min<uint64_t>(cap_, mb << 20) : cap_;
   }
 
   // Upper bound of a term's fetched bytes: Xet stores a chunk uncompressed when compression does

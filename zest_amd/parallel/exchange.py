@@ -342,6 +342,104 @@ def _import_vmm_peers(arena, vm, objs, rank, n_ranks, host_group, peers, deadlin
     return ok
 
 
+def open_signal_page(group, rank: int, n_slots: int, device):
+    """Collective over `group` (gloo): one shared page of `n_slots` 32-bit counters that every rank
+    maps and registers with HIP (csrc/bind/hip_signals.cpp), or None on every rank unless every rank
+    mapped it and its device can wait on a value (hipStreamWaitValue32)."""
+    import uuid
+
+    import torch.distributed as dist
+    H = ops.hip()
+    dev = device.index or 0
+
+    def agree(v: int) -> int:
+        t = torch.tensor([v], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return int(t.item())
+    try:
+        ok = int(bool(H.can_stream_wait_value(dev)))
+    except Exception:  # noqa: BLE001
+        ok = 0
+    box = [f"/dev/shm/zest-sig-{uuid.uuid4().hex}" if rank == 0 else None]
+    dist.broadcast_object_list(box, src=dist.get_process_group_ranks(group)[0], group=group)
+    path = box[0]
+    sig = None
+    if rank == 0 and ok:
+        try:
+            sig = H.signals_open(path, n_slots, True, dev)
+        except Exception:  # noqa: BLE001
+            ok = 0
+    ok = agree(ok)  # the page exists (or nobody opens it)
+    if ok and rank != 0:
+        try:
+            sig = H.signals_open(path, n_slots, False, dev)
+        except Exception:  # noqa: BLE001
+            sig, ok = None, 0
+    ok = agree(ok)  # everyone mapped it: the name is no longer needed
+    if rank == 0:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    return sig if ok else None
+
+
+# ----------------------------------------------------------------------------------------------
+# Peer windows: fixed exchange buffers mapped once per process
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class PeerWindows:
+    """Every rank's exchange window -- `slots` slots of `slot_bytes` (+ 256 alignment bytes) of HIP
+    VMM memory -- mapped into every rank of the group ONCE per process (tools/vmm_oneway_probe.py: the
+    HIP runtime keeps a released VMM import alive until the importing process exits, and a re-import
+    after a release read the old allocation's bytes, profiles/r6/vmm_release_r6h_r6i/).  The public
+    pull's arenas are then ordinary allocations, freed with the caller's tensors, and nothing is
+    imported per pull.  ``signals``: 2n counters -- ready[r] (slot r) and read[r] (slot n + r), both
+    equal to the window rounds rank r has published / finished reading; ``sent``: this rank's count."""
+    window: "torch.Tensor"
+    mapped: PeerArenas
+    slots: int
+    slot_bytes: int
+    stride: int
+    signals: object = None
+    sent: int = 0
+
+
+_WINDOWS: dict = {}
+
+
+def window_key(device, group, n_ranks: int) -> tuple:
+    import torch.distributed as dist
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(n_ranks))
+    return (device.index, ranks)
+
+
+def peer_windows(device, rank: int, n_ranks: int, group, slot_bytes: int, slots: int):
+    """Collective: the group's PeerWindows, created and mapped now -- once per process and group
+    (the caller agreed beforehand that some rank lacks usable windows) -- or None when the mapping or
+    the counter page cannot be had (the caller then uses an RCCL exchange)."""
+    key = window_key(device, group, n_ranks)
+    stride = (int(slot_bytes) + 256 + 4095) // 4096 * 4096
+    try:
+        win = ops.vmm_empty(slots * stride, device)
+    except Exception:  # noqa: BLE001
+        win = None
+    import torch.distributed as dist
+    ok = torch.tensor([int(win is not None)], dtype=torch.int64, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if not int(ok.item()):
+        return None
+    mapped = map_peer_arenas(win, rank, n_ranks, group)
+    if mapped is None:
+        return None
+    sig = open_signal_page(mapped.host_group, rank, 2 * n_ranks, device)
+    if sig is None:
+        return None
+    pw = PeerWindows(win, mapped, int(slots), int(slot_bytes), stride, sig, 0)
+    _WINDOWS[key] = pw  # kept for the process: releasing an import would not return its memory
+    return pw
+
+
 # ----------------------------------------------------------------------------------------------
 # The exchange
 # ----------------------------------------------------------------------------------------------
@@ -376,6 +474,7 @@ class RoundExchange:
         self._signals = None          # shared ready counters (enable_signals)
         self._sig_sent = 0            # signal_ready calls so far (= this rank's counter value)
         self._pa = None               # the PeerArenas of enable_ipc
+        self._win = None              # PeerWindows of enable_window (peer-mapped modes through windows)
 
     # -- helpers ------------------------------------------------------------------------------
     def backend(self) -> str:
@@ -411,6 +510,82 @@ class RoundExchange:
         self._ipc_streams = [role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
         return True
 
+    def enable_window(self, pw: "PeerWindows", resync: int | None = None) -> bool:
+        """Peer-mapped exchanges (``ipc`` / ``xgmi``) through the group's PeerWindows instead of
+        mapped arenas: per window round the owner copies its region piece into its window slot and
+        publishes it (ready counter), the readers copy it out of the owner's window into their own
+        arenas and report it read (read counter), which frees the slot for the owner `slots` rounds
+        later -- every wait on the GPU.  `resync` (the highest window-round count any rank reached,
+        agreed by the caller): every rank's counters continue from there."""
+        if not self.is_cuda or self.n_ranks == 1 or pw is None or pw.signals is None:
+            return False
+        if resync is not None and int(resync) != pw.sent:
+            pw.signals.store(self.rank, int(resync))
+            pw.signals.store(self.n_ranks + self.rank, int(resync))
+            pw.sent = int(resync)
+        self._win = pw
+        self._host_group = pw.mapped.host_group
+        self._peer_arenas = pw.mapped.peers  # (marks the exchange peer-mapped: autotune times ipc / xgmi)
+        self._ipc_streams = [role_stream(self.device, f"ipc{i}") for i in range(min(self.n_ranks - 1, 4))]
+        self._signal_stream = role_stream(self.device, "signal")
+        return True
+
+    def _exchange_window(self, regions, kernel: bool, event=None) -> list:
+        pw, H = self._win, ops.hip()
+        sig, n, me = pw.signals, self.n_ranks, self.rank
+        ss = self._signal_stream
+        ss.wait_stream(torch.cuda.current_stream(self.device))
+        if event:
+            H.stream_wait_event(ss.cuda_stream, int(event))  # the owner's region is written
+        size = max((hi - lo for lo, hi in regions), default=0)
+        pieces = max(1, -(-size // pw.slot_bytes))
+
+        def piece(r, j):
+            lo, hi = regions[r]
+            a = lo + j * pw.slot_bytes
+            return (a, min(hi, a + pw.slot_bytes)) if a < hi else (0, 0)
+        wbase, abase = pw.window.data_ptr(), self.arena.data_ptr()
+        streams = self._ipc_streams[:1] if kernel else self._ipc_streams
+        fin = streams[0]
+        for j in range(pieces):
+            k = pw.sent  # window round: the same sequence on every rank
+            pw.sent += 1
+            slot = k % pw.slots
+            if k >= pw.slots:  # every reader finished the slot's previous round
+                for r in range(n):
+                    if r != me:
+                        sig.wait_on(n + r, k - pw.slots + 1, ss.cuda_stream)
+            a, b = piece(me, j)
+            if b > a:
+                H.memcpy_async(wbase + slot * pw.stride + (a & 255), abase + a, b - a, ss.cuda_stream)
+            sig.set_after(me, k + 1, ss.cuda_stream)
+            segs = []
+            for p in range(n):
+                pa_, pb = piece(p, j) if p != me else (0, 0)
+                if pb > pa_:
+                    segs.append((p, self._peer_arenas[p].data_ptr() + slot * pw.stride + (pa_ & 255), abase + pa_,
+                                 pb - pa_))
+            used = []
+            if kernel:
+                for p, _, _, _ in segs:
+                    sig.wait_on(p, k + 1, fin.cuda_stream)
+                for i in range(0, len(segs), 16):
+                    part = segs[i:i + 16]
+                    H.peer_gather([x[1] for x in part], [x[2] for x in part], [x[3] for x in part], fin.cuda_stream)
+            else:
+                for i, (p, src, dst, nb) in enumerate(segs):
+                    st = streams[i % len(streams)]
+                    sig.wait_on(p, k + 1, st.cuda_stream)
+                    H.memcpy_async(dst, src, nb, st.cuda_stream)
+                    if st is not fin and st not in used:
+                        used.append(st)
+                for st in used:
+                    fin.wait_stream(st)
+            if segs:
+                self._inject_gather_fault([(sg[0], sg[2] - abase, sg[2] - abase + sg[3]) for sg in segs], fin)
+            sig.set_after(n + me, k + 1, fin.cuda_stream)  # this rank has read window round k
+        return [StreamJoin(fin)]
+
     # -- device-side readiness (csrc/bind/hip_signals.cpp) ------------------------------------
     @property
     def signaled(self) -> bool:
@@ -421,8 +596,6 @@ class RoundExchange:
         peer-mapped exchanges wait on the GPU (hipStreamWaitValue32 on the owner's counter) instead
         of a host event synchronize + host barrier per round.  Off with ZEST_IPC_SIGNALS=0; False
         (and nothing changes) unless every rank mapped the page and its device can wait on a value."""
-        import uuid
-
         import torch.distributed as dist
         if self._peer_arenas is None or self._host_group is None:
             return False
@@ -461,32 +634,8 @@ class RoundExchange:
             self._signals, self._sig_sent = pa.signals, top
             self._signal_stream = role_stream(self.device, "signal")
             return True
-        try:
-            ok = int(bool(H.can_stream_wait_value(dev)))
-        except Exception:  # noqa: BLE001
-            ok = 0
-        box = [f"/dev/shm/zest-sig-{uuid.uuid4().hex}" if self.rank == 0 else None]
-        dist.broadcast_object_list(box, src=dist.get_process_group_ranks(g)[0], group=g)
-        path = box[0]
-        sig = None
-        if self.rank == 0 and ok:
-            try:
-                sig = H.signals_open(path, self.n_ranks, True, dev)
-            except Exception:  # noqa: BLE001
-                ok = 0
-        ok = agree(ok)  # the page exists (or nobody opens it)
-        if ok and self.rank != 0:
-            try:
-                sig = H.signals_open(path, self.n_ranks, False, dev)
-            except Exception:  # noqa: BLE001
-                sig, ok = None, 0
-        ok = agree(ok)  # everyone mapped it: the name is no longer needed
-        if self.rank == 0:
-            try:
-                os.unlink(path)
-            except OSError:
-                pass
-        if not ok:
+        sig = open_signal_page(g, self.rank, self.n_ranks, self.device)
+        if sig is None:
             return False
         self._signals = sig
         self._sig_sent = 0
@@ -500,6 +649,9 @@ class RoundExchange:
         rank's counter would never advance -- and stop using the page (the mapping forgets it: its
         sequence is broken).  Copies already queued read whatever the dead owner left; the caller
         re-sends or re-fetches those ranges."""
+        if self._win is not None and self._win.signals is not None:
+            self._win.signals.release()
+            self._win.signals = None  # (the windows stay mapped; the next pull opens a fresh page)
         sig = self._signals
         if sig is None:
             return
@@ -543,6 +695,10 @@ class RoundExchange:
             return self.exchange(regions, mode)
         H = ops.hip()
         cur = torch.cuda.current_stream(self.device)
+        if mode in PEER_MAPPED_MODES and self._win is not None:
+            regions = [(int(lo), int(hi)) for lo, hi in regions]
+            self.bytes_moved += sum(hi - lo for p, (lo, hi) in enumerate(regions) if p != self.rank and hi > lo)
+            return self._exchange_window(regions, kernel=(mode == "xgmi"), event=event)
         if mode in PEER_MAPPED_MODES:
             if self._signals is not None:
                 ss = self._signal_stream
@@ -577,6 +733,8 @@ class RoundExchange:
         mode = mode or self.mode
         regions = [(int(lo), int(hi)) for lo, hi in regions]
         self.bytes_moved += sum(hi - lo for p, (lo, hi) in enumerate(regions) if p != self.rank and hi > lo)
+        if mode in PEER_MAPPED_MODES and self._win is not None:
+            return self._exchange_window(regions, kernel=(mode == "xgmi"))
         if mode in PEER_MAPPED_MODES:
             return self._exchange_ipc(regions, kernel=(mode == "xgmi"), ready=ready, synced=synced,
                                       seq=seq if self._signals is not None else None)

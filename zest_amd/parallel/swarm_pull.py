@@ -60,7 +60,8 @@ import torch.distributed as dist
 
 from .. import _core, ops
 from .. import device as zdev
-from .exchange import EXCHANGE_MODES, PEER_MAPPED_MODES, RoundExchange, map_peer_arenas, role_stream, tuned_mode
+from .exchange import (_WINDOWS, EXCHANGE_MODES, PEER_MAPPED_MODES, RoundExchange, peer_windows, role_stream,
+                       tuned_mode, window_key)
 from .split import even_bounds
 
 FILE_ALIGN = 4096
@@ -87,6 +88,13 @@ def staging_slot_bytes(staging_bytes: int, round_bytes: int, world: int) -> int:
         return int(staging_bytes)
     split = 4 if world <= 2 else 2
     return min(int(staging_bytes), max(64 << 20, int(round_bytes) // split))
+
+
+def _window_shape() -> tuple[int, int]:
+    """(slot bytes, slots) of the exchange windows: ZEST_SWARM_WINDOW_MB (256) x ZEST_SWARM_WINDOW_SLOTS
+    (4) -- a round's region larger than a slot goes through it in several window rounds."""
+    return (max(1, int(os.environ.get("ZEST_SWARM_WINDOW_MB", "256"))) << 20,
+            max(2, int(os.environ.get("ZEST_SWARM_WINDOW_SLOTS", "4"))))
 
 
 class SwarmPullError(RuntimeError):
@@ -776,23 +784,28 @@ class _Swarm:
         self._mark("possession_s", t)
 
     def _arena_local(self):
-        """This rank's side of the arena reuse decision (agreed in gather_possession)."""
+        """This rank's side of the arena-reuse and exchange-window decisions (agreed in
+        gather_possession)."""
         n = max(1, self.plan.arena_bytes)
         self._want_map = (self.cuda and self.m.world > 1 and os.environ.get("ZEST_EXCHANGE_IPC", "1") != "0"
                           and self.exchange_req in ("auto", "ipc", "xgmi"))
-        # reuse_arena None (default): peer-mapped arenas are kept and reused whenever no tensor of the
-        # previous pull is alive (a released peer-mapped arena stayed counted as used on the box,
-        # ARCHITECTURE 15.8, so a fresh one per pull would pile up); True: reuse regardless.
-        self._use_cache = self.reuse_arena is True or (self.reuse_arena is None and self._want_map)
-        self._arena_key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks), self._want_map)
+        # reuse_arena True: the arena of this process's previous pull over the same group is reused
+        # (bench.py's repeated pulls); None / False (default): a fresh ordinary allocation, freed with
+        # the caller's tensors -- the peer-mapped exchanges go through the group's exchange windows
+        # (mapped once per process), not through a peer mapping of the arena.
+        self._use_cache = self.reuse_arena is True
+        self._arena_key = (self.device.index if self.cuda else -1, self.m.world, tuple(self.m.granks))
         cached = _ARENAS.get(self._arena_key) if self._use_cache else None
         self._cached = cached
-        self._have_local = int(cached is not None and cached[0].numel() >= n
-                               and (cached[1] is not None or not self._want_map)
-                               and (self.reuse_arena is True or not _arena_in_use(cached)))
-        pa = cached[1] if cached is not None else None
-        self._sig_local = (bool(self._have_local and pa is not None and getattr(pa, "signals", None) is not None),
-                           int(getattr(pa, "sig_sent", 0) if pa is not None else 0))
+        self._have_local = int(cached is not None and cached[0].numel() >= n)
+        # exchange windows: every rank must already hold the group's windows (of the wanted shape)
+        # with a live counter page to use them without a collective; their window-round counts are
+        # agreed (max) with the same all-gather
+        pw = _WINDOWS.get(window_key(self.device, self.m.data, self.m.world)) if self._want_map else None
+        slot, slots = _window_shape()
+        self._win_local = (bool(pw is not None and pw.signals is not None and pw.slot_bytes == slot and pw.slots == slots),
+                           int(pw.sent) if pw is not None else 0)
+        self._sig_local = self._win_local  # (gathered with the possession bits)
 
     def allocate(self):
         t = time.perf_counter()
@@ -800,23 +813,24 @@ class _Swarm:
         n = max(1, P.arena_bytes)
         if not hasattr(self, "_have_all"):  # (no possession gather ran: agree on the arena here)
             self._arena_local()
-            self._have_all = int(all(self._gather(self._have_local))) if self.m.world > 1 else self._have_local
-            self._sig_agreed = (False, 0)
-        want_map = self._want_map
+            allv = self._gather((self._have_local, *self._win_local)) if self.m.world > 1 else \
+                [(self._have_local, *self._win_local)]
+            self._have_all = int(all(v[0] for v in allv))
+            self._sig_agreed = (bool(all(v[1] for v in allv)), max(int(v[2]) for v in allv))
         self.arena = None
         # (device memory free before the arena, and the arena's own allocation time: a pull after
         # another pull in the same process spent 4.5 s here, profiles/r5/bench70b_r5ai.log)
         self.alloc_info = {"free_before_GB": round(torch.cuda.mem_get_info(self.device)[0] / 1e9, 2)} if self.cuda else {}
         t_a = time.perf_counter()
-        # reuse_arena: the arena (and, peer-mapped, every peer's mapping of it) of this process's
-        # previous pull of at least this size, when every rank has one -- the caller holds no tensor
-        # of that pull any more.  A fresh 141 GB arena per pull costs the driver's reclaim of the last
-        # one (~4 s, profiles/r5/alloc_probe_141g_r5aj.log) and, peer-mapped, a new export/import.
+        # reuse_arena=True: the arena of this process's previous pull of at least this size, when
+        # every rank has one (a fresh 141 GB arena per pull costs the driver's reclaim of the last
+        # one, ~4 s, profiles/r5/alloc_probe_141g_r5aj.log)
         key, use_cache, cached = self._arena_key, self._use_cache, self._cached
         have = self._have_all if use_cache else 0
         self.reused_arena = bool(have)
+        self.mapped = None
         if have:
-            full, self.mapped, _ = cached
+            full = cached[0]
             self.arena = full[:n]
             self.alloc_info["reused"] = True
             self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
@@ -824,22 +838,11 @@ class _Swarm:
             self._mark("alloc_s", t)
             return
         _ARENAS.pop(key, None)  # (a smaller cached arena is dropped before the new one is made)
-        if want_map:
-            try:
-                self.arena = ops.vmm_empty(n, self.device)
-            except Exception:  # noqa: BLE001 - torch allocation, RCCL exchanges only
-                self.arena = None
-        if self.arena is None:
-            self.arena = ops.padded_empty(n, self.device) if self.cuda else torch.empty(n + ops.PAD, dtype=torch.uint8)[:n]
+        self.arena = ops.padded_empty(n, self.device) if self.cuda else torch.empty(n + ops.PAD, dtype=torch.uint8)[:n]
         self.alloc_info["arena_s"] = round(time.perf_counter() - t_a, 4)
         self._alloc_tables(P)
-        self.mapped = None
-        if want_map and self.exchange_req != "p2p":
-            t_map = time.perf_counter()
-            self.mapped = map_peer_arenas(self.arena, self.m.rank, self.m.world, self.m.data)
-            self._mark("map_s", t_map)
         if use_cache:
-            _ARENAS[key] = (self.arena, self.mapped, _storage_refs(self.arena))
+            _ARENAS[key] = (self.arena, None, _storage_refs(self.arena))
         self._mark("alloc_s", t)
 
     def _alloc_tables(self, P):
@@ -923,10 +926,19 @@ class _Swarm:
         t = time.perf_counter()
         W = self.m.world
         self.xchg = RoundExchange(self.arena, self.m.rank, W, self.m.data, "p2p")
-        if self.mapped is not None and self.xchg.enable_ipc(self.mapped) and self.streamed:
-            # streamed rounds wait for the owners on the GPU (ready counters), not in host barriers;
-            # a kept arena's page continues from the counter values agreed in gather_possession
-            self.xchg.enable_signals(agreed=self._sig_agreed if getattr(self, "reused_arena", False) else None)
+        if getattr(self, "_want_map", False) and self.m.world > 1:
+            # peer-mapped exchanges go through the group's exchange windows: mapped once per process
+            # (every rank kept usable ones: no collective, counters continue from the agreed count),
+            # else made now (collective); none -> RCCL exchanges only
+            t_w = time.perf_counter()
+            key = window_key(self.device, self.m.data, self.m.world)
+            slot, slots = _window_shape()
+            agreed = getattr(self, "_sig_agreed", (False, 0))
+            pw = _WINDOWS.get(key) if agreed[0] else peer_windows(self.device, self.m.rank, self.m.world, self.m.data,
+                                                                  slot, slots)
+            if pw is not None:
+                self.xchg.enable_window(pw, resync=agreed[1] if agreed[0] else None)
+            self._mark("windows_s", t_w)
         self.verify_stream = role_stream(self.device, "verify") if self.cuda else None
         self._hash_scratch = ops.HashScratch(self.device) if self.cuda else None
         if W == 1:
@@ -1597,15 +1609,16 @@ def _arena_in_use(entry) -> bool:
 
 
 def adopt_arena(arena: torch.Tensor, mapped=None, group=None) -> None:
-    """Seed the reuse_arena cache with an arena the caller already holds (with `mapped`, the
-    PeerArenas of it when peer-mapped): the next reuse_arena pull over `group` of at most its size
-    lands in it instead of allocating.  bench.py hands its engine's arena to the public-path row:
-    freeing 141 GB and allocating it again costs the driver's reclaim, and a freed peer-mapped arena
-    stayed counted as used in the 4-rank rehearsal (profiles/r5/rehearsal_n4_reclaim_r5ao.log)."""
+    """Seed the reuse_arena cache with an arena the caller already holds: the next reuse_arena=True
+    pull over `group` of at most its size lands in it instead of allocating.  bench.py hands its
+    engine's arena to the public-path row: freeing 141 GB and allocating it again costs the driver's
+    reclaim -- and the engine's arena is peer-imported, and an imported VMM allocation is not returned
+    before the importing process exits (profiles/r6/vmm_release_r6h_r6i/).  (`mapped`: unused; the
+    public path exchanges through its own windows.)"""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     granks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(world))
     dev = arena.device.index if arena.device.type == "cuda" else -1
-    _ARENAS[(dev, world, granks, mapped is not None)] = (arena, mapped, _storage_refs(arena))
+    _ARENAS[(dev, world, granks)] = (arena, None, _storage_refs(arena))
 
 
 # Memberships kept by reuse_pipeline pulls (control / data groups, heartbeat), keyed by the group's
@@ -1669,12 +1682,15 @@ def swarm_pull(repo: str, revision: str = "main", group=None, device=None, *, p2
     the fetch pipelines (pinned staging, Xet session) for the next pull of the same repository in
     this process; release_pipelines() frees them.  `reuse_arena`: True -- the pull lands in the
     arena kept from this process's previous pull over the same group (large enough) instead of a
-    fresh one, overwriting that pull's tensors (bench.py's repeated pulls); None (default) -- the
-    same for peer-mapped arenas (N > 1), but only when no tensor of the previous pull is still alive
-    (a fresh peer-mapped arena per pull would pile up: a released one stayed counted as used on the
-    box); False -- always a fresh arena.  Kept arenas hold their memory until the next pull or
-    release_pipelines().  `files_out`, if given, receives {path: uint8 tensor} -- every pulled
-    safetensors file's verified bytes (views of the arena), e.g. for writing a snapshot."""
+    fresh one, overwriting that pull's tensors (bench.py's repeated pulls; kept until the next pull
+    or release_pipelines()); None / False (default) -- a fresh arena, an ordinary device allocation
+    that is freed once the caller drops the returned tensors.  At N > 1 the peer-mapped exchanges
+    read the owners' exchange windows (fixed buffers of ZEST_SWARM_WINDOW_SLOTS x
+    ZEST_SWARM_WINDOW_MB per rank, mapped into the group once per process), never a peer's arena:
+    a released VMM import is not returned by the HIP runtime until the importing process exits
+    (profiles/r6/vmm_release_r6h_r6i/).  `files_out`, if given, receives {path: uint8 tensor} --
+    every pulled safetensors file's verified bytes (views of the arena), e.g. for writing a
+    snapshot."""
     if reuse_pipeline is None:
         reuse_pipeline = os.environ.get("ZEST_SWARM_REUSE", "0") == "1"
     if os.environ.get("ZEST_SWARM_STAGING_MB"):  # per-slot staging of the fetch pipelines (A/B knob)
