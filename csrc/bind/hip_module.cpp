@@ -178,6 +178,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("lo"), py::arg("hi"), py::arg("err"), py::arg("stream"), py::arg("clip_scratch") = 0);
   m.attr("CLIP_SCRATCH_BYTES") = ZG_CLIP_SCRATCH_BYTES;
   m.def("hash_scratch_bytes", [](int n, uint64_t total_bytes) { return zg_hash_scratch_bytes(n, total_bytes); });
+  m.def("ingest_scratch_bytes", [](int n, uint64_t total_bytes) { return zg_ingest_scratch_bytes(n, total_bytes); });
   m.def("hash_chunks", [](uintptr_t dst, uint64_t dst_n, uintptr_t chunks, int n, uintptr_t hashes, uintptr_t sizes,
                           uint32_t base, uintptr_t st, uintptr_t scratch, size_t scratch_bytes) {
     check(zg_hash_chunks(P<const uint8_t>(dst), dst_n, P<const ZgChunk>(chunks), n, P<uint8_t>(hashes),

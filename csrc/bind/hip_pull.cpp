@@ -164,6 +164,8 @@ void bind_hip_pull(py::module_& m) {
            py::arg("cancel") = false,
            "wait for every submitted item and forget them (between pulls); cancel: abandon the ones still "
            "fetching first")
+      .def("order_after", [](DeviceXetPull& self, uintptr_t event) { self.order_after(event); }, py::arg("event"),
+           "queue everything this pipeline does from now on behind the caller's hipEvent_t (int)")
       .def("settle", [](DeviceXetPull& self, const std::string& hex, bool ok) {
              py::gil_scoped_release nogil;
              return self.settle(hex, ok);

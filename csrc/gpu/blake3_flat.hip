@@ -408,9 +408,12 @@ extern "C" {
 size_t zg_hash_scratch_bytes(int n, uint64_t total_bytes) {
   if (n <= 0) return 0;
   const uint64_t cap = total_bytes / 1024 + uint64_t(n) + 64;
-  const size_t hash = size_t(cv_offset(n, cap) + 32 * cap);
-  // the same buffer serves an ingest launch's BG4 decode staging first (zg_ingest_chunks)
-  const size_t stage = zg_lz4_stage_bytes(n);
+  return size_t(cv_offset(n, cap) + 32 * cap);
+}
+
+size_t zg_ingest_scratch_bytes(int n, uint64_t total_bytes) {
+  // an ingest launch's scratch serves its BG4 decode staging first, then the place/hash pass
+  const size_t hash = zg_hash_scratch_bytes(n, total_bytes), stage = zg_lz4_stage_bytes(n);
   return hash > stage ? hash : stage;
 }
 

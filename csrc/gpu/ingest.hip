@@ -919,7 +919,7 @@ hipError_t zg_ingest_chunks(const uint8_t* src, uint64_t src_n, uint8_t* dst, ui
   int hashed = 0;  // the decoder hashed the compressed chunks itself (zg_lz4_decode_ingest)
   if (has_compressed) {
     // the hash scratch doubles as the BG4 staging of the decoder (which finishes before the place/hash
-    // pass below uses it: one stream); zg_hash_scratch_bytes sizes it for both
+    // pass below uses it: one stream); zg_ingest_scratch_bytes sizes it for both
     const hipError_t e = zg_lz4_decode_ingest(src, src_n, dst, dst_n, chunks, n_chunks, err, h, sz, &hashed, scratch,
                                               scratch_bytes, stream);
     if (e != hipSuccess) return e;

@@ -98,6 +98,8 @@ hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t src_n, uint8_
 // bytes) of device memory owned by the caller, one per concurrently running launch) the leaf-flat
 // pipeline of blake3_flat.hip runs; without it, one wave per message (ingest.hip).
 size_t zg_hash_scratch_bytes(int n, uint64_t total_bytes);
+// Scratch of one zg_ingest_chunks launch (hash scratch + the decoder's BG4 staging, which share it).
+size_t zg_ingest_scratch_bytes(int n, uint64_t total_bytes);
 hipError_t zg_hash_chunks(const uint8_t* dst, uint64_t dst_n, const ZgChunk* chunks, int n_chunks,
                           uint8_t* hashes, uint64_t* sizes, uint32_t hash_index_base, uint8_t* scratch,
                           size_t scratch_bytes, hipStream_t stream);

@@ -359,6 +359,13 @@ struct DeviceXetPull::Impl {
     return out;
   }
 
+  // Order everything this pipeline queues from now on after `ev` (a caller's event, e.g. the zero-fill
+  // of the tables its kernels write): only the compute stream writes caller memory.
+  void order_after(hipEvent_t ev) {
+    init_device();
+    hip_check(hipStreamWaitEvent(stream_, ev, 0), "hipStreamWaitEvent (order_after)");
+  }
+
   size_t settle(const std::string& hex, bool ok) { return sh_->book.settle(*sh_->bridge, hex, ok); }
   void flush_cache_writes() {
     if (sh_->writer) sh_->writer->flush();
@@ -790,7 +797,7 @@ struct DeviceXetPull::Impl {
           for (size_t i = bt.begin; i < bt.end; ++i) ubytes += gt[i].ulen;
           bool compressed = false;
           for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.recs()[c].scheme != 0;
-          const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
+          const size_t hs_bytes = zg_ingest_scratch_bytes(nchunks, ubytes);
           // the slot's device staging, records and scratch are read by batch b - S's kernels
           if (b >= S && (s.chunks_dev.n < size_t(nchunks ? nchunks : 1) || s.scratch.n < hs_bytes))
             hip_check(hipEventSynchronize(ev[2 * (b - S) + 1]), "hipEventSynchronize");  // growing: wait, then free
@@ -1103,7 +1110,7 @@ struct DeviceXetPull::Impl {
       uint64_t ub = 0;
       for (size_t i = bt.begin; i < bt.end; ++i) ub += it.gt[i].ulen;
       max_recs = std::max<size_t>(max_recs, size_t(bt.c_hi - bt.c_lo));
-      max_hs = std::max(max_hs, zg_hash_scratch_bytes(int(bt.c_hi - bt.c_lo), ub));
+      max_hs = std::max(max_hs, zg_ingest_scratch_bytes(int(bt.c_hi - bt.c_lo), ub));
     }
     bool grow = false;
     for (const auto& sl : slots_) grow |= sl.rec_cap < max_recs || sl.chunks_dev.n < max_recs || sl.scratch.n < max_hs;
@@ -1268,7 +1275,7 @@ struct DeviceXetPull::Impl {
           for (size_t i = bt.begin; i < bt.end; ++i) ubytes += it.gt[i].ulen;
           bool compressed = false;
           for (int c = 0; c < nchunks && !compressed; ++c) compressed = s.recs()[c].scheme != 0;
-          const size_t hs_bytes = zg_hash_scratch_bytes(nchunks, ubytes);
+          const size_t hs_bytes = zg_ingest_scratch_bytes(nchunks, ubytes);
           if (skern_set_[slot]) hip_check(hipStreamWaitEvent(copy_stream_, skern_[slot], 0), "hipStreamWaitEvent");
           if (timing_)
             for (auto& e : bt.tev) hip_check(hipEventCreate(&e), "hipEventCreate");
@@ -1581,6 +1588,7 @@ DeviceXetPull::ItemResult DeviceXetPull::wait_item(uint64_t ticket) {
 }
 unsigned long long DeviceXetPull::item_error(uint64_t ticket) { return impl_->item_error(ticket); }
 void DeviceXetPull::stream_reset(bool cancel) { impl_->s_reset(cancel); }
+void DeviceXetPull::order_after(uintptr_t event) { impl_->order_after(reinterpret_cast<hipEvent_t>(event)); }
 size_t DeviceXetPull::settle(const std::string& xet_hash, bool ok) { return impl_->settle(xet_hash, ok); }
 std::vector<TermShape> DeviceXetPull::term_shapes(const std::string& xet_hash) { return impl_->term_shapes(xet_hash); }
 std::vector<TermKey> DeviceXetPull::term_keys(const std::string& xet_hash) { return impl_->sh_->recs->keys(xet_hash); }

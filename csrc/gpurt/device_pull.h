@@ -85,6 +85,8 @@ class DeviceXetPull {
   // Wait for every submitted item (GPU included) and forget them and their events; `cancel` first
   // abandons the items still fetching (their remaining terms are skipped).
   void stream_reset(bool cancel = false);
+  // Everything this pipeline queues from now on runs after the caller's hipEvent_t `event` completed.
+  void order_after(uintptr_t event);
   size_t settle(const std::string& xet_hash, bool ok);
   std::vector<TermShape> term_shapes(const std::string& xet_hash);  // (ulen, chunks) per term
   std::vector<TermKey> term_keys(const std::string& xet_hash);      // (xorb hex, chunk range) per term

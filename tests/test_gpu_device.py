@@ -426,7 +426,7 @@ def _swarm_repeat_worker(rank, world_size, port, repo, q):
         def pull():
             st = {}
             t = swarm_pull(repo, device="cuda:0", p2p=False, dht=False, stats=st, exchange="xgmi",
-                           round_bytes=512 << 10)
+                           round_bytes=64 << 20)
             return t, st
 
         def host(t):
@@ -460,9 +460,12 @@ def _swarm_repeat_worker(rank, world_size, port, repo, q):
         f3 = free()  # t2 and t3 held
         del t2, t3
         f4 = free()
+        t4, _ = pull()
+        del t4
+        f5 = free()  # a fourth pull, dropped: nothing accumulates pull after pull
         arena = st1["total_bytes"]
         q.put((rank, got1, [st1.get("phases", {}).get("windows_s"), st2.get("phases", {}).get("windows_s")],
-               got2 == got1, kept2 == got1, got3 == got1, (f1, f2, f3, f4, arena),
+               got2 == got1, kept2 == got1, got3 == got1, (f1, f2, f3, f4, f5, arena),
                [st1["exchange"], st2["exchange"], st3["exchange"]]))
     except Exception:  # noqa: BLE001
         import traceback
@@ -476,9 +479,11 @@ def test_swarm_pull_arenas_are_freed_and_windows_mapped_once(tmp_path, monkeypat
 
     import torch.multiprocessing as mp
 
-    spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
-    world = SyntheticWorld(spec, seed=23, mode="bf16")
-    hub = FakeHub(policy="auto", max_xorb_bytes=256 << 10)
+    # a ~0.5 GB model: a per-pull leak of the size of an arena (what released peer-mapped VMM arenas
+    # did, profiles/r6/vmm_release_r6h_r6i/) stands out from allocator noise
+    spec = dataclasses.replace(models.get("gpt2"), max_shard_bytes=200_000_000)
+    world = SyntheticWorld(spec, seed=23, mode="random")
+    hub = FakeHub(policy="none", max_xorb_bytes=32 << 20)
     hub.start()
     try:
         hub.add_world(world)
@@ -497,12 +502,12 @@ def test_swarm_pull_arenas_are_freed_and_windows_mapped_once(tmp_path, monkeypat
             assert isinstance(got1, dict), got1
             assert same2 and kept2 and same3
             assert modes == ["xgmi"] * 3, modes
-            f1, f2, f3, f4, arena = mem
-            slack = 64 << 20  # allocator granularity, hash tables, a few staging buffers
+            f1, f2, f3, f4, f5, arena = mem
+            slack = 256 << 20  # allocator granularity, tables, staging of the two ranks' pipelines
             # two ranks share the GPU: "one arena" per pull is two arenas of the device
             assert f1 - f2 <= 2 * arena + slack, mem                  # one live pull: its arenas only
             assert f2 - f3 <= 2 * arena + slack, mem                  # held tensors: one more arena each
-            assert f4 >= f1 - slack, mem                              # dropped: memory comes back
+            assert f4 >= f1 - slack and f5 >= f1 - slack, mem         # dropped: memory comes back
     finally:
         hub.stop()
 
@@ -713,6 +718,7 @@ def test_swarm_load_device(tmp_path, monkeypatch, corrupt):
 
     import torch.multiprocessing as mp
     import zest_amd
+    import zest_amd.client  # noqa: F401  (submodule used below)
 
     spec = dataclasses.replace(models.get("llama-tiny"), max_shard_bytes=700_000)
     world = SyntheticWorld(spec, seed=23, mode="bf16")

@@ -243,24 +243,29 @@ def test_decoder_hash_matches_place_hash(policy, monkeypatch):
         assert (rec["scheme"] == 0).any()
     base = 5
     got = {}
-    for env in ("1", "0"):
+    # (fused hash, BG4 staging): staged decode writes the grouped stream to the scratch slice and the
+    # final bytes once (ingest scratch); unstaged scatters straight into place
+    for env, stage in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("ZG_FUSED_HASH", env)
+        monkeypatch.setenv("ZG_BG4_STAGE", stage)
         dst = ops.padded_empty(len(data), DEV)
         dst.fill_(0x3C)
         hashes = torch.full((nck + base, 32), 0x77, dtype=torch.uint8, device=DEV)
         sizes = torch.full((nck + base,), -1, dtype=torch.int64, device=DEV)
         err = torch.zeros(1, dtype=torch.int64, device=DEV)
-        sp, sb = ops.HashScratch(DEV).get(nck, len(data))
+        sp, sb = ops.HashScratch(DEV, ingest=True).get(nck, len(data))
         H.ingest_chunks(src.data_ptr(), len(body), dst.data_ptr(), len(data), ws.chunks.data_ptr(), nck, True,
                         err.data_ptr(), hashes.data_ptr(), sizes.data_ptr(), base,
                         torch.cuda.current_stream().cuda_stream, sp, sb)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
-        assert dst.cpu().numpy().tobytes() == data
-        got[env] = (hashes.cpu().numpy(), sizes.cpu().numpy())
+        assert dst.cpu().numpy().tobytes() == data, (env, stage)
+        got[env + stage] = (hashes.cpu().numpy(), sizes.cpu().numpy())
     monkeypatch.delenv("ZG_FUSED_HASH")
-    (h1, s1), (h0, s0) = got["1"], got["0"]
+    monkeypatch.delenv("ZG_BG4_STAGE")
+    (h1, s1), (h0, s0), (hu, su) = got["11"], got["01"], got["10"]
     assert np.array_equal(h1, h0) and np.array_equal(s1, s0)
+    assert np.array_equal(h1, hu) and np.array_equal(s1, su)
     assert h1[base:].tobytes() == b"".join(b.chunk_hashes())
     assert (h1[:base] == 0x77).all() and (s1[:base] == -1).all()
     assert s1[base:].tolist() == list(np.diff([0] + list(ends)))

@@ -173,12 +173,14 @@ class HashScratch:
     can share the buffer, and when it grows the caching allocator hands the old block only to later
     allocations on that same stream, i.e. after the launches already queued on it."""
 
-    def __init__(self, device):
+    def __init__(self, device, ingest: bool = False):
         self.device = torch.device(device)
         self.buf = None
+        self.ingest = ingest  # an ingest launch's scratch (also the decoder's BG4 staging)
 
     def get(self, n: int, total_bytes: int) -> tuple[int, int]:
-        need = hip().hash_scratch_bytes(int(n), int(total_bytes))
+        H = hip()
+        need = (H.ingest_scratch_bytes if self.ingest else H.hash_scratch_bytes)(int(n), int(total_bytes))
         if self.buf is None or self.buf.numel() < need:
             self.buf = torch.empty(need + (need >> 3), dtype=torch.uint8, device=self.device)
         return self.buf.data_ptr(), self.buf.numel()
@@ -233,7 +235,7 @@ class IngestWorkspace:
         self.terms_host = torch.empty(max_terms * TERM_DTYPE.itemsize, dtype=torch.uint8).pin_memory() \
             if self.device.type == "cuda" else None
         self._clip_scratch = None
-        self.hash_scratch = HashScratch(self.device) if self.device.type == "cuda" else None
+        self.hash_scratch = HashScratch(self.device, ingest=True) if self.device.type == "cuda" else None
 
     def index_scratch(self, H, n_terms: int) -> tuple[int, int]:
         """(ptr, bytes) of this workspace's parallel header-walk scratch, grown to n_terms."""

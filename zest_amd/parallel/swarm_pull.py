@@ -522,6 +522,11 @@ class _Fetcher:
             return self.impl.pull_terms(jobs, hashes.data_ptr(), sizes.data_ptr() if sizes is not None else 0, repair)
         return self.impl.fetch_terms(jobs, hashes.data_ptr(), repair)
 
+    def order_after(self, event) -> None:
+        """GPU pipelines: queue everything from now on behind `event` (a torch.cuda.Event)."""
+        if self.device.type == "cuda" and event is not None:
+            self.impl.order_after(event.cuda_event)
+
     # -- streaming submission (the streamed round loop) ----------------------------------------
     def submit(self, jobs, hashes: torch.Tensor, sizes: torch.Tensor | None):
         """Queue one item (a round's term ranges) behind the ones already submitted; returns a
@@ -854,7 +859,7 @@ class _Swarm:
         self.hashes = torch.zeros((nck, 32), dtype=torch.uint8, device=self.device)
         self.sizes = torch.zeros(nck, dtype=torch.int64, device=self.device) if self.cuda else None
         self.lens = np.zeros(nck, dtype=np.uint32)   # every chunk's size, filled as rounds are agreed
-        if self.cuda:
+        if self.cuda and os.environ.get("ZEST_SWARM_UNORDERED_TABLES") != "1":
             # The fetch pipelines write these tables (and the arena) from streams of their own
             # (DeviceXetPull's compute stream), which are not ordered after torch's current stream:
             # the zero-fill must have run before the first ingest kernel, or it wipes the chunk hashes
@@ -863,9 +868,10 @@ class _Swarm:
             # streams concurrently (other staging sizes, other rank counts; at will with 16 hardware
             # queues per process, profiles/r6/), and tests/test_gpu_device.py pins it with a delayed
             # zero-fill (ZEST_SWARM_FAULT_SLOWZERO; ZEST_SWARM_UNORDERED_TABLES=1 brings the race back for
-            # that test's negative control).
-            if os.environ.get("ZEST_SWARM_UNORDERED_TABLES") != "1":
-                torch.cuda.current_stream(self.device).synchronize()
+            # that test's negative control).  The pipelines wait for this event on the GPU (_Fetcher.
+            # order_after) -- a host synchronize here cost up to 22 ms on a GPU shared by 4 ranks.
+            self.tables_ready = torch.cuda.Event()
+            self.tables_ready.record(torch.cuda.current_stream(self.device))
 
     def shard(self):
         """Per-rank queues of items (term ranges), identical on every rank."""
@@ -1223,6 +1229,8 @@ class _Swarm:
         self.round_no = 0
         self.pending_events: list = []   # (event, items) of received rounds not yet known to be hashed
         self.unagreed: list = []
+        for f in self.fetchers:  # (the tables are zeroed before any fetch pipeline writes them)
+            f.order_after(getattr(self, "tables_ready", None))
         streamed = self.streamed
         while True:
             try:
