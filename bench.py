@@ -416,7 +416,7 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     return res
 
 
-def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
+def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> dict:
     """Time the public path on the world the engine just pulled: zest_amd.parallel.swarm_pull (what
     zest_amd.pull(repo, device="all") runs), listing + reconstructions from an in-process fake hub,
     every term's CDN fetch served from this rank's pinned origin through a mem:// memory CAS (the
@@ -443,25 +443,22 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
     cuda = device.type == "cuda"
     wd.arm("swarm_setup")
     t_setup = time.time()
-    # the engine's device buffers go first: the swarm pull allocates its own 141 GB arena.  At N > 1
-    # the peers' imports of this rank's old arena must be gone too (a peer-mapped VMM chunk lives until
-    # every importer released it): every rank drops its mappings here, before swarm_pull's first
-    # collective, and gc runs so no reference cycle keeps a mapping past it.
+    # The engine's device buffers go first (its staging and tables; the row's pipelines allocate
+    # their own).  The row's pulls land in the engine's arena: freeing 141 GB and allocating it again
+    # costs the driver's reclaim, and a peer-imported VMM arena is not returned before every importing
+    # process exits (profiles/r6/vmm_release_r6h_r6i/), so a fresh one would not fit next to it.  The
+    # arena -- and the peers' mappings of it, which the next mode's engine exchanges through -- stay in
+    # `arenas`.  The arena is poisoned first, on every rank before the barrier below, so the row's
+    # first exchange is verified against bytes no earlier pull wrote.
     free0 = torch.cuda.mem_get_info(device)[0] if cuda else 0
     puller.release_device()
-    arena, mapped = keep.pop("arena", None), keep.pop("peers", None)
-    # The row's pulls land in the engine's arena (and, peer-mapped, its peers' mappings of it):
-    # freeing 141 GB and allocating it again costs the driver's reclaim (~4 s), and in the 4-rank
-    # rehearsal a released peer-mapped arena stayed counted as used, so a fresh one did not fit next
-    # to the others (8 ranks: out of device memory).  The arena is poisoned first, on every rank
-    # before the barrier below, so the row's first exchange is verified against bytes no earlier
-    # pull wrote.
-    if arena is not None and (world_size == 1 or mapped is not None):
+    arena = (arenas or {}).get("arena")
+    if arena is not None:
         if cuda:
             arena.fill_(0xA5)
             torch.cuda.synchronize()
-        sp.adopt_arena(arena, mapped if world_size > 1 else None)
-    del arena, mapped
+        sp.adopt_arena(arena)
+    del arena
     import gc
     gc.collect()
     if cuda:
@@ -469,11 +466,9 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         torch.cuda.empty_cache()
     free1 = torch.cuda.mem_get_info(device)[0] if cuda else 0
     if dist is not None and world_size > 1:
-        # A peer-mapped arena's memory is freed only once every importer has released its mapping:
-        # wait until every rank has dropped its mappings before any rank allocates the row's arena.
-        # Without this a rank could hold its old 141 GB arena (kept alive by a slower peer's import)
-        # next to the new one; the 8-rank one-GPU rehearsal ran out of device memory exactly so
-        # (hipMalloc in a fetch pipeline, profiles/r5/rehearsal_n8_r5am.log).
+        # every rank has released the engine's device buffers before any rank allocates the row's
+        # pipelines (the 8-rank one-GPU rehearsal shares one card's memory between the ranks:
+        # profiles/r5/rehearsal_n8_r5am.log ran out of it without this barrier)
         dist.barrier()
         if cuda:
             torch.cuda.synchronize()
@@ -552,7 +547,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd) -> dict:
         times.append(time.perf_counter() - t0)
         # every timed step's phases on this rank (a slow step is then attributable to a phase and
         # a rank: VERDICT r5 weak 2); "other_s" = the call's wall time outside the named phases
-        ph = {k: v for k, v in (st.get("phases") or {}).items() if not k.startswith("plan_")}
+        ph = {k: v for k, v in (st.get("phases") or {}).items() if k == "plan_s" or not k.startswith("plan_")}
         named = sum(v for k, v in ph.items() if k in ("init_s", "plan_s", "possession_s", "alloc_s", "shard_s",
                                                        "setup_exchange_s", "pull_s", "verify_s", "repair_s",
                                                        "tensors_s"))
@@ -644,6 +639,72 @@ def _log_split_check(world, puller, world_size, sp) -> None:
                                f"swarm rank {int(owner[bad[0]])}, engine rank {int(eng[idx[bad[0]]])})" if len(bad) else ""))
     except Exception as e:  # noqa: BLE001 - diagnostics only
         log(0, f"[swarm_pull] split check failed: {type(e).__name__}: {e}")
+
+
+def _headline(a, spec, results, world_size, cuda, backend, rccl_ranks, devices, distinct, numa_cpus) -> dict:
+    """The JSON line of the modes measured so far (the first mode is the headline `value`)."""
+    head = results[0]
+    seeders = head["seeders"]
+    out = {
+        "metric": metric_name(spec),
+        "value": round(head["value"], 3),
+        "unit": "GB/s",
+        "n_gpus": world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(head["step_s"] * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": _data_note(head) + ("" if cuda else "; CPU gloo rehearsal, not a GPU measurement"),
+        "p2p_ratio": round(head["p2p_ratio"], 4),
+        "ingest_GBps": round(head["ingest_GBps"], 3),
+        "extra": {f"{r['mode']}_GBps": round(r["value"], 3) for r in results}
+        | {f"{r['mode']}_ms_per_step": round(r["step_s"] * 1e3, 3) for r in results}
+        | {f"{r['mode']}_p2p_ratio": round(r["p2p_ratio"], 4) for r in results}
+        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results},
+        "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,
+                   "parallelism": (f"swarm{world_size}" if seeders == world_size
+                                   else f"seed{seeders}-leech{world_size - seeders}"),
+                   "data_mode": head["mode"], "modes": [r["mode"] for r in results],
+                   "model_bytes": head["model_bytes"], "files": head["files"],
+                   "chunks": head["chunks"], "xorbs": head["xorbs"], "terms": head["terms"],
+                   "rounds": head["rounds"], "round_mb": a.round_mb, "exchange": head["exchange"],
+                   "exchange_autotune_s": head["exchange_autotune_s"],
+                   "verify": "blake3 of every chunk on every rank + merkle file hashes",
+                   "numa_bound_cpus": len(numa_cpus), "hip_graph": head["hip_graph"],
+                   "pipeline": head["pipeline"], "device": a.device,
+                   "backend": backend if world_size > 1 else "none",
+                   "rccl_ranks": rccl_ranks, "devices": devices, "distinct_devices": distinct,
+                   "phase_s": head["phase_s"], "exchange_rx_GBps": head["exchange_rx_GBps"]},
+    }
+    if "ipc_host_wait_ms_per_step" in head:
+        out["extra"]["ipc_host_wait_ms_per_step"] = head["ipc_host_wait_ms_per_step"]
+        out["extra"]["ipc_signals"] = head.get("ipc_signals", False)
+    return out
+
+
+def _swarm_extra(rows: dict, results: list) -> dict:
+    """extra fields of the public-path rows: the first mode's row under the plain swarm_pull_* keys,
+    every mode's throughput under swarm_pull_<mode>_* with its ratio to the engine on the same world."""
+    if not rows:
+        return {}
+    first = next(iter(rows))
+    ex = dict(rows[first])
+    engine = {r["mode"]: r["value"] for r in results}
+    by_mode = {}
+    for mode, row in rows.items():
+        if "swarm_pull_GBps" not in row:
+            ex[f"swarm_pull_{mode}_error"] = row.get("swarm_pull_error")
+            continue
+        ex[f"swarm_pull_{mode}_GBps"] = row["swarm_pull_GBps"]
+        ex[f"swarm_pull_{mode}_ms_per_step"] = row["swarm_pull_ms_per_step"]
+        ex[f"swarm_pull_{mode}_vs_engine"] = round(row["swarm_pull_GBps"] / engine[mode], 4) if engine.get(mode) else None
+        by_mode[mode] = {k: row.get(f"swarm_pull_{k}") for k in ("GBps", "ms_per_step", "step_s", "streamed", "exchange",
+                                                                  "p2p_ratio", "phases", "first_call_phases")}
+    ex["swarm_pull_modes"] = by_mode
+    return ex
 
 
 def _data_note(r: dict) -> str:
@@ -741,85 +802,48 @@ def rank_main(a) -> None:
     results, pick, arenas = [], None, {}
     # (CPU rehearsals run it only when asked: --swarm-row on)
     swarm_row = ((a.swarm_row == "auto" and cuda) or a.swarm_row == "on") and a.seeders in (0, world_size)
-    keep = {} if swarm_row else None
+    swarm_rows: dict = {}  # mode -> the public-path row measured on that mode's world
+    out: dict = {}
+    printed = [False]
+
+    def emit(extra_fields: dict) -> None:  # the one JSON line, printed once by rank 0
+        if rank == 0 and not printed[0] and out:
+            printed[0] = True
+            print(json.dumps(out | {"extra": out["extra"] | extra_fields}), flush=True)
+
     for i, mode in enumerate(a.modes):
-        last = i == len(a.modes) - 1
+        keep = {} if swarm_row else None
         r = run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=pick, arenas=arenas,
-                     keep=keep if last else None)
+                     keep=keep)
         pick = r["exchange"] if world_size > 1 else None
         log(rank, f"[{mode}] {r['value']:.3f} GB/s aggregate, {r['step_s'] * 1e3:.1f} ms/step, "
                   f"exchange {r['exchange']}")
         results.append(r)
-    head = results[0]
-    seeders = head["seeders"]
-    out = {
-        "metric": metric_name(spec),
-        "value": round(head["value"], 3),
-        "unit": "GB/s",
-        "n_gpus": world_size,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(head["step_s"] * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
-        "data": _data_note(head) + ("" if cuda else "; CPU gloo rehearsal, not a GPU measurement"),
-        "p2p_ratio": round(head["p2p_ratio"], 4),
-        "ingest_GBps": round(head["ingest_GBps"], 3),
-        "extra": {f"{r['mode']}_GBps": round(r["value"], 3) for r in results}
-        | {f"{r['mode']}_ms_per_step": round(r["step_s"] * 1e3, 3) for r in results}
-        | {f"{r['mode']}_p2p_ratio": round(r["p2p_ratio"], 4) for r in results}
-        | {f"{r['mode']}_stored_ratio": round(r["stored_ratio"], 4) for r in results},
-        "config": {"model": spec.repo_id, "global_batch": world_size, "seq_len": None,
-                   "parallelism": (f"swarm{world_size}" if seeders == world_size
-                                   else f"seed{seeders}-leech{world_size - seeders}"),
-                   "data_mode": head["mode"], "modes": [r["mode"] for r in results],
-                   "model_bytes": head["model_bytes"], "files": head["files"],
-                   "chunks": head["chunks"], "xorbs": head["xorbs"], "terms": head["terms"],
-                   "rounds": head["rounds"], "round_mb": a.round_mb, "exchange": head["exchange"],
-                   "exchange_autotune_s": head["exchange_autotune_s"],
-                   "verify": "blake3 of every chunk on every rank + merkle file hashes",
-                   "numa_bound_cpus": len(numa_cpus), "hip_graph": head["hip_graph"],
-                   "pipeline": head["pipeline"], "device": a.device,
-                   "backend": backend if world_size > 1 else "none",
-                   "rccl_ranks": rccl_ranks, "devices": devices, "distinct_devices": distinct,
-                   "phase_s": head["phase_s"], "exchange_rx_GBps": head["exchange_rx_GBps"]},
-    }
-    if "ipc_host_wait_ms_per_step" in head:
-        out["extra"]["ipc_host_wait_ms_per_step"] = head["ipc_host_wait_ms_per_step"]
-        out["extra"]["ipc_signals"] = head.get("ipc_signals", False)
-    printed = [False]
-
-    def emit(extra_fields: dict) -> None:  # the one JSON line, printed once by rank 0
-        if rank == 0 and not printed[0]:
-            printed[0] = True
-            print(json.dumps(out | {"extra": out["extra"] | extra_fields}), flush=True)
-
-    if keep:
-        # The public-path row runs after the headline is measured.  At N > 1 it must not cost the
-        # headline: an exception is recorded in extra.swarm_pull_error, and a phase that overruns its
-        # deadline prints the headline line with the row marked failed and exits 0 (Watchdog.fallback).
-        keep["mode"] = results[-1]["mode"]
-        keep["arena"] = arenas.pop("arena", None)
-        keep["peers"] = arenas.pop("peers", None)
-        arenas.clear()
-        if world_size > 1:
-            wd.fallback = lambda reason: emit({"swarm_pull_error": reason})
-        try:
-            swarm = run_swarm_row(a, keep, device, rank, world_size, dist, wd)
-            log(rank, f"[swarm_pull {keep['mode']}] {swarm['swarm_pull_GBps']:.3f} GB/s aggregate, "
-                      f"{swarm['swarm_pull_ms_per_step']:.1f} ms/step (public path, memory CAS)")
-        except Exception as e:  # noqa: BLE001 - the headline stands without the row
-            if world_size == 1:
-                raise
-            swarm = {"swarm_pull_error": f"{type(e).__name__}: {e}"[:1000]}
-            log(rank, f"[swarm_pull] failed: {swarm['swarm_pull_error']}")
-        out["extra"].update(swarm)
-        keep["puller"].close()
-        keep.clear()
+        out = _headline(a, spec, results, world_size, cuda, backend, rccl_ranks, devices, distinct, numa_cpus)
+        if keep:
+            # The public-path row runs on every data mode's world, right after the engine measured it
+            # (its CDN is served from that world's pinned origin).  At N > 1 it must not cost the
+            # headline: an exception is recorded in extra.swarm_pull_error, and a phase that overruns its
+            # deadline prints the headline line (the modes measured so far) with the row marked failed
+            # and exits 0 (Watchdog.fallback).
+            keep["mode"] = mode
+            if world_size > 1:
+                wd.fallback = lambda reason: emit(_swarm_extra(swarm_rows, results) | {"swarm_pull_error": reason})
+            try:
+                swarm_rows[mode] = run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas)
+                log(rank, f"[swarm_pull {mode}] {swarm_rows[mode]['swarm_pull_GBps']:.3f} GB/s aggregate, "
+                          f"{swarm_rows[mode]['swarm_pull_ms_per_step']:.1f} ms/step (public path, memory CAS)")
+            except Exception as e:  # noqa: BLE001 - the headline stands without the row
+                if world_size == 1:
+                    raise
+                swarm_rows[mode] = {"swarm_pull_error": f"{type(e).__name__}: {e}"[:1000]}
+                log(rank, f"[swarm_pull {mode}] failed: {swarm_rows[mode]['swarm_pull_error']}")
+            keep["puller"].close()
+            keep.clear()
+            wd.fallback = None
+    if swarm_row:
         wd.arm("report")
-    emit({})
+    emit(_swarm_extra(swarm_rows, results))
     # (the pinned origin pool is left to the process exit: unregistering ~141 GB one buffer at a time
     # only delays it)
     if dist is not None:

@@ -83,10 +83,10 @@ def test_bench_launcher_timeout_kills_group():
 
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_bench_swarm_row_times_the_public_path(gpus):
-    """--swarm-row on: after the engine modes, the same world is pulled through the public
-    swarm_pull path from a mem:// memory CAS (every rank's pinned origin), and extra.swarm_pull_*
-    reports it -- here on gloo CPU ranks."""
-    p, _ = _run(["--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--modes", "random", "--swarm-row", "on",
+    """--swarm-row on: after each engine mode, the same world is pulled through the public
+    swarm_pull path from a mem:// memory CAS (every rank's pinned origin); extra.swarm_pull_* reports
+    the first mode's row and swarm_pull_<mode>_* every mode's -- here on gloo CPU ranks."""
+    p, _ = _run(["--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--modes", "random,bf16", "--swarm-row", "on",
                  "--swarm-steps", "2", "--swarm-warmup", "1"])
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
@@ -98,6 +98,10 @@ def test_bench_swarm_row_times_the_public_path(gpus):
     assert ex["swarm_pull_fetch"]["bytes_from_cdn"] > 0 and not ex["swarm_pull_fetch"]["bytes_from_peer"]
     if gpus > 1:
         assert ex["swarm_pull_p2p_ratio"] > 0.3 and ex["swarm_pull_exchange"] in ("bcast", "allgather", "p2p")
+    for mode in ("random", "bf16"):  # the row ran on both worlds, each against its own engine number
+        assert ex[f"swarm_pull_{mode}_GBps"] > 0
+        assert ex[f"swarm_pull_{mode}_vs_engine"] == pytest.approx(ex[f"swarm_pull_{mode}_GBps"] / ex[f"{mode}_GBps"], rel=1e-2)
+        assert len(ex["swarm_pull_modes"][mode]["step_s"]) == 2
 
 
 def test_bench_swarm_row_multi_file_three_ranks():
