@@ -364,12 +364,13 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     barrier()
     sync()
     hw0 = dict(puller.xchg.host_wait_s)
-    t0 = time.perf_counter()
+    t0, c0 = time.perf_counter(), time.process_time()
     for _ in range(a.steps):
         puller.step()
     sync()
     barrier()
     t1 = time.perf_counter()
+    phase["timed_cpu_s"] = round(time.process_time() - c0, 3)  # this rank's CPU seconds over the timed steps
     wd.arm("report")
     puller.check()  # all timed steps verified (first error persists)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
@@ -538,11 +539,12 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         tdist.barrier()
         if cuda:
             torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.process_time()
         n_t = one(st)
         if cuda:
             torch.cuda.synchronize()
         t_pull = time.perf_counter() - t0
+        cpu = time.process_time() - c0  # CPU seconds of every thread of this rank during the call
         tdist.barrier()
         times.append(time.perf_counter() - t0)
         # every timed step's phases on this rank (a slow step is then attributable to a phase and
@@ -551,7 +553,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         named = sum(v for k, v in ph.items() if k in ("init_s", "plan_s", "possession_s", "alloc_s", "shard_s",
                                                        "setup_exchange_s", "pull_s", "verify_s", "repair_s",
                                                        "tensors_s"))
-        step_phases.append(ph | {"call_s": round(t_pull, 4), "other_s": round(t_pull - named, 4),
+        step_phases.append(ph | {"call_s": round(t_pull, 4), "other_s": round(t_pull - named, 4), "cpu_s": round(cpu, 4),
                                  "item_ready_s": st.get("item_ready_s", []),
                                  "timeline": st.get("device_timeline", {})})
     if mark:

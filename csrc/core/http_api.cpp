@@ -48,6 +48,10 @@ std::string ApiServer::status_json() const {
   w.key("total_peers").num_u(s.total_peers);
   w.key("not_found").num_u(s.not_found);
   w.key("rejected").num_u(s.rejected);
+  // connection-thread seconds spent finding runs, waiting for device copies and writing sockets
+  w.key("serve_lookup_s").num(double(s.lookup_ns) * 1e-9, 4);
+  w.key("serve_wait_s").num(double(s.wait_ns) * 1e-9, 4);
+  w.key("serve_send_s").num(double(s.send_ns) * 1e-9, 4);
   w.key("uptime_s").num(std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count(), 1);
   w.key("peer_id").str(std::string(reinterpret_cast<const char*>(cfg_.peer_id.data()), 8));
   if (extra_) w.key("device").raw(extra_());

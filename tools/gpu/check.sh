@@ -57,7 +57,7 @@ for step in "$@"; do
     bench) timeout -k 10 900 python -u bench.py --steps $STEPS --warmup $WARMUP > $log 2>&1 || fail $step $? $log
            grep -h "aggregate" $log; tail -1 $log | cut -c1-400 ;;
     rehearsal) ZEST_BENCH_BACKEND=gloo ZEST_BENCH_LOG_ALL=1 timeout -k 10 700 python -u bench.py --gpus ${RANKS:-2} \
-                 --model llama-3.1-8b --steps 3 --warmup 1 > $log 2>&1 || fail $step $? $log
+                 --model llama-3.1-8b --steps 3 --warmup 1 ${REHEARSAL_ARGS:-} > $log 2>&1 || fail $step $? $log
                grep -h "mapped\|autotune\|GB/s aggregate" $log | head -12; tail -1 $log | cut -c1-600 ;;
     ipc) timeout -k 10 400 $PYT -v tests/test_gpu_ipc.py > $log 2>&1 || fail $step $? $log
          grep -E "PASSED|FAILED|SKIPPED" $log ;;

@@ -39,6 +39,7 @@ def main() -> int:
     ap.add_argument("--rate-mbps", type=float, default=0.0,
                     help="cap each seeder's uplink (zest serve --fault rate:<MB/s>, shared by its connections): "
                          "1250 ~ a 10 Gbps LAN peer")
+    ap.add_argument("--jobs", type=int, default=0, help="leecher --concurrency (default: the CLI's 16)")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
     shard = a.mb * 1_000_000 // a.shards
@@ -51,7 +52,7 @@ def main() -> int:
     work = Path(tempfile.mkdtemp(prefix="zest-stripe-"))
     nodes = []
     res = {"bytes": total, "repo": "org/stripe", "data": f"random bytes, {a.shards} Xet shards, raw chunks",
-           "seeder_rate_mbps": a.rate_mbps or None}
+           "seeder_rate_mbps": a.rate_mbps or None, "leech_jobs": a.jobs or 16}
     try:
         hub.add_repo("org/stripe", files, xet_min_size=1000)
         seeders = [Node(hub, work, "s0")]
@@ -68,24 +69,35 @@ def main() -> int:
         for s in seeders:
             s.wait_healthy(timeout=30)
         for label, use in (("1_seeder", seeders[:1]), ("3_seeders", seeders)):
-            before = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
+            st0 = [json.loads(s.api("/v1/status")[1]) for s in seeders]
+            before = [x["bytes_served"] for x in st0]
             leech = Node(hub, work, f"leech_{label}")
             nodes.append(leech)
-            args = ["pull", "org/stripe", "--no-dht", "--no-serve"]
+            args = ["pull", "org/stripe", "--no-dht", "--no-serve"] + (["-j", str(a.jobs)] if a.jobs else [])
             for s in use:
                 args += ["--peer", f"127.0.0.1:{s.listen_port}"]
             t0 = time.time()
             env = {"ZEST_TRACE": str(Path(a.trace).resolve() / f"leech_{label}.json")} if a.trace else None
             r = leech.run(*args, timeout=1800, env=env)
             dt = time.time() - t0
-            after = [json.loads(s.api("/v1/status")[1])["bytes_served"] for s in seeders]
+            st1 = [json.loads(s.api("/v1/status")[1]) for s in seeders]
+            after = [x["bytes_served"] for x in st1]
+            # each seeder's connection-thread seconds in run lookups and socket writes during this pull
+            split = {k: [round(b.get(k, 0) - a_.get(k, 0), 3) for a_, b in zip(st0, st1)]
+                     for k in ("serve_lookup_s", "serve_wait_s", "serve_send_s")}
             served = [b - a_ for a_, b in zip(before, after)]
             res[label] = {"seconds": round(dt, 3), "GBps": round(total / dt / 1e9, 3), "p2p_ratio": p2p_ratio(r.stdout),
-                          "served_share": [round(x / max(1, sum(served)), 3) for x in served]}
+                          "served_share": [round(x / max(1, sum(served)), 3) for x in served], "seeders": split}
             if a.trace:  # the peer-transfer phase alone (first request start .. last response end)
                 ev = json.load(open(Path(a.trace) / f"leech_{label}.json"))
                 ev = ev["traceEvents"] if isinstance(ev, dict) else ev
                 req = [e for e in ev if e.get("ph") == "X" and e.get("cat") == "peer" and e.get("name") == "request"]
+                tot: dict = {}
+                for e in ev:  # where the leecher's threads spent their time (summed over threads)
+                    if e.get("ph") == "X":
+                        k = f"{e.get('cat')}/{e.get('name')}"
+                        tot[k] = tot.get(k, 0.0) + e.get("dur", 0) / 1e3
+                res[label]["span_ms"] = {k: round(v, 1) for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]}
                 if req:
                     span = (max(e["ts"] + e["dur"] for e in req) - min(e["ts"] for e in req)) / 1e6
                     res[label]["transfer_s"] = round(span, 3)

@@ -70,24 +70,22 @@ TAIL_TAPER = (0.5, 0.25, 0.125)
 
 
 def staging_slot_bytes(staging_bytes: int, round_bytes: int, world: int) -> int:
-    """Staging slot size of a device swarm pull at `world` ranks.
+    """Staging slot size of a round-synchronous device swarm pull (`_rounds`: ZEST_SWARM_STREAM=0,
+    and the reassigned ranges after a recovery) at `world` ranks.
 
-    At N > 1 every round is one pull_terms call, and a call drains its pipeline before it
-    returns: with 1 GiB staging slots a 1 GiB round was a single batch (its H2D and its
-    kernels in series).  Slots of a quarter round keep 4 batches in flight within a round:
-    public-path row 81.0 -> 92.4 GB/s at 2 ranks, 108.6 -> 133.8 at 4 (one shared GPU,
-    8B random, profiles/r5/swarm_staging_r5as/).  At 8 ranks quarter slots stalled one
-    pull in three or five for ~2.5 s (three runs, cause not found) while half-round slots
-    never did in 10 pulls and still beat 1 GiB: 159.3 / 161.8 vs 144.3 GB/s
-    (profiles/r5/swarm_staging_r5av/).  A 4-rank rehearsal then stalled the same way with quarter
-    slots (steps 2.41 / 0.53 s, profiles/r5/rehearsal_n2_n4_r5bb/), so only 2 ranks take quarter
-    slots and larger worlds half-round slots.  N = 1 pulls its share in one call and keeps the
-    large slots.
+    There every round is one pull_terms call, and a call drains its pipeline before it returns: with
+    1 GiB staging slots a 1 GiB round was a single batch (its H2D and its kernels in series).  Slots
+    of a quarter round keep 4 batches in flight within a round: public-path row 81.0 -> 92.4 GB/s at
+    2 ranks, 108.6 -> 133.8 at 4 (one shared GPU, 8B random, profiles/r5/swarm_staging_r5as/).
+    Round 5 gave 4 and 8 ranks half-round slots because quarter slots "stalled one pull in three";
+    that stall was the hash-table zero-fill racing the first ingest kernels (a CDN repair,
+    docs/ARCHITECTURE.md 16.2), fixed in _alloc_tables, so every N > 1 takes quarter slots again.
+    N = 1 pulls its share in one call and keeps the large slots.  (Streamed pulls size their slots
+    in _Swarm.__init__.)
     """
     if world <= 1:
         return int(staging_bytes)
-    split = 4 if world <= 2 else 2
-    return min(int(staging_bytes), max(64 << 20, int(round_bytes) // split))
+    return min(int(staging_bytes), max(64 << 20, int(round_bytes) // 4))
 
 
 def _window_shape() -> tuple[int, int]:
@@ -1570,11 +1568,19 @@ class _Swarm:
         out: dict[str, torch.Tensor] = {}
         views = [(f, self.arena[o:o + f["size"]]) for f, o in zip(self.xet_files, self.plan.file_off)]
         views += list(zip(self.plain_files, plain_bufs))
-        for f, buf in views:
-            if f["size"] == 0:
-                continue
-            hlen = int.from_bytes(buf[:8].cpu().numpy().tobytes(), "little")
-            start, meta_ = zdev.parse_safetensors_header(buf[: 8 + hlen].cpu().numpy().tobytes())
+        views = [(f, buf) for f, buf in views if f["size"] >= 8]
+        if not views:
+            return out
+        # every file's header length, then every header, in one device -> host copy each (two copies
+        # per file cost a synchronizing round trip each: up to 60 ms per pull on a shared GPU)
+        lens = torch.cat([buf[:8] for _, buf in views]).cpu().numpy().view("<u8")
+        hlens = [min(int(h), int(f["size"]) - 8) for (f, _), h in zip(views, lens)]
+        heads = torch.cat([buf[8:8 + h] for (_, buf), h in zip(views, hlens)]).cpu().numpy().tobytes()
+        pos = 0
+        for (f, buf), hlen in zip(views, hlens):
+            head = int(hlen).to_bytes(8, "little") + heads[pos:pos + hlen]
+            pos += hlen
+            start, meta_ = zdev.parse_safetensors_header(head)
             for k, v in zdev.tensor_views(buf, start, meta_).items():
                 if k in out:
                     raise ValueError(f"duplicate tensor {k} in {f['path']}")
