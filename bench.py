@@ -364,13 +364,14 @@ def run_mode(a, mode, spec, device, rank, world_size, dist, wd, exchange_pick=No
     barrier()
     sync()
     hw0 = dict(puller.xchg.host_wait_s)
-    t0, c0 = time.perf_counter(), time.process_time()
+    t0, c0, thr0 = time.perf_counter(), time.process_time(), _thread_cpu()
     for _ in range(a.steps):
         puller.step()
     sync()
     barrier()
     t1 = time.perf_counter()
     phase["timed_cpu_s"] = round(time.process_time() - c0, 3)  # this rank's CPU seconds over the timed steps
+    phase["timed_thread_cpu_s"] = _thread_cpu_delta(thr0, _thread_cpu(), top=6)
     wd.arm("report")
     puller.check()  # all timed steps verified (first error persists)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
@@ -534,6 +535,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
     if mark:  # a distinctive kernel brackets the timed window in a kernel trace (overlap.py --between)
         torch.cuda._sleep(1000)
     times, st, step_phases = [], {}, []
+    thr0 = _thread_cpu()
     for _ in range(a.swarm_steps):
         st = {}
         tdist.barrier()
@@ -556,6 +558,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         step_phases.append(ph | {"call_s": round(t_pull, 4), "other_s": round(t_pull - named, 4), "cpu_s": round(cpu, 4),
                                  "item_ready_s": st.get("item_ready_s", []),
                                  "timeline": st.get("device_timeline", {})})
+    thr = _thread_cpu_delta(thr0, _thread_cpu())  # where this rank's CPU went over the timed calls
     if mark:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
@@ -571,10 +574,12 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
               f"{st.get('received_bytes')} items {st.get('items')} rounds {st.get('rounds')} exchange {st.get('exchange')}")
     times = el.cpu().tolist()
     step_s = float(sum(times) / len(times))
-    all_phases = [step_phases]
+    all_phases, all_thr = [step_phases], [thr]
     if world_size > 1:
         all_phases = [None] * world_size
         tdist.all_gather_object(all_phases, step_phases)
+        all_thr = [None] * world_size
+        tdist.all_gather_object(all_thr, thr)
     sp.release_pipelines()
     ops.mem_origin_clear()
     hub.stop()
@@ -590,6 +595,8 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
             "swarm_pull_streamed": st.get("streamed"),
             # [rank][timed step] -> phases of that call on that rank
             "swarm_pull_step_phases": all_phases,
+            # [rank] -> CPU seconds per thread name over the timed calls
+            "swarm_pull_thread_cpu_s": all_thr,
             "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
                                                                                   "bytes_from_peer")},
             "swarm_pull_device_timeline": st.get("device_timeline"),
@@ -598,6 +605,35 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
             "swarm_pull_arena_reused": bool(st.get("alloc", {}).get("reused", False)),
             "swarm_pull_rank_terms": [a_r, b_r], "swarm_pull_n_origin_runs": len(ts),
             "swarm_pull_verify": "merkle file hashes of every file on every rank"}
+
+
+def _thread_cpu() -> dict:
+    """CPU seconds (user + system) of every thread of this process, by (tid, name) -- Linux /proc."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as fh:
+                comm = fh.read().strip()
+            with open(f"/proc/self/task/{tid}/stat") as fh:
+                st = fh.read()
+            f = st[st.rindex(")") + 2:].split()
+            out[(tid, comm)] = (int(f[11]) + int(f[12])) / tick
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def _thread_cpu_delta(a: dict, b: dict, top: int = 10) -> dict:
+    """CPU seconds per thread name between two _thread_cpu() snapshots (the largest `top`)."""
+    by: dict = {}
+    for k, v in b.items():
+        by[k[1]] = by.get(k[1], 0.0) + v - a.get(k, 0.0)
+    return {k: round(v, 3) for k, v in sorted(by.items(), key=lambda kv: -kv[1])[:top] if v > 0}
 
 
 def _wait_device_reclaim(device, timeout_s: float = 30.0, quiet_s: float = 0.5) -> float:

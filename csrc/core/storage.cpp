@@ -3,6 +3,7 @@
 #include "trace.h"
 #include "xet_hash.h"
 #include "cdc.h"
+#include <pthread.h>
 #include <thread>
 
 #include <dirent.h>
@@ -590,8 +591,14 @@ namespace zest::storage {
 
 CacheWriter::CacheWriter(XorbCache* cache, size_t max_bytes, int threads)
     : cache_(cache), max_bytes_(max_bytes), queues_(size_t(std::max(1, threads))) {
-  for (int q = 0; q < int(queues_.size()); ++q) threads_.emplace_back([this, q] { worker(q); });
-  for (int k = 0; k < 2; ++k) copy_threads_.emplace_back([this] { copier(); });
+  for (int q = 0; q < int(queues_.size()); ++q) threads_.emplace_back([this, q] {
+    pthread_setname_np(pthread_self(), "zest-cachewr");
+    worker(q);
+  });
+  for (int k = 0; k < 2; ++k) copy_threads_.emplace_back([this] {
+    pthread_setname_np(pthread_self(), "zest-cachecp");
+    copier();
+  });
 }
 
 CacheWriter::~CacheWriter() {

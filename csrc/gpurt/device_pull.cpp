@@ -1,6 +1,7 @@
 #include "device_pull.h"
 
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 
 #include <algorithm>
 #include <array>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "../gpu/zgpu.h"
+#include "hip_wait.h"
 #include "pinned.h"
 #include "bridge.h"
 #include "config.h"
@@ -36,6 +38,17 @@
 // -- no host-side wait for kernels anywhere, so the copy of batch b + 1 overlaps the kernels of
 // batch b and PCIe stays busy.  The chunk records come from the header index the fetch workers
 // build anyway while validating each run, so the GPU has no header walk to do.
+
+// Flags of the events host threads wait on.  ZEST_EVENT_BLOCKING=1 adds hipEventBlockingSync: a
+// waiting thread sleeps in the driver instead of polling (CPU time per pull vs wake-up latency; the
+// one-GPU rehearsals share 16 CPUs between all ranks).
+static unsigned sync_event_flags() {
+  static const unsigned f = [] {
+    const char* v = std::getenv("ZEST_EVENT_BLOCKING");
+    return unsigned(hipEventDisableTiming) | ((v && v[0] == '1') ? unsigned(hipEventBlockingSync) : 0u);
+  }();
+  return f;
+}
 
 namespace zest::gpurt {
 
@@ -184,7 +197,7 @@ struct DeviceXetPull::Impl {
   hipEvent_t* take_events(size_t n) {
     while (events_.size() < n) {
       hipEvent_t e = nullptr;
-      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&e, sync_event_flags()), "hipEventCreate");
       events_.push_back(e);
     }
     return events_.data();
@@ -539,7 +552,7 @@ struct DeviceXetPull::Impl {
       hip_check(zg_merkle(hashes_.p, sizes_.p, merkle_job_.p, int(nf), root_.p, merkle_scratch_.p, sb, stream_),
                 "merkle");
       hip_check(hipMemcpyAsync(roots.data(), root_.p, 32 * nf, hipMemcpyDeviceToHost, stream_), "root D2H");
-      hip_check(hipStreamSynchronize(stream_), "sync");
+      hip_check(gpu::idle_stream_sync(stream_), "sync");
     }
     for (size_t f = 0; f < nf; ++f) {
       xet::Hash h;
@@ -678,6 +691,7 @@ struct DeviceXetPull::Impl {
         cv.notify_all();
       };
       auto worker = [&]() {
+        pthread_setname_np(pthread_self(), "zest-fetch");
         while (true) {
           const size_t i = k.fetch_add(1);
           if (i >= n) return;
@@ -732,6 +746,7 @@ struct DeviceXetPull::Impl {
       // batch, so nothing is re-recorded under its feet.
       std::deque<size_t> issued;  // batches queued on the GPU, in order; SIZE_MAX ends the thread
       auto releaser = [&]() {
+        pthread_setname_np(pthread_self(), "zest-release");
         (void)hipSetDevice(device_);
         while (true) {
           size_t b;
@@ -742,7 +757,7 @@ struct DeviceXetPull::Impl {
             issued.pop_front();
           }
           if (b == SIZE_MAX) return;
-          const bool copied = hipEventSynchronize(ev[2 * b]) == hipSuccess;
+          const bool copied = gpu::idle_event_sync(ev[2 * b]) == hipSuccess;
           {
             std::unique_lock<std::mutex> g(mu);
             if (!copied) {
@@ -753,7 +768,7 @@ struct DeviceXetPull::Impl {
             ready[b % S] = b + S;
             cv.notify_all();
           }
-          if (progress && copied && hipEventSynchronize(ev[2 * b + 1]) == hipSuccess) {
+          if (progress && copied && gpu::idle_event_sync(ev[2 * b + 1]) == hipSuccess) {
             // batches run in term order, and terms are in segment order: each touched segment's
             // bytes are complete up to the end of its last term in this batch
             const Batch& bt = batches[b];
@@ -800,7 +815,7 @@ struct DeviceXetPull::Impl {
           const size_t hs_bytes = zg_ingest_scratch_bytes(nchunks, ubytes);
           // the slot's device staging, records and scratch are read by batch b - S's kernels
           if (b >= S && (s.chunks_dev.n < size_t(nchunks ? nchunks : 1) || s.scratch.n < hs_bytes))
-            hip_check(hipEventSynchronize(ev[2 * (b - S) + 1]), "hipEventSynchronize");  // growing: wait, then free
+            hip_check(gpu::idle_event_sync(ev[2 * (b - S) + 1]), "hipEventSynchronize");  // growing: wait, then free
           s.chunks_dev.ensure(size_t(nchunks ? nchunks : 1));
           s.scratch.ensure(hs_bytes);
           trace::Span submit_span("device", "queue H2D + place/hash");
@@ -858,8 +873,8 @@ struct DeviceXetPull::Impl {
       }
       for (auto& t : ts) t.join();
       copies_done();
-      const hipError_t e1 = hipStreamSynchronize(copy_stream_);
-      const hipError_t e2 = hipStreamSynchronize(stream_);
+      const hipError_t e1 = gpu::idle_stream_sync(copy_stream_);
+      const hipError_t e2 = gpu::idle_stream_sync(stream_);
       stop_releaser();
       hip_check(e1, "sync copy stream");
       hip_check(e2, "sync compute stream");
@@ -928,8 +943,8 @@ struct DeviceXetPull::Impl {
     skern_set_.assign(S, 0);
     sready_.resize(S);
     for (size_t i = 0; i < S; ++i) {
-      hip_check(hipEventCreateWithFlags(&sh2d_[i], hipEventDisableTiming), "hipEventCreate");
-      hip_check(hipEventCreateWithFlags(&skern_[i], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&sh2d_[i], sync_event_flags()), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&skern_[i], sync_event_flags()), "hipEventCreate");
       sready_[i] = i;
     }
     serr_.ensure(kErrRing);
@@ -972,8 +987,8 @@ struct DeviceXetPull::Impl {
       std::unique_lock<std::mutex> g(smu_);
       scv_.wait(g, [&] { return sreleased_ == sbatch_total_; });
     }
-    hip_check(hipStreamSynchronize(copy_stream_), "sync copy stream");
-    hip_check(hipStreamSynchronize(stream_), "sync compute stream");
+    hip_check(gpu::idle_stream_sync(copy_stream_), "sync copy stream");
+    hip_check(gpu::idle_stream_sync(stream_), "sync compute stream");
   }
 
   // Forget every item (their events too): between pulls, once the caller waited for all of them.
@@ -1126,7 +1141,7 @@ struct DeviceXetPull::Impl {
         sl.scratch.ensure(max_hs);
       }
     }
-    hip_check(hipEventCreateWithFlags(&it.done, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&it.done, sync_event_flags()), "hipEventCreate");
     uint64_t ticket;
     {
       std::lock_guard<std::mutex> g(smu_);
@@ -1155,6 +1170,7 @@ struct DeviceXetPull::Impl {
   }
 
   void s_worker() {
+    pthread_setname_np(pthread_self(), "zest-sfetch");  // (per-thread CPU time in /proc: bench.py)
     (void)hipSetDevice(device_);
     const size_t S = nslots_;
     while (true) {
@@ -1234,6 +1250,7 @@ struct DeviceXetPull::Impl {
   }
 
   void s_submitter() {
+    pthread_setname_np(pthread_self(), "zest-ssubmit");  // (per-thread CPU time in /proc: bench.py)
     (void)hipSetDevice(device_);
     const size_t S = nslots_;
     while (true) {
@@ -1324,6 +1341,7 @@ struct DeviceXetPull::Impl {
   }
 
   void s_releaser() {
+    pthread_setname_np(pthread_self(), "zest-srelease");  // (per-thread CPU time in /proc: bench.py)
     (void)hipSetDevice(device_);
     const size_t S = nslots_;
     while (true) {
@@ -1337,7 +1355,7 @@ struct DeviceXetPull::Impl {
         sissued_.pop_front();
         bp = &sbatches_[g - sb0_];
       }
-      const bool ok = !bp->gpu || hipEventSynchronize(sh2d_[g % S]) == hipSuccess;
+      const bool ok = !bp->gpu || gpu::idle_event_sync(sh2d_[g % S]) == hipSuccess;
       {
         std::unique_lock<std::mutex> lk(smu_);
         if (!ok && !bp->item->failed) {
@@ -1411,7 +1429,7 @@ struct DeviceXetPull::Impl {
       itp = s_find(ticket);
       if (!itp->queued) throw Error("InvalidArgument", "item_error before wait_item");
     }
-    hip_check(hipEventSynchronize(itp->done), "hipEventSynchronize (item)");
+    hip_check(gpu::idle_event_sync(itp->done), "hipEventSynchronize (item)");
     return reinterpret_cast<volatile unsigned long long*>(serr_host_.data())[itp->eslot];
   }
 

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
+import resource
 import shutil
 import sys
 import tempfile
@@ -28,6 +30,16 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 from e2e_util import Node, p2p_ratio  # noqa: E402
 from zest_amd.testing import FakeHub  # noqa: E402
+
+
+def _proc_cpu(pid: int) -> float:
+    """CPU seconds (user + system) of a live process."""
+    try:
+        with open(f"/proc/{pid}/stat") as fh:
+            f = fh.read().rsplit(")", 1)[1].split()
+        return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError):
+        return 0.0
 
 
 def main() -> int:
@@ -76,10 +88,16 @@ def main() -> int:
             args = ["pull", "org/stripe", "--no-dht", "--no-serve"] + (["-j", str(a.jobs)] if a.jobs else [])
             for s in use:
                 args += ["--peer", f"127.0.0.1:{s.listen_port}"]
+            scpu0 = [_proc_cpu(s.procs[-1].pid) for s in seeders]
+            lcpu0 = resource.getrusage(resource.RUSAGE_CHILDREN)
             t0 = time.time()
             env = {"ZEST_TRACE": str(Path(a.trace).resolve() / f"leech_{label}.json")} if a.trace else None
             r = leech.run(*args, timeout=1800, env=env)
             dt = time.time() - t0
+            lcpu1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+            # CPU seconds of the leecher (a finished child) and of each seeder process during the pull
+            cpu = {"leecher": round(lcpu1.ru_utime + lcpu1.ru_stime - lcpu0.ru_utime - lcpu0.ru_stime, 3),
+                   "seeders": [round(_proc_cpu(s.procs[-1].pid) - c, 3) for s, c in zip(seeders, scpu0)]}
             st1 = [json.loads(s.api("/v1/status")[1]) for s in seeders]
             after = [x["bytes_served"] for x in st1]
             # each seeder's connection-thread seconds in run lookups and socket writes during this pull
@@ -87,7 +105,8 @@ def main() -> int:
                      for k in ("serve_lookup_s", "serve_wait_s", "serve_send_s")}
             served = [b - a_ for a_, b in zip(before, after)]
             res[label] = {"seconds": round(dt, 3), "GBps": round(total / dt / 1e9, 3), "p2p_ratio": p2p_ratio(r.stdout),
-                          "served_share": [round(x / max(1, sum(served)), 3) for x in served], "seeders": split}
+                          "served_share": [round(x / max(1, sum(served)), 3) for x in served], "seeders": split,
+                          "cpu_s": cpu, "cpus_busy": round((cpu["leecher"] + sum(cpu["seeders"])) / dt, 2)}
             if a.trace:  # the peer-transfer phase alone (first request start .. last response end)
                 ev = json.load(open(Path(a.trace) / f"leech_{label}.json"))
                 ev = ev["traceEvents"] if isinstance(ev, dict) else ev

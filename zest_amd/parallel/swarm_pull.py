@@ -112,6 +112,57 @@ class _Agree:
     nck: list        # chunks of each rank's item
 
 
+class _AgreeThread:
+    """Finishes a streamed pull's round agreements in order on a thread of its own
+    (_Swarm._finish_agree: wait for the round's gather, apply it, hash the received chunks).  The
+    first error stops the processing (later rounds are dropped) and is re-raised by raise_error()
+    on the pulling thread."""
+
+    def __init__(self, sw: "_Swarm"):
+        import queue
+        self.sw = sw
+        self.q: "queue.Queue" = queue.Queue()
+        self.error: BaseException | None = None
+        self.abandon = False
+        self.busy_s = 0.0
+        self.th = threading.Thread(target=self._run, name="zest-swarm-agree", daemon=True)
+        self.th.start()
+
+    def _run(self):
+        try:  # (the thread's name in /proc: bench.py's per-thread CPU accounting)
+            import ctypes
+            ctypes.CDLL(None).prctl(15, b"zest-agree", 0, 0, 0)
+        except Exception:  # noqa: BLE001
+            pass
+        if self.sw.cuda:
+            torch.cuda.set_device(self.sw.device)  # (HIP's current device is per thread)
+        while True:
+            ag = self.q.get()
+            if ag is None:
+                return
+            if self.error is not None or self.abandon:
+                continue
+            t = time.perf_counter()
+            try:
+                self.sw._finish_agree(ag)
+            except BaseException as e:  # noqa: BLE001 - handed to the pulling thread
+                self.error = e
+            self.busy_s += time.perf_counter() - t
+
+    def put(self, ag) -> None:
+        self.q.put(ag)
+
+    def close(self, abandon: bool = False) -> None:
+        """Wait until every queued agreement is finished (abandon: skip those not started)."""
+        self.abandon = abandon
+        self.q.put(None)
+        self.th.join()
+
+    def raise_error(self) -> None:
+        if self.error is not None:
+            raise self.error
+
+
 class _RankLost(RuntimeError):
     """A collective failed or timed out: some rank is gone (handled by _Membership.rebuild)."""
 
@@ -1127,6 +1178,28 @@ class _Swarm:
             self.xchg.order_after(torch.cuda.current_stream(self.device))
         lag = max(0, int(os.environ.get("ZEST_SWARM_AGREE_LAG", "3")))
         pending = collections.deque()
+        # The agreements are finished on a thread of their own (ZEST_SWARM_AGREE_THREAD, default on):
+        # a round's received chunks are hashed as soon as its gather completes, instead of when this
+        # thread next comes back from waiting for its own item -- and this thread never blocks on a
+        # slower peer before its last exchange is issued.
+        agree = _AgreeThread(self) if os.environ.get("ZEST_SWARM_AGREE_THREAD", "1") != "0" else None
+        try:
+            self._stream_loop(rounds, tickets, injected, pending, lag, agree)
+        except BaseException:
+            if agree is not None:
+                agree.close(abandon=True)  # (the rounds not agreed yet stay in self.unagreed)
+            raise
+        if agree is not None:
+            t = time.perf_counter()
+            agree.close()
+            self._mark("agree_s", t)
+            self.times["agree_thread_s"] = round(self.times.get("agree_thread_s", 0.0) + agree.busy_s, 4)
+            agree.raise_error()
+        self._tickets = []
+
+    def _stream_loop(self, rounds, tickets, injected, pending, lag, agree):
+        P = self.plan
+        me = self.m.rank
         for k, items in enumerate(rounds):
             rno = self.round_no
             if (self.m.me, rno) in self.fault["exit"]:
@@ -1156,8 +1229,13 @@ class _Swarm:
                 except Exception as e:  # noqa: BLE001
                     raise _RankLost(str(e)) from e
             self._mark("exchange_issue_s", t)
-            pending.append(self._post_agree(rno, items, err, lens, info, works))
+            ag = self._post_agree(rno, items, err, lens, info, works)
             self.round_no += 1
+            if agree is not None:
+                agree.put(ag)
+                agree.raise_error()  # (a failed agreement: stop issuing; run() recovers or fails)
+                continue
+            pending.append(ag)
             t = time.perf_counter()
             while pending and (len(pending) > lag or pending[0].work.is_completed()):
                 self._finish_agree(pending.popleft())
@@ -1166,7 +1244,6 @@ class _Swarm:
         while pending:
             self._finish_agree(pending.popleft())
         self._mark("agree_s", t)
-        self._tickets = []
 
     def _post_agree(self, rno: int, items: list, err: str, lens: bytes, info: dict, works: list) -> "_Agree":
         """Start round rno's agreement: an async all_gather of [status, chunk sizes...] per rank
@@ -1251,7 +1328,7 @@ class _Swarm:
     def _settle_received(self):
         for ev, items in self.pending_events:
             if ev is not None:
-                ev.synchronize()
+                _idle_wait(ev)
             self.have.update(items)
         self.pending_events = []
 
@@ -1458,6 +1535,11 @@ class _Swarm:
             sizes = torch.from_numpy(self.lens.astype(np.int64))
             sizes = sizes.to(self.device) if self.cuda else sizes
             if self.cuda:
+                # (the received chunks' hashes first, waited for with sleeps: the Merkle copy below
+                # would otherwise poll a core for the hashing backlog)
+                done = torch.cuda.Event()
+                done.record(self.verify_stream)
+                _idle_wait(done)
                 torch.cuda.current_stream(self.device).wait_stream(self.verify_stream)
             roots = ops.merkle_roots(self.hashes, sizes, jobs, file_hash=True).cpu().numpy()
             for j, i in enumerate(idx):
@@ -1586,6 +1668,15 @@ class _Swarm:
                     raise ValueError(f"duplicate tensor {k} in {f['path']}")
                 out[k] = v
         return out
+
+
+def _idle_wait(ev) -> None:
+    """Wait for a torch.cuda.Event with short sleeps: Event.synchronize() polls a core for as long
+    as the GPU takes (the one-GPU rehearsals share 16 CPUs between all ranks)."""
+    d = 5e-6
+    while not ev.query():
+        time.sleep(d)
+        d = min(d * 2, 1e-4)
 
 
 def _merged_stats(parts: list) -> dict:
