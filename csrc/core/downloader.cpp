@@ -409,7 +409,10 @@ FileResult ParallelDownloader::reconstruct(const std::string& hex, const std::st
     for (auto& h : hashes)
       for (auto& x : h) r.chunk_lens.push_back(uint32_t(x.size));
   } else {
-    ::fdatasync(fd);
+    {
+      trace::Span sp("download", "fdatasync");  // (the disk's share of a pull's wall time)
+      ::fdatasync(fd);
+    }
     close_fd();
     if (::rename(tmp.c_str(), out_path.c_str()) != 0) throw Error("IoError", "rename " + out_path);
     storage::remove_file(side);

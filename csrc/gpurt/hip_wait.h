@@ -15,7 +15,7 @@
 
 namespace zest::gpu {
 
-inline hipError_t idle_event_sync(hipEvent_t e, int max_us = 100) {
+inline hipError_t idle_event_sync(hipEvent_t e, int max_us = 50) {
   hipError_t r = hipEventQuery(e);
   int us = 5;
   while (r == hipErrorNotReady) {
@@ -27,7 +27,7 @@ inline hipError_t idle_event_sync(hipEvent_t e, int max_us = 100) {
 }
 
 // The same for everything queued on `s` so far (an event recorded behind it).
-inline hipError_t idle_stream_sync(hipStream_t s, int max_us = 100) {
+inline hipError_t idle_stream_sync(hipStream_t s, int max_us = 50) {
   hipEvent_t e = nullptr;
   if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return hipStreamSynchronize(s);
   hipError_t r = hipEventRecord(e, s);
