@@ -580,6 +580,20 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         tdist.all_gather_object(all_phases, step_phases)
         all_thr = [None] * world_size
         tdist.all_gather_object(all_thr, thr)
+    # agree_s is this rank's wait at the end of a streamed pull for the last rounds' gathers: the
+    # time until the slowest rank queued its last item (skew) plus the agreement's own cost.  Per
+    # timed step: the largest own cost over the ranks (agree_s - skew), as a fraction of pull_s.
+    own = []
+    try:
+        for k in range(len(all_phases[0])):
+            last = [ph[k]["item_ready_s"][-1] for ph in all_phases if ph[k].get("item_ready_s")]
+            if len(last) != len(all_phases):
+                break
+            mx = max(last)
+            own.append(max((ph[k].get("agree_s", 0.0) - (mx - ph[k]["item_ready_s"][-1])) / max(1e-9, ph[k].get("pull_s", 0.0))
+                           for ph in all_phases))
+    except (KeyError, IndexError, TypeError):
+        own = []
     sp.release_pipelines()
     ops.mem_origin_clear()
     hub.stop()
@@ -595,6 +609,7 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
             "swarm_pull_streamed": st.get("streamed"),
             # [rank][timed step] -> phases of that call on that rank
             "swarm_pull_step_phases": all_phases,
+            "swarm_pull_agree_own_frac": [round(x, 4) for x in own],
             # [rank] -> CPU seconds per thread name over the timed calls
             "swarm_pull_thread_cpu_s": all_thr,
             "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
