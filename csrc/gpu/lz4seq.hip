@@ -374,8 +374,11 @@ __device__ __forceinline__ void emit(Batch& B, uint32_t lane, uint32_t lp, uint3
 // nothing is ever written through the scalar cache.  Bytes p .. p+4 are valid in the result.
 __device__ __forceinline__ uint64_t sload8(const uint32_t* w4, uint32_t p) {
   uint64_t v;
-  const uint32_t off = p & ~3u;
-  asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(w4), "s"(off));
+  // (restated uniform: free when the compiler already holds them in SGPRs, and the "s" constraints
+  // below cannot take a VGPR where its divergence analysis loses track)
+  const uint32_t off = uni(p & ~3u);
+  const uint32_t* const base = reinterpret_cast<const uint32_t*>(uni64(reinterpret_cast<uintptr_t>(w4)));
+  asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v >> (8 * (p & 3));
 }
 
@@ -621,6 +624,10 @@ __device__ void ungroup_bg4(const uint8_t* __restrict__ st, uint8_t* __restrict_
 constexpr uint32_t kPairSlots = 4;
 constexpr uint32_t kPairEnd = 0x80000000u;   // n field of an end marker (| status code)
 constexpr uint32_t kPairSpinMax = 1u << 22;  // ~0.1 s of s_sleep 1
+// Ticket ring of the dynamic chunk schedule.  Every ticketed chunk publishes at least its end marker,
+// and the producer is at most kPairSlots publishes ahead of the consumer, so it is never more than
+// kPairSlots + 1 tickets ahead: 8 entries are never overwritten unread.
+constexpr uint32_t kPairTickets = 8;
 
 struct PairLds {
   uint32_t rl[kPairSlots][kWave], rh[kPairSlots][kWave], rx[kPairSlots][kWave];
@@ -630,6 +637,8 @@ struct PairLds {
   uint32_t abort;             // chunk index + 1 whose execution failed
   uint32_t dead;              // a wait ran out: both waves leave
   uint32_t heads[kWave];
+  uint32_t ticket[kPairTickets];  // dynamic scheduling: the chunk of the block's k-th ticket
+  uint32_t tseq[kPairTickets];    // k + 1 once ticket k is written
   __attribute__((aligned(16))) uint8_t ring[kRing];
 };
 
@@ -668,15 +677,62 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
                                                   const ZgChunk* __restrict__ chunks, int n_chunks,
                                                   unsigned long long* err, uint64_t src_n, uint64_t dst_n,
                                                   uint8_t* __restrict__ hashes, uint64_t* __restrict__ sizes,
-                                                  uint8_t* __restrict__ stage) {
+                                                  uint8_t* __restrict__ stage, uint32_t dbg,
+                                                  uint32_t* __restrict__ work) {
   __shared__ PairLds L;
   const uint32_t lane = lane_id();
   const bool producer = uni(threadIdx.x >> 6) == 0;
   if (threadIdx.x < kPairSlots) L.full[threadIdx.x] = L.done[threadIdx.x] = 0;
+  if (threadIdx.x < kPairTickets) L.tseq[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.abort = L.dead = 0;
   __syncthreads();
   uint32_t q = 0;  // batch sequence number, counted identically by both waves
-  for (int c = int(uni(blockIdx.x)); c < n_chunks; c += int(gridDim.x)) {
+  // Chunk schedule.  Static (work == nullptr): block b takes chunks b, b + grid, ...  Dynamic: the
+  // producer takes the next chunk from the launch's work counter (one vector atomic from lane 0)
+  // whenever it starts one, and hands it to the consumer through the LDS ticket ring -- a block that
+  // finished a small chunk takes the next one at once, so a launch is no longer as long as the
+  // blocks that were dealt one chunk more than the others (a 256 MiB batch: ~4.2 k chunks on 4096
+  // blocks, 98 of them decoding two in a row, tools/gpu/lz4_split_probe.py).  Stored chunks and
+  // chunks that fail the range checks never get a ticket: the producer settles them itself.
+  int cs = int(uni(blockIdx.x));
+  uint32_t tk = 0;  // tickets taken (dynamic)
+  while (true) {
+    int c;
+    if (work != nullptr) {
+      const uint32_t slot = tk % kPairTickets;
+      if (producer) {
+        while (true) {
+          uint32_t v = 0;
+          if (lane == 0) v = atomicAdd(work, 1u);
+          c = int(uni(v));
+          if (c >= n_chunks) break;
+          const ZgChunk h = chunks[c];
+          const uint32_t sc = uni(h.scheme), cl = uni(h.clen), ul = uni(h.ulen);
+          const uint64_t so = uni64(h.src), dso = uni64(h.dst);
+          if (sc == 0) continue;
+          const bool range_bad = so + cl > src_n || dso + ul > dst_n;
+          if (range_bad || ul > kMaxChunk) {
+            if (lane == 0) report(err, range_bad ? ZG_ERR_RANGE : ZG_ERR_CAPACITY, uint32_t(c));
+            if (kHash) {
+              if (lane < 8) reinterpret_cast<uint32_t*>(hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
+              if (sizes && lane == 0) sizes[c] = 0;
+            }
+            continue;
+          }
+          break;
+        }
+        if (lane == 0) L.ticket[slot] = uint32_t(c < n_chunks ? c : n_chunks);
+        lds_release(&L.tseq[slot], tk + 1u, lane);
+      } else {
+        if (!lds_wait(L, &L.tseq[slot], tk + 1u, lane)) return;
+        c = int(uni(L.ticket[slot]));
+      }
+      ++tk;
+    } else {
+      c = cs;
+      cs += int(gridDim.x);
+    }
+    if (c >= n_chunks) break;
     ZgChunk ch = chunks[c];
     ch.src = uni64(ch.src);
     ch.dst = uni64(ch.dst);
@@ -771,7 +827,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           }
           break;
         }
-        if (!failed && !exec_batch(B, X, lane)) {
+        // (dbg & 1, diagnostics only: the consumer takes the records without executing them -- the
+        // launch then times the parse alone, tools/gpu/lz4_split_probe.py; the chunk reports a size error)
+        if (!failed && !(dbg & 1u) && !exec_batch(B, X, lane)) {
           failed = true;
           if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
           lds_release(&L.abort, cmark, lane);
@@ -1028,10 +1086,23 @@ extern "C" hipError_t zg_lz4_batched_decode_grid(const uint8_t* src, uint64_t sr
 
 constexpr int kPairGrid = 4096;  // 4096 pairs = 8 waves / SIMD
 
-// Staging bytes for BG4 chunks of a pair launch over n chunks (one kMaxChunk slice per block).
+constexpr size_t kWorkBytes = 256;  // the dynamic schedule's counter (one dword, padded)
+
+// Staging bytes for BG4 chunks of a pair launch over n chunks (one kMaxChunk slice per block), plus
+// the dynamic schedule's work counter.
 extern "C" size_t zg_lz4_stage_bytes(int n_chunks) {
   if (n_chunks <= 0) return 0;
-  return size_t(n_chunks < kPairGrid ? n_chunks : kPairGrid) * kMaxChunk;
+  return size_t(n_chunks < kPairGrid ? n_chunks : kPairGrid) * kMaxChunk + kWorkBytes;
+}
+
+static bool dynamic_enabled() {
+  const char* v = getenv("ZG_PAIR_DYNAMIC");  // read per launch: A/B of the chunk schedule
+  return !(v && atoi(v) == 0);
+}
+
+static uint32_t pair_debug() {
+  const char* v = getenv("ZG_PAIR_DEBUG");  // diagnostics (k_lz4_pair `dbg`); unset in every real run
+  return v ? uint32_t(atoi(v)) : 0u;
 }
 
 static bool stage_enabled() {
@@ -1046,13 +1117,21 @@ extern "C" hipError_t zg_lz4_pair_decode_hash_staged(const uint8_t* src, uint64_
   if (n_chunks <= 0) return hipSuccess;
   if (grid_cap <= 0 || grid_cap > 8192) grid_cap = kPairGrid;
   const int grid = n_chunks < grid_cap ? n_chunks : grid_cap;
+  // the dynamic schedule's work counter lives in the scratch right after the staging slices (the
+  // scratch is this pipeline's: its launches are ordered on one stream), zeroed before the launch
+  uint32_t* work = nullptr;
+  if (stage && dynamic_enabled() && stage_bytes >= size_t(grid) * kMaxChunk + kWorkBytes) {
+    work = reinterpret_cast<uint32_t*>(stage + size_t(grid) * kMaxChunk);
+    const hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+  }
   if (!stage_enabled() || !stage || stage_bytes < size_t(grid) * kMaxChunk) stage = nullptr;
   if (hashes)
     hipLaunchKernelGGL(k_lz4_pair<true>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
-                       src_n, dst_n, hashes, sizes, stage);
+                       src_n, dst_n, hashes, sizes, stage, pair_debug(), work);
   else
     hipLaunchKernelGGL(k_lz4_pair<false>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
-                       src_n, dst_n, hashes, sizes, stage);
+                       src_n, dst_n, hashes, sizes, stage, pair_debug(), work);
   return hipGetLastError();
 }
 
