@@ -536,6 +536,11 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         torch.cuda._sleep(1000)
     times, st, step_phases = [], {}, []
     thr0 = _thread_cpu()
+    prof = None
+    if os.environ.get("ZEST_BENCH_PYPROF") == "1":  # Python profile of the timed calls (pulling thread)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     for _ in range(a.swarm_steps):
         st = {}
         tdist.barrier()
@@ -559,6 +564,13 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
                                  "item_ready_s": st.get("item_ready_s", []),
                                  "timeline": st.get("device_timeline", {})})
     thr = _thread_cpu_delta(thr0, _thread_cpu())  # where this rank's CPU went over the timed calls
+    if prof is not None:
+        import io
+        import pstats
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+        log(rank, f"[swarm_pull] Python profile of the timed calls (pulling thread):\n{buf.getvalue()}")
     if mark:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()

@@ -229,3 +229,56 @@ def test_staging_slot_bytes_by_world():
     assert staging_slot_bytes(gib, gib, 8) == 256 * mib
     assert staging_slot_bytes(gib, 128 * mib, 2) == 64 * mib
     assert staging_slot_bytes(128 * mib, 4 * gib, 8) == 128 * mib
+
+
+def test_agree_thread_finishes_in_order_and_hands_errors_back():
+    """_AgreeThread (the streamed pull's agreements): rounds are finished in submission order on the
+    thread; the first error stops the processing, later rounds are skipped, and raise_error()
+    re-raises it on the pulling thread; close(abandon=True) skips rounds not started."""
+    from zest_amd.parallel.swarm_pull import _AgreeThread
+
+    class Sw:
+        cuda = False
+        device = torch.device("cpu")
+
+        def __init__(self, fail_at=None):
+            self.done, self.fail_at = [], fail_at
+
+        def _finish_agree(self, ag):
+            if ag == self.fail_at:
+                raise RuntimeError(f"round {ag} failed")
+            self.done.append(ag)
+
+    sw = Sw()
+    t = _AgreeThread(sw)
+    for k in range(20):
+        t.put(k)
+    t.close()
+    t.raise_error()
+    assert sw.done == list(range(20))
+
+    sw = Sw(fail_at=5)
+    t = _AgreeThread(sw)
+    for k in range(10):
+        t.put(k)
+    t.close()
+    assert sw.done == [0, 1, 2, 3, 4]
+    with pytest.raises(RuntimeError, match="round 5 failed"):
+        t.raise_error()
+
+    import threading
+    gate = threading.Event()
+
+    class Slow(Sw):
+        def _finish_agree(self, ag):
+            gate.wait(5)
+            super()._finish_agree(ag)
+
+    sw = Slow()
+    t = _AgreeThread(sw)
+    for k in range(5):
+        t.put(k)
+    t.abandon = True  # (what close(abandon=True) sets before it joins)
+    gate.set()
+    t.close(abandon=True)
+    assert len(sw.done) <= 1  # the round in progress may finish; the queued ones are skipped

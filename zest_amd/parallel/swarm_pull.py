@@ -129,6 +129,24 @@ class _AgreeThread:
         self.th.start()
 
     def _run(self):
+        if os.environ.get("ZEST_BENCH_PYPROF") == "1":  # (bench.py: a Python profile of this thread too)
+            import cProfile
+            import io
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                self._loop()
+            finally:
+                prof.disable()
+                buf = io.StringIO()
+                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(15)
+                import sys
+                print(f"[swarm_pull agree thread] Python profile:\n{buf.getvalue()}", file=sys.stderr, flush=True)
+            return
+        self._loop()
+
+    def _loop(self):
         try:  # (the thread's name in /proc: bench.py's per-thread CPU accounting)
             import ctypes
             ctypes.CDLL(None).prctl(15, b"zest-agree", 0, 0, 0)
@@ -1039,16 +1057,23 @@ class _Swarm:
         # The chunk tables go up first, from pinned memory on the (idle) current stream: a pageable
         # copy issued on the verify stream would block the host until that stream -- which waits for
         # this round's exchange -- got there, serializing the next round's fetch behind the exchange.
+        # Every chunk has its own slot in the pull's layout buffers (pinned + device, kept across
+        # pulls), so nothing is allocated or pinned per item (a pinned allocation per item and table
+        # doubled the pulling process's CPU time in the 8-rank rehearsal).
         jobs = []
         if self.verify:
             up = torch.cuda.current_stream(self.device)
+            h_off, h_len, d_off, d_len = _layout_bufs(self.device, max(1, self.plan.n_chunks))
             for it in recv_items:
                 offs, lens, c0 = self._chunk_layout(it)
-                if not len(lens):
+                n = len(lens)
+                if not n:
                     continue
-                od = torch.from_numpy(offs.view(np.int64)).pin_memory().to(self.device, non_blocking=True)
-                ld = torch.from_numpy(lens.view(np.int32)).pin_memory().to(self.device, non_blocking=True)
-                jobs.append((od, ld, lens, c0))
+                h_off[c0:c0 + n].numpy()[:] = offs.view(np.int64)
+                h_len[c0:c0 + n].numpy()[:] = lens.view(np.int32)
+                d_off[c0:c0 + n].copy_(h_off[c0:c0 + n], non_blocking=True)
+                d_len[c0:c0 + n].copy_(h_len[c0:c0 + n], non_blocking=True)
+                jobs.append((d_off[c0:c0 + n], d_len[c0:c0 + n], lens, c0))
             self.verify_stream.wait_stream(up)
         with torch.cuda.stream(self.verify_stream):
             for w in works:
@@ -1057,8 +1082,6 @@ class _Swarm:
                 sp, sb = self._hash_scratch.get(len(lens), int(lens.sum(dtype=np.uint64)))
                 H.hash_ranges(self.arena.data_ptr(), od.data_ptr(), ld.data_ptr(), len(lens),
                               self.hashes.data_ptr() + 32 * c0, ops.KEY_DATA, self.verify_stream.cuda_stream, sp, sb)
-                od.record_stream(self.verify_stream)
-                ld.record_stream(self.verify_stream)
             ev = torch.cuda.Event()
             ev.record(self.verify_stream)
         del P
@@ -1668,6 +1691,24 @@ class _Swarm:
                     raise ValueError(f"duplicate tensor {k} in {f['path']}")
                 out[k] = v
         return out
+
+
+# Per device: (pinned int64 offsets, pinned int32 sizes, device int64 offsets, device int32 sizes)
+# with one slot per chunk of a pull (grown to the largest pull so far), for the received chunks'
+# hash tables (_Swarm._hash_received).  A pull writes each chunk's slot once; the next pull reuses
+# them only after its predecessor's verify waited for every hash.
+_LAYOUT: dict = {}
+
+
+def _layout_bufs(device, n: int):
+    key = device.index
+    b = _LAYOUT.get(key)
+    if b is None or b[0].numel() < n:
+        cap = max(int(n), 1 << 16)
+        b = (torch.empty(cap, dtype=torch.int64).pin_memory(), torch.empty(cap, dtype=torch.int32).pin_memory(),
+             torch.empty(cap, dtype=torch.int64, device=device), torch.empty(cap, dtype=torch.int32, device=device))
+        _LAYOUT[key] = b
+    return b
 
 
 def _idle_wait(ev) -> None:
