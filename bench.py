@@ -536,6 +536,8 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         torch.cuda._sleep(1000)
     times, st, step_phases = [], {}, []
     thr0 = _thread_cpu()
+    ctx0 = {k[0]: _thread_ctx(k[0]) for k in thr0}
+    sampler = _SyscallSampler() if os.environ.get("ZEST_BENCH_SPIN_PROBE") == "1" else None
     prof = None
     if os.environ.get("ZEST_BENCH_PYPROF") == "1":  # Python profile of the timed calls (pulling thread)
         import cProfile
@@ -563,7 +565,11 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
         step_phases.append(ph | {"call_s": round(t_pull, 4), "other_s": round(t_pull - named, 4), "cpu_s": round(cpu, 4),
                                  "item_ready_s": st.get("item_ready_s", []),
                                  "timeline": st.get("device_timeline", {})})
-    thr = _thread_cpu_delta(thr0, _thread_cpu())  # where this rank's CPU went over the timed calls
+    thr1 = _thread_cpu()
+    thr = _thread_cpu_delta(thr0, thr1)  # where this rank's CPU went over the timed calls
+    busiest = _busiest_threads(thr0, thr1, ctx0)
+    if sampler is not None and busiest:
+        busiest[0].append(sampler.report(busiest[0][1]))  # what the busiest thread was doing
     if prof is not None:
         import io
         import pstats
@@ -586,12 +592,14 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
               f"{st.get('received_bytes')} items {st.get('items')} rounds {st.get('rounds')} exchange {st.get('exchange')}")
     times = el.cpu().tolist()
     step_s = float(sum(times) / len(times))
-    all_phases, all_thr = [step_phases], [thr]
+    all_phases, all_thr, all_busy = [step_phases], [thr], [busiest]
     if world_size > 1:
         all_phases = [None] * world_size
         tdist.all_gather_object(all_phases, step_phases)
         all_thr = [None] * world_size
         tdist.all_gather_object(all_thr, thr)
+        all_busy = [None] * world_size
+        tdist.all_gather_object(all_busy, busiest)
     # agree_s is this rank's wait at the end of a streamed pull for the last rounds' gathers: the
     # time until the slowest rank queued its last item (skew) plus the agreement's own cost.  Per
     # timed step: the largest own cost over the ranks (agree_s - skew), as a fraction of pull_s.
@@ -624,6 +632,8 @@ def run_swarm_row(a, keep, device, rank, world_size, dist, wd, arenas=None) -> d
             "swarm_pull_agree_own_frac": [round(x, 4) for x in own],
             # [rank] -> CPU seconds per thread name over the timed calls
             "swarm_pull_thread_cpu_s": all_thr,
+            # [rank] -> the busiest threads: [name, tid, cpu_s, voluntary, involuntary switches]
+            "swarm_pull_busiest_threads": all_busy,
             "swarm_pull_fetch": {k: st.get("fetch_stats", {}).get(k) for k in ("bytes_from_cdn", "bytes_from_cache",
                                                                                   "bytes_from_peer")},
             "swarm_pull_device_timeline": st.get("device_timeline"),
@@ -653,6 +663,107 @@ def _thread_cpu() -> dict:
         except (OSError, ValueError, IndexError):
             continue
     return out
+
+
+def _thread_ctx(tid: str) -> tuple[int, int]:
+    """(voluntary, involuntary) context switches of a thread of this process."""
+    v = n = 0
+    try:
+        with open(f"/proc/self/task/{tid}/status") as fh:
+            for ln in fh:
+                if ln.startswith("voluntary_ctxt_switches"):
+                    v = int(ln.split()[1])
+                elif ln.startswith("nonvoluntary_ctxt_switches"):
+                    n = int(ln.split()[1])
+    except (OSError, ValueError):
+        pass
+    return v, n
+
+
+def _busiest_threads(a: dict, b: dict, ctx0: dict, top: int = 6) -> list:
+    """The `top` threads by CPU seconds between two _thread_cpu() snapshots: [name, tid, cpu_s,
+    voluntary switches, involuntary switches] -- a thread that polls shows CPU with few voluntary
+    switches."""
+    rows = []
+    for k, v in b.items():
+        d = v - a.get(k, 0.0)
+        if d > 0:
+            c1 = _thread_ctx(k[0])
+            c0 = ctx0.get(k[0], (0, 0))
+            rows.append([k[1], int(k[0]), round(d, 3), c1[0] - c0[0], c1[1] - c0[1]])
+    rows.sort(key=lambda r: -r[2])
+    return rows[:top]
+
+
+class _SyscallSampler:
+    """ZEST_BENCH_SPIN_PROBE=1: samples /proc/self/task/*/syscall every 20 ms on a thread of its own
+    and reports, for a given thread, how often it was in user space ("running") or in which system
+    call, and the libraries its system calls were made from (their pc against /proc/self/maps)."""
+
+    def __init__(self):
+        import collections
+        self.hist = collections.defaultdict(collections.Counter)
+        self.libs = collections.defaultdict(collections.Counter)
+        self.stop = threading.Event()
+        self.maps = []
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _lib(self, pc: int) -> str:
+        if not self.maps:
+            try:
+                with open("/proc/self/maps") as fh:
+                    for ln in fh:
+                        f = ln.split()
+                        lo, hi = (int(x, 16) for x in f[0].split("-"))
+                        self.maps.append((lo, hi, f[5] if len(f) > 5 else "?"))
+            except OSError:
+                return "?"
+        for lo, hi, name in self.maps:
+            if lo <= pc < hi:
+                return os.path.basename(name)
+        return "?"
+
+    def _caller(self, sp: int) -> str:
+        """The first return address on the thread's stack (near sp) that lies outside libc: the
+        library that made the system call (a heuristic scan of 64 words)."""
+        import ctypes
+        import struct
+        try:
+            words = struct.unpack("<64Q", ctypes.string_at(sp, 512))
+        except (OSError, ValueError, struct.error):
+            return "?"
+        for w in words:
+            lib = self._lib(w)
+            if lib not in ("?", "libc.so.6", "[stack]", "[heap]", "") and not lib.startswith("["):
+                return lib
+        return "libc.so.6"
+
+    def _run(self):
+        while not self.stop.wait(0.02):
+            try:
+                tids = os.listdir("/proc/self/task")
+            except OSError:
+                continue
+            for tid in tids:
+                try:
+                    with open(f"/proc/self/task/{tid}/syscall") as fh:
+                        f = fh.read().split()
+                except OSError:
+                    continue
+                if not f:
+                    continue
+                self.hist[int(tid)][f[0]] += 1
+                if f[0] not in ("running", "-1") and len(f) >= 9:
+                    try:
+                        self.libs[int(tid)][self._caller(int(f[7], 16))] += 1
+                    except ValueError:
+                        pass
+
+    def report(self, tid: int) -> dict:
+        self.stop.set()
+        self.th.join(1.0)
+        return {"states": dict(self.hist[tid].most_common(6)), "libs": dict(self.libs[tid].most_common(4))}
 
 
 def _thread_cpu_delta(a: dict, b: dict, top: int = 10) -> dict:
