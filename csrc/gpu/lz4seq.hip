@@ -367,7 +367,8 @@ __device__ __forceinline__ void emit(Batch& B, uint32_t lane, uint32_t lp, uint3
 }
 
 // Stream reader for the (wave-uniform) parse: 8 bytes at stream position p through a scalar
-// load (s_load_dwordx2 at the dword below p).  The compressed payload is read-only for the whole
+// load (s_load_dwordx2 at the dword below p: a scalar load ignores the two low bits of its byte
+// offset, so p goes in as it is -- one scalar instruction less per sequence on the parse's chain).  The compressed payload is read-only for the whole
 // kernel, so the scalar data cache may serve it, and the parse then never waits on the vector
 // memory counter -- which on gfx9 also counts this wave's output stores (the compiler cannot prove
 // the payload unclobbered by those stores, so it would otherwise emit vector loads).  Loads only;
@@ -376,7 +377,7 @@ __device__ __forceinline__ uint64_t sload8(const uint32_t* w4, uint32_t p) {
   uint64_t v;
   // (restated uniform: free when the compiler already holds them in SGPRs, and the "s" constraints
   // below cannot take a VGPR where its divergence analysis loses track)
-  const uint32_t off = uni(p & ~3u);
+  const uint32_t off = uni(p);
   const uint32_t* const base = reinterpret_cast<const uint32_t*>(uni64(reinterpret_cast<uintptr_t>(w4)));
   asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v >> (8 * (p & 3));
