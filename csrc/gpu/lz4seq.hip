@@ -432,8 +432,11 @@ __device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& f
           const uint32_t iters0 = uni(ip < lim_blk ? min(kWave - B.n, (lim_blk - ip + 16) / 17) : 0u);
           uint32_t iters = iters0;
           // the record's lane counts down in a VGPR (lane - n): one VALU op per sequence instead of
-          // a scalar increment on the CU's one scalar unit, which bounds this loop
+          // a scalar increment on the CU's one scalar unit, which bounds this loop; the sequences
+          // left in the counted run are read off the same countdown (lim_v + dn, equal on every
+          // lane), so the loop spends no scalar instruction on its own count either
           int32_t dn = int32_t(lane) - int32_t(B.n);
+          const int32_t lim_v = int32_t(iters0) + int32_t(B.n) - int32_t(lane);
           // single-exit loop (a `break` makes the structurizer route the exit flag through VALU)
           // continue while iters > 0 and neither nibble is 15: one integer test (min of the three),
           // computed by the vector unit from a VGPR copy of the loaded bytes (the scalar unit, which
@@ -442,7 +445,6 @@ __device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& f
           uint32_t lit = token >> 4;
           uint32_t lp = ip + 1;  // literal position of the current sequence (its token is at lp - 1)
           while (go != 0) {
-            iters = uni(iters - 1);
             const uint32_t p = lp + lit;
             const uint32_t y = uint32_t(sload8(w4, p));  // offset lo, offset hi, next token
             uint32_t yv;
@@ -454,8 +456,11 @@ __device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& f
             --dn;
             lit = (y >> 20) & 15;  // the next token's literal count: all the scalar unit needs of it
             const uint32_t tv = yv >> 16;
-            go = __builtin_amdgcn_readfirstlane(min(min(iters, (~tv) & 15), ((tv >> 4) & 15) ^ 15));
+            uint32_t rem;  // counted sequences left (an asm add: the compiler would rebuild a scalar count)
+            asm volatile("v_add_u32 %0, %1, %2" : "=v"(rem) : "v"(lim_v), "v"(dn));
+            go = __builtin_amdgcn_readfirstlane(min(min(rem, (~tv) & 15), ((tv >> 4) & 15) ^ 15));
           }
+          iters = uni(uint32_t(lim_v + dn));
           ip = uni(lp - 1);
           const uint32_t n = uni(B.n + (iters0 - iters));
           B.n = n;

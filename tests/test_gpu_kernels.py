@@ -1015,3 +1015,56 @@ def test_index_scan_random_lookalikes(seed):
     fb = []
     (serial, e0), (scan, e1) = _index_both(src, terms, nck, fb)
     assert e0 == 0 and e1 == e0 and scan == serial, (fb, e0, e1)
+
+
+@pytest.mark.gpu
+def test_ingest_many_small_bg4_chunks_dynamic_schedule(monkeypatch):
+    """More chunks than decoder blocks (4096): under the dynamic schedule every block takes chunk
+    after chunk from the work counter (LDS ticket ring between its producer and consumer waves),
+    interleaved with stored chunks the producer settles itself; bytes and hashes equal the host
+    builder's, and the static schedule's."""
+    rng = np.random.default_rng(11)
+    b = C.XorbBuilder("auto")
+    parts = []
+    for i in range(5000):
+        n = int(rng.integers(600, 2600))
+        if i % 7 == 3:
+            p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()  # incompressible: stored
+        else:
+            w = rng.standard_normal(n // 2).astype(np.float32) * 0.02
+            p = (w.view(np.uint32) >> 16).astype(np.uint16).tobytes()
+        assert b.fits(len(p))
+        b.add_chunk(p)
+        parts.append(p)
+    data = b"".join(parts)
+    body = b.serialize(False)
+    nck = len(parts)
+    H = ops.hip()
+    src = ops.padded_empty(len(body), DEV)
+    src.copy_(torch.frombuffer(bytearray(body), dtype=torch.uint8))
+    terms = np.zeros(1, dtype=ops.TERM_DTYPE)
+    terms[0] = (0, len(body), 0, 0, nck, len(data))
+    ws = ops.IngestWorkspace(DEV, 1, nck)
+    terms_d = torch.from_numpy(terms.view(np.uint8).copy()).to(DEV)
+    ops.index_terms(H, src.data_ptr(), len(body), terms_d.data_ptr(), 1, ws.chunks.data_ptr(), ws.err.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream, ws)
+    torch.cuda.synchronize()
+    rec = np.frombuffer(ws.chunks[: nck * ops.CHUNK_DTYPE.itemsize].cpu().numpy().tobytes(), dtype=ops.CHUNK_DTYPE)
+    assert (rec["scheme"] != 0).sum() > 4096 and (rec["scheme"] == 0).any()
+    got = {}
+    for dyn in ("1", "0"):
+        monkeypatch.setenv("ZG_PAIR_DYNAMIC", dyn)
+        dst = ops.padded_empty(len(data), DEV)
+        dst.fill_(0x3C)
+        hashes = torch.full((nck, 32), 0x77, dtype=torch.uint8, device=DEV)
+        err = torch.zeros(1, dtype=torch.int64, device=DEV)
+        sp, sb = ops.HashScratch(DEV, ingest=True).get(nck, len(data))
+        H.ingest_chunks(src.data_ptr(), len(body), dst.data_ptr(), len(data), ws.chunks.data_ptr(), nck, True,
+                        err.data_ptr(), hashes.data_ptr(), 0, 0, torch.cuda.current_stream().cuda_stream, sp, sb)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0, dyn
+        assert dst.cpu().numpy().tobytes() == data, dyn
+        got[dyn] = hashes.cpu().numpy()
+    monkeypatch.delenv("ZG_PAIR_DYNAMIC")
+    assert np.array_equal(got["1"], got["0"])
+    assert got["1"].tobytes() == b"".join(b.chunk_hashes())
