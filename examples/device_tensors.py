@@ -1,9 +1,15 @@
-"""Pull a model straight into HBM: every safetensors file is loaded onto the GPU and verified there
-against its Xet file hash (GPU CDC + BLAKE3 + Merkle), then exposed as torch tensors.
+"""Pull a model straight into HBM: every term is fetched (xorb cache -> peers -> CDN) into pinned
+staging, copied to the GPU, decoded (LZ4 / BG4) and BLAKE3-hashed there, every file is checked
+against its Xet hash (Merkle), and the weights come back as torch tensors -- no disk snapshot unless
+save_snapshot=True.
 
 Single GPU:   python examples/device_tensors.py meta-llama/Llama-3.1-8B
 All 8 GPUs:   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/device_tensors.py <repo> all
-              (each file is read from disk by one rank and replicated over xGMI with RCCL)
+              (each rank fetches a byte-balanced share of the terms; the shares are replicated over
+              xGMI through per-process exchange windows, RCCL as the fallback; every rank verifies
+              its whole replica -- zest_amd.parallel.swarm_pull)
+One command:  zest pull <repo> --gpus 8 --device all [--save-snapshot]
+              (starts the ranks itself: zest_amd/replicate.py)
 """
 import sys
 
