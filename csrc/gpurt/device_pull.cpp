@@ -159,8 +159,16 @@ struct DeviceXetPull::Impl {
     if (device_ready_) return;
     trace::Span sp("device", "init: staging alloc");
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    hip_check(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate");
+    // The pull's own work (H2D copies, decode/place/hash) is the critical path of a swarm pull: its
+    // streams run at the device's greatest priority, the receive-side hashing and the exchanges at
+    // normal priority fill what it leaves idle -- the engine's split (zest_amd/engine.py); it
+    // matters where ranks share a GPU.  ZEST_PULL_STREAM_PRIORITY=0: normal priority.
+    int least = 0, greatest = 0;
+    const char* pv = std::getenv("ZEST_PULL_STREAM_PRIORITY");
+    if (!(pv && pv[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    if (pv && pv[0] == '0') greatest = 0;
+    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest), "hipStreamCreate");
+    hip_check(hipStreamCreateWithPriority(&copy_stream_, hipStreamNonBlocking, greatest), "hipStreamCreate");
     std::vector<std::string> errs(nslots_);
     std::vector<std::thread> pins;
     for (size_t i = 1; i < nslots_; ++i)
