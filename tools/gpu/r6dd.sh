@@ -1,5 +1,7 @@
 # round-6 call dd: kernel + copy trace of every rank in the 8-rank bf16 rehearsal; GPU activity inside
-# the public-path row's timed window (ZEST_BENCH_MARK=1 sleep kernels bracket it)
+# the public-path row's timed window (ZEST_BENCH_MARK=1 sleep kernels bracket it).
+# NOTE: every rank died with SIGSEGV at start-up under --kernel-trace --memory-copy-trace (host side;
+# the 1-rank `check.sh prof` kernel trace works): not rerun -- see profiles/r6/stream_priority_r6cc/.
 set -o pipefail
 export ZEST_SKIP_BUILD=1 TMPDIR=/tmp
 mkdir -p gpurun_out/r6dd
