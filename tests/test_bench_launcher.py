@@ -129,3 +129,25 @@ def test_bench_swarm_row_overrun_keeps_the_headline():
     assert len(lines) == 1, p.stdout
     assert lines[0]["value"] > 0 and "swarm_timed" in lines[0]["extra"]["swarm_pull_error"]
     assert "swarm_pull_GBps" not in lines[0]["extra"]
+
+
+def test_swarm_extra_reports_each_mode_and_errors():
+    """_swarm_extra: the first mode's row under swarm_pull_*, every mode's throughput and its ratio to
+    the engine on the same world under swarm_pull_<mode>_*, a failed mode's error under
+    swarm_pull_<mode>_error (and no throughput for it)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    rows = {"bf16": {"swarm_pull_GBps": 62.0, "swarm_pull_ms_per_step": 2270.0, "swarm_pull_step_s": [2.27],
+                     "swarm_pull_streamed": False, "swarm_pull_exchange": "none"},
+            "random": {"swarm_pull_error": "RuntimeError: boom"}}
+    results = [{"mode": "bf16", "value": 64.0}, {"mode": "random", "value": 56.0}]
+    ex = bench._swarm_extra(rows, results)
+    assert ex["swarm_pull_GBps"] == 62.0 and ex["swarm_pull_bf16_GBps"] == 62.0
+    assert ex["swarm_pull_bf16_vs_engine"] == round(62.0 / 64.0, 4)
+    assert ex["swarm_pull_random_error"] == "RuntimeError: boom"
+    assert "swarm_pull_random_GBps" not in ex and set(ex["swarm_pull_modes"]) == {"bf16"}
+    assert bench._swarm_extra({}, results) == {}
