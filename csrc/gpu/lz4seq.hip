@@ -841,6 +841,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           lds_release(&L.abort, cmark, lane);
         }
       }
+      if (dbg & 2u) whole = false;  // (diagnostics: execute only -- no ungroup, no hash)
       if (staged) {
         if (whole) {
           // the staged stream is complete in L2 (this wave's stores acknowledged, L1 dropped): write

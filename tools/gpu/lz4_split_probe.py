@@ -8,7 +8,8 @@ the chunk records from the host header walk, and times one fused decode + hash l
   * all chunks (the real launch), checked byte-exact, with the dynamic chunk schedule (default) and
     the static one (ZG_PAIR_DYNAMIC=0);
   * all chunks with ZG_PAIR_DEBUG=1 -- the consumer wave takes the records without executing them,
-    so the launch times the parse alone (its size errors are expected and ignored);
+    so the launch times the parse alone (its size errors are expected and ignored); and with
+    ZG_PAIR_DEBUG=2 -- parse and execute, but no BG4 ungroup and no fused hash;
   * only the largest quarter of the chunks, and only the smallest quarter: with one chunk per
     producer/consumer pair (a 256 MiB batch is ~4 k chunks for 4 k resident pairs) a launch lasts as
     long as its slowest chunk.
@@ -92,11 +93,25 @@ def main() -> int:
             os.environ.pop("ZG_PAIR_DYNAMIC", None)
         out["static_ms"] = round(ns_s / 1e6, 3)
         out["static_GBps"] = round(len(raw) / ns_s, 2)
+        os.environ["ZG_FUSED_HASH"] = "0"  # decode only, then the place/hash pass hashes every chunk
+        try:
+            dst.zero_()
+            ns_u = _time(launch(allc), a.runs)
+            torch.cuda.synchronize()
+            ops.raise_on_error(ws.err)
+            if dst[:len(raw)].cpu().numpy().tobytes() != raw:
+                raise RuntimeError("decoded bytes differ from the input (unfused hash)")
+        finally:
+            os.environ.pop("ZG_FUSED_HASH", None)
+        out["unfused_hash_ms"] = round(ns_u / 1e6, 3)
+        out["unfused_hash_GBps"] = round(len(raw) / ns_u, 2)
         out["largest_quarter_ms"] = round(_time(launch(order[-q:]), a.runs) / 1e6, 3)
         out["smallest_quarter_ms"] = round(_time(launch(order[:q]), a.runs) / 1e6, 3)
         os.environ["ZG_PAIR_DEBUG"] = "1"
         try:
             out["parse_only_ms"] = round(_time(launch(allc), a.runs) / 1e6, 3)
+            os.environ["ZG_PAIR_DEBUG"] = "2"  # parse + execute, no ungroup / hash
+            out["no_ungroup_hash_ms"] = round(_time(launch(allc), a.runs) / 1e6, 3)
         finally:
             os.environ.pop("ZG_PAIR_DEBUG", None)
             torch.cuda.synchronize()
