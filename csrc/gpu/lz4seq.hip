@@ -586,9 +586,10 @@ __device__ void ungroup_bg4(const uint8_t* __restrict__ st, uint8_t* __restrict_
   const bool a1 = (g1 & 3) == 0, a2 = (g2 & 3) == 0, a3 = (g3 & 3) == 0;  // group starts (slice is aligned)
   const bool oal = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   const uint32_t q4 = q & ~3u;  // whole 4-index steps
-  for (uint32_t p0 = 4 * lane; p0 < q4; p0 += 4 * kWave) {
-    const uint32_t a = *reinterpret_cast<const uint32_t*>(st + p0);
-    const uint32_t b = load4(st + g1 + p0, a1), c = load4(st + g2 + p0, a2), d = load4(st + g3 + p0, a3);
+  // four steps' loads are issued before any of their stores: the staged bytes come back from L2, and
+  // one step at a time left every step waiting out a full L2 round trip
+  constexpr uint32_t kU = 4;
+  auto step = [&](uint32_t p0, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     const uint32_t d0 = (a & 0xFFu) | (b & 0xFFu) << 8 | (c & 0xFFu) << 16 | (d & 0xFFu) << 24;
     const uint32_t d1 = (a >> 8 & 0xFFu) | (b & 0xFF00u) | (c & 0xFF00u) << 8 | (d & 0xFF00u) << 16;
     const uint32_t d2 = (a >> 16 & 0xFFu) | (b >> 8 & 0xFF00u) | (c & 0xFF0000u) | (d & 0xFF0000u) << 8;
@@ -601,7 +602,24 @@ __device__ void ungroup_bg4(const uint8_t* __restrict__ st, uint8_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
     }
+  };
+  uint32_t p0 = 4 * lane;
+  for (; p0 + (kU - 1) * 4 * kWave < q4; p0 += kU * 4 * kWave) {
+    uint32_t a[kU], b[kU], c[kU], d[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t p = p0 + u * 4 * kWave;
+      a[u] = *reinterpret_cast<const uint32_t*>(st + p);
+      b[u] = load4(st + g1 + p, a1);
+      c[u] = load4(st + g2 + p, a2);
+      d[u] = load4(st + g3 + p, a3);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) step(p0 + u * 4 * kWave, a[u], b[u], c[u], d[u]);
   }
+  for (; p0 < q4; p0 += 4 * kWave)
+    step(p0, *reinterpret_cast<const uint32_t*>(st + p0), load4(st + g1 + p0, a1), load4(st + g2 + p0, a2),
+         load4(st + g3 + p0, a3));
   // the last q - q4 indices of every group, then the r leftover bytes (groups 0 .. r-1 hold one more)
   const uint32_t tail = 4 * (q - q4) + r;
   if (lane < tail) {
