@@ -53,6 +53,8 @@ def main() -> int:
                          "1250 ~ a 10 Gbps LAN peer")
     ap.add_argument("--jobs", type=int, default=0, help="leecher --concurrency (default: the CLI's 16)")
     a = ap.parse_args()
+    if a.trace:
+        Path(a.trace).mkdir(parents=True, exist_ok=True)
     rng = np.random.default_rng(1)
     shard = a.mb * 1_000_000 // a.shards
     files = {f"model-{i:05d}-of-{a.shards:05d}.safetensors": rng.integers(0, 256, shard, dtype=np.uint8).tobytes()
