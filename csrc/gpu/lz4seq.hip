@@ -696,13 +696,35 @@ __device__ __forceinline__ bool lds_wait(PairLds& L, const uint32_t* p, uint32_t
 // decoder issues little VALU work (~15 % of wave-cycles), so the hashing mostly fills idle issue
 // slots; only the last chunks' hashes add to the launch.  A chunk that fails hashes as all-ones.
 // (A template: kHash = false is the decode-only kernel, register allocation untouched by the hash.)
-template <bool kHash>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_pair(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  const ZgChunk* __restrict__ chunks, int n_chunks,
-                                                  unsigned long long* err, uint64_t src_n, uint64_t dst_n,
-                                                  uint8_t* __restrict__ hashes, uint64_t* __restrict__ sizes,
-                                                  uint8_t* __restrict__ stage, uint32_t dbg,
-                                                  uint32_t* __restrict__ work) {
+// (kDiag: the diagnostics build -- `dbg` bits read; the production kernels compile them out, so the
+// flags cost them no registers)
+// Kernel arguments of k_lz4_pair.  The kernel reads each field from the kernarg segment where it
+// uses it (pair_args(): an opaque copy of the segment pointer per use, so no field is hoisted and
+// held in a register across the decode loops) -- the producer's parse keeps ~80 SGPRs busy, and
+// arguments held live across it were spilled to VGPR lanes and from there to scratch memory.
+struct PairArgs {
+  const uint8_t* src;
+  uint8_t* dst;
+  const ZgChunk* chunks;
+  unsigned long long* err;
+  uint64_t src_n, dst_n;
+  uint8_t* hashes;
+  uint64_t* sizes;
+  uint8_t* stage;
+  uint32_t* work;
+  int n_chunks;
+  uint32_t dbg;
+};
+typedef const __attribute__((address_space(4))) PairArgs* PairArgsPtr;
+
+__device__ __forceinline__ PairArgsPtr pair_args() {
+  PairArgsPtr p = (PairArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+template <bool kHash, bool kDiag>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lz4_pair(const PairArgs args) {
   __shared__ PairLds L;
   const uint32_t lane = lane_id();
   const bool producer = uni(threadIdx.x >> 6) == 0;
@@ -718,28 +740,29 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
   // blocks that were dealt one chunk more than the others (a 256 MiB batch: ~4.2 k chunks on 4096
   // blocks, 98 of them decoding two in a row, tools/gpu/lz4_split_probe.py).  Stored chunks and
   // chunks that fail the range checks never get a ticket: the producer settles them itself.
-  int cs = int(uni(blockIdx.x));
-  uint32_t tk = 0;  // tickets taken (dynamic)
+  uint32_t tk = 0;  // chunks taken: dynamic, tickets; static, block b's k-th chunk is b + k * grid
   while (true) {
+    const PairArgsPtr A = pair_args();
+    const int n_chunks = A->n_chunks;
     int c;
-    if (work != nullptr) {
+    if (A->work != nullptr) {
       const uint32_t slot = tk % kPairTickets;
       if (producer) {
         while (true) {
           uint32_t v = 0;
-          if (lane == 0) v = atomicAdd(work, 1u);
+          if (lane == 0) v = atomicAdd(A->work, 1u);
           c = int(uni(v));
           if (c >= n_chunks) break;
-          const ZgChunk h = chunks[c];
+          const ZgChunk h = A->chunks[c];
           const uint32_t sc = uni(h.scheme), cl = uni(h.clen), ul = uni(h.ulen);
           const uint64_t so = uni64(h.src), dso = uni64(h.dst);
           if (sc == 0) continue;
-          const bool range_bad = so + cl > src_n || dso + ul > dst_n;
+          const bool range_bad = so + cl > A->src_n || dso + ul > A->dst_n;
           if (range_bad || ul > kMaxChunk) {
-            if (lane == 0) report(err, range_bad ? ZG_ERR_RANGE : ZG_ERR_CAPACITY, uint32_t(c));
+            if (lane == 0) report(pair_args()->err, range_bad ? ZG_ERR_RANGE : ZG_ERR_CAPACITY, uint32_t(c));
             if (kHash) {
-              if (lane < 8) reinterpret_cast<uint32_t*>(hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
-              if (sizes && lane == 0) sizes[c] = 0;
+              if (lane < 8) reinterpret_cast<uint32_t*>(pair_args()->hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
+              if (pair_args()->sizes && lane == 0) pair_args()->sizes[c] = 0;
             }
             continue;
           }
@@ -753,11 +776,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
       }
       ++tk;
     } else {
-      c = cs;
-      cs += int(gridDim.x);
+      c = int(uni(blockIdx.x + tk * gridDim.x));
+      ++tk;
     }
     if (c >= n_chunks) break;
-    ZgChunk ch = chunks[c];
+    ZgChunk ch = A->chunks[c];
     ch.src = uni64(ch.src);
     ch.dst = uni64(ch.dst);
     ch.clen = uni(ch.clen);
@@ -766,22 +789,22 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     if (ch.scheme == 0) continue;
     auto bad_hash = [&]() {  // (consumer) a chunk that is not decoded hashes as all-ones
       if (!kHash) return;
-      if (lane < 8) reinterpret_cast<uint32_t*>(hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
-      if (sizes && lane == 0) sizes[c] = 0;
+      if (lane < 8) reinterpret_cast<uint32_t*>(pair_args()->hashes + 32 * uint64_t(c))[lane] = 0xFFFFFFFFu;
+      if (pair_args()->sizes && lane == 0) pair_args()->sizes[c] = 0;
     };
-    if (ch.src + ch.clen > src_n || ch.dst + ch.ulen > dst_n) {
-      if (!producer && lane == 0) report(err, ZG_ERR_RANGE, uint32_t(c));
+    if (ch.src + ch.clen > A->src_n || ch.dst + ch.ulen > A->dst_n) {
+      if (!producer && lane == 0) report(pair_args()->err, ZG_ERR_RANGE, uint32_t(c));
       if (!producer) bad_hash();
       continue;
     }
     if (ch.ulen > kMaxChunk) {
-      if (!producer && lane == 0) report(err, ZG_ERR_CAPACITY, uint32_t(c));
+      if (!producer && lane == 0) report(pair_args()->err, ZG_ERR_CAPACITY, uint32_t(c));
       if (!producer) bad_hash();
       continue;
     }
     Ctx X;
-    X.pay = src + ch.src;
-    X.out = dst + ch.dst;
+    X.pay = A->src + ch.src;
+    X.out = A->dst + ch.dst;
     X.clen = ch.clen;
     X.ulen = ch.ulen;
     X.bg4 = ch.scheme == 2;
@@ -794,10 +817,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     X.heads = L.heads;
     X.ring = L.ring;
     // BG4 with a staging slice: decode the grouped stream contiguously into it (see ungroup_bg4)
-    uint8_t* const final_out = X.out;
-    const bool staged = stage != nullptr && X.bg4;
+    const bool staged = A->stage != nullptr && X.bg4;
     if (staged) {
-      X.out = stage + size_t(blockIdx.x) * kMaxChunk;
+      X.out = A->stage + size_t(blockIdx.x) * kMaxChunk;
       X.bg4 = false;
     }
     const uint32_t cmark = uint32_t(c) + 1u;
@@ -827,7 +849,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
       while (true) {
         const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
         if (!lds_wait(L, &L.full[slot], uses + 1u, lane)) {
-          if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
+          if (lane == 0) report(pair_args()->err, ZG_ERR_LZ4, uint32_t(c));
           bad_hash();
           return;
         }
@@ -842,9 +864,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           const uint32_t code = B.n & ~kPairEnd;
           if (!failed) {
             if (code) {
-              if (lane == 0) report(err, code, uint32_t(c));
+              if (lane == 0) report(pair_args()->err, code, uint32_t(c));
             } else if (X.obase != X.ulen) {
-              if (lane == 0) report(err, ZG_ERR_SIZE, uint32_t(c));
+              if (lane == 0) report(pair_args()->err, ZG_ERR_SIZE, uint32_t(c));
             } else {
               whole = true;
             }
@@ -853,14 +875,16 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
         }
         // (dbg & 1, diagnostics only: the consumer takes the records without executing them -- the
         // launch then times the parse alone, tools/gpu/lz4_split_probe.py; the chunk reports a size error)
-        if (!failed && !(dbg & 1u) && !exec_batch(B, X, lane)) {
+        if (!failed && !(kDiag && (pair_args()->dbg & 1u)) && !exec_batch(B, X, lane)) {
           failed = true;
-          if (lane == 0) report(err, ZG_ERR_LZ4, uint32_t(c));
+          if (lane == 0) report(pair_args()->err, ZG_ERR_LZ4, uint32_t(c));
           lds_release(&L.abort, cmark, lane);
         }
       }
-      if (dbg & 2u) whole = false;  // (diagnostics: execute only -- no ungroup, no hash)
+      if (kDiag && (pair_args()->dbg & 2u)) whole = false;  // (diagnostics: execute only -- no ungroup, no hash)
       if (staged) {
+        // (the chunk's final place re-read, not held across the batch loop)
+        uint8_t* const final_out = pair_args()->dst + uni64(pair_args()->chunks[c].dst);
         if (whole) {
           // the staged stream is complete in L2 (this wave's stores acknowledged, L1 dropped): write
           // the chunk's final bytes once
@@ -881,8 +905,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           uint32_t h[8];
           zg::wave_hash(X.out, X.ulen, zg::kDataKeyW, zg::KEYED_HASH, reinterpret_cast<uint32_t*>(L.ring), lane, h);
-          zg::store_hash(hashes + 32 * uint64_t(c), h, lane);
-          if (sizes && lane == 0) sizes[c] = X.ulen;
+          zg::store_hash(pair_args()->hashes + 32 * uint64_t(c), h, lane);
+          if (pair_args()->sizes && lane == 0) pair_args()->sizes[c] = X.ulen;
           __builtin_amdgcn_wave_barrier();  // the next chunk's exec_batch reuses the ring
         } else {
           bad_hash();
@@ -1151,12 +1175,14 @@ extern "C" hipError_t zg_lz4_pair_decode_hash_staged(const uint8_t* src, uint64_
     if (e != hipSuccess) return e;
   }
   if (!stage_enabled() || !stage || stage_bytes < size_t(grid) * kMaxChunk) stage = nullptr;
-  if (hashes)
-    hipLaunchKernelGGL(k_lz4_pair<true>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
-                       src_n, dst_n, hashes, sizes, stage, pair_debug(), work);
+  const uint32_t dbg = pair_debug();
+  const PairArgs args{src, dst, chunks, err, src_n, dst_n, hashes, sizes, stage, work, n_chunks, dbg};
+  if (hashes && dbg)
+    hipLaunchKernelGGL((k_lz4_pair<true, true>), dim3(grid), dim3(2 * kWave), 0, stream, args);
+  else if (hashes)
+    hipLaunchKernelGGL((k_lz4_pair<true, false>), dim3(grid), dim3(2 * kWave), 0, stream, args);
   else
-    hipLaunchKernelGGL(k_lz4_pair<false>, dim3(grid), dim3(2 * kWave), 0, stream, src, dst, chunks, n_chunks, err,
-                       src_n, dst_n, hashes, sizes, stage, pair_debug(), work);
+    hipLaunchKernelGGL((k_lz4_pair<false, false>), dim3(grid), dim3(2 * kWave), 0, stream, args);
   return hipGetLastError();
 }
 
