@@ -255,7 +255,8 @@ Bytes CasClient::fetch(const FetchInfo& fi, int timeout_ms) const {
   http::Response r = http::get_range(fi.url, fi.url_range.start, fi.url_range.end, h, opt);
   if (r.status != 200 && r.status != 206) throw Error("HttpError", "xorb fetch status " + std::to_string(r.status));
   if (r.status == 200 && out.size() > want) {
-    // Server ignored Range: slice it ourselves.
+    // Server ignored Range: slice it ourselves (the whole object must reach past the range).
+    if (out.size() - want < fi.url_range.start) throw Error("ShortRead", "xorb object shorter than its range");
     Bytes s(out.begin() + long(fi.url_range.start), out.begin() + long(fi.url_range.start + want));
     return s;
   }
