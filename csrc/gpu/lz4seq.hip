@@ -96,6 +96,7 @@ struct Ctx {
   uint32_t obase;       // output (grouped) offset of the next batch
   uint32_t* heads;      // this wave's 64-entry LDS scratch
   uint8_t* ring;        // this wave's kRing-byte LDS history of recent output
+  uint32_t* pf = nullptr;  // 64-dword LDS sink of the parse's stream prefetch (nullptr: none)
 };
 
 // Grouped-stream position -> byte offset in the chunk (identity unless BG4).
@@ -383,6 +384,22 @@ __device__ __forceinline__ uint64_t sload8(const uint32_t* w4, uint32_t p) {
   return v >> (8 * (p & 3));
 }
 
+// L2 prefetch of the compressed stream ahead of the parse: one wave-wide load, a dword per lane
+// 64 bytes apart (4 KiB of stream), issued as an LDS-DMA load (global_load_lds_dword into a 256-byte
+// sink nobody reads) so no VGPR waits for it -- the parse's scalar loads then miss the scalar cache
+// into L2 instead of into HBM.  The waits it can cause: an LDS access the compiler cannot tell apart
+// from the sink waits for the vector memory counter, i.e. the next batch publish (~64 sequences on).
+constexpr uint32_t kPfSpan = 4096;   // stream bytes per prefetch
+constexpr uint32_t kPfLead = 8192;   // keep the prefetch this far ahead of the parse
+
+__device__ __forceinline__ void prefetch_stream(const uint32_t* w4, uint32_t pos, uint32_t end, uint32_t* sink,
+                                                uint32_t lane) {
+  const uint32_t q = pos + lane * (kPfSpan / kWave);
+  if (q < end)
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(w4 + (q >> 2)),
+                                     (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
+}
+
 // Parse one LZ4 frame chunk into batches of records, handing each full batch to `flush` (which
 // executes it here, or passes it to a consumer wave in k_lz4_pair); returns 0 or an error code.
 // The caller checks the decoded size.
@@ -398,8 +415,13 @@ __device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& f
   uint32_t ip = k0 + 7 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
   const uint32_t bck = (flg & 0x10) ? 4 : 0;
   Batch B{0, 0, 0, 0};
+  uint32_t pf = ip;  // stream position up to which the prefetch is issued
   while (true) {
     if (B.n > kFlushAbove && !flush(B)) return ZG_ERR_LZ4;
+    if (X.pf && pf < end && pf < ip + kPfLead) {
+      prefetch_stream(w4, pf, end, X.pf, lane);
+      pf += kPfSpan;
+    }
     if (ip > end || end - ip < 4) return ZG_ERR_LZ4;
     const uint32_t bs = uint32_t(sload8(w4, ip));
     ip += 4;
@@ -418,6 +440,10 @@ __device__ __forceinline__ uint32_t parse_frame(Ctx& X, uint32_t lane, Flush&& f
         ip = uni(ip);
         B.n = uni(B.n);
         if (B.n > kFlushAbove && !flush(B)) return ZG_ERR_LZ4;
+        if (X.pf && pf < end && pf < ip + kPfLead) {  // (after the flush: its LDS waits come a batch later)
+          prefetch_stream(w4, pf, end, X.pf, lane);
+          pf = uni(pf + kPfSpan);
+        }
         if (ip >= bend) return ZG_ERR_LZ4;
         // Fast loop over the common short sequence (literals < 15, match < 19: no length bytes):
         // one 8-byte read at the end of its literals gives the offset and the NEXT token, so the
@@ -663,6 +689,7 @@ struct PairLds {
   uint32_t heads[kWave];
   uint32_t ticket[kPairTickets];  // dynamic scheduling: the chunk of the block's k-th ticket
   uint32_t tseq[kPairTickets];    // k + 1 once ticket k is written
+  uint32_t pf[kWave];             // the producer's stream-prefetch sink (written, never read)
   __attribute__((aligned(16))) uint8_t ring[kRing];
 };
 
@@ -714,6 +741,7 @@ struct PairArgs {
   uint32_t* work;
   int n_chunks;
   uint32_t dbg;
+  uint32_t prefetch;  // the producer's stream prefetch (ZG_PAIR_PREFETCH=0: off, for A/Bs)
 };
 typedef const __attribute__((address_space(4))) PairArgs* PairArgsPtr;
 
@@ -824,6 +852,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     const uint32_t cmark = uint32_t(c) + 1u;
     if (producer) {
+      X.pf = pair_args()->prefetch ? L.pf : nullptr;
       bool alive = true;
       auto publish = [&](uint32_t n, uint32_t rl, uint32_t rh, uint32_t rx) -> bool {
         const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
@@ -843,6 +872,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
         B.rl = B.rh = B.rx = 0;
         return ok;
       });
+      // the prefetches' LDS writes land before the block can exit (and its LDS be reallocated)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!alive || !publish(kPairEnd | code, 0u, 0u, 0u)) return;
     } else {
       bool failed = false, whole = false;
@@ -1176,7 +1207,9 @@ extern "C" hipError_t zg_lz4_pair_decode_hash_staged(const uint8_t* src, uint64_
   }
   if (!stage_enabled() || !stage || stage_bytes < size_t(grid) * kMaxChunk) stage = nullptr;
   const uint32_t dbg = pair_debug();
-  const PairArgs args{src, dst, chunks, err, src_n, dst_n, hashes, sizes, stage, work, n_chunks, dbg};
+  const char* pfv = getenv("ZG_PAIR_PREFETCH");  // read per launch: A/B of the stream prefetch
+  const uint32_t prefetch = (pfv && atoi(pfv) == 0) ? 0u : 1u;
+  const PairArgs args{src, dst, chunks, err, src_n, dst_n, hashes, sizes, stage, work, n_chunks, dbg, prefetch};
   if (hashes && dbg)
     hipLaunchKernelGGL((k_lz4_pair<true, true>), dim3(grid), dim3(2 * kWave), 0, stream, args);
   else if (hashes)

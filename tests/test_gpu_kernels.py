@@ -245,11 +245,14 @@ def test_decoder_hash_matches_place_hash(policy, monkeypatch):
     got = {}
     # (fused hash, BG4 staging, chunk schedule): staged decode writes the grouped stream to the scratch
     # slice and the final bytes once (ingest scratch); unstaged scatters straight into place; the
-    # dynamic schedule (work counter in the scratch) and the static one decode the same bytes
-    for env, stage, dyn in (("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "1", "0")):
+    # dynamic schedule (work counter in the scratch) and the static one decode the same bytes, and so
+    # does the parse without its L2 stream prefetch
+    for env, stage, dyn, pf in (("1", "1", "1", "1"), ("1", "0", "1", "1"), ("0", "1", "1", "1"), ("1", "1", "0", "1"),
+                                ("1", "1", "1", "0")):
         monkeypatch.setenv("ZG_FUSED_HASH", env)
         monkeypatch.setenv("ZG_BG4_STAGE", stage)
         monkeypatch.setenv("ZG_PAIR_DYNAMIC", dyn)
+        monkeypatch.setenv("ZG_PAIR_PREFETCH", pf)
         dst = ops.padded_empty(len(data), DEV)
         dst.fill_(0x3C)
         hashes = torch.full((nck + base, 32), 0x77, dtype=torch.uint8, device=DEV)
@@ -261,15 +264,18 @@ def test_decoder_hash_matches_place_hash(policy, monkeypatch):
                         torch.cuda.current_stream().cuda_stream, sp, sb)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
-        assert dst.cpu().numpy().tobytes() == data, (env, stage, dyn)
-        got[env + stage + dyn] = (hashes.cpu().numpy(), sizes.cpu().numpy())
+        assert dst.cpu().numpy().tobytes() == data, (env, stage, dyn, pf)
+        got[env + stage + dyn + pf] = (hashes.cpu().numpy(), sizes.cpu().numpy())
     monkeypatch.delenv("ZG_FUSED_HASH")
     monkeypatch.delenv("ZG_BG4_STAGE")
     monkeypatch.delenv("ZG_PAIR_DYNAMIC")
-    (h1, s1), (h0, s0), (hu, su), (hs, ss) = got["111"], got["011"], got["101"], got["110"]
+    monkeypatch.delenv("ZG_PAIR_PREFETCH")
+    (h1, s1), (h0, s0), (hu, su), (hs, ss) = got["1111"], got["0111"], got["1011"], got["1101"]
+    hp, sp_ = got["1110"]
     assert np.array_equal(h1, h0) and np.array_equal(s1, s0)
     assert np.array_equal(h1, hu) and np.array_equal(s1, su)
     assert np.array_equal(h1, hs) and np.array_equal(s1, ss)
+    assert np.array_equal(h1, hp) and np.array_equal(s1, sp_)
     assert h1[base:].tobytes() == b"".join(b.chunk_hashes())
     assert (h1[:base] == 0x77).all() and (s1[:base] == -1).all()
     assert s1[base:].tolist() == list(np.diff([0] + list(ends)))

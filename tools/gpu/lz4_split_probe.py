@@ -6,7 +6,7 @@ Builds N(0, 0.02) bf16 weights as BG4-LZ4 xorbs (the gpubench `lz4_decode_gpu_ho
 the chunk records from the host header walk, and times one fused decode + hash launch over:
 
   * all chunks (the real launch), checked byte-exact, with the dynamic chunk schedule (default) and
-    the static one (ZG_PAIR_DYNAMIC=0);
+    the static one (ZG_PAIR_DYNAMIC=0), and without the parse's stream prefetch (ZG_PAIR_PREFETCH=0);
   * all chunks with ZG_PAIR_DEBUG=1 -- the consumer wave takes the records without executing them,
     so the launch times the parse alone (its size errors are expected and ignored); and with
     ZG_PAIR_DEBUG=2 -- parse and execute, but no BG4 ungroup and no fused hash;
@@ -91,6 +91,18 @@ def main() -> int:
                 raise RuntimeError("decoded bytes differ from the input (static schedule)")
         finally:
             os.environ.pop("ZG_PAIR_DYNAMIC", None)
+        os.environ["ZG_PAIR_PREFETCH"] = "0"  # no L2 prefetch of the compressed stream ahead of the parse
+        try:
+            dst.zero_()
+            ns_p = _time(launch(allc), a.runs)
+            torch.cuda.synchronize()
+            ops.raise_on_error(ws.err)
+            if dst[:len(raw)].cpu().numpy().tobytes() != raw:
+                raise RuntimeError("decoded bytes differ from the input (no prefetch)")
+        finally:
+            os.environ.pop("ZG_PAIR_PREFETCH", None)
+        out["no_prefetch_ms"] = round(ns_p / 1e6, 3)
+        out["no_prefetch_GBps"] = round(len(raw) / ns_p, 2)
         out["static_ms"] = round(ns_s / 1e6, 3)
         out["static_GBps"] = round(len(raw) / ns_s, 2)
         os.environ["ZG_FUSED_HASH"] = "0"  # decode only, then the place/hash pass hashes every chunk
