@@ -855,6 +855,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
       X.pf = pair_args()->prefetch ? L.pf : nullptr;
       bool alive = true;
       auto publish = [&](uint32_t n, uint32_t rl, uint32_t rh, uint32_t rx) -> bool {
+        q = uni(q);  // (wave-uniform: keeps the slot waits on the scalar unit)
         const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
         if (!lds_wait(L, &L.done[slot], uses, lane)) return alive = false;
         L.rl[slot][lane] = rl;
@@ -878,6 +879,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))
     } else {
       bool failed = false, whole = false;
       while (true) {
+        q = uni(q);  // (wave-uniform: keeps the slot waits on the scalar unit)
         const uint32_t slot = q & (kPairSlots - 1), uses = q / kPairSlots;
         if (!lds_wait(L, &L.full[slot], uses + 1u, lane)) {
           if (lane == 0) report(pair_args()->err, ZG_ERR_LZ4, uint32_t(c));
